@@ -1,0 +1,212 @@
+/* loner_amd.h — C ABI of the MI355X-native LONER implicit-map optimisation path.
+ *
+ * Every entry point replaces one piece of the reference's sigma-field step
+ * (esulimma/LONER @ 2024_08_07; file:line relative to /root/reference):
+ *
+ *   lnr_hashgrid_fwd/_bwd(_rays)  tinycudann HashGrid encode used by
+ *                                 tcnn.NetworkWithInputEncoding  src/models/nerf_tcnn.py:35-38,68/71
+ *                                 and tcnn.Encoding              src/models/nerf_tcnn.py:40,64
+ *   lnr_sigma_mlp_fwd/_bwd        tcnn FullyFusedMLP (32->64 ReLU->1, no bias)
+ *                                 src/models/nerf_tcnn.py:35-38, cfg/nerf_config/default_nerf_hash.yaml:26-31
+ *   lnr_sample_ogm / _uniform     OccGridRaySampler / UniformRaySampler + sample_pdf
+ *                                 src/models/ray_sampling.py:18-92, src/models/rendering_tcnn.py:19-68
+ *   lnr_composite                 raw2outputs / raw2outputs_adjusted src/models/rendering_tcnn.py:70-295
+ *   lnr_composite_loss_bwd        compute_loss (LiDAR branch) + autograd through raw2outputs
+ *                                 src/mapping/optimizer.py:701-859, src/models/losses.py:29-51
+ *   lnr_field_train               fused sigma MLP fwd + composite + loss + composite bwd + MLP bwd
+ *                                 (the body of one optimiser step, src/mapping/optimizer.py:436-450)
+ *   lnr_loss_finalize             scalar loss / mean depth-eps from per-ray partials (optimizer.py:767,838-844)
+ *   lnr_adam_step                 torch.optim.Adam step on the flat params  src/mapping/optimizer.py:255-265,460
+ *   lnr_ogm_update                Optimizer._step_occupancy_grid  src/mapping/optimizer.py:897-908
+ *
+ * Conventions:
+ *   - all data pointers are DEVICE pointers owned by the caller (PyTorch); no allocation, no host
+ *     synchronisation inside any call; every call only enqueues work on `stream` (a hipStream_t,
+ *     NULL = default stream) and is safe to capture in a hipGraph;
+ *   - return 0 (LNR_OK) or a negative error code; lnr_last_error() returns a thread-local message;
+ *   - stateless and re-entrant.
+ *
+ * Layouts:
+ *   rays     (R, 13) fp32  [o(3) d(3) viewdir(3) 0 0 near far]   src/common/ray_utils.py:314-317
+ *   z        (R, S)  fp32  sorted sample depths (normalised units)
+ *   table    (n_entries, 2) fp16 forward shadow; fp32 master/grad/m/v in the optimiser
+ *   enc      "level-major": element (sample n, level l) at enc[l * enc_stride + n], one half2
+ *            (uint32) per element; enc_stride >= N.  The tcnn-compatible AoS layout (N, 2L) is
+ *            produced by lnr_enc_to_aos.
+ *   d_enc    same indexing, one float2 per element
+ *   mlp      sigma MLP weights, row-major [out][in] per layer: W0 (64,32) then W1 (16,64); fp16
+ */
+#ifndef LONER_AMD_H
+#define LONER_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LNR_OK 0
+#define LNR_ERR_ARG (-1)
+#define LNR_ERR_HIP (-2)
+
+#define LNR_MAX_LEVELS 32
+
+const char* lnr_last_error(void);
+int lnr_version(void);
+
+/* ---------------------------------------------------------------- hash grid */
+typedef struct lnr_grid_desc {
+  uint32_t n_levels;          /* tcnn "n_levels" */
+  uint32_t n_features;        /* tcnn "n_features_per_level"; must be 2 */
+  uint32_t log2_hashmap_size; /* tcnn "log2_hashmap_size" */
+  uint32_t base_resolution;   /* tcnn "base_resolution" */
+  float per_level_scale;      /* tcnn "per_level_scale" (default 2.0) */
+  uint32_t n_entries;         /* sum of level sizes */
+  float scale[LNR_MAX_LEVELS];
+  uint32_t resolution[LNR_MAX_LEVELS];
+  uint32_t size[LNR_MAX_LEVELS];
+  uint32_t offset[LNR_MAX_LEVELS + 1];
+} lnr_grid_desc;
+
+/* Fill `d` exactly as tcnn v1.7's GridEncodingTemplated constructor lays the levels out. */
+int lnr_grid_desc_init(lnr_grid_desc* d, uint32_t n_levels, uint32_t n_features, uint32_t log2_hashmap_size,
+                       uint32_t base_resolution, float per_level_scale);
+
+/* pos01 (N,3) fp32 in [0,1]^3 -> enc (level-major half2).  tcnn Encoding forward.
+ * bwd_ws (optional, may be NULL): the backward workspace of the SAME positions; when given, the
+ * forward also records the backward's per-block record histogram, so a following backward can be
+ * called with LNR_BWD_COUNTS_READY and skips its counting pass. */
+int lnr_hashgrid_fwd(const lnr_grid_desc* d, const float* pos01, int64_t n, const uint16_t* table,
+                     uint32_t* enc, int64_t enc_stride, void* bwd_ws, int64_t bwd_ws_bytes, void* stream);
+/* Positions generated from rays and samples: pos01 = (o + d*z + 1) / 2 (nerf_tcnn.py:63). */
+int lnr_hashgrid_fwd_rays(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
+                          int32_t n_samples, const uint16_t* table, uint32_t* enc, int64_t enc_stride,
+                          void* bwd_ws, int64_t bwd_ws_bytes, void* stream);
+/* Backward: d_table (n_entries,2) fp32 = scatter of corner weights * d_enc, as an atomic-free
+ * binned scatter with int64 fixed-point accumulation.  d_table must be zero on entry
+ * (chunks spanning several work slices add into it); `workspace` holds at least
+ * lnr_hashgrid_bwd_workspace_bytes(d, N) bytes. */
+#define LNR_BWD_COUNTS_READY 1
+int64_t lnr_hashgrid_bwd_workspace_bytes(const lnr_grid_desc* d, int64_t n);
+int lnr_hashgrid_bwd(const lnr_grid_desc* d, const float* pos01, int64_t n, const float* d_enc,
+                     int64_t enc_stride, float* d_table, void* workspace, int64_t workspace_bytes, int32_t flags,
+                     void* stream);
+int lnr_hashgrid_bwd_rays(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
+                          int32_t n_samples, const float* d_enc, int64_t enc_stride, float* d_table,
+                          void* workspace, int64_t workspace_bytes, int32_t flags, void* stream);
+/* Same result with one fp32 atomic pair per corner (coarse levels merged in-wave); d_table
+ * accumulates.  Kept as an independent implementation for cross-checking and A/B timing. */
+int lnr_hashgrid_bwd_atomic(const lnr_grid_desc* d, const float* pos01, int64_t n, const float* d_enc,
+                            int64_t enc_stride, float* d_table, void* stream);
+int lnr_hashgrid_bwd_rays_atomic(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
+                                 int32_t n_samples, const float* d_enc, int64_t enc_stride, float* d_table,
+                                 void* stream);
+/* level-major half2 -> tcnn AoS (N, 2L) fp16, and AoS fp16/fp32 grads -> level-major float2. */
+int lnr_enc_to_aos(const uint32_t* enc, int64_t enc_stride, int64_t n, uint32_t n_levels, uint16_t* out, void* stream);
+int lnr_aos_grad_to_enc(const uint16_t* g_aos_f16, const float* g_aos_f32, int64_t n, uint32_t n_levels,
+                        float* d_enc, int64_t enc_stride, void* stream);
+
+/* ---------------------------------------------------------------- sigma MLP */
+#define LNR_SIGMA_W0 (64 * 32)
+#define LNR_SIGMA_W1 (16 * 64)
+#define LNR_SIGMA_MLP_PARAMS (LNR_SIGMA_W0 + LNR_SIGMA_W1)
+
+/* sigma (N) fp16 = MLP(enc).  Non-finite outputs are clamped to +-65504 (nerf_tcnn.py:74-78). */
+int lnr_sigma_mlp_fwd(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, int64_t n, uint16_t* sigma,
+                      void* stream);
+/* Number of fp32 words of workspace lnr_sigma_mlp_bwd / lnr_field_train need for dW slabs. */
+int64_t lnr_dw_workspace_words(int64_t n_rows);
+/* d_sigma (N) fp32 -> d_enc (level-major float2, overwritten) and d_w (3072 fp32, ACCUMULATED). */
+int lnr_sigma_mlp_bwd(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, int64_t n, const float* d_sigma,
+                      float* d_enc, float* d_w, float* workspace, void* stream);
+
+/* ---------------------------------------------------------------- sampling */
+/* Random draws: when u_* is NULL, draws come from the counter-based generator keyed by `key`
+ * (see lnr_step_key) and the GLOBAL ray index ray_offset + r, so a sharded batch draws exactly
+ * what the unsharded batch draws.  Otherwise u_jitter is (R, S/2) and u_pdf is (R, S/2). */
+uint32_t lnr_step_key(uint32_t seed, uint32_t step);
+int lnr_sample_ogm(const float* rays, int64_t n_rays, int32_t n_samples, const float* occ, int32_t occ_res,
+                   float perturb, const float* u_jitter, const float* u_pdf, uint32_t key, int64_t ray_offset,
+                   float* z, void* stream);
+int lnr_sample_uniform(const float* rays, int64_t n_rays, int32_t n_samples, float perturb, const float* u_jitter,
+                       uint32_t key, int64_t ray_offset, float* z, void* stream);
+
+/* ---------------------------------------------------------------- compositing + loss */
+#define LNR_RENDER_DEFAULT 0
+#define LNR_RENDER_ADJUSTED 1
+
+#define LNR_LOSS_L1_JS 0
+#define LNR_LOSS_L2_JS 1
+#define LNR_LOSS_L1_LOS 2
+#define LNR_LOSS_L2_LOS 3
+
+typedef struct lnr_loss_params {
+  int32_t kind;            /* LNR_LOSS_* (optimizer.py:757-791) */
+  float scale;             /* world-cube scale factor (metres per normalised unit) */
+  float los_lambda;        /* already decayed for this global step (optimizer.py:712-716) */
+  float depthloss_lambda;  /* loss.depthloss_lambda */
+  float min_depth_eps;     /* loss.min_depth_eps */
+  float min_js, max_js, js_alpha; /* loss.JS_loss */
+  float los_eps;           /* L*_LOS only: decayed depth_eps for this iteration (optimizer.py:781-785) */
+  float far_ref;           /* far bound of GLOBAL ray 0: optimizer.py:724 compares every ray with it */
+  float inv_n_opaque;      /* 1 / (global opaque-ray count) */
+  float inv_rs;            /* 1 / (global rays * samples) */
+  const float* dev_n_opaque; /* optional DEVICE scalar: global opaque count (e.g. after an all-reduce);
+                                when non-NULL it overrides inv_n_opaque (= 1/max(count,1)) */
+} lnr_loss_params;
+
+/* Per-ray partial sums written by the loss kernels: [depth_sq_err, los_sum, opacity_abs_err, eps, opaque] */
+#define LNR_RAY_STATS 5
+
+/* Forward compositing from given sigma (R,S) fp32 (fp16-valued) and noise (R,S) (NULL + noise_std>0 ->
+ * generated; noise_std==0 -> none).  Outputs may be NULL except depth. */
+int lnr_composite(const float* rays, const float* z, const float* sigma, int64_t n_rays, int32_t n_samples,
+                  int32_t strategy, float noise_std, const float* noise, uint32_t key, int64_t ray_offset,
+                  float* weights, float* depth, float* opacity, float* variance, void* stream);
+/* Training loss + gradient from given sigma: d_sigma (R,S) fp32, ray_stats (R, LNR_RAY_STATS). */
+int lnr_composite_loss_bwd(const float* rays, const float* z, const float* sigma, const float* depth_gt,
+                           int64_t n_rays, int32_t n_samples, float noise_std, const float* noise, uint32_t key,
+                           int64_t ray_offset, const lnr_loss_params* lp, float* weights, float* depth,
+                           float* opacity, float* d_sigma, float* ray_stats, void* stream);
+/* Fused: sigma MLP forward from enc, compositing, loss, compositing backward, MLP backward.
+ * Writes d_enc (level-major float2), accumulates d_w (3072 fp32), per-ray stats; optional outputs NULL. */
+int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, const float* rays, const float* z,
+                    const float* depth_gt, int64_t n_rays, int32_t n_samples, float noise_std, const float* noise,
+                    uint32_t key, int64_t ray_offset, const lnr_loss_params* lp, float* d_enc, float* d_w,
+                    float* workspace, float* ray_stats, float* depth, float* opacity, float* weights, void* stream);
+/* Forward-only fused render from enc (inference path, C3 shape): sigma MLP + compositing. */
+int lnr_field_render(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, const float* rays, const float* z,
+                     int64_t n_rays, int32_t n_samples, int32_t strategy, float noise_std, const float* noise,
+                     uint32_t key, int64_t ray_offset, float* depth, float* opacity, float* variance,
+                     float* weights, void* stream);
+/* out[0] = loss, out[1] = mean eps, out[2..4] = depth/los/opacity terms, out[5] = opaque count,
+ * from (R, LNR_RAY_STATS). */
+int lnr_loss_finalize(const float* ray_stats, int64_t n_rays, const lnr_loss_params* lp, float* out, void* stream);
+
+/* out[0] = number of opaque rays: depth_gt > 0 && !(depth_gt > far_ref) (optimizer.py:724-727). */
+int lnr_count_opaque(const float* depth_gt, int64_t n_rays, float far_ref, float* out, void* stream);
+
+/* ---------------------------------------------------------------- optimiser */
+/* torch.optim.Adam (no weight decay); step is 1-based.  shadow (fp16) may be NULL. */
+int lnr_adam_step(float* param, uint16_t* shadow, const float* grad, float* m, float* v, int64_t n, int32_t step,
+                  float lr, float beta1, float beta2, float eps, void* stream);
+/* OGM update: occ (res^3) -= lr * grid_sample^T(logits_grad(z*scale - depth_gt*scale)). grad_ws (res^3) fp32
+ * is zeroed and used as accumulation workspace. */
+int lnr_ogm_update(const float* rays, const float* z, const float* depth_gt, int64_t n_rays, int32_t n_samples,
+                   float scale, float lr, float* occ, float* grad_ws, int32_t occ_res, void* stream);
+
+/* Split form for data-parallel runs: grad_ws += grid_sample^T(logits_grad) (caller zeroes), then
+ * occ -= lr * grad_ws after the caller has all-reduced grad_ws. */
+int lnr_ogm_grad(const float* rays, const float* z, const float* depth_gt, int64_t n_rays, int32_t n_samples,
+                 float scale, float* grad_ws, int32_t occ_res, void* stream);
+int lnr_sgd_step(float* param, const float* grad, int64_t n, float lr, void* stream);
+
+/* ---------------------------------------------------------------- utilities */
+/* dst[i] = lo + (hi-lo) * U(splitmix64(((uint64)seed << 32) + start + i)) */
+int lnr_fill_uniform(float* dst, int64_t n, uint32_t seed, float lo, float hi, int64_t start, void* stream);
+int lnr_f32_to_f16(const float* src, uint16_t* dst, int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LONER_AMD_H */

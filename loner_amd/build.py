@@ -1,0 +1,82 @@
+"""Build the HIP C-ABI library ``loner_amd/_lib/libloner_amd.so`` for gfx950 (in-tree, so the
+built .so travels to the GPU box with the repo snapshot).
+
+    python -m loner_amd.build [--jobs N] [--force]
+
+Plain hipcc, one object per translation unit, then a shared link.  No torch types cross the
+boundary: the library exports exactly the symbols declared in ``include/loner_amd.h``.
+"""
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "_lib")
+LIB = os.path.join(LIBDIR, "libloner_amd.so")
+OBJDIR = os.path.join(ROOT, "build", "obj")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("LONER_ARCH", "gfx950")
+# -ffp-contract=off: elementwise fp32 math rounds after every op, like the reference's torch ops.
+FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-ffp-contract=off", "-Wall",
+         "-Wno-unused-function", "-I", os.path.join(ROOT, "include")]
+
+
+def _sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+
+def _deps():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hpp")) + [os.path.join(ROOT, "include", "loner_amd.h")])
+
+
+def _compile(src):
+    obj = os.path.join(OBJDIR, os.path.basename(src).replace(".hip", ".o"))
+    newest_dep = max(os.path.getmtime(p) for p in _deps() + [src])
+    if os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
+        return obj, ""
+    cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+    return obj, r.stderr
+
+
+def build(jobs=8, force=False, verbose=False):
+    os.makedirs(OBJDIR, exist_ok=True)
+    os.makedirs(LIBDIR, exist_ok=True)
+    if force:
+        for o in glob.glob(os.path.join(OBJDIR, "*.o")):
+            os.remove(o)
+    srcs = _sources()
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        results = list(ex.map(_compile, srcs))
+    objs = [o for o, _ in results]
+    if verbose:
+        for o, err in results:
+            if err.strip():
+                print(f"[{os.path.basename(o)}]\n{err}", file=sys.stderr)
+    if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
+        return LIB
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    return LIB
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args()
+    print(build(a.jobs, a.force, a.verbose))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,108 @@
+// Shared device/host helpers for the LONER MI355X path (gfx950, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstdarg>
+#include <cmath>
+
+#include "../../include/loner_amd.h"
+
+namespace lnr {
+
+// ------------------------------------------------------------------ errors (host)
+void set_error(const char* fmt, ...);
+#define LNR_REQUIRE(cond, ...)                     \
+  do {                                             \
+    if (!(cond)) {                                 \
+      ::lnr::set_error(__VA_ARGS__);               \
+      return LNR_ERR_ARG;                          \
+    }                                              \
+  } while (0)
+#define LNR_RETURN_LAUNCH(what)                                                   \
+  do {                                                                            \
+    hipError_t e_ = hipGetLastError();                                            \
+    if (e_ != hipSuccess) {                                                       \
+      ::lnr::set_error("%s: HIP launch failed: %s", what, hipGetErrorString(e_)); \
+      return LNR_ERR_HIP;                                                         \
+    }                                                                             \
+    return LNR_OK;                                                                \
+  } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+constexpr int kWave = 64;
+
+// ------------------------------------------------------------------ RNG (oracle/rng.py)
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+__host__ __device__ __forceinline__ uint32_t rand_u32(uint32_t key, uint32_t stream, uint32_t a, uint32_t b) {
+  uint32_t h = mix32(key ^ (stream * 0x9E3779B9u));
+  h = mix32(h ^ a);
+  h = mix32(h ^ (b * 0x85EBCA6Bu + 0x632BE5ABu));
+  return h;
+}
+__device__ __forceinline__ float rand_uniform(uint32_t key, uint32_t stream, uint32_t a, uint32_t b) {
+  return (float)(rand_u32(key, stream, a, b) >> 8) * 5.9604644775390625e-08f;  // 2^-24
+}
+__device__ __forceinline__ float rand_normal(uint32_t key, uint32_t stream, uint32_t a, uint32_t b) {
+  float u1 = ((float)(rand_u32(key, stream, a, b) >> 8) + 1.0f) * 5.9604644775390625e-08f;
+  float u2 = (float)(rand_u32(key, stream + 1, a, b) >> 8) * 5.9604644775390625e-08f;
+  return sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2);
+}
+enum : uint32_t { kStreamJitter = 1, kStreamPdf = 2, kStreamNoise = 3 };
+
+// ------------------------------------------------------------------ fp16
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef float float4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float h2f(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
+__device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+__device__ __forceinline__ float round_f16(float f) { return (float)(_Float16)f; }
+__device__ __forceinline__ float2 half2_to_float2(uint32_t v) {
+  return make_float2(h2f((uint16_t)(v & 0xFFFFu)), h2f((uint16_t)(v >> 16)));
+}
+
+// ------------------------------------------------------------------ wave / block reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum of K values for a block of NT threads (NT/64 waves).  `scratch` needs
+// K * (NT/64) floats; all threads receive the totals.  Contains two barriers.
+template <int NT, int K>
+__device__ __forceinline__ void block_sum(float (&v)[K], float* scratch) {
+  constexpr int NW = NT / kWave;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = wave_sum(v[k]);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) scratch[k * NW + wid] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) s += scratch[k * NW + w];
+    v[k] = s;
+  }
+  __syncthreads();
+}
+
+}  // namespace lnr

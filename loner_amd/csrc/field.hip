@@ -1,0 +1,652 @@
+// Per-ray fused kernels: sigma MLP -> volume compositing -> LiDAR loss -> compositing backward ->
+// MLP backward, one 256-thread workgroup per ray (persistent over rays).
+//
+// Reference semantics (file:line in /root/reference):
+//   raw2outputs            src/models/rendering_tcnn.py:219-295  (default; noise active, far term)
+//   raw2outputs_adjusted   src/models/rendering_tcnn.py:70-214   (T <= 0.5 crossing; overrides inert)
+//   compute_loss (LiDAR)   src/mapping/optimizer.py:718-844, losses.py:29-51, JS/KL optimizer.py:913-925
+//   autograd of the above  replaced by the division-free reverse affine scan documented in
+//                          oracle/render.py::composite_backward
+// Every per-sample intermediate (alpha, T, w, w_gt, dL/dw, dL/dsigma, hidden activations) lives in
+// registers/LDS; HBM sees z, the level-major encodings in, d_enc out and per-ray scalars.
+#include "common.hpp"
+#include "mlp.hpp"
+
+namespace lnr {
+
+constexpr int NT = 256;  // threads per ray-block
+constexpr int NW = NT / 64;
+
+enum SigmaSrc { kSigmaGiven = 0, kSigmaMLP = 1 };
+
+struct FieldArgs {
+  const float* rays;
+  const float* z;
+  const float* sigma_in;   // kSigmaGiven
+  const uint16_t* w;       // kSigmaMLP
+  const uint32_t* enc;
+  int64_t enc_stride;
+  const float* depth_gt;
+  const float* noise;
+  int64_t n_rays;
+  int32_t S;
+  float noise_std;
+  uint32_t key;
+  int64_t ray_offset;
+  lnr_loss_params lp;
+  // outputs
+  float* weights;
+  float* depth;
+  float* opacity;
+  float* variance;
+  float* d_sigma;     // kSigmaGiven + train
+  float* d_enc;       // kSigmaMLP + train
+  float* dw_slab;     // kSigmaMLP + train: [gridDim.x][3072]
+  float* ray_stats;   // train: [R][LNR_RAY_STATS]
+};
+
+struct RayShared {
+  float* sig;        // [S] sigma, then dL/dsigma
+  float* red;        // reduction scratch [16 * NW]
+  double* dscan;     // [NW] wave products
+  float* fscan;      // [2 * NW] affine wave totals
+  float* lastT;      // [NT]
+  float* slot;       // [4]
+  _Float16* mlp;     // [NW][64*32 + 32*32]
+};
+
+// ---------------------------------------------------------------- block scans
+// Exclusive multiplicative scan of per-thread doubles across the block.
+__device__ __forceinline__ double block_excl_prod(double p, double* dscan) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  double inc = p;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    double q = __shfl_up(inc, o, 64);
+    if (lane >= o) inc *= q;
+  }
+  if (lane == 63) dscan[wid] = inc;
+  __syncthreads();
+  double pre = 1.0;
+  for (int w = 0; w < wid; ++w) pre *= dscan[w];
+  double excl = __shfl_up(inc, 1, 64);
+  if (lane == 0) excl = 1.0;
+  __syncthreads();
+  return pre * excl;
+}
+
+// Reverse (suffix) scan of affine maps F_t(x) = A x + B; returns X_t = (F_{t+1} o ... o F_last)(0).
+__device__ __forceinline__ float block_suffix_affine(float A, float B, float* fscan) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float qa = A, qb = B;  // inclusive suffix composition Q_t = F_t o Q_{t+1}
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    float na = __shfl_down(qa, o, 64), nb = __shfl_down(qb, o, 64);
+    if (lane + o < 64) {
+      qb = qa * nb + qb;
+      qa = qa * na;
+    }
+  }
+  if (lane == 0) {
+    fscan[2 * wid] = qa;
+    fscan[2 * wid + 1] = qb;
+  }
+  __syncthreads();
+  // value entering this wave from the right: (W_{w+1} o ... o W_last)(0)
+  float xw = 0.f;
+  for (int w = NW - 1; w > wid; --w) xw = fscan[2 * w] * xw + fscan[2 * w + 1];
+  float na = __shfl_down(qa, 1, 64), nb = __shfl_down(qb, 1, 64);
+  float x = (lane == 63) ? xw : na * xw + nb;
+  __syncthreads();
+  return x;
+}
+
+// ---------------------------------------------------------------- compositing + loss for one ray
+template <int C, bool TRAIN, bool ADJ>
+__device__ void composite_ray(const FieldArgs& a, const RayShared& sh, int64_t r) {
+  const int t = threadIdx.x;
+  const int S = a.S;
+  const int i0 = t * C;
+  const bool active = i0 < S;
+  const float* ry = a.rays + 13 * r;
+  const float dx = ry[3], dy = ry[4], dz = ry[5];
+  const float far = ry[12];
+  const float dnorm = sqrtf(dx * dx + dy * dy + dz * dz);
+  const float* zr = a.z + r * S;
+  const int64_t gr = a.ray_offset + r;
+
+  float z[C], alpha[C], s[C], delta[C], x[C], w[C];
+  double tl[C];
+  double P = 1.0;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int i = i0 + c;
+    if (active && i < S) {
+      z[c] = zr[i];
+      const float zn = (i + 1 < S) ? zr[i + 1] : 0.f;
+      const float dl = (i + 1 < S) ? (zn - z[c]) : 1e10f;
+      delta[c] = dl * dnorm;
+      float nz = 0.f;
+      if (!ADJ) {
+        if (a.noise) nz = a.noise[r * S + i] * a.noise_std;
+        else if (a.noise_std > 0.f) nz = rand_normal(a.key, kStreamNoise, (uint32_t)gr, (uint32_t)i) * a.noise_std;
+      }
+      x[c] = sh.sig[i] + nz;
+      const float sr = fmaxf(x[c], 0.f);
+      alpha[c] = 1.0f - expf(-(delta[c] * sr));
+      s[c] = (1.0f - alpha[c]) + 1e-10f;
+    } else {
+      z[c] = 0.f; delta[c] = 0.f; x[c] = 0.f; alpha[c] = 0.f; s[c] = 1.f;
+    }
+    tl[c] = P;
+    P *= (double)s[c];
+  }
+  const double T0 = block_excl_prod(P, sh.dscan);
+  float T[C];
+  float sw = 0.f;
+  double acc_w = 0.0, acc_wz = 0.0, acc_wzs = 0.0;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    T[c] = (float)(T0 * tl[c]);
+    w[c] = alpha[c] * T[c];
+    if (active && i0 + c < S) {
+      acc_w += (double)w[c];
+      acc_wz += (double)(w[c] * z[c]);
+      if (TRAIN) acc_wzs += (double)((z[c] * a.lp.scale) * w[c]);
+    }
+  }
+  (void)sw;
+  float redA[3] = {(float)acc_w, (float)acc_wz, (float)acc_wzs};
+  // block sums in double-rounded float: wave sums of per-thread doubles cast to float are exact
+  // enough for S <= 4096 (see DESIGN.md numerics); the reference sums fp32 products.
+  block_sum<NT, 3>(redA, sh.red);
+  const float wsum = redA[0];
+  float depth;
+  if (ADJ) {
+    if (t == 0) sh.slot[0] = 0.f;
+    float lt = 1.0f;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      if (active && i0 + c < S) lt = T[c];
+    sh.lastT[t] = lt;
+    __syncthreads();
+    float Tprev = (t == 0) ? 1.0f : sh.lastT[t - 1];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      if (active && i0 + c < S) {
+        if (!(T[c] > 0.5f) && (Tprev > 0.5f)) sh.slot[0] = z[c];
+        Tprev = T[c];
+      }
+    }
+    __syncthreads();
+    depth = sh.slot[0];
+    __syncthreads();
+  } else {
+    const float tail = (1.0f - wsum) * far;
+    depth = (float)((double)redA[1] + (double)tail);
+  }
+  const float opacity = wsum;
+
+  // pass B: variance of the render, and the loss-side weighted variance
+  const float wden = wsum + 1e-10f;
+  const float mean = TRAIN ? redA[2] / wden : 0.f;
+  double acc_var = 0.0, acc_lv = 0.0;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    if (active && i0 + c < S) {
+      const float dd = depth - z[c];
+      acc_var += (double)(w[c] * (dd * dd));
+      if (TRAIN) {
+        const float e = z[c] * a.lp.scale - mean;
+        acc_lv += (double)((e * e) * w[c]);
+      }
+    }
+  }
+  float redB[2] = {(float)acc_var, (float)acc_lv};
+  block_sum<NT, 2>(redB, sh.red);
+  const float variance = redB[0];
+
+  if (t == 0) {
+    if (a.depth) a.depth[r] = depth;
+    if (a.opacity) a.opacity[r] = opacity;
+    if (a.variance) a.variance[r] = variance;
+  }
+  if (!TRAIN) {
+    if (a.weights && active)
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+        if (i0 + c < S) a.weights[r * S + i0 + c] = w[c];
+    return;
+  }
+
+  // ------------------------------------------------ loss (optimizer.py:718-844)
+  const lnr_loss_params& lp = a.lp;
+  const float inv_nop = lp.dev_n_opaque ? 1.0f / fmaxf(lp.dev_n_opaque[0], 1.0f) : lp.inv_n_opaque;
+  const float dgt = a.depth_gt[r];
+  const float g = dgt * lp.scale;
+  const bool opaque = (dgt > 0.f) && !(dgt > lp.far_ref);
+  const float lvar = redB[1] / wden + 1e-10f;
+  const float stdv = sqrtf(lvar);
+  float eps;
+  if (lp.kind == LNR_LOSS_L1_JS || lp.kind == LNR_LOSS_L2_JS) {
+    const float s1 = lp.min_depth_eps / 3.0f;
+    const float mm = 0.5f * (g + mean);
+    const float smv = 0.5f * sqrtf(s1 * s1 + stdv * stdv);
+    const float v2 = smv * smv;
+    const float kl1 = logf(smv / s1) + (s1 * s1 + (g - mm) * (g - mm)) / (2.0f * v2) - 0.5f;
+    const float kl2 = logf(smv / stdv) + (stdv * stdv + (mean - mm) * (mean - mm)) / (2.0f * v2) - 0.5f;
+    float js = 0.5f * kl1 + 0.5f * kl2;
+    if (js < lp.min_js) js = 0.f;
+    if (js > lp.max_js) js = lp.max_js;
+    eps = lp.min_depth_eps * (1.0f + lp.js_alpha * js);
+  } else {
+    eps = lp.los_eps;
+  }
+  // truncated Gaussian target (losses.py:29-51)
+  const float sg = eps / 9.0f;
+  const float clip_a = ((g - eps) - g) / sg;
+  const float clip_b = ((g + eps) - g) / sg;
+  const float cdf_a = 0.5f * (1.0f + erff(clip_a / 1.4142135623730951f));
+  const float cdf_b = 0.5f * (1.0f + erff(clip_b / 1.4142135623730951f));
+  const float zden = cdf_b - cdf_a;
+  float wgt[C];
+  double acc_gt = 0.0;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    wgt[c] = 0.f;
+    if (active && i0 + c < S) {
+      const float sm = z[c] * lp.scale;
+      const float xx = (sm - g) / sg;
+      const float pdf = 0.3989422804014327f * expf(-0.5f * (xx * xx));
+      const float v = pdf / sg / zden;
+      const bool inside = ((sm - (g - eps)) > 0.f) && (((g + eps) - sm) > 0.f);
+      wgt[c] = inside ? v : 0.f;
+      acc_gt += (double)wgt[c];
+    }
+  }
+  float redC[1] = {(float)acc_gt};
+  block_sum<NT, 1>(redC, sh.red);
+  const float gt_den = redC[0] + 1e-6f;
+  const bool l1 = (lp.kind == LNR_LOSS_L1_JS || lp.kind == LNR_LOSS_L1_LOS);
+  const float d_euc = depth * lp.scale;
+  const float ddiff = d_euc - g;
+  const float g_depth = opaque ? lp.depthloss_lambda * 2.0f * ddiff * lp.scale * inv_nop : 0.f;
+  const float operr = opacity - 1.0f;
+  const float g_op = opaque ? ((operr > 0.f) ? 1.f : (operr < 0.f ? -1.f : 0.f)) * inv_nop : 0.f;
+  float G[C];
+  double acc_los = 0.0;
+  float FA = 1.f, FB = 0.f;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    G[c] = 0.f;
+    if (active && i0 + c < S) {
+      const float wg = opaque ? wgt[c] / gt_den : 0.f;
+      const float dw = w[c] - wg;
+      float gw;
+      if (l1) {
+        gw = lp.los_lambda * ((dw > 0.f) ? 1.f : (dw < 0.f ? -1.f : 0.f)) * lp.inv_rs;
+        acc_los += (double)fabsf(dw);
+      } else {
+        gw = lp.los_lambda * 2.0f * dw * lp.inv_rs;
+        acc_los += (double)(dw * dw);
+      }
+      G[c] = gw + g_depth * (z[c] - far) + g_op;
+    }
+  }
+  // F_t composed right-to-left over the chunk: x <- G_k alpha_k + s_k x
+#pragma unroll
+  for (int c = C - 1; c >= 0; --c) {
+    if (active && i0 + c < S) {
+      FB = G[c] * alpha[c] + s[c] * FB;
+      FA = s[c] * FA;
+    }
+  }
+  float redD[1] = {(float)acc_los};
+  block_sum<NT, 1>(redD, sh.red);
+  float X = block_suffix_affine(FA, FB, sh.fscan);
+#pragma unroll
+  for (int c = C - 1; c >= 0; --c) {
+    if (active && i0 + c < S) {
+      const float dA = T[c] * (G[c] - X);
+      X = G[c] * alpha[c] + s[c] * X;
+      const float sr = fmaxf(x[c], 0.f);
+      const float dsig = (x[c] > 0.f) ? dA * (delta[c] * expf(-(delta[c] * sr))) : 0.f;
+      sh.sig[i0 + c] = dsig;
+      if (a.d_sigma) a.d_sigma[r * S + i0 + c] = dsig;
+    }
+  }
+  if (a.weights && active)
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      if (i0 + c < S) a.weights[r * S + i0 + c] = w[c];
+  if (t == 0) {
+    float* st = a.ray_stats + r * LNR_RAY_STATS;
+    st[0] = opaque ? ddiff * ddiff : 0.f;
+    st[1] = redD[0];
+    st[2] = opaque ? fabsf(operr) : 0.f;
+    st[3] = eps;
+    st[4] = opaque ? 1.f : 0.f;
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------- MLP phases
+__device__ __forceinline__ void mlp_forward_ray(const FieldArgs& a, const RayShared& sh, const SigmaWeights& sw,
+                                                int64_t r) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+  const int per_wave = a.S / NW;
+  for (int tb = wid * per_wave; tb < (wid + 1) * per_wave; tb += 16) {
+    const int64_t n = r * a.S + tb + c;
+    half8_t b = load_enc_operand(a.enc, a.enc_stride, n, true);
+    float h[16];
+    const float sg = sigma_tile_fwd(sw, b, h);
+    if (g == 0) sh.sig[tb + c] = sigma_to_f16(sg);
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void mlp_backward_ray(const FieldArgs& a, const RayShared& sh, const SigmaWeights& sw,
+                                                 int64_t r, DW0Acc& acc, float (&dw1)[16]) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+  const int per_wave = a.S / NW;
+  _Float16* lds = sh.mlp + wid * (64 * 32 + 32 * 32);
+  float2* denc = reinterpret_cast<float2*>(a.d_enc);
+  for (int tb = wid * per_wave; tb < (wid + 1) * per_wave; tb += 32) {
+    float h0[16], h1[16];
+    half8_t e0, e1;
+    float ds0, ds1;
+    {
+      const int64_t n = r * a.S + tb + c;
+      e0 = load_enc_operand(a.enc, a.enc_stride, n, true);
+      (void)sigma_tile_fwd(sw, e0, h0);
+      ds0 = sh.sig[tb + c];
+    }
+    const bool second = tb + 16 < (wid + 1) * per_wave;
+    {
+      const int64_t n = r * a.S + tb + 16 + c;
+      e1 = load_enc_operand(a.enc, a.enc_stride, n, second);
+      (void)sigma_tile_fwd(sw, e1, h1);
+      ds1 = second ? sh.sig[tb + 16 + c] : 0.f;
+    }
+    float mx = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      dw1[k] = fmaf(ds0, h0[k], dw1[k]);
+      dw1[k] = fmaf(ds1, h1[k], dw1[k]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fmaxf(fabsf((float)e0[j] * ds0), fabsf((float)e1[j] * ds1)));
+    const float scale = grad_scale(wave_max(mx));
+    float d[2][4];
+    sigma_tile_bwd_denc(sw, h0, d);
+    {
+      const int64_t n = r * a.S + tb + c;
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int lvl = 8 * m + 2 * g;
+        denc[(int64_t)lvl * a.enc_stride + n] = make_float2(d[m][0] * ds0, d[m][1] * ds0);
+        denc[(int64_t)(lvl + 1) * a.enc_stride + n] = make_float2(d[m][2] * ds0, d[m][3] * ds0);
+      }
+    }
+    sigma_tile_bwd_denc(sw, h1, d);
+    if (second) {
+      const int64_t n = r * a.S + tb + 16 + c;
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int lvl = 8 * m + 2 * g;
+        denc[(int64_t)lvl * a.enc_stride + n] = make_float2(d[m][0] * ds1, d[m][1] * ds1);
+        denc[(int64_t)(lvl + 1) * a.enc_stride + n] = make_float2(d[m][2] * ds1, d[m][3] * ds1);
+      }
+    }
+    dw0_pair(lds, sw, h0, h1, e0, e1, ds0, ds1, scale, acc);
+  }
+}
+
+// ---------------------------------------------------------------- kernels
+template <int C, bool TRAIN, bool ADJ, int SRC>
+__global__ void __launch_bounds__(NT) k_field(FieldArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  RayShared sh;
+  {
+    char* p = smem;
+    sh.sig = reinterpret_cast<float*>(p);
+    p += ((a.S * 4 + 15) / 16) * 16;
+    sh.red = reinterpret_cast<float*>(p);
+    p += 16 * NW * 4;
+    sh.dscan = reinterpret_cast<double*>(p);
+    p += NW * 8;
+    sh.fscan = reinterpret_cast<float*>(p);
+    p += 2 * NW * 4;
+    sh.lastT = reinterpret_cast<float*>(p);
+    p += NT * 4;
+    sh.slot = reinterpret_cast<float*>(p);
+    p += 16;
+    sh.mlp = reinterpret_cast<_Float16*>(p);
+  }
+  SigmaWeights sw;
+  DW0Acc acc;
+  float dw1[16];
+  if (SRC == kSigmaMLP) {
+    load_sigma_weights(a.w, sw);
+    if (TRAIN) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) dw1[k] = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc.v[t][m][q] = 0.f;
+    }
+  }
+  for (int64_t r = blockIdx.x; r < a.n_rays; r += gridDim.x) {
+    if (SRC == kSigmaMLP) {
+      mlp_forward_ray(a, sh, sw, r);
+    } else {
+      for (int i = threadIdx.x; i < a.S; i += NT) sh.sig[i] = a.sigma_in[r * a.S + i];
+      __syncthreads();
+    }
+    composite_ray<C, TRAIN, ADJ>(a, sh, r);
+    if (SRC == kSigmaMLP && TRAIN) mlp_backward_ray(a, sh, sw, r, acc, dw1);
+    __syncthreads();
+  }
+  if (SRC == kSigmaMLP && TRAIN) {
+    write_dw_slab<NT>(reinterpret_cast<float*>(smem), acc, dw1, a.dw_slab + (int64_t)blockIdx.x * LNR_SIGMA_MLP_PARAMS);
+  }
+}
+
+// dW[i] += sum_b slab[b][i]  (fixed order: deterministic)
+// dW[i] += sum_b slab[b][i]: blockIdx.y splits the slabs into groups of 32 (one atomic per group).
+__global__ void k_reduce_slabs(const float* __restrict__ slab, int nb, float* __restrict__ dw) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= LNR_SIGMA_MLP_PARAMS) return;
+  const int b0 = blockIdx.y * 32, b1 = b0 + 32 < nb ? b0 + 32 : nb;
+  float s = 0.f;
+  for (int b = b0; b < b1; ++b) s += slab[(int64_t)b * LNR_SIGMA_MLP_PARAMS + i];
+  atomicAdd(&dw[i], s);
+}
+
+__global__ void k_loss_finalize(const float* __restrict__ st, int64_t n, lnr_loss_params lp, float* out) {
+  __shared__ float red[5 * 4];
+  double a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0;
+  for (int64_t r = threadIdx.x; r < n; r += blockDim.x) {
+    const float* s = st + r * LNR_RAY_STATS;
+    a0 += s[0];
+    a1 += s[1];
+    a2 += s[2];
+    a3 += s[3];
+    a4 += s[4];
+  }
+  float v[5] = {(float)a0, (float)a1, (float)a2, (float)a3, (float)a4};
+  block_sum<256, 5>(v, red);
+  if (threadIdx.x == 0) {
+    const float inv_nop = lp.dev_n_opaque ? 1.0f / fmaxf(lp.dev_n_opaque[0], 1.0f) : lp.inv_n_opaque;
+    const float dterm = v[0] * inv_nop;
+    const float lterm = v[1] * lp.inv_rs;
+    const float oterm = v[2] * inv_nop;
+    out[0] = lp.depthloss_lambda * dterm + lp.los_lambda * lterm + oterm;
+    out[1] = n > 0 ? v[3] / (float)n : 0.f;
+    out[2] = dterm;
+    out[3] = lterm;
+    out[4] = oterm;
+    out[5] = v[4];
+  }
+}
+
+static int chunk_for(int S) {
+  int c = (S + NT - 1) / NT;
+  int p = 1;
+  while (p < c) p <<= 1;
+  return p;
+}
+
+static size_t smem_bytes(int S, bool mlp_train) {
+  size_t b = ((size_t)S * 4 + 15) / 16 * 16 + 16 * NW * 4 + NW * 8 + 2 * NW * 4 + NT * 4 + 16;
+  b = (b + 15) / 16 * 16;
+  if (mlp_train) b += (size_t)NW * (64 * 32 + 32 * 32) * 2;
+  if (mlp_train && b < LNR_SIGMA_MLP_PARAMS * 4) b = LNR_SIGMA_MLP_PARAMS * 4;
+  return b;
+}
+
+template <bool TRAIN, bool ADJ, int SRC>
+static int launch_field(const FieldArgs& a, int nblocks, hipStream_t st, const char* who) {
+  const int C = chunk_for(a.S);
+  const size_t sm = smem_bytes(a.S, SRC == kSigmaMLP && TRAIN);
+  dim3 grid(nblocks), block(NT);
+  switch (C) {
+    case 1: hipLaunchKernelGGL((k_field<1, TRAIN, ADJ, SRC>), grid, block, sm, st, a); break;
+    case 2: hipLaunchKernelGGL((k_field<2, TRAIN, ADJ, SRC>), grid, block, sm, st, a); break;
+    case 4: hipLaunchKernelGGL((k_field<4, TRAIN, ADJ, SRC>), grid, block, sm, st, a); break;
+    case 8: hipLaunchKernelGGL((k_field<8, TRAIN, ADJ, SRC>), grid, block, sm, st, a); break;
+    case 16: hipLaunchKernelGGL((k_field<16, TRAIN, ADJ, SRC>), grid, block, sm, st, a); break;
+    default: set_error("%s: n_samples=%d too large (max 4096)", who, a.S); return LNR_ERR_ARG;
+  }
+  LNR_RETURN_LAUNCH(who);
+}
+
+static int field_blocks(int64_t n_rays) { return (int)(n_rays < 1024 ? n_rays : 1024); }
+
+}  // namespace lnr
+
+using namespace lnr;
+
+extern "C" int64_t lnr_dw_workspace_words(int64_t n_rows) {
+  int64_t nb = n_rows < 1024 ? n_rows : 1024;
+  if (nb < 1) nb = 1;
+  return nb * LNR_SIGMA_MLP_PARAMS;
+}
+
+static int check_rays(const float* rays, const float* z, int64_t n_rays, int32_t S, const char* who) {
+  LNR_REQUIRE(n_rays >= 0, "%s: n_rays=%lld", who, (long long)n_rays);
+  LNR_REQUIRE(S >= 2 && S <= 4096, "%s: n_samples=%d not in [2,4096]", who, S);
+  LNR_REQUIRE(n_rays == 0 || (rays && z), "%s: null rays/z", who);
+  return LNR_OK;
+}
+
+extern "C" int lnr_composite(const float* rays, const float* z, const float* sigma, int64_t n_rays, int32_t n_samples,
+                             int32_t strategy, float noise_std, const float* noise, uint32_t key, int64_t ray_offset,
+                             float* weights, float* depth, float* opacity, float* variance, void* stream) {
+  if (int e = check_rays(rays, z, n_rays, n_samples, "lnr_composite")) return e;
+  LNR_REQUIRE(strategy == LNR_RENDER_DEFAULT || strategy == LNR_RENDER_ADJUSTED,
+              "Unknown render strategy: %d", strategy);  // rendering_tcnn.py:403-404 raises ValueError
+  if (n_rays == 0) return LNR_OK;
+  LNR_REQUIRE(sigma && depth, "lnr_composite: null sigma/depth");
+  FieldArgs a{};
+  a.rays = rays; a.z = z; a.sigma_in = sigma; a.n_rays = n_rays; a.S = n_samples;
+  a.noise_std = noise_std; a.noise = noise; a.key = key; a.ray_offset = ray_offset;
+  a.weights = weights; a.depth = depth; a.opacity = opacity; a.variance = variance;
+  const int nb = field_blocks(n_rays);
+  if (strategy == LNR_RENDER_ADJUSTED)
+    return launch_field<false, true, kSigmaGiven>(a, nb, as_stream(stream), "lnr_composite");
+  return launch_field<false, false, kSigmaGiven>(a, nb, as_stream(stream), "lnr_composite");
+}
+
+static int check_lp(const lnr_loss_params* lp, const char* who) {
+  LNR_REQUIRE(lp != nullptr, "%s: null loss params", who);
+  LNR_REQUIRE(lp->kind >= 0 && lp->kind <= 3, "Can't use unknown Loss %d", lp->kind);
+  return LNR_OK;
+}
+
+extern "C" int lnr_composite_loss_bwd(const float* rays, const float* z, const float* sigma, const float* depth_gt,
+                                      int64_t n_rays, int32_t n_samples, float noise_std, const float* noise,
+                                      uint32_t key, int64_t ray_offset, const lnr_loss_params* lp, float* weights,
+                                      float* depth, float* opacity, float* d_sigma, float* ray_stats, void* stream) {
+  if (int e = check_rays(rays, z, n_rays, n_samples, "lnr_composite_loss_bwd")) return e;
+  if (int e = check_lp(lp, "lnr_composite_loss_bwd")) return e;
+  if (n_rays == 0) return LNR_OK;
+  LNR_REQUIRE(sigma && depth_gt && d_sigma && ray_stats, "lnr_composite_loss_bwd: null pointer");
+  FieldArgs a{};
+  a.rays = rays; a.z = z; a.sigma_in = sigma; a.depth_gt = depth_gt; a.n_rays = n_rays; a.S = n_samples;
+  a.noise_std = noise_std; a.noise = noise; a.key = key; a.ray_offset = ray_offset; a.lp = *lp;
+  a.weights = weights; a.depth = depth; a.opacity = opacity; a.d_sigma = d_sigma; a.ray_stats = ray_stats;
+  return launch_field<true, false, kSigmaGiven>(a, field_blocks(n_rays), as_stream(stream), "lnr_composite_loss_bwd");
+}
+
+extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, const float* rays,
+                               const float* z, const float* depth_gt, int64_t n_rays, int32_t n_samples,
+                               float noise_std, const float* noise, uint32_t key, int64_t ray_offset,
+                               const lnr_loss_params* lp, float* d_enc, float* d_w, float* workspace,
+                               float* ray_stats, float* depth, float* opacity, float* weights, void* stream) {
+  if (int e = check_rays(rays, z, n_rays, n_samples, "lnr_field_train")) return e;
+  if (int e = check_lp(lp, "lnr_field_train")) return e;
+  LNR_REQUIRE(n_samples % 64 == 0, "lnr_field_train: n_samples=%d must be a multiple of 64", n_samples);
+  LNR_REQUIRE(enc_stride >= n_rays * (int64_t)n_samples, "lnr_field_train: enc_stride too small");
+  if (n_rays == 0) return LNR_OK;
+  LNR_REQUIRE(w && enc && depth_gt && d_enc && d_w && workspace && ray_stats, "lnr_field_train: null pointer");
+  FieldArgs a{};
+  a.w = w; a.enc = enc; a.enc_stride = enc_stride; a.rays = rays; a.z = z; a.depth_gt = depth_gt;
+  a.n_rays = n_rays; a.S = n_samples; a.noise_std = noise_std; a.noise = noise; a.key = key;
+  a.ray_offset = ray_offset; a.lp = *lp; a.d_enc = d_enc; a.dw_slab = workspace; a.ray_stats = ray_stats;
+  a.depth = depth; a.opacity = opacity; a.weights = weights;
+  const int nb = field_blocks(n_rays);
+  hipStream_t st = as_stream(stream);
+  int e = launch_field<true, false, kSigmaMLP>(a, nb, st, "lnr_field_train");
+  if (e) return e;
+  hipLaunchKernelGGL(k_reduce_slabs, dim3((LNR_SIGMA_MLP_PARAMS + 255) / 256, (nb + 31) / 32), dim3(256), 0, st, workspace, nb, d_w);
+  LNR_RETURN_LAUNCH("lnr_field_train(reduce)");
+}
+
+extern "C" int lnr_field_render(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, const float* rays,
+                                const float* z, int64_t n_rays, int32_t n_samples, int32_t strategy, float noise_std,
+                                const float* noise, uint32_t key, int64_t ray_offset, float* depth, float* opacity,
+                                float* variance, float* weights, void* stream) {
+  if (int e = check_rays(rays, z, n_rays, n_samples, "lnr_field_render")) return e;
+  LNR_REQUIRE(strategy == LNR_RENDER_DEFAULT || strategy == LNR_RENDER_ADJUSTED,
+              "Unknown render strategy: %d", strategy);
+  LNR_REQUIRE(n_samples % 64 == 0, "lnr_field_render: n_samples=%d must be a multiple of 64", n_samples);
+  LNR_REQUIRE(enc_stride >= n_rays * (int64_t)n_samples, "lnr_field_render: enc_stride too small");
+  if (n_rays == 0) return LNR_OK;
+  LNR_REQUIRE(w && enc && depth, "lnr_field_render: null pointer");
+  FieldArgs a{};
+  a.w = w; a.enc = enc; a.enc_stride = enc_stride; a.rays = rays; a.z = z; a.n_rays = n_rays; a.S = n_samples;
+  a.noise_std = noise_std; a.noise = noise; a.key = key; a.ray_offset = ray_offset;
+  a.depth = depth; a.opacity = opacity; a.variance = variance; a.weights = weights;
+  const int nb = field_blocks(n_rays);
+  if (strategy == LNR_RENDER_ADJUSTED)
+    return launch_field<false, true, kSigmaMLP>(a, nb, as_stream(stream), "lnr_field_render");
+  return launch_field<false, false, kSigmaMLP>(a, nb, as_stream(stream), "lnr_field_render");
+}
+
+__global__ void k_count_opaque(const float* __restrict__ dgt, int64_t n, float far_ref, float* out) {
+  __shared__ float red[4];
+  float c = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) c += (dgt[i] > 0.f && !(dgt[i] > far_ref)) ? 1.f : 0.f;
+  float v[1] = {c};
+  block_sum<256, 1>(v, red);
+  if (threadIdx.x == 0) out[0] = v[0];
+}
+
+extern "C" int lnr_count_opaque(const float* depth_gt, int64_t n_rays, float far_ref, float* out, void* stream) {
+  LNR_REQUIRE(n_rays >= 0 && out, "lnr_count_opaque: bad arguments");
+  LNR_REQUIRE(n_rays == 0 || depth_gt, "lnr_count_opaque: null depth_gt");
+  hipLaunchKernelGGL(k_count_opaque, dim3(1), dim3(256), 0, as_stream(stream), depth_gt, n_rays, far_ref, out);
+  LNR_RETURN_LAUNCH("lnr_count_opaque");
+}
+
+extern "C" int lnr_loss_finalize(const float* ray_stats, int64_t n_rays, const lnr_loss_params* lp, float* out,
+                                 void* stream) {
+  if (int e = check_lp(lp, "lnr_loss_finalize")) return e;
+  LNR_REQUIRE(ray_stats && out, "lnr_loss_finalize: null pointer");
+  hipLaunchKernelGGL(k_loss_finalize, dim3(1), dim3(256), 0, as_stream(stream), ray_stats, n_rays, *lp, out);
+  LNR_RETURN_LAUNCH("lnr_loss_finalize");
+}

@@ -1,0 +1,247 @@
+// Shared definitions of the multi-resolution hash grid (tiny-cuda-nn v1.7 HashGrid semantics):
+// level layout, corner indexing, sample positions, and the backward's bucket geometry.
+#pragma once
+#include "common.hpp"
+
+namespace lnr {
+
+struct LevelParams {
+  float scale;
+  uint32_t res;
+  uint32_t size;
+  uint32_t size_mask;  // size - 1 when size is a power of two, else 0
+  uint32_t offset;
+  uint32_t hashed;     // stride walk exceeded size -> coherent prime hash
+};
+
+// Backward buckets: each level's table slice is cut into chunks of 2^kChunkLog2 entries; one
+// chunk is one LDS accumulator of 4096 entries x 2 features x int64 fixed point = 64 KB.
+constexpr int kChunkLog2 = 12;
+constexpr int kChunk = 1 << kChunkLog2;
+constexpr int kMaxChunksPerLevel = 128;
+constexpr int kMaxBuckets = 2048;
+constexpr int64_t kSliceRecords = 1 << 20;  // records per accumulation work item
+
+struct GridArgs {
+  LevelParams lv[LNR_MAX_LEVELS];
+  uint32_t bucket_base[LNR_MAX_LEVELS + 1];
+  uint32_t n_levels;
+  uint32_t n_buckets;
+  uint32_t merge_levels;  // levels [0, merge_levels) merge equal corner indices across lanes
+};
+
+// Levels whose cell edge spans several consecutive samples of a ray (resolution <= 256 at the
+// reference's ray lengths / sample counts) produce runs of equal corner indices.
+inline uint32_t merge_levels_for(const lnr_grid_desc* d) {
+  uint32_t m = 0;
+  for (uint32_t l = 0; l < d->n_levels; ++l)
+    if (d->resolution[l] <= 256) m = l + 1;
+  return m;
+}
+
+inline GridArgs make_args(const lnr_grid_desc* d) {
+  GridArgs a{};
+  a.n_levels = d->n_levels;
+  for (uint32_t l = 0; l < d->n_levels; ++l) {
+    LevelParams& p = a.lv[l];
+    p.scale = d->scale[l];
+    p.res = d->resolution[l];
+    p.size = d->size[l];
+    p.size_mask = (p.size & (p.size - 1)) == 0 ? p.size - 1 : 0;
+    p.offset = d->offset[l];
+    // grid_index: dense stride walk while stride <= size; hashed iff final stride > size
+    uint64_t stride = 1;
+    for (int dim = 0; dim < 3 && stride <= p.size; ++dim) stride *= p.res;
+    p.hashed = stride > p.size ? 1u : 0u;
+  }
+  uint32_t b = 0;
+  for (uint32_t l = 0; l < d->n_levels; ++l) {
+    a.bucket_base[l] = b;
+    b += (d->size[l] + kChunk - 1) / kChunk;
+  }
+  a.bucket_base[d->n_levels] = b;
+  a.n_buckets = b;
+  a.merge_levels = merge_levels_for(d);
+  return a;
+}
+
+__device__ __forceinline__ uint32_t grid_index(const LevelParams& p, uint32_t x, uint32_t y, uint32_t z) {
+  uint32_t idx;
+  if (p.hashed) {
+    idx = x ^ (y * 2654435761u) ^ (z * 805459861u);
+  } else {
+    idx = x + y * p.res + z * p.res * p.res;
+  }
+  return p.size_mask ? (idx & p.size_mask) : (idx % p.size);
+}
+
+// Sample position in [0,1]^3.  From rays: xyz = o + d*z (rendering_tcnn.py:390), pos = (xyz+1)/2
+// (nerf_tcnn.py:63); compiled with -ffp-contract=off so the op order matches torch.
+struct PosFromArray {
+  const float* pos;
+  __device__ __forceinline__ void operator()(int64_t n, float& x, float& y, float& z) const {
+    x = pos[3 * n + 0];
+    y = pos[3 * n + 1];
+    z = pos[3 * n + 2];
+  }
+};
+struct PosFromRays {
+  const float* rays;
+  const float* zs;
+  int32_t n_samples;
+  __device__ __forceinline__ void operator()(int64_t n, float& x, float& y, float& z) const {
+    const int64_t r = n / n_samples;
+    const float* ry = rays + 13 * r;
+    const float t = zs[n];
+    x = (ry[0] + ry[3] * t + 1.0f) * 0.5f;
+    y = (ry[1] + ry[4] * t + 1.0f) * 0.5f;
+    z = (ry[2] + ry[5] * t + 1.0f) * 0.5f;
+  }
+};
+
+struct Corners {
+  uint32_t idx[8];
+  float w[8];
+};
+
+__device__ __forceinline__ void level_corners(const LevelParams& p, float x, float y, float z, Corners& c) {
+  // tcnn pos_fract: pos = fmaf(scale, x, 0.5); cell = floor(pos); frac = pos - cell
+  float px = fmaf(p.scale, x, 0.5f), py = fmaf(p.scale, y, 0.5f), pz = fmaf(p.scale, z, 0.5f);
+  float fx = floorf(px), fy = floorf(py), fz = floorf(pz);
+  uint32_t cx = (uint32_t)(int)fx, cy = (uint32_t)(int)fy, cz = (uint32_t)(int)fz;
+  float tx = px - fx, ty = py - fy, tz = pz - fz;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int bx = k & 1, by = (k >> 1) & 1, bz = (k >> 2) & 1;
+    float w = bx ? tx : 1.0f - tx;
+    w *= by ? ty : 1.0f - ty;
+    w *= bz ? tz : 1.0f - tz;
+    c.w[k] = w;
+    c.idx[k] = p.offset + grid_index(p, cx + bx, cy + by, cz + bz);
+  }
+}
+
+// Runs of equal keys across consecutive lanes: head/tail flags and the lane of the run head.
+struct RunInfo {
+  unsigned long long heads;
+  int head_lane;
+  bool tail;
+};
+__device__ __forceinline__ RunInfo lane_runs(uint32_t key) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t prev = __shfl_up(key, 1, 64);
+  const bool head = (lane == 0) || (prev != key);
+  RunInfo ri;
+  ri.heads = __ballot(head);
+  ri.head_lane = 63 - __clzll(ri.heads & ((2ull << lane) - 1ull));
+  ri.tail = (lane == 63) || ((ri.heads >> (lane + 1)) & 1ull);
+  return ri;
+}
+// Segmented inclusive sum: the tail lane of each run ends with the run total.
+__device__ __forceinline__ void run_sum(const RunInfo& ri, float& v0, float& v1) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float q0 = __shfl_up(v0, o, 64), q1 = __shfl_up(v1, o, 64);
+    if (lane - o >= ri.head_lane) {
+      v0 += q0;
+      v1 += q1;
+    }
+  }
+}
+
+// Rank of this lane's record among the block's records of the same bucket (LDS counters).
+// Coherent levels put most of a wave's records into one or two buckets: there each distinct
+// bucket of the wave does one atomic (ballot + popcount) instead of 64 same-address atomics.
+__device__ __forceinline__ uint32_t wave_bucket_rank(uint32_t* hist, uint32_t bucket, bool valid, bool coherent) {
+  if (!coherent) return valid ? atomicAdd(&hist[bucket], 1u) : 0u;
+  const int lane = threadIdx.x & 63;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  unsigned long long todo = __ballot(valid);
+  uint32_t rank = 0;
+  while (todo) {
+    const int leader = __ffsll((long long)todo) - 1;
+    const uint32_t b = __shfl(bucket, leader, 64);
+    const unsigned long long m = __ballot(valid && bucket == b);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&hist[b], (uint32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    if (valid && bucket == b) rank = base + (uint32_t)__popcll(m & lt);
+    todo &= ~m;
+  }
+  return rank;
+}
+
+// Backward workspace (device), carved from one caller-provided buffer.
+struct BwdWorkspace {
+  uint32_t* hist;        // [n_buckets][n_bx] records per (bucket, 256-sample block) -> exclusive offsets
+  float* blockmax;       // [n_levels][n_bx] max |record value| per block
+  float* level_max;      // [LNR_MAX_LEVELS]
+  uint32_t* counts;      // [kMaxBuckets]
+  uint64_t* seg_start;   // [kMaxBuckets + 1]
+  uint32_t* slice_pre;   // [kMaxBuckets + 1]
+  uint64_t* records;     // [8 * N * L] {idx in chunk (13b), g0 (fp25), g1 (fp25)}
+  int64_t n_bx;
+};
+
+inline int64_t bwd_n_bx(int64_t n) { return (n + 255) / 256; }
+
+inline int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
+
+inline int64_t bwd_workspace_bytes(const lnr_grid_desc* d, int64_t n) {
+  GridArgs a = make_args(d);
+  const int64_t nbx = bwd_n_bx(n);
+  int64_t b = 0;
+  b += align256((int64_t)a.n_buckets * nbx * 4);
+  b += align256((int64_t)d->n_levels * nbx * 4);
+  b += align256(LNR_MAX_LEVELS * 4);
+  b += align256(kMaxBuckets * 4);
+  b += align256((kMaxBuckets + 1) * 8);
+  b += align256((kMaxBuckets + 1) * 4);
+  b += align256(8 * n * (int64_t)d->n_levels * 8);
+  return b;
+}
+
+inline BwdWorkspace carve_workspace(void* base, const GridArgs& a, int64_t n) {
+  BwdWorkspace w{};
+  char* p = reinterpret_cast<char*>(base);
+  w.n_bx = bwd_n_bx(n);
+  w.hist = reinterpret_cast<uint32_t*>(p);
+  p += align256((int64_t)a.n_buckets * w.n_bx * 4);
+  w.blockmax = reinterpret_cast<float*>(p);
+  p += align256((int64_t)a.n_levels * w.n_bx * 4);
+  w.level_max = reinterpret_cast<float*>(p);
+  p += align256(LNR_MAX_LEVELS * 4);
+  w.counts = reinterpret_cast<uint32_t*>(p);
+  p += align256(kMaxBuckets * 4);
+  w.seg_start = reinterpret_cast<uint64_t*>(p);
+  p += align256((kMaxBuckets + 1) * 8);
+  w.slice_pre = reinterpret_cast<uint32_t*>(p);
+  p += align256((kMaxBuckets + 1) * 4);
+  w.records = reinterpret_cast<uint64_t*>(p);
+  return w;
+}
+
+// Per-(block, level) record histogram, written as column bx of the bucket-major hist array.
+// Shared by the forward (training mode) and the standalone count kernel: identical corners and
+// identical merge decisions as the scatter kernel, so counts and ranks agree exactly.
+__device__ __forceinline__ void count_block_records(const GridArgs& a, uint32_t l, const Corners& c, bool in,
+                                                    uint32_t* hist, const BwdWorkspace& ws) {
+  const uint32_t nb = a.bucket_base[l + 1] - a.bucket_base[l];
+  const bool coherent = l < a.merge_levels;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t idx = in ? c.idx[k] : 0xFFFFFFFFu;
+    bool valid = in;
+    if (coherent) {
+      const RunInfo ri = lane_runs(idx);  // every lane must take part in the shuffles/ballot
+      valid = in && ri.tail;
+    }
+    (void)wave_bucket_rank(hist, valid ? (idx - a.lv[l].offset) >> kChunkLog2 : 0u, valid, coherent);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x)
+    ws.hist[(int64_t)(a.bucket_base[l] + b) * ws.n_bx + blockIdx.x] = hist[b];
+}
+
+}  // namespace lnr

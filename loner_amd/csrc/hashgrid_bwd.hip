@@ -1,0 +1,325 @@
+// Hash-grid backward (tcnn kernel_grid_backward semantics) as an atomic-free binned scatter.
+//
+// Measured on MI355X: scattered fp32 global atomics run at ~20 G lane-ops/s (memory-side
+// execution) and LDS ds_add_f32 at only 0.33 lanes/clk/CU whatever the address pattern, while
+// ds_add_u64 runs at 4.8 lanes/clk/CU (scratch/ubench_*.hip).  So the backward is
+//   count   per (256-sample block, level) record histogram per 4096-entry table chunk
+//           (emitted by the training forward, or by k_bwd_count)
+//   scan    column prefix over blocks -> exact record offsets (no global atomics, no capacity guess)
+//   scatter records {idx in chunk, g0, g1 as fp25} staged in LDS in bucket order and written
+//           as coalesced runs; per-block max |g| for the fixed-point scale
+//   accum   one workgroup per (bucket, slice): int64 fixed-point sums in a 64 KB LDS chunk with
+//           ds_add_u64, converted back to fp32 and stored (float atomic adds only when a bucket
+//           spans several slices)
+// Coherent coarse levels merge runs of equal corner indices across lanes before emitting.
+#include "hashgrid.hpp"
+
+namespace lnr {
+
+__device__ __forceinline__ uint32_t f32_to_f25(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x3Fu + ((u >> 7) & 1u);
+  return u >> 7;
+}
+__device__ __forceinline__ float f25_to_f32(uint32_t v) { return __uint_as_float(v << 7); }
+
+template <class PosFn>
+__global__ void __launch_bounds__(256) k_bwd_count(GridArgs a, PosFn pos, int64_t n, BwdWorkspace ws) {
+  __shared__ uint32_t hist[kMaxChunksPerLevel];
+  const uint32_t l = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool in = i < n;
+  for (int b = threadIdx.x; b < kMaxChunksPerLevel; b += blockDim.x) hist[b] = 0;
+  __syncthreads();
+  float x = 0.f, y = 0.f, z = 0.f;
+  if (in) pos(i, x, y, z);
+  Corners c;
+  level_corners(a.lv[l], x, y, z, c);
+  count_block_records(a, l, c, in, hist, ws);
+}
+
+// Exclusive scan of one bucket's column (over blocks); total -> counts[bucket].
+__global__ void __launch_bounds__(1024) k_bwd_scan_columns(BwdWorkspace ws) {
+  __shared__ uint32_t wsum[16];
+  const uint32_t b = blockIdx.x;
+  uint32_t* col = ws.hist + (int64_t)b * ws.n_bx;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  uint32_t carry = 0;
+  for (int64_t base = 0; base < ws.n_bx; base += 1024) {
+    const int64_t j = base + t;
+    const uint32_t v = j < ws.n_bx ? col[j] : 0u;
+    uint32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t q = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += q;
+    }
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+    for (int w = 0; w < 16; ++w) {
+      if (w < wid) pre += wsum[w];
+      tot += wsum[w];
+    }
+    if (j < ws.n_bx) col[j] = carry + pre + inc - v;
+    carry += tot;
+    __syncthreads();
+  }
+  if (t == 0) ws.counts[b] = carry;
+}
+
+__global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint32_t n_buckets) {
+  __shared__ uint64_t s_seg[kMaxBuckets + 1];
+  __shared__ uint32_t s_sl[kMaxBuckets + 1];
+  if (threadIdx.x == 0) {
+    uint64_t acc = 0;
+    uint32_t sl = 0;
+    for (uint32_t b = 0; b < n_buckets; ++b) {
+      s_seg[b] = acc;
+      s_sl[b] = sl;
+      const uint32_t c = ws.counts[b];
+      acc += c;
+      const uint32_t k = (uint32_t)((c + kSliceRecords - 1) / kSliceRecords);
+      sl += k > 0 ? k : 1;
+    }
+    s_seg[n_buckets] = acc;
+    s_sl[n_buckets] = sl;
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b <= n_buckets; b += blockDim.x) {
+    ws.seg_start[b] = s_seg[b];
+    ws.slice_pre[b] = s_sl[b];
+  }
+}
+
+template <class PosFn>
+__global__ void __launch_bounds__(256) k_bwd_scatter(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ d_enc,
+                                                     int64_t stride, BwdWorkspace ws) {
+  __shared__ uint32_t hist[kMaxChunksPerLevel];
+  __shared__ uint32_t start[kMaxChunksPerLevel + 1];
+  __shared__ uint64_t gbase[kMaxChunksPerLevel];
+  __shared__ uint64_t stage[8 * 256];
+  __shared__ uint8_t sb[8 * 256];
+  __shared__ float wmax[4];
+  const uint32_t l = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool in = i < n;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t b0 = a.bucket_base[l];
+  const uint32_t nb = a.bucket_base[l + 1] - b0;
+  for (uint32_t b = threadIdx.x; b < kMaxChunksPerLevel; b += 256) {
+    hist[b] = 0;
+    if (b < nb) gbase[b] = ws.seg_start[b0 + b] + ws.hist[(int64_t)(b0 + b) * ws.n_bx + blockIdx.x];
+  }
+  __syncthreads();
+  float x = 0.f, y = 0.f, z = 0.f;
+  float2 g = make_float2(0.f, 0.f);
+  if (in) {
+    pos(i, x, y, z);
+    g = d_enc[(int64_t)l * stride + i];
+  }
+  Corners c;
+  level_corners(a.lv[l], x, y, z, c);
+  const bool coherent = l < a.merge_levels;
+  const uint32_t off = a.lv[l].offset;
+  uint32_t e[8], rank[8];
+  uint64_t rec[8];
+  bool valid[8];
+  float m = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t idx = in ? c.idx[k] : 0xFFFFFFFFu;
+    float v0 = c.w[k] * g.x, v1 = c.w[k] * g.y;
+    valid[k] = in;
+    if (coherent) {
+      const RunInfo ri = lane_runs(idx);
+      run_sum(ri, v0, v1);
+      valid[k] = in && ri.tail;
+    }
+    e[k] = valid[k] ? idx - off : 0u;
+    rank[k] = wave_bucket_rank(hist, e[k] >> kChunkLog2, valid[k], coherent);
+    const uint32_t q0 = f32_to_f25(v0), q1 = f32_to_f25(v1);
+    rec[k] = (uint64_t)(e[k] & (kChunk - 1)) | ((uint64_t)q0 << 13) | ((uint64_t)q1 << 38);
+    if (valid[k]) m = fmaxf(m, fmaxf(fabsf(f25_to_f32(q0)), fabsf(f25_to_f32(q1))));
+  }
+  m = wave_max(m);
+  if (lane == 0) wmax[wid] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (uint32_t b = 0; b < nb; ++b) {
+      start[b] = acc;
+      acc += hist[b];
+    }
+    start[nb] = acc;
+    ws.blockmax[(int64_t)l * ws.n_bx + blockIdx.x] = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (valid[k]) {
+      const uint32_t ch = e[k] >> kChunkLog2;
+      const uint32_t slot = start[ch] + rank[k];
+      stage[slot] = rec[k];
+      sb[slot] = (uint8_t)ch;
+    }
+  }
+  __syncthreads();
+  const uint32_t total = start[nb];
+  for (uint32_t t = threadIdx.x; t < total; t += 256) {
+    const uint32_t ch = sb[t];
+    ws.records[gbase[ch] + (t - start[ch])] = stage[t];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_bwd_level_max(BwdWorkspace ws) {
+  __shared__ float red[4];
+  const float* col = ws.blockmax + (int64_t)blockIdx.x * ws.n_bx;
+  float m = 0.f;
+  for (int64_t j = threadIdx.x; j < ws.n_bx; j += 256) m = fmaxf(m, col[j]);
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) ws.level_max[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+__global__ void __launch_bounds__(512) k_bwd_accum(GridArgs a, BwdWorkspace ws, float* __restrict__ d_table) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [kChunk][2] int64 fixed point
+  const uint32_t nbk = a.n_buckets;
+  const uint32_t total = ws.slice_pre[nbk];
+  const int lane = threadIdx.x & 63;
+  for (uint32_t s = blockIdx.x; s < total; s += gridDim.x) {
+    uint32_t lo = 0, hi = nbk;  // bucket b with slice_pre[b] <= s < slice_pre[b+1]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (ws.slice_pre[mid] <= s) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t b = lo;
+    const uint32_t nsl = ws.slice_pre[b + 1] - ws.slice_pre[b];
+    const uint32_t j = s - ws.slice_pre[b];
+    const uint64_t beg = ws.seg_start[b] + (uint64_t)j * kSliceRecords;
+    uint64_t end = ws.seg_start[b + 1];
+    if (beg + kSliceRecords < end) end = beg + kSliceRecords;
+    uint32_t l = 0;
+    while (l + 1 < a.n_levels && a.bucket_base[l + 1] <= b) ++l;
+    const uint32_t chunk = b - a.bucket_base[l];
+    const uint32_t ent0 = chunk * kChunk;
+    const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
+    // fixed-point scale: |v| < 2^E, at most `cnt` records -> |sum| < 2^62
+    int E;
+    frexpf(ws.level_max[l], &E);
+    const uint64_t cnt = end > beg ? end - beg : 1;
+    const int lg = 64 - __clzll((long long)cnt);  // ceil-ish log2(cnt + 1)
+    int k2 = 62 - lg - E;
+    k2 = k2 > 120 ? 120 : (k2 < -120 ? -120 : k2);
+    const float scale = ldexpf(1.f, k2);
+    for (int t = threadIdx.x; t < 2 * kChunk; t += blockDim.x) acc[t] = 0ull;
+    __syncthreads();
+    const bool coherent = l < a.merge_levels;
+    const uint64_t* rec = ws.records;
+    for (uint64_t rb = beg + (threadIdx.x & ~63u); rb < end; rb += 4 * blockDim.x) {  // wave-uniform trips
+      const uint64_t r = rb + lane;
+      uint64_t q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t rr = r + (uint64_t)u * blockDim.x;
+        q[u] = rr < end ? rec[rr] : ~0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool ok = q[u] != ~0ull;
+        const uint32_t ee = ok ? (uint32_t)(q[u] & (kChunk - 1)) : 0xFFFFFFFFu;
+        float v0 = ok ? f25_to_f32((uint32_t)(q[u] >> 13) & 0x1FFFFFFu) : 0.f;
+        float v1 = ok ? f25_to_f32((uint32_t)(q[u] >> 38) & 0x1FFFFFFu) : 0.f;
+        bool emit = ok;
+        if (coherent) {  // records of coherent levels arrive in runs of equal entries
+          const RunInfo ri = lane_runs(ee);
+          run_sum(ri, v0, v1);
+          emit = ok && ri.tail;
+        }
+        if (emit) {
+          atomicAdd(&acc[2 * ee + 0], (unsigned long long)__float2ll_rn(v0 * scale));
+          atomicAdd(&acc[2 * ee + 1], (unsigned long long)__float2ll_rn(v1 * scale));
+        }
+      }
+    }
+    __syncthreads();
+    const float inv = ldexpf(1.f, -k2);
+    float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0);
+    if (nsl == 1) {
+      for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) dst[t] = (float)(long long)acc[t] * inv;
+    } else {
+      for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) {
+        const float v = (float)(long long)acc[t] * inv;
+        if (v != 0.f) atomicAdd(&dst[t], v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <class PosFn>
+static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, const float* d_enc, int64_t stride,
+                               float* d_table, void* workspace, int64_t ws_bytes, int32_t flags, hipStream_t st,
+                               const char* who) {
+  GridArgs a = make_args(d);
+  LNR_REQUIRE(a.n_buckets <= (uint32_t)kMaxBuckets, "%s: too many table chunks (%u)", who, a.n_buckets);
+  for (uint32_t l = 0; l < d->n_levels; ++l)
+    LNR_REQUIRE(a.bucket_base[l + 1] - a.bucket_base[l] <= (uint32_t)kMaxChunksPerLevel,
+                "%s: level %u has more than %d table chunks", who, l, kMaxChunksPerLevel);
+  LNR_REQUIRE(workspace != nullptr && ws_bytes >= bwd_workspace_bytes(d, n),
+              "%s: workspace too small (%lld < %lld bytes)", who, (long long)ws_bytes,
+              (long long)bwd_workspace_bytes(d, n));
+  BwdWorkspace w = carve_workspace(workspace, a, n);
+  dim3 grid((unsigned)w.n_bx, d->n_levels);
+  if (!(flags & LNR_BWD_COUNTS_READY)) hipLaunchKernelGGL(k_bwd_count<PosFn>, grid, dim3(256), 0, st, a, pos, n, w);
+  hipLaunchKernelGGL(k_bwd_scan_columns, dim3(a.n_buckets), dim3(1024), 0, st, w);
+  hipLaunchKernelGGL(k_bwd_scan_buckets, dim3(1), dim3(1024), 0, st, w, a.n_buckets);
+  hipLaunchKernelGGL(k_bwd_scatter<PosFn>, grid, dim3(256), 0, st, a, pos, n, reinterpret_cast<const float2*>(d_enc),
+                     stride, w);
+  hipLaunchKernelGGL(k_bwd_level_max, dim3(d->n_levels), dim3(256), 0, st, w);
+  const int64_t max_slices = a.n_buckets + (8 * n * (int64_t)d->n_levels) / kSliceRecords + 1;
+  const unsigned g = (unsigned)(max_slices < 4096 ? max_slices : 4096);
+  hipLaunchKernelGGL(k_bwd_accum, dim3(g), dim3(512), 2 * kChunk * sizeof(unsigned long long), st, a, w, d_table);
+  LNR_RETURN_LAUNCH(who);
+}
+
+static int check_desc_bwd(const lnr_grid_desc* d, const char* who) {
+  LNR_REQUIRE(d != nullptr && d->n_levels >= 1 && d->n_levels <= LNR_MAX_LEVELS && d->n_features == 2,
+              "%s: invalid grid descriptor", who);
+  return LNR_OK;
+}
+
+}  // namespace lnr
+
+using namespace lnr;
+
+extern "C" int64_t lnr_hashgrid_bwd_workspace_bytes(const lnr_grid_desc* d, int64_t n) {
+  if (d == nullptr || n < 0) return -1;
+  return bwd_workspace_bytes(d, n);
+}
+
+extern "C" int lnr_hashgrid_bwd(const lnr_grid_desc* d, const float* pos01, int64_t n, const float* d_enc,
+                                int64_t enc_stride, float* d_table, void* workspace, int64_t workspace_bytes,
+                                int32_t flags, void* stream) {
+  if (int e = check_desc_bwd(d, "lnr_hashgrid_bwd")) return e;
+  LNR_REQUIRE(n >= 0 && enc_stride >= n, "lnr_hashgrid_bwd: bad sizes");
+  if (n == 0) return LNR_OK;
+  LNR_REQUIRE(pos01 && d_enc && d_table, "lnr_hashgrid_bwd: null pointer");
+  return launch_bwd_bucketed(d, PosFromArray{pos01}, n, d_enc, enc_stride, d_table, workspace, workspace_bytes, flags,
+                             as_stream(stream), "lnr_hashgrid_bwd");
+}
+
+extern "C" int lnr_hashgrid_bwd_rays(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
+                                     int32_t n_samples, const float* d_enc, int64_t enc_stride, float* d_table,
+                                     void* workspace, int64_t workspace_bytes, int32_t flags, void* stream) {
+  if (int e = check_desc_bwd(d, "lnr_hashgrid_bwd_rays")) return e;
+  const int64_t n = n_rays * (int64_t)n_samples;
+  LNR_REQUIRE(n_rays >= 0 && n_samples > 0 && enc_stride >= n, "lnr_hashgrid_bwd_rays: bad sizes");
+  if (n == 0) return LNR_OK;
+  LNR_REQUIRE(rays && z && d_enc && d_table, "lnr_hashgrid_bwd_rays: null pointer");
+  return launch_bwd_bucketed(d, PosFromRays{rays, z, n_samples}, n, d_enc, enc_stride, d_table, workspace,
+                             workspace_bytes, flags, as_stream(stream), "lnr_hashgrid_bwd_rays");
+}

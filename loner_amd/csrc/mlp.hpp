@@ -1,0 +1,210 @@
+// Sigma MLP (tcnn FullyFusedMLP 32 -> 64 ReLU -> 1(pad 16), no bias) on gfx950 MFMA.
+//
+// One wave computes a tile of 16 samples with v_mfma_f32_16x16x32_f16 (fp16 operands, fp32
+// accumulate).  Operand maps (cdna_hip_programming.md §3): lane l, g = l>>4 holds
+// A[row l&15][k 8g+j], B[k 8g+j][col l&15]; D[row 4g+r][col l&15].
+//
+// Forward computes H^T = W0 * Enc^T so the accumulator (hid on rows, sample on the lane) is
+// directly usable as the B operand of the backward product dEnc^T = W0^T * dH^T with the k index
+// permuted as hid(s,g,j) = 32s + 16(j>>2) + 4g + (j&3) — the permutation is applied to the W0^T
+// operand once at load time, so no LDS round trip is needed between the two products.
+// The 64->1 output layer is a per-lane dot product + two xor-shuffles (only row 0 of the padded
+// 16-row W1 contributes to sigma).
+#pragma once
+#include "common.hpp"
+
+namespace lnr {
+
+struct SigmaWeights {
+  half8_t a0[4];     // layer-0 A operand per hid tile t: W0[16t + (l&15)][8g + j]
+  half8_t bt[2][2];  // backward A operand [in tile m][k-step s]: W0[hid(s,g,j)][16m + (l&15)]
+  float w1[16];      // W1[0][16t + 4g + r] at index 4t + r
+};
+
+__device__ __forceinline__ int hid_perm(int s, int g, int j) { return 32 * s + 16 * (j >> 2) + 4 * g + (j & 3); }
+
+__device__ __forceinline__ void load_sigma_weights(const uint16_t* __restrict__ w, SigmaWeights& sw) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const uint16_t* w0 = w;                  // (64, 32)
+  const uint16_t* w1 = w + LNR_SIGMA_W0;   // (16, 64), row 0 used
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const uint16_t* row = w0 + (16 * t + c) * 32 + 8 * g;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sw.a0[t][j] = __builtin_bit_cast(_Float16, row[j]);
+  }
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sw.bt[m][s][j] = __builtin_bit_cast(_Float16, w0[hid_perm(s, g, j) * 32 + 16 * m + c]);
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sw.w1[4 * t + r] = h2f(w1[16 * t + 4 * g + r]);
+}
+
+// B operand of the forward product for sample n (lane column): features 8g..8g+7 = levels 4g..4g+3.
+__device__ __forceinline__ half8_t load_enc_operand(const uint32_t* __restrict__ enc, int64_t stride, int64_t n,
+                                                    bool valid) {
+  const int g = (threadIdx.x & 63) >> 4;
+  half8_t b;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t v = valid ? enc[(int64_t)(4 * g + q) * stride + n] : 0u;
+    b[2 * q + 0] = __builtin_bit_cast(_Float16, (uint16_t)(v & 0xFFFFu));
+    b[2 * q + 1] = __builtin_bit_cast(_Float16, (uint16_t)(v >> 16));
+  }
+  return b;
+}
+
+// Forward of one 16-sample tile.  h[4t+r] = fp16(relu(H))[hid 16t+4g+r][sample l&15];
+// returns sigma for sample l&15 (fp32 accumulate of fp16 operands, NOT yet rounded).
+__device__ __forceinline__ float sigma_tile_fwd(const SigmaWeights& sw, const half8_t& benc, float (&h)[16]) {
+  float part = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    float4_t acc = {0.f, 0.f, 0.f, 0.f};
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(sw.a0[t], benc, acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = round_f16(fmaxf(acc[r], 0.f));
+      h[4 * t + r] = v;
+      part = fmaf(sw.w1[4 * t + r], v, part);
+    }
+  }
+  part += __shfl_xor(part, 16, 64);
+  part += __shfl_xor(part, 32, 64);
+  return part;
+}
+
+// tcnn returns fp16; DecoupledNeRF then replaces non-finite values (nerf_tcnn.py:74-78):
+// nan_to_num(posinf=65504, neginf=-65504) — NaN becomes 0.
+__device__ __forceinline__ float sigma_to_f16(float s) {
+  float r = round_f16(s);
+  if (isnan(r)) return 0.f;
+  if (isinf(r)) return r > 0 ? 65504.f : -65504.f;
+  return r;
+}
+
+// Power-of-two scale that lifts the largest |value| of the wave to ~2^13 for fp16 MFMA operands.
+__device__ __forceinline__ float grad_scale(float maxabs) {
+  if (!(maxabs > 0.f) || !isfinite(maxabs)) return 1.f;
+  int e;
+  frexpf(maxabs, &e);  // maxabs = m * 2^e, m in [0.5,1)
+  int k = 13 - e;
+  k = k > 100 ? 100 : (k < -100 ? -100 : k);
+  return ldexpf(1.f, k);
+}
+
+// Backward of one tile for d_sigma = 1: dH^T[hid][s] = w1[hid] * (h > 0) is exact in fp16, so the
+// MFMA result is exact up to fp32 accumulation; the caller multiplies by the sample's d_sigma.
+// d[m][r] = dEnc[sample l&15][in 16m + 4g + r] / d_sigma.
+__device__ __forceinline__ void sigma_tile_bwd_denc(const SigmaWeights& sw, const float (&h)[16], float (&d)[2][4]) {
+  half8_t b[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 4 * (2 * s + (j >> 2)) + (j & 3);
+      b[s][j] = (_Float16)((h[k] > 0.f) ? sw.w1[k] : 0.f);
+    }
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    float4_t acc = {0.f, 0.f, 0.f, 0.f};
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(sw.bt[m][0], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(sw.bt[m][1], b[1], acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) d[m][r] = acc[r];
+  }
+}
+
+// dW0 accumulation for a PAIR of tiles (32 samples) through a per-wave LDS transpose.
+// lds: 64*32 + 32*32 halves (6 KB) per wave.  acc[t][m][r] += dW0[16t+4g+r][16m+(l&15)].
+struct DW0Acc {
+  float v[4][2][4];
+};
+
+__device__ __forceinline__ void dw0_pair(_Float16* __restrict__ lds, const SigmaWeights& sw, const float (&h0)[16],
+                                         const float (&h1)[16], const half8_t& e0, const half8_t& e1, float ds0,
+                                         float ds1, float scale, DW0Acc& acc) {
+  // dW0[hid][in] = w1[hid] * sum_s mask[hid][s] * (ds_s * Enc[s][in]); the mask operand is exact,
+  // ds_s * Enc is lifted by a per-pair power of two for the fp16 operand.
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  _Float16* mk = lds;             // [64 hid][32 samples] ReLU mask
+  _Float16* ens = lds + 64 * 32;  // [32 in][32 samples] scaled ds * Enc
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int hid = 16 * t + 4 * g + r;
+      mk[hid * 32 + c] = (_Float16)((h0[4 * t + r] > 0.f) ? 1.f : 0.f);
+      mk[hid * 32 + 16 + c] = (_Float16)((h1[4 * t + r] > 0.f) ? 1.f : 0.f);
+    }
+  const float s0 = ds0 * scale, s1 = ds1 * scale;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ens[(8 * g + j) * 32 + c] = (_Float16)((float)e0[j] * s0);
+    ens[(8 * g + j) * 32 + 16 + c] = (_Float16)((float)e1[j] * s1);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-local hand-off through LDS
+  __builtin_amdgcn_wave_barrier();
+  const float inv = 1.f / scale;
+  half8_t a[4], b[2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) a[t] = *reinterpret_cast<const half8_t*>(mk + (16 * t + c) * 32 + 8 * g);
+#pragma unroll
+  for (int m = 0; m < 2; ++m) b[m] = *reinterpret_cast<const half8_t*>(ens + (16 * m + c) * 32 + 8 * g);
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      float4_t d = {0.f, 0.f, 0.f, 0.f};
+      d = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[t], b[m], d, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc.v[t][m][r] = fmaf(d[r], sw.w1[4 * t + r] * inv, acc.v[t][m][r]);
+    }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Block-level write of the per-block dW slab (3072 fp32, layout W0 (64,32) then W1 (16,64)).
+// red: LDS scratch of 3072 floats.  dw1 is per-lane (hid 16t+4g+r) summed over the lane's samples.
+template <int NT>
+__device__ __forceinline__ void write_dw_slab(float* __restrict__ red, const DW0Acc& acc, const float (&dw1)[16],
+                                              float* __restrict__ slab) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15, wid = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < LNR_SIGMA_MLP_PARAMS; i += NT) red[i] = 0.f;
+  __syncthreads();
+  float v1[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    float x = dw1[i];
+    x += __shfl_xor(x, 1, 64);
+    x += __shfl_xor(x, 2, 64);
+    x += __shfl_xor(x, 4, 64);
+    x += __shfl_xor(x, 8, 64);
+    v1[i] = x;
+  }
+  for (int w = 0; w < NT / 64; ++w) {
+    if (wid == w) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) red[(16 * t + 4 * g + r) * 32 + 16 * m + c] += acc.v[t][m][r];
+      if (c == 0) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) red[LNR_SIGMA_W0 + 16 * t + 4 * g + r] += v1[4 * t + r];
+      }
+    }
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < LNR_SIGMA_MLP_PARAMS; i += NT) slab[i] = red[i];
+}
+
+}  // namespace lnr

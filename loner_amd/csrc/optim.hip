@@ -1,0 +1,220 @@
+// Optimiser-side kernels: fused Adam over the flat sigma parameters, the occupancy-grid (OGM)
+// update, parameter init and dtype conversion.
+//
+// Adam  : torch.optim.Adam as constructed per window at src/mapping/optimizer.py:255-265 and
+//         stepped at :460 (betas 0.9/0.999, eps 1e-8, no weight decay) on fp32 master params,
+//         writing the fp16 forward shadow in the same pass (tcnn forwards with fp16 params).
+// OGM   : Optimizer._step_occupancy_grid src/mapping/optimizer.py:897-908 — grid_sample backward of
+//         get_logits_grad (src/models/losses.py:54-62) followed by SGD (lr from occ_model.lr).
+#include "common.hpp"
+
+namespace lnr {
+
+__global__ void __launch_bounds__(256) k_adam(float* __restrict__ p, uint16_t* __restrict__ shadow,
+                                              const float* __restrict__ g, float* __restrict__ m,
+                                              float* __restrict__ v, int64_t n, float one_minus_b1, float b2,
+                                              float one_minus_b2, float step_size, float bc2_sqrt, float eps) {
+  const int64_t n4 = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    const float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    float* pa = &pp.x;
+    const float* ga = &gg.x;
+    float* ma = &mm.x;
+    float* va = &vv.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      ma[k] = ma[k] + one_minus_b1 * (ga[k] - ma[k]);           // exp_avg.lerp_(grad, 1-b1)
+      va[k] = va[k] * b2 + one_minus_b2 * ga[k] * ga[k];         // mul_(b2).addcmul_(g, g, 1-b2)
+      const float denom = sqrtf(va[k]) / bc2_sqrt + eps;
+      pa[k] = pa[k] + (-step_size) * (ma[k] / denom);           // addcdiv_(m, denom, -step_size)
+    }
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+    if (shadow) {
+      uint2 h;
+      h.x = (uint32_t)f2h(pa[0]) | ((uint32_t)f2h(pa[1]) << 16);
+      h.y = (uint32_t)f2h(pa[2]) | ((uint32_t)f2h(pa[3]) << 16);
+      reinterpret_cast<uint2*>(shadow)[i] = h;
+    }
+  }
+  // tail
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const int64_t i = n4 * 4 + threadIdx.x;
+    float mk = m[i] + one_minus_b1 * (g[i] - m[i]);
+    float vk = v[i] * b2 + one_minus_b2 * g[i] * g[i];
+    float pk = p[i] + (-step_size) * (mk / (sqrtf(vk) / bc2_sqrt + eps));
+    m[i] = mk;
+    v[i] = vk;
+    p[i] = pk;
+    if (shadow) shadow[i] = f2h(pk);
+  }
+}
+
+// logits "gradient" of losses.py:54-62 with eps=2, l_free=0.25, l_occ=2.5; H(0)=0.
+__device__ __forceinline__ float logits_grad(float x) {
+  const float eps = 2.0f;
+  const float fr = ((-x - eps) > 0.f) ? 1.f : 0.f;
+  const float oc = (((x + eps) > 0.f) ? 1.f : 0.f) * (((eps - x) > 0.f) ? 1.f : 0.f);
+  return 0.25f * fr - 2.5f * oc;
+}
+
+__global__ void __launch_bounds__(256) k_ogm_grad(const float* __restrict__ rays, const float* __restrict__ z,
+                                                  const float* __restrict__ dgt, int64_t n_rays, int32_t S,
+                                                  float scale, float* __restrict__ grad, int32_t R) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const bool valid = i < n_rays * (int64_t)S;
+  float gval = 0.f, px = 0.f, py = 0.f, pz = 0.f;
+  if (valid) {
+    const int64_t r = i / S;
+    const float* ry = rays + 13 * r;
+    const float t = z[i];
+    px = ry[0] + ry[3] * t;
+    py = ry[1] + ry[4] * t;
+    pz = ry[2] + ry[5] * t;
+    gval = logits_grad(t * scale - dgt[r] * scale);
+  }
+  const float ix = ((px + 1.f) * (float)R - 1.f) / 2.f;
+  const float iy = ((py + 1.f) * (float)R - 1.f) / 2.f;
+  const float iz = ((pz + 1.f) * (float)R - 1.f) / 2.f;
+  const float fx = floorf(ix), fy = floorf(iy), fz = floorf(iz);
+  const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
+  const float wx[2] = {(float)(x0 + 1) - ix, ix - (float)x0};
+  const float wy[2] = {(float)(y0 + 1) - iy, iy - (float)y0};
+  const float wz[2] = {(float)(z0 + 1) - iz, iz - (float)z0};
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int bx = c & 1, by = (c >> 1) & 1, bz = (c >> 2) & 1;
+    const int cx = x0 + bx, cy = y0 + by, cz = z0 + bz;
+    const bool inb = valid && gval != 0.f && cx >= 0 && cx < R && cy >= 0 && cy < R && cz >= 0 && cz < R;
+    const int64_t idx = inb ? (((int64_t)cz * R + cy) * R + cx) : -1;
+    float p = inb ? wx[bx] * wy[by] * wz[bz] * gval : 0.f;
+    // merge runs of equal voxel indices across consecutive samples before the atomic
+    const int64_t prev = __shfl_up(idx, 1, 64);
+    const bool head = (lane == 0) || (prev != idx);
+    const unsigned long long heads = __ballot(head);
+    const int head_lane = 63 - __clzll(heads & ((2ull << lane) - 1ull));
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float q = __shfl_up(p, o, 64);
+      if (lane - o >= head_lane) p += q;
+    }
+    const bool tail = (lane == 63) || ((heads >> (lane + 1)) & 1ull);
+    if (tail && idx >= 0) atomicAdd(&grad[idx], p);
+  }
+}
+
+__global__ void k_sgd(float* __restrict__ p, const float* __restrict__ g, int64_t n, float lr) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = p[i] + (-lr) * g[i];
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ void k_fill_uniform(float* __restrict__ dst, int64_t n, uint32_t seed, float lo, float hi, int64_t start) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t h = splitmix64(((uint64_t)seed << 32) + (uint64_t)(start + i));
+  const float u = (float)(h >> 40) * 5.9604644775390625e-08f;
+  dst[i] = lo + (hi - lo) * u;
+}
+
+__global__ void k_f32_to_f16(const float* __restrict__ s, uint16_t* __restrict__ d, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) d[i] = f2h(s[i]);
+}
+
+static unsigned grid1d(int64_t n, int64_t cap = 1 << 20) {
+  int64_t b = (n + 255) / 256;
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+}  // namespace lnr
+
+using namespace lnr;
+
+extern "C" int lnr_adam_step(float* param, uint16_t* shadow, const float* grad, float* m, float* v, int64_t n,
+                             int32_t step, float lr, float beta1, float beta2, float eps, void* stream) {
+  LNR_REQUIRE(n >= 0 && step >= 1, "lnr_adam_step: n=%lld step=%d", (long long)n, step);
+  if (n == 0) return LNR_OK;
+  LNR_REQUIRE(param && grad && m && v, "lnr_adam_step: null pointer");
+  LNR_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) % 16 == 0 &&
+                  (shadow == nullptr || (uintptr_t)shadow % 8 == 0),
+              "lnr_adam_step: buffers must be 16-byte aligned");
+  const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+  const float step_size = (float)((double)lr / bc1);
+  const float bc2_sqrt = (float)std::sqrt(bc2);
+  hipLaunchKernelGGL(k_adam, dim3(grid1d(n / 4, 8192)), dim3(256), 0, as_stream(stream), param, shadow, grad, m, v, n,
+                     (float)(1.0 - (double)beta1), beta2, (float)(1.0 - (double)beta2), step_size, bc2_sqrt, eps);
+  LNR_RETURN_LAUNCH("lnr_adam_step");
+}
+
+extern "C" int lnr_ogm_update(const float* rays, const float* z, const float* depth_gt, int64_t n_rays,
+                              int32_t n_samples, float scale, float lr, float* occ, float* grad_ws, int32_t occ_res,
+                              void* stream) {
+  LNR_REQUIRE(n_rays >= 0 && n_samples >= 1 && occ_res >= 1, "lnr_ogm_update: bad sizes");
+  LNR_REQUIRE(occ && grad_ws, "lnr_ogm_update: null grid");
+  const int64_t nv = (int64_t)occ_res * occ_res * occ_res;
+  hipStream_t st = as_stream(stream);
+  if (hipMemsetAsync(grad_ws, 0, nv * sizeof(float), st) != hipSuccess) {
+    set_error("lnr_ogm_update: hipMemsetAsync failed");
+    return LNR_ERR_HIP;
+  }
+  const int64_t n = n_rays * (int64_t)n_samples;
+  if (n > 0) {
+    LNR_REQUIRE(rays && z && depth_gt, "lnr_ogm_update: null pointer");
+    hipLaunchKernelGGL(k_ogm_grad, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rays, z, depth_gt, n_rays,
+                       n_samples, scale, grad_ws, occ_res);
+  }
+  hipLaunchKernelGGL(k_sgd, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, occ, grad_ws, nv, lr);
+  LNR_RETURN_LAUNCH("lnr_ogm_update");
+}
+
+extern "C" int lnr_ogm_grad(const float* rays, const float* z, const float* depth_gt, int64_t n_rays,
+                            int32_t n_samples, float scale, float* grad_ws, int32_t occ_res, void* stream) {
+  LNR_REQUIRE(n_rays >= 0 && n_samples >= 1 && occ_res >= 1 && grad_ws, "lnr_ogm_grad: bad arguments");
+  const int64_t n = n_rays * (int64_t)n_samples;
+  if (n == 0) return LNR_OK;
+  LNR_REQUIRE(rays && z && depth_gt, "lnr_ogm_grad: null pointer");
+  hipLaunchKernelGGL(k_ogm_grad, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), rays, z, depth_gt,
+                     n_rays, n_samples, scale, grad_ws, occ_res);
+  LNR_RETURN_LAUNCH("lnr_ogm_grad");
+}
+
+extern "C" int lnr_sgd_step(float* param, const float* grad, int64_t n, float lr, void* stream) {
+  LNR_REQUIRE(n >= 0, "lnr_sgd_step: n < 0");
+  if (n == 0) return LNR_OK;
+  LNR_REQUIRE(param && grad, "lnr_sgd_step: null pointer");
+  hipLaunchKernelGGL(k_sgd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), param, grad, n, lr);
+  LNR_RETURN_LAUNCH("lnr_sgd_step");
+}
+
+extern "C" int lnr_fill_uniform(float* dst, int64_t n, uint32_t seed, float lo, float hi, int64_t start, void* stream) {
+  LNR_REQUIRE(n >= 0, "lnr_fill_uniform: n < 0");
+  if (n == 0) return LNR_OK;
+  LNR_REQUIRE(dst, "lnr_fill_uniform: null pointer");
+  hipLaunchKernelGGL(k_fill_uniform, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), dst, n, seed,
+                     lo, hi, start);
+  LNR_RETURN_LAUNCH("lnr_fill_uniform");
+}
+
+extern "C" int lnr_f32_to_f16(const float* src, uint16_t* dst, int64_t n, void* stream) {
+  LNR_REQUIRE(n >= 0, "lnr_f32_to_f16: n < 0");
+  if (n == 0) return LNR_OK;
+  LNR_REQUIRE(src && dst, "lnr_f32_to_f16: null pointer");
+  hipLaunchKernelGGL(k_f32_to_f16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), src, dst, n);
+  LNR_RETURN_LAUNCH("lnr_f32_to_f16");
+}

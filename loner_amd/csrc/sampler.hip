@@ -1,0 +1,241 @@
+// Per-ray depth sampling: stratified (jittered) + occupancy-grid importance sampling, sorted.
+//
+// Reference: OccGridRaySampler.get_samples   src/models/ray_sampling.py:53-92
+//            UniformRaySampler.get_samples   src/models/ray_sampling.py:22-43
+//            OccupancyGridModel.interpolate  src/models/model_tcnn.py:126-134 (grid_sample 3-D,
+//                                            trilinear, align_corners=False, zeros padding)
+//            sample_pdf                      src/models/rendering_tcnn.py:19-68 (det=False)
+// One 256-thread workgroup per ray (grid-stride over rays).  The 100^3 fp32 occupancy grid (4 MB)
+// stays L2/MALL resident; the cdf, bins and the bitonic sort buffer live in LDS.
+#include "common.hpp"
+
+namespace lnr {
+
+constexpr int SNT = 256;
+
+__device__ __forceinline__ float linspace01(int i, int n) {
+  // torch linspace(0, 1, n): start + step*i for i < n/2, end - step*(n-1-i) otherwise
+  const float step = 1.0f / (float)(n - 1);
+  return (i < n / 2) ? (0.0f + step * (float)i) : (1.0f - step * (float)(n - 1 - i));
+}
+
+__device__ __forceinline__ float grid_sample(const float* __restrict__ occ, int R, float x, float y, float z) {
+  const float ix = ((x + 1.f) * (float)R - 1.f) / 2.f;
+  const float iy = ((y + 1.f) * (float)R - 1.f) / 2.f;
+  const float iz = ((z + 1.f) * (float)R - 1.f) / 2.f;
+  const float fx = floorf(ix), fy = floorf(iy), fz = floorf(iz);
+  const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
+  const float wx[2] = {(float)(x0 + 1) - ix, ix - (float)x0};
+  const float wy[2] = {(float)(y0 + 1) - iy, iy - (float)y0};
+  const float wz[2] = {(float)(z0 + 1) - iz, iz - (float)z0};
+  float acc = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int bx = c & 1, by = (c >> 1) & 1, bz = (c >> 2) & 1;
+    const int cx = x0 + bx, cy = y0 + by, cz = z0 + bz;
+    const float w = wx[bx] * wy[by] * wz[bz];
+    if (cx >= 0 && cx < R && cy >= 0 && cy < R && cz >= 0 && cz < R) acc += occ[((int64_t)cz * R + cy) * R + cx] * w;
+  }
+  return acc;
+}
+
+struct SamplerArgs {
+  const float* rays;
+  int64_t n_rays;
+  int32_t S;       // total samples per ray
+  int32_t H;       // stratified samples (S/2 for OGM, S for uniform)
+  const float* occ;
+  int32_t occ_res;
+  float perturb;
+  const float* u_jitter;
+  const float* u_pdf;
+  uint32_t key;
+  int64_t ray_offset;
+  float* z;
+  int32_t P2;      // next power of two >= S (sort width)
+};
+
+template <bool OGM>
+__global__ void __launch_bounds__(SNT) k_sampler(SamplerArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* zs = reinterpret_cast<float*>(smem);  // [H] stratified (jittered)
+  float* cdf = zs + a.H;                       // [H-1]
+  float* prob = cdf + a.H;                     // [H]
+  float* buf = prob + a.H;                     // [P2] sort buffer
+  double* red = reinterpret_cast<double*>(smem + ((((size_t)3 * a.H + a.P2) * 4 + 7) & ~(size_t)7));  // [SNT/64+2]
+  const int H = a.H, S = a.S, t = threadIdx.x;
+  const int lane = t & 63, wid = t >> 6;
+  for (int64_t r = blockIdx.x; r < a.n_rays; r += gridDim.x) {
+    const float* ry = a.rays + 13 * r;
+    const float near = ry[11], far = ry[12];
+    const uint32_t gr = (uint32_t)(a.ray_offset + r);
+    // 1. linspace + jitter (ray_sampling.py:59-72)
+    for (int i = t; i < H; i += SNT) {
+      const float tt = linspace01(i, H);
+      zs[i] = near * (1.0f - tt) + far * tt;
+    }
+    __syncthreads();
+    float zj[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = t + k * SNT;
+      float z = 0.f;
+      if (i < H) {
+        z = zs[i];
+        if (a.perturb > 0.f) {
+          const float zl = zs[i > 0 ? i - 1 : 0], zu = zs[i + 1 < H ? i + 1 : H - 1];
+          const float upper = (i + 1 < H) ? 0.5f * (z + zu) : z;
+          const float lower = (i > 0) ? 0.5f * (zl + z) : z;
+          const float u = a.u_jitter ? a.u_jitter[r * H + i] : rand_uniform(a.key, kStreamJitter, gr, (uint32_t)i);
+          z = lower + (upper - lower) * (a.perturb * u);
+        }
+      }
+      zj[k] = z;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = t + k * SNT;
+      if (i < H) zs[i] = zj[k];
+    }
+    __syncthreads();
+    if (!OGM) {
+      for (int i = t; i < S; i += SNT) a.z[r * S + i] = zs[i];
+      __syncthreads();
+      continue;
+    }
+    // 2. occupancy probabilities at the stratified points (ray_sampling.py:74-81)
+    for (int i = t; i < H; i += SNT) {
+      const float z = zs[i];
+      const float px = ry[0] + ry[3] * z, py = ry[1] + ry[4] * z, pz = ry[2] + ry[5] * z;
+      const float l = grid_sample(a.occ, a.occ_res, px, py, pz);
+      float p = 1.0f / (1.0f + expf(-l));
+      p = 2.0f * (fminf(fmaxf(p, 0.5f), 1.0f) - 0.5f);
+      prob[i] = p;
+    }
+    __syncthreads();
+    // 3. sample_pdf over bins = midpoints (H-1), weights = prob[1:H-1] (H-2 values) + 1e-5
+    const int M = H - 2;
+    double wsum = 0.0;
+    for (int i = t; i < M; i += SNT) wsum += (double)(prob[i + 1] + 1e-5f);
+    {
+      float v[1] = {(float)wsum};
+      // block sum in float of per-thread doubles (reference: torch.sum fp32)
+      block_sum<SNT, 1>(v, reinterpret_cast<float*>(red));
+      wsum = v[0];
+    }
+    const float wtot = (float)wsum;
+    // inclusive cumsum of pdf in double, per contiguous chunk per thread
+    const int K = (M + SNT - 1) / SNT;
+    const int j0 = t * K;
+    double loc = 0.0;
+    for (int k = 0; k < K; ++k) {
+      const int j = j0 + k;
+      if (j < M) loc += (double)((prob[j + 1] + 1e-5f) / wtot);
+    }
+    double inc = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      double q = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += q;
+    }
+    if (lane == 63) red[wid] = inc;
+    __syncthreads();
+    double pre = 0.0;
+    for (int w = 0; w < wid; ++w) pre += red[w];
+    double run = pre + inc - loc;
+    for (int k = 0; k < K; ++k) {
+      const int j = j0 + k;
+      if (j < M) {
+        run += (double)((prob[j + 1] + 1e-5f) / wtot);
+        cdf[j + 1] = (float)run;
+      }
+    }
+    if (t == 0) cdf[0] = 0.f;
+    __syncthreads();
+    // bins (midpoints of the jittered stratified depths) reuse prob[]
+    for (int i = t; i < H - 1; i += SNT) prob[i] = 0.5f * (zs[i] + zs[i + 1]);
+    __syncthreads();
+    // 4. inverse CDF (searchsorted right=True over H-1 cdf entries)
+    for (int i = t; i < H; i += SNT) {
+      const float u = a.u_pdf ? a.u_pdf[r * H + i] : rand_uniform(a.key, kStreamPdf, gr, (uint32_t)i);
+      int lo = 0, hi = H - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cdf[mid] <= u) lo = mid + 1;
+        else hi = mid;
+      }
+      const int below = lo - 1 > 0 ? lo - 1 : 0;
+      const int above = lo < M ? lo : M;
+      const float c0 = cdf[below], c1 = cdf[above];
+      const float b0 = prob[below], b1 = prob[above];
+      float denom = c1 - c0;
+      if (denom < 1e-5f) denom = 1.0f;
+      buf[H + i] = b0 + (u - c0) / denom * (b1 - b0);
+      buf[i] = zs[i];
+    }
+    for (int i = S + t; i < a.P2; i += SNT) buf[i] = INFINITY;
+    __syncthreads();
+    // 5. bitonic sort of P2 values (torch.sort(..., -1), ray_sampling.py:90)
+    for (int k = 2; k <= a.P2; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int q = t; q < a.P2 / 2; q += SNT) {
+          const int i = 2 * j * (q / j) + (q % j);
+          const int l = i + j;
+          const bool up = (i & k) == 0;
+          const float x = buf[i], y = buf[l];
+          if ((x > y) == up) {
+            buf[i] = y;
+            buf[l] = x;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    for (int i = t; i < S; i += SNT) a.z[r * S + i] = buf[i];
+    __syncthreads();
+  }
+}
+
+static size_t sampler_smem(int H, int P2) { return ((size_t)3 * H + P2 + 2) * 4 + (SNT / 64 + 2) * 8 + 16; }
+
+}  // namespace lnr
+
+using namespace lnr;
+
+extern "C" uint32_t lnr_step_key(uint32_t seed, uint32_t step) { return mix32(mix32(seed) ^ step); }
+
+extern "C" int lnr_sample_ogm(const float* rays, int64_t n_rays, int32_t n_samples, const float* occ, int32_t occ_res,
+                              float perturb, const float* u_jitter, const float* u_pdf, uint32_t key, int64_t ray_offset,
+                              float* z, void* stream) {
+  LNR_REQUIRE(n_rays >= 0, "lnr_sample_ogm: n_rays < 0");
+  LNR_REQUIRE(n_samples >= 8 && n_samples % 2 == 0 && n_samples <= 4096,
+              "lnr_sample_ogm: n_samples=%d must be even in [8,4096]", n_samples);
+  LNR_REQUIRE(occ_res >= 1, "lnr_sample_ogm: occ_res=%d", occ_res);
+  if (n_rays == 0) return LNR_OK;
+  LNR_REQUIRE(rays && occ && z, "lnr_sample_ogm: null pointer");
+  SamplerArgs a{};
+  a.rays = rays; a.n_rays = n_rays; a.S = n_samples; a.H = n_samples / 2; a.occ = occ; a.occ_res = occ_res;
+  a.perturb = perturb; a.u_jitter = u_jitter; a.u_pdf = u_pdf; a.key = key; a.ray_offset = ray_offset; a.z = z;
+  int p2 = 1;
+  while (p2 < n_samples) p2 <<= 1;
+  a.P2 = p2;
+  LNR_REQUIRE(a.H <= 8 * SNT, "lnr_sample_ogm: too many samples");
+  const int nb = (int)(n_rays < 4096 ? n_rays : 4096);
+  hipLaunchKernelGGL(k_sampler<true>, dim3(nb), dim3(SNT), sampler_smem(a.H, p2), as_stream(stream), a);
+  LNR_RETURN_LAUNCH("lnr_sample_ogm");
+}
+
+extern "C" int lnr_sample_uniform(const float* rays, int64_t n_rays, int32_t n_samples, float perturb,
+                                  const float* u_jitter, uint32_t key, int64_t ray_offset, float* z, void* stream) {
+  LNR_REQUIRE(n_rays >= 0, "lnr_sample_uniform: n_rays < 0");
+  LNR_REQUIRE(n_samples >= 2 && n_samples <= 2048, "lnr_sample_uniform: n_samples=%d not in [2,2048]", n_samples);
+  if (n_rays == 0) return LNR_OK;
+  LNR_REQUIRE(rays && z, "lnr_sample_uniform: null pointer");
+  SamplerArgs a{};
+  a.rays = rays; a.n_rays = n_rays; a.S = n_samples; a.H = n_samples; a.perturb = perturb; a.u_jitter = u_jitter;
+  a.key = key; a.ray_offset = ray_offset; a.z = z; a.P2 = 0;
+  const int nb = (int)(n_rays < 4096 ? n_rays : 4096);
+  hipLaunchKernelGGL(k_sampler<false>, dim3(nb), dim3(SNT), sampler_smem(a.H, 0), as_stream(stream), a);
+  LNR_RETURN_LAUNCH("lnr_sample_uniform");
+}

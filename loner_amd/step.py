@@ -1,0 +1,264 @@
+"""Fused optimiser step on the HIP C-ABI: the MI355X-native body of
+``Optimizer._do_iterate_optimizer``'s step loop (src/mapping/optimizer.py:354-475).
+
+One step = OGM sampling -> hash-grid encode -> fused [sigma MLP, compositing, LiDAR loss,
+compositing backward, MLP backward] -> hash-grid backward -> (all-reduce) -> Adam
+[-> OGM update every ``N_iters_acc`` global steps, checked before the increment as at
+optimizer.py:466-469].  All buffers are allocated once; a step only enqueues kernels on the
+current stream (no host synchronisation) and can be captured in a HIP graph.
+
+Parameter layout (tcnn ``NetworkWithInputEncoding``: network first, then encoding):
+    params[0:3072]            sigma MLP, W0 (64,32) then W1 (16,64), row-major [out][in]
+    params[3072:]             hash table, (n_entries, 2), level-major
+fp32 master + Adam moments; an fp16 shadow of the whole buffer feeds the forward kernels.
+"""
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _lib as L
+
+
+@dataclass
+class LossConfig:
+    """``model_config.loss`` (cfg/model_config/default_model_config.yaml:40-60)."""
+    loss_selection: str = "L1_JS"
+    min_js_score: float = 1.0
+    max_js_score: float = 10.0
+    js_alpha: float = 1.0
+    decay_los_lambda: bool = False
+    los_lambda: float = 1000.0
+    min_los_lambda: float = 10.0
+    los_lambda_decay_rate: float = 0.001
+    los_lambda_decay_steps: float = 15000
+    decay_depth_eps: bool = True
+    depth_eps: float = 3.0
+    min_depth_eps: float = 0.5
+    depth_eps_decay_rate: float = 0.95
+    depth_eps_decay_steps: float = 1
+    depthloss_lambda: float = 0.005
+
+    @staticmethod
+    def from_dict(d):
+        js = d.get("JS_loss", {})
+        keys = {k: d[k] for k in LossConfig.__dataclass_fields__ if k in d}
+        return LossConfig(**keys, min_js_score=js.get("min_js_score", 1.0), max_js_score=js.get("max_js_score", 10.0),
+                          js_alpha=js.get("alpha", 1.0))
+
+    def los_lambda_at(self, global_step):
+        # optimizer.py:712-716 (and :846-848): decay evaluated on global_step + 1
+        if self.decay_los_lambda:
+            return max(self.los_lambda * (self.los_lambda_decay_rate ** ((global_step + 1) / self.los_lambda_decay_steps)),
+                       self.min_los_lambda)
+        return self.los_lambda
+
+    def los_eps_at(self, iteration_idx):
+        # optimizer.py:781-785
+        if self.decay_depth_eps:
+            return max(self.depth_eps * (self.depth_eps_decay_rate ** (iteration_idx / self.depth_eps_decay_steps)),
+                       self.min_depth_eps)
+        return self.depth_eps
+
+
+@dataclass
+class StepConfig:
+    n_samples: int = 512              # render.N_samples_train
+    perturb: float = 1.0              # render.perturb
+    raw_noise_std: float = 1.0        # render.raw_noise_std
+    lr: float = 0.01                  # train.lrate_sigma_mlp
+    occ_res: int = 100                # occ_model.voxel_size
+    occ_lr: float = 1e-4              # occ_model.lr
+    n_iters_acc: int = 10             # occ_model.N_iters_acc
+    sampler: str = "OGM"              # samples_selection.strategy
+    n_levels: int = 16
+    log2_hashmap_size: int = 18
+    base_resolution: int = 16
+    per_level_scale: float = 2.0
+    loss: LossConfig = field(default_factory=LossConfig)
+
+
+class FieldState:
+    """Parameters, Adam moments, fp16 shadow and the occupancy grid, resident on one GPU."""
+
+    def __init__(self, cfg: StepConfig, device="cuda", seed=1337, table_init=1e-4):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.desc = L.grid_desc(cfg.n_levels, 2, cfg.log2_hashmap_size, cfg.base_resolution, cfg.per_level_scale)
+        self.n_entries = int(self.desc.n_entries)
+        self.n_mlp = L.SIGMA_MLP_PARAMS
+        self.n_params = self.n_mlp + 2 * self.n_entries
+        self.n_padded = (self.n_params + 3) // 4 * 4
+        dev = self.device
+        self.params = torch.zeros(self.n_padded, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros_like(self.params)
+        self.m = torch.zeros_like(self.params)
+        self.v = torch.zeros_like(self.params)
+        self.shadow = torch.zeros(self.n_padded, dtype=torch.float16, device=dev)
+        self.occ = torch.zeros(cfg.occ_res ** 3, dtype=torch.float32, device=dev)
+        self.occ_ws = torch.zeros_like(self.occ)
+        self.adam_step = 0
+        self.init_params(seed, table_init)
+
+    # tcnn init: FullyFusedMLP xavier-uniform per matrix, HashGrid U(-1e-4, 1e-4) (restated with a
+    # counter-based generator: tcnn's PCG stream is not reproducible here)
+    def init_params(self, seed=1337, table_init=1e-4):
+        s = L.stream(self.device)
+        a0 = math.sqrt(6.0 / (32 + 64))
+        a1 = math.sqrt(6.0 / (64 + 16))
+        p = self.params
+        L.call("lnr_fill_uniform", (p), 64 * 32, seed, -a0, a0, 0, s)
+        L.call("lnr_fill_uniform", L.ctypes.c_void_p(p.data_ptr() + 4 * 64 * 32), 16 * 64, seed + 1, -a1, a1, 0, s)
+        L.call("lnr_fill_uniform", L.ctypes.c_void_p(p.data_ptr() + 4 * self.n_mlp), 2 * self.n_entries, seed + 2,
+               -table_init, table_init, 0, s)
+        self.refresh_shadow()
+
+    def refresh_shadow(self):
+        L.call("lnr_f32_to_f16", (self.params), (self.shadow), self.n_padded, L.stream(self.device))
+
+    def reset_optimizer(self):
+        """A new torch.optim.Adam per window / iteration config (optimizer.py:255-265)."""
+        self.m.zero_()
+        self.v.zero_()
+        self.adam_step = 0
+
+    # views
+    @property
+    def mlp_f16(self):
+        return self.shadow[:self.n_mlp]
+
+    @property
+    def table_f16(self):
+        return self.shadow[self.n_mlp:self.n_mlp + 2 * self.n_entries]
+
+    @property
+    def grad_table(self):
+        return self.grad[self.n_mlp:self.n_mlp + 2 * self.n_entries]
+
+    @property
+    def grad_mlp(self):
+        return self.grad[:self.n_mlp]
+
+    def state_dict(self):
+        return {"params": self.params[:self.n_params].clone(), "occupancy_grid": self.occ.clone(),
+                "adam_step": self.adam_step, "m": self.m[:self.n_params].clone(), "v": self.v[:self.n_params].clone()}
+
+    def load_state_dict(self, sd):
+        self.params[:self.n_params].copy_(sd["params"])
+        self.occ.copy_(sd["occupancy_grid"].reshape(-1))
+        if "m" in sd:
+            self.m[:self.n_params].copy_(sd["m"])
+            self.v[:self.n_params].copy_(sd["v"])
+            self.adam_step = int(sd.get("adam_step", 0))
+        self.refresh_shadow()
+
+
+class StepEngine:
+    """Preallocated workspaces for a fixed ray-batch size; ``step`` runs one optimiser step."""
+
+    def __init__(self, state: FieldState, n_rays: int, seed: int = 0, allreduce=None, ray_offset: int = 0):
+        self.state = state
+        self.cfg = state.cfg
+        self.n_rays = n_rays
+        self.S = self.cfg.n_samples
+        self.N = n_rays * self.S
+        self.seed = seed
+        self.ray_offset = ray_offset
+        self.allreduce = allreduce  # callable(tensor) summing in place across ranks, or None
+        dev = state.device
+        self.z = torch.empty(n_rays, self.S, dtype=torch.float32, device=dev)
+        self.enc = torch.empty(self.cfg.n_levels, self.N, dtype=torch.int32, device=dev)
+        self.d_enc = torch.empty(self.cfg.n_levels, self.N, 2, dtype=torch.float32, device=dev)
+        self.ws = torch.empty(L.lib().lnr_dw_workspace_words(n_rays), dtype=torch.float32, device=dev)
+        self.bwd_ws_bytes = int(L.lib().lnr_hashgrid_bwd_workspace_bytes(L.ctypes.byref(state.desc), self.N))
+        self.bwd_ws = torch.empty(self.bwd_ws_bytes, dtype=torch.uint8, device=dev)
+        self.stats = torch.zeros(n_rays, L.RAY_STATS, dtype=torch.float32, device=dev)
+        self.depth = torch.empty(n_rays, dtype=torch.float32, device=dev)
+        self.opacity = torch.empty(n_rays, dtype=torch.float32, device=dev)
+        self.loss_out = torch.zeros(8, dtype=torch.float32, device=dev)
+        self.n_opaque = torch.zeros(1, dtype=torch.float32, device=dev)
+
+    def loss_params(self, global_step, iteration_idx, scale, far_ref, n_rays_global):
+        lc = self.cfg.loss
+        lp = L.LossParams()
+        lp.kind = L.LOSS_KINDS[lc.loss_selection]
+        lp.scale = float(scale)
+        lp.los_lambda = float(lc.los_lambda_at(global_step))
+        lp.depthloss_lambda = lc.depthloss_lambda
+        lp.min_depth_eps = lc.min_depth_eps
+        lp.min_js = lc.min_js_score
+        lp.max_js = lc.max_js_score
+        lp.js_alpha = lc.js_alpha
+        lp.los_eps = float(lc.los_eps_at(iteration_idx))
+        lp.far_ref = float(far_ref)
+        lp.inv_n_opaque = 0.0
+        lp.inv_rs = 1.0 / float(n_rays_global * self.S)
+        lp.dev_n_opaque = self.n_opaque.data_ptr()
+        return lp
+
+    def step(self, rays, depth_gt, global_step, iteration_idx=0, scale=1.0, far_ref=None, n_rays_global=None,
+             u_jitter=None, u_pdf=None, noise=None, update_ogm=None):
+        """rays (R,13) fp32, depth_gt (R,) fp32 normalised, both on this GPU.  Returns the device loss
+        buffer [loss, mean_eps, depth_term, los_term, opacity_term, n_opaque] (no host sync)."""
+        st = self.state
+        cfg = self.cfg
+        R, S, N = self.n_rays, self.S, self.N
+        assert rays.shape == (R, 13) and depth_gt.shape == (R,)
+        s = L.stream(st.device)
+        key = L.step_key(self.seed, global_step)
+        if far_ref is None:
+            raise ValueError("far_ref (far bound of global ray 0) is required; optimizer.py:724")
+        n_glob = R if n_rays_global is None else n_rays_global
+        # 1. opaque count (global): local count + all-reduce
+        L.call("lnr_count_opaque", (depth_gt), R, float(far_ref), (self.n_opaque), s)
+        if self.allreduce is not None:
+            self.allreduce(self.n_opaque)
+        lp = self.loss_params(global_step, iteration_idx, scale, far_ref, n_glob)
+        # 2. sampling
+        if cfg.sampler == "OGM":
+            L.call("lnr_sample_ogm", (rays), R, S, (st.occ), cfg.occ_res, cfg.perturb, (u_jitter),
+                   (u_pdf), key, self.ray_offset, (self.z), s)
+        else:
+            L.call("lnr_sample_uniform", (rays), R, S, cfg.perturb, (u_jitter), key, self.ray_offset,
+                   (self.z), s)
+        # 3. encode
+        L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(st.desc), (rays), (self.z), R, S, (st.table_f16),
+               (self.enc), N, self.bwd_ws, self.bwd_ws_bytes, s)
+        # 4. fused field + loss + backward through compositing and MLP
+        st.grad.zero_()
+        L.call("lnr_field_train", (st.mlp_f16), (self.enc), N, (rays), (self.z), (depth_gt), R,
+               S, cfg.raw_noise_std, (noise), key, self.ray_offset, L.ctypes.byref(lp), (self.d_enc),
+               (st.grad_mlp), (self.ws), (self.stats), (self.depth), (self.opacity), None, s)
+        # 5. hash-grid backward
+        L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(st.desc), (rays), (self.z), R, S, (self.d_enc),
+               N, (st.grad_table), self.bwd_ws, self.bwd_ws_bytes, L.BWD_COUNTS_READY, s)
+        # 6. data-parallel gradient exchange (one all-reduce of table + MLP grads)
+        if self.allreduce is not None:
+            self.allreduce(st.grad)
+        # 7. Adam (+ fp16 shadow)
+        st.adam_step += 1
+        L.call("lnr_adam_step", (st.params), (st.shadow), (st.grad), (st.m), (st.v),
+               st.n_padded, st.adam_step, cfg.lr, 0.9, 0.999, 1e-8, s)
+        # 8. loss scalars (device)
+        L.call("lnr_loss_finalize", (self.stats), R, L.ctypes.byref(lp), (self.loss_out), s)
+        # 9. OGM every N_iters_acc global steps (optimizer.py:466-469)
+        if update_ogm is None:
+            update_ogm = (global_step % cfg.n_iters_acc == 0)
+        if update_ogm:
+            self.ogm_update(rays, depth_gt, scale)
+        return self.loss_out
+
+    def ogm_update(self, rays, depth_gt, scale):
+        """Optimizer._step_occupancy_grid (optimizer.py:897-908).  Data-parallel: the grid gradient
+        is all-reduced before the SGD step so every replica applies the global-batch update."""
+        st = self.state
+        s = L.stream(st.device)
+        if self.allreduce is None:
+            L.call("lnr_ogm_update", (rays), (self.z), (depth_gt), self.n_rays, self.S, float(scale),
+                   self.cfg.occ_lr, (st.occ), (st.occ_ws), self.cfg.occ_res, s)
+            return
+        st.occ_ws.zero_()
+        L.call("lnr_ogm_grad", (rays), (self.z), (depth_gt), self.n_rays, self.S, float(scale),
+               (st.occ_ws), self.cfg.occ_res, s)
+        self.allreduce(st.occ_ws)
+        L.call("lnr_sgd_step", (st.occ), (st.occ_ws), st.occ.numel(), self.cfg.occ_lr, s)

@@ -1,0 +1,341 @@
+"""Parity of the HIP path (through the C ABI) against the CPU oracle and the reference's golden
+vectors.  GPU only: run with ``pytest -m gpu`` on an MI355X.
+
+Tolerances: integer/index work bit-exact (encoding indices, sorted sample
+order); fp32 elementwise within a few ulp; fp16 outputs (encodings, sigma) within 1-2 fp16 ulp;
+reductions/scans within 1e-5 relative; gradients of fp32 atomics within 1e-4 relative L2.
+"""
+import ast
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import hashgrid as ohg
+from oracle import loss as oloss
+from oracle import mlp as omlp
+from oracle import optim as ooptim
+from oracle import render as orender
+from oracle import rng as orng
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from loner_amd import _lib
+    _lib.lib()
+    return _lib
+
+
+def cu(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.cuda()
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+def enc_levelmajor_to_aos(enc_i32, n, L_):
+    e = host(enc_i32).view(np.uint32).reshape(L_, -1)[:, :n]
+    lo = (e & 0xFFFF).astype(np.uint16).view(np.float16)
+    hi = (e >> 16).astype(np.uint16).view(np.float16)
+    out = np.empty((n, 2 * L_), np.float16)
+    out[:, 0::2] = lo.T
+    out[:, 1::2] = hi.T
+    return out
+
+
+# ------------------------------------------------------------------ hash grid
+def test_hashgrid_fwd_bitexact_indices(L):
+    rng = np.random.default_rng(0)
+    n = 5000
+    lay = ohg.GridLayout(16, 2, 18, 16)
+    d = L.grid_desc(16, 2, 18, 16)
+    pos = rng.uniform(0, 1, (n, 3)).astype(np.float32)
+    pos[:5] = [[0, 0, 0], [1, 1, 1], [0.5, 0.5, 0.5], [1, 0, 1], [0.999999, 0.3, 0.0]]
+    table = rng.uniform(-1, 1, (lay.n_entries, 2)).astype(np.float16)
+    enc = torch.empty(16, n, dtype=torch.int32, device="cuda")
+    L.call("lnr_hashgrid_fwd", ctypes.byref(d), (cu(pos)), n, (cu(table.view(np.uint16).view(np.int16))),
+           (enc), n, None, 0, L.stream())
+    got = enc_levelmajor_to_aos(enc, n, 16).astype(np.float32)
+    ref = ohg.encode(pos, table, lay).astype(np.float32)
+    # identical corner indices and weights; only fp32 fma-vs-mul/add rounding differs -> <= 1 fp16 ulp
+    ulp = np.abs(ref) * 2.0 ** -10 + 2.0 ** -24
+    assert np.all(np.abs(got - ref) <= 1.01 * ulp), np.abs(got - ref).max()
+
+
+def test_hashgrid_fwd_rays_matches_positions(L):
+    g = np.load("tests/golden/samplers.npz")
+    rays, z = g["rays"], g["z_ogm"]
+    R, S = z.shape
+    lay = ohg.GridLayout(16, 2, 19, 16)  # the RGB-head grid (T=2^19)
+    d = L.grid_desc(16, 2, 19, 16)
+    rng = np.random.default_rng(1)
+    table = rng.uniform(-1, 1, (lay.n_entries, 2)).astype(np.float16)
+    enc = torch.empty(16, R * S, dtype=torch.int32, device="cuda")
+    L.call("lnr_hashgrid_fwd_rays", ctypes.byref(d), (cu(rays)), (cu(z)), R, S,
+           (cu(table.view(np.int16))), (enc), R * S, None, 0, L.stream())
+    xyz = (rays[:, None, 0:3] + rays[:, None, 3:6] * z[:, :, None]).astype(np.float32)
+    pos = ((xyz + np.float32(1)) / np.float32(2)).astype(np.float32).reshape(-1, 3)
+    ref = ohg.encode(pos, table, lay).astype(np.float32)
+    got = enc_levelmajor_to_aos(enc, R * S, 16).astype(np.float32)
+    ulp = np.abs(ref) * 2.0 ** -10 + 2.0 ** -24
+    assert np.all(np.abs(got - ref) <= 1.01 * ulp)
+
+
+@pytest.mark.parametrize("variant", ["bucketed", "bucketed_fwd_counts", "atomic"])
+def test_hashgrid_bwd(L, variant):
+    rng = np.random.default_rng(2)
+    # a few "rays" of sorted samples so the coarse-level run merge is exercised
+    R, S = 40, 256
+    o = rng.uniform(-0.5, 0.5, (R, 3))
+    dr = rng.normal(0, 1, (R, 3))
+    dr /= np.linalg.norm(dr, axis=1, keepdims=True)
+    t = np.sort(rng.uniform(0.0, 0.4, (R, S)), 1)
+    pos = (((o[:, None] + dr[:, None] * t[:, :, None]) + 1) / 2).reshape(-1, 3).astype(np.float32)
+    n = R * S - 77  # ragged tail
+    pos = pos[:n]
+    lay = ohg.GridLayout(16, 2, 18, 16)
+    d = L.grid_desc(16, 2, 18, 16)
+    denc = rng.normal(0, 1, (n, 32)).astype(np.float32)
+    denc_lm = np.ascontiguousarray(denc.reshape(n, 16, 2).transpose(1, 0, 2))
+    gt = torch.zeros(lay.n_entries * 2, dtype=torch.float32, device="cuda")
+    if variant.startswith("bucketed"):
+        nb = int(L.lib().lnr_hashgrid_bwd_workspace_bytes(ctypes.byref(d), n))
+        ws = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    if variant == "bucketed_fwd_counts":
+        table = torch.zeros(lay.n_entries * 2, dtype=torch.int16, device="cuda")
+        enc = torch.empty(16, n, dtype=torch.int32, device="cuda")
+        L.call("lnr_hashgrid_fwd", ctypes.byref(d), cu(pos), n, table, enc, n, ws, nb, L.stream())
+        L.call("lnr_hashgrid_bwd", ctypes.byref(d), cu(pos), n, cu(denc_lm), n, gt, ws, nb, L.BWD_COUNTS_READY,
+               L.stream())
+    elif variant == "bucketed":
+        L.call("lnr_hashgrid_bwd", ctypes.byref(d), cu(pos), n, cu(denc_lm), n, gt, ws, nb, 0, L.stream())
+    else:
+        L.call("lnr_hashgrid_bwd_atomic", ctypes.byref(d), cu(pos), n, cu(denc_lm), n, gt, L.stream())
+    got = host(gt).reshape(-1, 2)
+    ref = ohg.encode_backward(pos, denc, lay)
+    err = np.linalg.norm(got - ref) / np.linalg.norm(ref)
+    assert err < 1e-5, err
+    assert np.abs(got - ref).max() < 1e-4 * np.abs(ref).max()
+    # untouched entries stay exactly zero
+    assert np.all(got[ref == 0] == 0)
+
+
+# ------------------------------------------------------------------ sigma MLP
+def _mlp_setup(rng, n):
+    shapes = omlp.layer_shapes(32, 1, 64, 1)
+    w0 = rng.uniform(-0.4, 0.4, shapes[0]).astype(np.float16)
+    w1 = rng.uniform(-0.4, 0.4, shapes[1]).astype(np.float16)
+    x = rng.uniform(-1, 1, (n, 32)).astype(np.float16)
+    wflat = np.concatenate([w0.reshape(-1), w1.reshape(-1)])
+    x_lm = np.ascontiguousarray(x.reshape(n, 16, 2).transpose(1, 0, 2)).view(np.int32).reshape(16, n)
+    return w0, w1, x, wflat, x_lm
+
+
+def test_sigma_mlp_fwd(L):
+    rng = np.random.default_rng(3)
+    n = 1000  # not a multiple of 16: tail tile
+    w0, w1, x, wflat, x_lm = _mlp_setup(rng, n)
+    sig = torch.empty(n, dtype=torch.int16, device="cuda")
+    L.call("lnr_sigma_mlp_fwd", (cu(wflat.view(np.int16))), (cu(x_lm)), n, n, (sig), L.stream())
+    got = host(sig).view(np.float16).astype(np.float32)
+    out, _ = omlp.forward(x, [w0, w1])
+    ref = out[:, 0].astype(np.float32)
+    assert np.all(np.abs(got - ref) <= np.abs(ref) * 2.0 ** -9 + 2.0 ** -14), np.abs(got - ref).max()
+
+
+def test_sigma_mlp_bwd(L):
+    rng = np.random.default_rng(4)
+    n = 4000
+    w0, w1, x, wflat, x_lm = _mlp_setup(rng, n)
+    dsig = (rng.normal(0, 1, n) * 10.0 ** rng.uniform(-6, 0, n)).astype(np.float32)
+    # samples whose hidden pre-activation sits at 0 within fp32-vs-fp64 rounding have an ambiguous
+    # ReLU mask; give them no gradient so both sides agree on every contribution
+    pre = np.abs(x.astype(np.float64) @ w0.astype(np.float64).T).min(1)
+    tie = pre < 1e-6
+    dsig[tie] = 0.0
+    denc = torch.empty(16, n, 2, dtype=torch.float32, device="cuda")
+    dw = torch.zeros(3072, dtype=torch.float32, device="cuda")
+    ws = torch.empty(L.lib().lnr_dw_workspace_words(n), dtype=torch.float32, device="cuda")
+    L.call("lnr_sigma_mlp_bwd", (cu(wflat.view(np.int16))), (cu(x_lm)), n, n, (cu(dsig)), (denc),
+           (dw), (ws), L.stream())
+    out, hid = omlp.forward(x, [w0, w1])
+    dout = np.zeros((n, 16))
+    dout[:, 0] = dsig
+    dx, dws = omlp.backward(x, [w0, w1], hid, dout)
+    got_dx = host(denc).transpose(1, 0, 2).reshape(n, 32)
+    # unit-d_sigma MFMA (exact fp16 operands) then fp32 scaling: fp32-accumulation accurate
+    assert tie.sum() <= 3
+    ok = ~tie
+    per = np.where(ok, np.abs(got_dx - dx).max(1), 0)
+    worst = np.argsort(per)[-6:]
+    err = per.max() / np.abs(dx).max()
+    assert err < 1e-5, (err, worst, per[worst], dsig[worst], pre[worst], got_dx[worst[-1]], dx[worst[-1]])
+    gw = host(dw)
+    ref_w = np.concatenate([dws[0].reshape(-1), dws[1].reshape(-1)])
+    err = np.linalg.norm(gw - ref_w) / np.linalg.norm(ref_w)
+    assert err < 2e-3, err
+    assert np.all(gw[2048 + 64:] == 0)  # padded output rows get no gradient
+
+
+# ------------------------------------------------------------------ sampling
+def test_ogm_sampler_golden(L):
+    g = np.load("tests/golden/samplers.npz")
+    rays, occ = g["rays"], g["occ"]
+    R = rays.shape[0]
+    z = torch.empty(R, 512, dtype=torch.float32, device="cuda")
+    L.call("lnr_sample_ogm", (cu(rays)), R, 512, (cu(occ)), 100, 1.0, (cu(g["u_jitter"])),
+           (cu(g["u_pdf"])), 0, 0, (z), L.stream())
+    got = host(z)
+    assert np.all(np.diff(got, axis=1) >= 0)
+    np.testing.assert_allclose(got, g["z_ogm"], rtol=1e-5, atol=5e-6)
+
+
+def test_uniform_sampler_golden(L):
+    g = np.load("tests/golden/samplers.npz")
+    rays = g["rays"]
+    R = rays.shape[0]
+    z = torch.empty(R, 64, dtype=torch.float32, device="cuda")
+    L.call("lnr_sample_uniform", (cu(rays)), R, 64, 1.0, (cu(g["u_jitter_uniform"])), 0, 0, (z),
+           L.stream())
+    np.testing.assert_allclose(host(z), g["z_uniform"], rtol=1e-6, atol=1e-7)
+
+
+def test_ogm_sampler_inkernel_rng_matches_oracle(L):
+    g = np.load("tests/golden/samplers.npz")
+    rays, occ = g["rays"], g["occ"]
+    R = rays.shape[0]
+    key, off = orng.step_key(7, 3), 1000
+    z = torch.empty(R, 512, dtype=torch.float32, device="cuda")
+    L.call("lnr_sample_ogm", (cu(rays)), R, 512, (cu(occ)), 100, 1.0, None, None, key, off, (z),
+           L.stream())
+    a, b = orng.ray_sample_grid(np.arange(off, off + R), 256)
+    uj = orng.uniform(key, orng.STREAM_JITTER, a, b)
+    up = orng.uniform(key, orng.STREAM_PDF, a, b)
+    ref = orender.ogm_samples(rays, 512, occ, uj, up)
+    np.testing.assert_allclose(host(z), ref, rtol=1e-5, atol=5e-6)
+
+
+# ------------------------------------------------------------------ compositing + loss
+def test_composite_default_and_adjusted_golden(L):
+    g = np.load("tests/golden/composite.npz")
+    rays, z, sig, noise = g["rays"], g["z"], g["sigma"], g["noise"]
+    R, S = z.shape
+    outs = {k: torch.empty(R, dtype=torch.float32, device="cuda") for k in ("depth", "opacity", "variance")}
+    w = torch.empty(R, S, dtype=torch.float32, device="cuda")
+    L.call("lnr_composite", (cu(rays)), (cu(z)), (cu(sig)), R, S, 0, 1.0, (cu(noise)), 0, 0,
+           (w), (outs["depth"]), (outs["opacity"]), (outs["variance"]), L.stream())
+    np.testing.assert_allclose(host(w), g["weights"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(host(outs["depth"]), g["depth"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(host(outs["opacity"]), g["opacity"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(host(outs["variance"]), g["variance"], rtol=1e-3, atol=1e-8)
+    L.call("lnr_composite", (cu(rays)), (cu(z)), (cu(sig)), R, S, 1, 0.0, None, 0, 0, (w),
+           (outs["depth"]), (outs["opacity"]), (outs["variance"]), L.stream())
+    np.testing.assert_allclose(host(w), g["adj_weights"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_array_equal(host(outs["depth"]), g["adj_depth"])
+    with pytest.raises(RuntimeError, match="Unknown render strategy"):
+        L.call("lnr_composite", (cu(rays)), (cu(z)), (cu(sig)), R, S, 7, 0.0, None, 0, 0, None,
+               (outs["depth"]), None, None, L.stream())
+
+
+def _lp(L, cfg, scale, gstep, it_idx, far_ref, n_op, R, S):
+    lp = L.LossParams()
+    lp.kind = L.LOSS_KINDS[cfg["loss_selection"]]
+    lp.scale = float(scale)
+    lp.los_lambda = oloss.los_lambda(cfg, gstep)
+    lp.depthloss_lambda = cfg["depthloss_lambda"]
+    lp.min_depth_eps = cfg["min_depth_eps"]
+    lp.min_js = cfg["JS_loss"]["min_js_score"]
+    lp.max_js = cfg["JS_loss"]["max_js_score"]
+    lp.js_alpha = cfg["JS_loss"]["alpha"]
+    lp.los_eps = oloss.los_depth_eps(cfg, it_idx)
+    lp.far_ref = float(far_ref)
+    lp.inv_n_opaque = 1.0 / max(n_op, 1)
+    lp.inv_rs = 1.0 / (R * S)
+    lp.dev_n_opaque = None
+    return lp
+
+
+@pytest.mark.parametrize("tag", ["l1js_default", "l1js_haveri", "l1los", "l2js"])
+def test_composite_loss_bwd_golden(L, tag):
+    g = np.load(f"tests/golden/loss_{tag}.npz")
+    cfg = ast.literal_eval(str(g["cfg_json"]))
+    rays, z, sig, noise, dgt = g["rays"], g["z"], g["sigma"], g["noise"], g["depth_gt"]
+    R, S = z.shape
+    n_op = int(((dgt > 0) & ~(dgt > rays[0, -1])).sum())
+    lp = _lp(L, cfg, g["scale"], int(g["global_step"]), int(g["iteration_idx"]), rays[0, -1], n_op, R, S)
+    w = torch.empty(R, S, dtype=torch.float32, device="cuda")
+    depth = torch.empty(R, dtype=torch.float32, device="cuda")
+    op = torch.empty(R, dtype=torch.float32, device="cuda")
+    dsig = torch.empty(R, S, dtype=torch.float32, device="cuda")
+    stats = torch.empty(R, L.RAY_STATS, dtype=torch.float32, device="cuda")
+    out = torch.empty(8, dtype=torch.float32, device="cuda")
+    L.call("lnr_composite_loss_bwd", (cu(rays)), (cu(z)), (cu(sig)), (cu(dgt)), R, S, 1.0,
+           (cu(noise)), 0, 0, ctypes.byref(lp), (w), (depth), (op), (dsig), (stats),
+           L.stream())
+    L.call("lnr_loss_finalize", (stats), R, ctypes.byref(lp), (out), L.stream())
+    o = host(out)
+    assert o[0] == pytest.approx(float(g["loss"]), rel=1e-4)
+    assert o[1] == pytest.approx(float(g["depth_eps"]), rel=1e-5)
+    np.testing.assert_allclose(host(w), g["weights"], rtol=1e-4, atol=1e-6)
+    ref = g["dsigma"].reshape(R, S)
+    got = host(dsig)
+    err = np.abs(got - ref).max() / np.abs(ref).max()
+    assert err < 1e-4, err
+
+
+def test_ogm_update_golden(L):
+    g = np.load("tests/golden/loss_l1js_default.npz")
+    occ = np.load("tests/golden/samplers.npz")["occ"]
+    rays, z, dgt = g["rays"], g["z"], g["depth_gt"]
+    R, S = z.shape
+    grid = cu(occ.reshape(-1).copy())
+    ws = torch.empty_like(grid)
+    L.call("lnr_ogm_update", (cu(rays)), (cu(z)), (cu(dgt)), R, S, float(g["scale"]),
+           float(g["occ_lr"]), (grid), (ws), 100, L.stream())
+    delta = host(grid) - occ.reshape(-1)
+    idx = g["occ_delta_idx"]
+    np.testing.assert_allclose(delta[idx], g["occ_delta"], rtol=1e-3, atol=2e-7)
+    mask = np.ones(delta.size, bool)
+    mask[idx] = False
+    assert np.abs(delta[mask]).max() < 1e-7
+
+
+# ------------------------------------------------------------------ Adam
+def test_adam_matches_torch_semantics(L):
+    rng = np.random.default_rng(5)
+    n = 10003
+    p = rng.normal(0, 1, n).astype(np.float32)
+    m = np.zeros(n, np.float32)
+    v = np.zeros(n, np.float32)
+    tp, tm, tv = cu(np.pad(p, (0, 1))), cu(np.zeros(n + 1, np.float32)), cu(np.zeros(n + 1, np.float32))
+    sh = torch.empty(n + 1, dtype=torch.float16, device="cuda")
+    for step in range(1, 4):
+        grad = rng.normal(0, 1e-3, n).astype(np.float32)
+        ooptim.adam_step(p, grad, m, v, step, 0.01)
+        L.call("lnr_adam_step", (tp), (sh), (cu(np.pad(grad, (0, 1)))), (tm), (tv), n, step,
+               0.01, 0.9, 0.999, 1e-8, L.stream())
+    np.testing.assert_allclose(host(tp)[:n], p, rtol=1e-6, atol=1e-7)
+    np.testing.assert_array_equal(host(sh)[:n], host(tp)[:n].astype(np.float16))
+    # torch.optim.Adam itself on the same data (CPU reference semantics)
+    rng = np.random.default_rng(6)
+    q = torch.nn.Parameter(torch.from_numpy(rng.normal(0, 1, 64).astype(np.float32)))
+    opt = torch.optim.Adam([q], lr=0.01)
+    tq = cu(q.detach().numpy().copy())
+    tm2, tv2 = torch.zeros(64, device="cuda"), torch.zeros(64, device="cuda")
+    for step in range(1, 6):
+        gr = rng.normal(0, 1, 64).astype(np.float32)
+        q.grad = torch.from_numpy(gr)
+        opt.step()
+        L.call("lnr_adam_step", (tq), None, (cu(gr)), (tm2), (tv2), 64, step, 0.01, 0.9, 0.999,
+               1e-8, L.stream())
+    np.testing.assert_allclose(host(tq), q.detach().numpy(), rtol=1e-6, atol=1e-7)
