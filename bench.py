@@ -1,0 +1,190 @@
+#!/usr/bin/env python3
+"""Benchmark: ray-samples/s per optimiser step of the LONER sigma-field path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--no-cpu-baseline]
+
+A "step" is one full optimiser step of the reference's step loop (src/mapping/optimizer.py:354-475)
+on one ray batch: OGM sampling -> hash-grid encode -> sigma MLP -> compositing -> LiDAR loss ->
+backward -> [all-reduce] -> Adam (+ the OGM update every N_iters_acc=10 global steps, which falls
+inside the timed region as in the reference).  Default workload: BASELINE.json configs[1],
+Newer College quad-easy: 16 keyframes x 512 rays = 8192 rays x 512 samples, L=16 hash grid +
+64-wide MLP, synthetic analytic scene (no datasets reachable), rays resident in HBM before timing.
+
+Multi-GPU (torchrun): one process per GPU, each rank optimises its own 8192-ray shard of a global
+batch of 8192*N rays (weak scaling) and the sigma gradients (7.4 M params, 29.7 MB fp32) plus the
+loss normaliser are all-reduced over RCCL once per step.
+
+Rank 0 prints one JSON line (contract in the task statement), including
+  roofline      hash-grid backward stage (the dominant stage) against HBM peak, algorithmic bytes
+                1024 B/sample, duration from HIP events on the launch stream
+  cpu_baseline  the numpy oracle (oracle/step.py) on a bounded sample, single host thread
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 TB/s measured copy)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="C2", choices=["C1", "C2", "C4"])
+    ap.add_argument("--batches", type=int, default=4, help="distinct resident ray batches cycled per rank")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rays", type=int, default=64, help="rays per CPU-baseline step (x512 samples)")
+    ap.add_argument("--cpu-steps", type=int, default=16)
+    return ap.parse_args()
+
+
+LOSS_PRESETS = {
+    # cfg/model_config/default_model_config.yaml:40-60
+    "default": dict(loss_selection="L1_JS", JS_loss=dict(min_js_score=1.0, max_js_score=10.0, alpha=1.0),
+                    decay_los_lambda=False, los_lambda=1000.0, min_los_lambda=10.0, los_lambda_decay_rate=0.001,
+                    los_lambda_decay_steps=15000, decay_depth_eps=True, depth_eps=3.0, min_depth_eps=0.5,
+                    depth_eps_decay_rate=0.95, depth_eps_decay_steps=1, depthloss_lambda=0.005),
+    # cfg/haveri_hpk/02_02_04.yaml:92-107
+    "haveri": dict(loss_selection="L1_JS", JS_loss=dict(min_js_score=0.1, max_js_score=10.0, alpha=1.0),
+                   decay_los_lambda=True, los_lambda=1000.0, min_los_lambda=10.0, los_lambda_decay_rate=0.0001,
+                   los_lambda_decay_steps=15000, decay_depth_eps=True, depth_eps=3.0, min_depth_eps=0.5,
+                   depth_eps_decay_rate=0.95, depth_eps_decay_steps=100, depthloss_lambda=0.005),
+}
+
+
+def cpu_baseline(cfg_name, n_rays, n_steps):
+    """The numpy oracle on a bounded sample of the same workload (rank 0, N=1 only)."""
+    from oracle import step as ostep
+    from loner_amd import synthetic as syn
+    kind, nkf, rpk, spk, strat, S, preset = syn.CONFIGS[cfg_name]
+    win = syn.make_window(kind, 2, seed=99)
+    rays, dgt = syn.build_batch(win, kind, n_rays // 2, 0, strat, seed=7)
+    rays, dgt = rays.numpy(), dgt.numpy()
+    field = ostep.OracleField()
+    scale = syn.CUBES[kind][0]
+    ostep.train_step(field, rays, dgt, scale, LOSS_PRESETS[preset], 1, n_samples=S)  # warm-up (discarded)
+    t0 = time.perf_counter()
+    for it in range(n_steps):
+        ostep.train_step(field, rays, dgt, scale, LOSS_PRESETS[preset], 2 + it, n_samples=S, key=it)
+    dt = time.perf_counter() - t0
+    return {"value": rays.shape[0] * S * n_steps / dt, "unit": "ray-samples/s", "cores": 1, "kind": "port",
+            "sample": f"{n_steps} optimiser steps of {rays.shape[0]} rays x {S} samples ({cfg_name} scene), "
+                      f"numpy oracle (oracle/step.py), {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist = None
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local)
+
+    from loner_amd import step as S_
+    from loner_amd import synthetic as syn
+    kind, nkf, rpk, spk, strat, n_samples, preset = syn.CONFIGS[args.config]
+    scale = syn.CUBES[kind][0]
+
+    # ---- workload: distinct resident batches for this rank's shard
+    batches = []
+    for b in range(args.batches):
+        win = syn.make_window(kind, nkf, seed=1000 * rank + b, start=17 * b + 5 * rank)
+        rays, dgt = syn.build_batch(win, kind, rpk, spk, strat, seed=31 * b + rank)
+        batches.append((rays.to(dev), dgt.to(dev)))
+    R = batches[0][0].shape[0]
+    assert all(b[0].shape[0] == R for b in batches)
+    far_ref = [float(b[0][0, -1]) for b in batches]
+
+    cfg = S_.StepConfig(n_samples=n_samples, occ_lr=1e-3 if preset == "haveri" else 1e-4,
+                        loss=S_.LossConfig.from_dict(LOSS_PRESETS[preset]))
+    state = S_.FieldState(cfg, device=dev)
+    allreduce = None
+    if dist is not None:
+        def allreduce(t):
+            dist.all_reduce(t)
+    eng = S_.StepEngine(state, R, seed=12345, allreduce=allreduce, ray_offset=rank * R)
+
+    def run(i, prof=None):
+        rays, dgt = batches[i % len(batches)]
+        return eng.step(rays, dgt, global_step=i, scale=scale, far_ref=far_ref[i % len(batches)],
+                        n_rays_global=R * world, prof=prof)
+
+    for i in range(args.warmup):
+        run(i)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    prof = {}
+    t0 = time.perf_counter()
+    for i in range(args.warmup, args.warmup + args.steps):
+        out = run(i, prof)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist is not None:
+        dist.barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    loss = out.cpu().numpy()
+    stage_ms = {k: float(np.mean([v[j].elapsed_time(v[j + 1]) for j in range(0, len(v), 2)])) for k, v in prof.items()}
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    N = R * n_samples
+    ms = elapsed / args.steps * 1e3
+    value = world * N * args.steps / elapsed
+    bwd_ms = stage_ms["grid_bwd"]
+    achieved = 1024.0 * N / (bwd_ms * 1e-3) / 1e9
+    line = {
+        "metric": "ray-samples/sec per optimizer step",
+        "value": value,
+        "unit": "ray-samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp16 params/activations, fp32 accumulate+optimizer",
+        "data": f"synthetic {kind} LiDAR scene (analytic ray-cast), rays resident in HBM; random-init sigma field",
+        "config": {"workload": f"{args.config}: {nkf} KF x ({rpk} + {spk} sky) rays x {n_samples} samples per GPU, "
+                               f"L=16 T=2^18 hash grid + 64-wide sigma MLP, {preset} loss (L1_JS)",
+                   "rays_per_gpu": R, "samples_per_ray": n_samples, "global_rays": R * world,
+                   "parallelism": f"dp{world}" if world > 1 else "single"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "hash-grid backward stage (k_bwd_scan_*, k_bwd_scatter, k_bwd_level_max, k_bwd_accum)",
+                     "algorithmic_bytes_per_launch": 1024 * N, "ms_per_launch": bwd_ms},
+        "stage_ms": stage_ms,
+        "loss": float(loss[0]),
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_rays, args.cpu_steps)
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

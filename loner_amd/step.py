@@ -196,10 +196,19 @@ class StepEngine:
         lp.dev_n_opaque = self.n_opaque.data_ptr()
         return lp
 
+    @staticmethod
+    def _mark(prof, stage):
+        """Record a HIP event on the current stream (the stream every kernel here is launched on)."""
+        if prof is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            prof.setdefault(stage, []).append(ev)
+
     def step(self, rays, depth_gt, global_step, iteration_idx=0, scale=1.0, far_ref=None, n_rays_global=None,
-             u_jitter=None, u_pdf=None, noise=None, update_ogm=None):
+             u_jitter=None, u_pdf=None, noise=None, update_ogm=None, prof=None):
         """rays (R,13) fp32, depth_gt (R,) fp32 normalised, both on this GPU.  Returns the device loss
-        buffer [loss, mean_eps, depth_term, los_term, opacity_term, n_opaque] (no host sync)."""
+        buffer [loss, mean_eps, depth_term, los_term, opacity_term, n_opaque] (no host sync).
+        ``prof``: optional dict collecting (begin, end) HIP event pairs per stage."""
         st = self.state
         cfg = self.cfg
         R, S, N = self.n_rays, self.S, self.N
@@ -209,43 +218,57 @@ class StepEngine:
         if far_ref is None:
             raise ValueError("far_ref (far bound of global ray 0) is required; optimizer.py:724")
         n_glob = R if n_rays_global is None else n_rays_global
+        m = self._mark
         # 1. opaque count (global): local count + all-reduce
-        L.call("lnr_count_opaque", (depth_gt), R, float(far_ref), (self.n_opaque), s)
+        L.call("lnr_count_opaque", depth_gt, R, float(far_ref), self.n_opaque, s)
         if self.allreduce is not None:
             self.allreduce(self.n_opaque)
         lp = self.loss_params(global_step, iteration_idx, scale, far_ref, n_glob)
         # 2. sampling
+        m(prof, "sample")
         if cfg.sampler == "OGM":
-            L.call("lnr_sample_ogm", (rays), R, S, (st.occ), cfg.occ_res, cfg.perturb, (u_jitter),
-                   (u_pdf), key, self.ray_offset, (self.z), s)
+            L.call("lnr_sample_ogm", rays, R, S, st.occ, cfg.occ_res, cfg.perturb, u_jitter, u_pdf, key,
+                   self.ray_offset, self.z, s)
         else:
-            L.call("lnr_sample_uniform", (rays), R, S, cfg.perturb, (u_jitter), key, self.ray_offset,
-                   (self.z), s)
-        # 3. encode
-        L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(st.desc), (rays), (self.z), R, S, (st.table_f16),
-               (self.enc), N, self.bwd_ws, self.bwd_ws_bytes, s)
+            L.call("lnr_sample_uniform", rays, R, S, cfg.perturb, u_jitter, key, self.ray_offset, self.z, s)
+        m(prof, "sample")
+        # 3. encode (+ backward record histogram)
+        m(prof, "encode")
+        L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(st.desc), rays, self.z, R, S, st.table_f16, self.enc, N,
+               self.bwd_ws, self.bwd_ws_bytes, s)
+        m(prof, "encode")
         # 4. fused field + loss + backward through compositing and MLP
         st.grad.zero_()
-        L.call("lnr_field_train", (st.mlp_f16), (self.enc), N, (rays), (self.z), (depth_gt), R,
-               S, cfg.raw_noise_std, (noise), key, self.ray_offset, L.ctypes.byref(lp), (self.d_enc),
-               (st.grad_mlp), (self.ws), (self.stats), (self.depth), (self.opacity), None, s)
+        m(prof, "field")
+        L.call("lnr_field_train", st.mlp_f16, self.enc, N, rays, self.z, depth_gt, R, S, cfg.raw_noise_std, noise, key,
+               self.ray_offset, L.ctypes.byref(lp), self.d_enc, st.grad_mlp, self.ws, self.stats, self.depth,
+               self.opacity, None, s)
+        m(prof, "field")
         # 5. hash-grid backward
-        L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(st.desc), (rays), (self.z), R, S, (self.d_enc),
-               N, (st.grad_table), self.bwd_ws, self.bwd_ws_bytes, L.BWD_COUNTS_READY, s)
+        m(prof, "grid_bwd")
+        L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(st.desc), rays, self.z, R, S, self.d_enc, N, st.grad_table,
+               self.bwd_ws, self.bwd_ws_bytes, L.BWD_COUNTS_READY, s)
+        m(prof, "grid_bwd")
         # 6. data-parallel gradient exchange (one all-reduce of table + MLP grads)
         if self.allreduce is not None:
+            m(prof, "allreduce")
             self.allreduce(st.grad)
+            m(prof, "allreduce")
         # 7. Adam (+ fp16 shadow)
         st.adam_step += 1
-        L.call("lnr_adam_step", (st.params), (st.shadow), (st.grad), (st.m), (st.v),
-               st.n_padded, st.adam_step, cfg.lr, 0.9, 0.999, 1e-8, s)
+        m(prof, "adam")
+        L.call("lnr_adam_step", st.params, st.shadow, st.grad, st.m, st.v, st.n_padded, st.adam_step, cfg.lr, 0.9,
+               0.999, 1e-8, s)
+        m(prof, "adam")
         # 8. loss scalars (device)
-        L.call("lnr_loss_finalize", (self.stats), R, L.ctypes.byref(lp), (self.loss_out), s)
+        L.call("lnr_loss_finalize", self.stats, R, L.ctypes.byref(lp), self.loss_out, s)
         # 9. OGM every N_iters_acc global steps (optimizer.py:466-469)
         if update_ogm is None:
             update_ogm = (global_step % cfg.n_iters_acc == 0)
         if update_ogm:
+            m(prof, "ogm")
             self.ogm_update(rays, depth_gt, scale)
+            m(prof, "ogm")
         return self.loss_out
 
     def ogm_update(self, rays, depth_gt, scale):

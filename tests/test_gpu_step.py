@@ -161,11 +161,14 @@ def test_step_engine_one_step_vs_oracle(L):
     w1 = sh0[2048:3072].reshape(16, 64)
     table = sh0[n_mlp:n_mlp + 2 * st.n_entries].reshape(-1, 2)
     lay = ohg.GridLayout(16, 2, 18, 16)
-    xyz = (rays[:, None, 0:3] + rays[:, None, 3:6] * z[:, :, None]).astype(np.float32)
+    # field/loss/backward on the GPU's samples: the sampler is checked above to ~1 ulp, and a 1-ulp
+    # depth difference moves the finest levels' (cell ~2e-6) trilinear weights by percents
+    zg = host(eng.z)
+    xyz = (rays[:, None, 0:3] + rays[:, None, 3:6] * zg[:, :, None]).astype(np.float32)
     pos = ((xyz + np.float32(1)) / np.float32(2)).astype(np.float32).reshape(-1, 3)
     x = ohg.encode(pos, table, lay)
-    sig, ro, res, dx, dws = _oracle_field(x, w0, w1, z, rays, noise, dgt, scale, L2JS, 20)
-    assert loss[0] == pytest.approx(res["loss"], rel=2e-3)
+    sig, ro, res, dx, dws = _oracle_field(x, w0, w1, zg, rays, noise, dgt, scale, L2JS, 20)
+    assert loss[0] == pytest.approx(res["loss"], rel=2e-4)
     g_table = ohg.encode_backward(pos, dx, lay).reshape(-1)
     g_ref = np.concatenate([dws[0].reshape(-1), dws[1].reshape(-1), g_table])
     # gradient actually applied: reconstruct from the first Adam step, p1 = p0 - lr * g/(|g| + eps')
@@ -178,10 +181,10 @@ def test_step_engine_one_step_vs_oracle(L):
     agree = np.mean(np.sign(p1[big] - p0[big]) == np.sign(pr[big] - p0[big]))
     assert agree > 0.995, agree
     g_got = host(st.grad)[:len(g_ref)]
-    assert np.linalg.norm(g_got - g_ref) / np.linalg.norm(g_ref) < 3e-3
+    assert np.linalg.norm(g_got - g_ref) / np.linalg.norm(g_ref) < 1e-4
     # OGM update happened with these z (optimizer.py:466-469)
     grid = occ.copy()
-    ooptim.ogm_step(grid, rays, z, dgt, scale, 1e-3)
+    ooptim.ogm_step(grid, rays, zg, dgt, scale, 1e-3)
     np.testing.assert_allclose(host(st.occ).reshape(occ.shape), grid, rtol=1e-5, atol=1e-6)
 
 
