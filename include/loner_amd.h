@@ -106,6 +106,10 @@ int lnr_enc_to_aos(const uint32_t* enc, int64_t enc_stride, int64_t n, uint32_t 
 int lnr_aos_grad_to_enc(const uint16_t* g_aos_f16, const float* g_aos_f32, int64_t n, uint32_t n_levels,
                         float* d_enc, int64_t enc_stride, void* stream);
 
+/* tcnn "SphericalHarmonics" encoding (colour head, nerf_tcnn.py:43,86): dir01 (N,3) fp32 in [0,1]^3
+ * -> out (N, degree^2) fp16 row-major.  degree 1..4 (LONER uses 4). */
+int lnr_sh_encode(const float* dir01, int64_t n, int32_t degree, uint16_t* out, void* stream);
+
 /* ---------------------------------------------------------------- sigma MLP */
 #define LNR_SIGMA_W0 (64 * 32)
 #define LNR_SIGMA_W1 (16 * 64)
@@ -168,6 +172,14 @@ int lnr_composite_loss_bwd(const float* rays, const float* z, const float* sigma
                            int64_t n_rays, int32_t n_samples, float noise_std, const float* noise, uint32_t key,
                            int64_t ray_offset, const lnr_loss_params* lp, float* weights, float* depth,
                            float* opacity, float* d_sigma, float* ray_stats, void* stream);
+/* Autograd backward of lnr_composite (the tcnn-compatible render_rays path, where the loss is the
+ * caller's torch code): d_sigma (R,S) fp32 from upstream gradients of weights (R,S), depth, opacity
+ * and variance (R); any of them may be NULL (= zero).  Same noise arguments as the forward, so the
+ * noise is regenerated bit-identically instead of being stored. */
+int lnr_composite_bwd(const float* rays, const float* z, const float* sigma, int64_t n_rays, int32_t n_samples,
+                      int32_t strategy, float noise_std, const float* noise, uint32_t key, int64_t ray_offset,
+                      const float* g_weights, const float* g_depth, const float* g_opacity, const float* g_variance,
+                      float* d_sigma, void* stream);
 /* Fused: sigma MLP forward from enc, compositing, loss, compositing backward, MLP backward.
  * Writes d_enc (level-major float2), accumulates d_w (3072 fp32), per-ray stats; optional outputs NULL. */
 int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, const float* rays, const float* z,

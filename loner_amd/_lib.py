@@ -61,6 +61,7 @@ _SIGNATURES = {
                                                     c_p]),
     "lnr_enc_to_aos": (ctypes.c_int, [c_p, c_i64, c_i64, c_u32, c_p, c_p]),
     "lnr_aos_grad_to_enc": (ctypes.c_int, [c_p, c_p, c_i64, c_u32, c_p, c_i64, c_p]),
+    "lnr_sh_encode": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_p]),
     "lnr_sigma_mlp_fwd": (ctypes.c_int, [c_p, c_p, c_i64, c_i64, c_p, c_p]),
     "lnr_dw_workspace_words": (c_i64, [c_i64]),
     "lnr_sigma_mlp_bwd": (ctypes.c_int, [c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p]),
@@ -69,6 +70,8 @@ _SIGNATURES = {
     "lnr_sample_uniform": (ctypes.c_int, [c_p, c_i64, c_i32, c_f, c_p, c_u32, c_i64, c_p, c_p]),
     "lnr_composite": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_i32, c_f, c_p, c_u32, c_i64, c_p, c_p, c_p, c_p,
                                      c_p]),
+    "lnr_composite_bwd": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_i32, c_f, c_p, c_u32, c_i64, c_p, c_p, c_p,
+                                         c_p, c_p, c_p]),
     "lnr_composite_loss_bwd": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_u32, c_i64,
                                               ctypes.POINTER(LossParams), c_p, c_p, c_p, c_p, c_p, c_p]),
     "lnr_field_train": (ctypes.c_int, [c_p, c_p, c_i64, c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_u32, c_i64,

@@ -43,7 +43,15 @@ struct FieldArgs {
   float* d_enc;       // kSigmaMLP + train
   float* dw_slab;     // kSigmaMLP + train: [gridDim.x][3072]
   float* ray_stats;   // train: [R][LNR_RAY_STATS]
+  // kLossExternal: upstream gradients of the render outputs (any may be NULL = zero)
+  const float* g_weights;   // (R,S)
+  const float* g_depth;     // (R)
+  const float* g_opacity;   // (R)
+  const float* g_variance;  // (R)
 };
+
+// lnr_loss_params.kind for the plain autograd backward of the render (no loss inside the kernel)
+constexpr int32_t kLossExternal = 100;
 
 struct RayShared {
   float* sig;        // [S] sigma, then dL/dsigma
@@ -219,8 +227,50 @@ __device__ void composite_ray(const FieldArgs& a, const RayShared& sh, int64_t r
     return;
   }
 
-  // ------------------------------------------------ loss (optimizer.py:718-844)
   const lnr_loss_params& lp = a.lp;
+  if (lp.kind == kLossExternal) {
+    // autograd of raw2outputs(_adjusted) w.r.t. sigma given dL/d{weights, depth, opacity, variance}
+    // (rendering_tcnn.py:262-293): variance = sum w (depth - z)^2 feeds w directly and via depth;
+    // depth = sum w z + (1 - sum w) far feeds w_k with (z_k - far).  The adjusted depth is a
+    // piecewise-constant pick of z, so it passes no gradient (:130-132).
+    const float gv = a.g_variance ? a.g_variance[r] : 0.f;
+    const float gd = ADJ ? 0.f : (a.g_depth ? a.g_depth[r] : 0.f) + gv * 2.0f * (depth * opacity - redA[1]);
+    const float go = a.g_opacity ? a.g_opacity[r] : 0.f;
+    float G[C];
+    float FA = 1.f, FB = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      G[c] = 0.f;
+      if (active && i0 + c < S) {
+        const float dd = depth - z[c];
+        const float gw = a.g_weights ? a.g_weights[r * S + i0 + c] : 0.f;
+        G[c] = gw + gv * (dd * dd) + (ADJ ? 0.f : gd * (z[c] - far)) + go;
+      }
+    }
+#pragma unroll
+    for (int c = C - 1; c >= 0; --c) {
+      if (active && i0 + c < S) {
+        FB = G[c] * alpha[c] + s[c] * FB;
+        FA = s[c] * FA;
+      }
+    }
+    float X = block_suffix_affine(FA, FB, sh.fscan);
+#pragma unroll
+    for (int c = C - 1; c >= 0; --c) {
+      if (active && i0 + c < S) {
+        const float dA = T[c] * (G[c] - X);
+        X = G[c] * alpha[c] + s[c] * X;
+        const float sr = fmaxf(x[c], 0.f);
+        const float dsig = (x[c] > 0.f) ? dA * (delta[c] * expf(-(delta[c] * sr))) : 0.f;
+        sh.sig[i0 + c] = dsig;
+        if (a.d_sigma) a.d_sigma[r * S + i0 + c] = dsig;
+      }
+    }
+    __syncthreads();
+    return;
+  }
+
+  // ------------------------------------------------ loss (optimizer.py:718-844)
   const float inv_nop = lp.dev_n_opaque ? 1.0f / fmaxf(lp.dev_n_opaque[0], 1.0f) : lp.inv_n_opaque;
   const float dgt = a.depth_gt[r];
   const float g = dgt * lp.scale;
@@ -580,6 +630,27 @@ extern "C" int lnr_composite_loss_bwd(const float* rays, const float* z, const f
   a.noise_std = noise_std; a.noise = noise; a.key = key; a.ray_offset = ray_offset; a.lp = *lp;
   a.weights = weights; a.depth = depth; a.opacity = opacity; a.d_sigma = d_sigma; a.ray_stats = ray_stats;
   return launch_field<true, false, kSigmaGiven>(a, field_blocks(n_rays), as_stream(stream), "lnr_composite_loss_bwd");
+}
+
+extern "C" int lnr_composite_bwd(const float* rays, const float* z, const float* sigma, int64_t n_rays,
+                                 int32_t n_samples, int32_t strategy, float noise_std, const float* noise, uint32_t key,
+                                 int64_t ray_offset, const float* g_weights, const float* g_depth,
+                                 const float* g_opacity, const float* g_variance, float* d_sigma, void* stream) {
+  if (int e = check_rays(rays, z, n_rays, n_samples, "lnr_composite_bwd")) return e;
+  LNR_REQUIRE(strategy == LNR_RENDER_DEFAULT || strategy == LNR_RENDER_ADJUSTED,
+              "Unknown render strategy: %d", strategy);
+  if (n_rays == 0) return LNR_OK;
+  LNR_REQUIRE(sigma && d_sigma, "lnr_composite_bwd: null sigma/d_sigma");
+  FieldArgs a{};
+  a.rays = rays; a.z = z; a.sigma_in = sigma; a.n_rays = n_rays; a.S = n_samples;
+  a.noise_std = noise_std; a.noise = noise; a.key = key; a.ray_offset = ray_offset;
+  a.lp.kind = kLossExternal;
+  a.g_weights = g_weights; a.g_depth = g_depth; a.g_opacity = g_opacity; a.g_variance = g_variance;
+  a.d_sigma = d_sigma;
+  const int nb = field_blocks(n_rays);
+  if (strategy == LNR_RENDER_ADJUSTED)
+    return launch_field<true, true, kSigmaGiven>(a, nb, as_stream(stream), "lnr_composite_bwd");
+  return launch_field<true, false, kSigmaGiven>(a, nb, as_stream(stream), "lnr_composite_bwd");
 }
 
 extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, const float* rays,

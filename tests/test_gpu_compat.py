@@ -1,0 +1,299 @@
+"""The tcnn-compatible host layer (loner_amd.tcnn / nerf / rendering / ray_sampling / model) on the
+GPU, against the CPU oracle and a float64 torch autograd restatement of the reference's
+raw2outputs.  These read like the reference's own usage: module constructed from the YAML dicts,
+called on (B, 3) positions, gradients through ``.backward()``.
+
+Tolerances: fp16 outputs within 1 fp16 ulp of the oracle (both round an fp32 value); gradients
+within 1e-4 relative L2 (fp32 accumulation order); sampler depths within 2 ulp; compositing
+within 1e-5 relative (fp32 scan vs fp64)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import hashgrid as ohg
+from oracle import mlp as omlp
+from oracle import render as orender
+from oracle import rng as orng
+
+pytestmark = pytest.mark.gpu
+
+SIGMA_ENC = dict(otype="HashGrid", n_levels=16, n_features_per_level=2, log2_hashmap_size=18, base_resolution=16)
+SIGMA_NET = dict(otype="FullyFusedMLP", activation="ReLU", output_activation="None", n_neurons=64, n_hidden_layers=1)
+NERF_CFG = {  # cfg/nerf_config/default_nerf_hash.yaml
+    "enable_view_dependence": True,
+    "pos_encoding_sigma": SIGMA_ENC,
+    "sigma_network": SIGMA_NET,
+    "pos_encoding_intensity": dict(otype="HashGrid", n_levels=16, n_features_per_level=2, log2_hashmap_size=19,
+                                   base_resolution=16),
+    "dir_encoding_intensity": dict(otype="SphericalHarmonics", degree=4),
+    "intensity_network": dict(otype="FullyFusedMLP", activation="ReLU", output_activation="None", n_neurons=64,
+                              n_hidden_layers=4),
+}
+
+
+@pytest.fixture(scope="module")
+def tc():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from loner_amd import tcnn
+    return tcnn
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+def f16_close(a, b, ulps=1):
+    a = np.asarray(a, np.float16).astype(np.float32)
+    b = np.asarray(b, np.float16).astype(np.float32)
+    tol = ulps * np.maximum(np.spacing(np.abs(b).astype(np.float16)).astype(np.float32), 6e-8)
+    return np.abs(a - b) <= tol + 1e-12
+
+
+def sigma_close(got, ref):
+    """fp16 sigma within the bound of test_gpu_parity.test_sigma_mlp_fwd.  The hidden layer is
+    rounded to fp16 after an fp32 (MFMA) vs fp64 (oracle) sum; where that sum sits on a rounding
+    boundary one hidden value lands an fp16 ulp apart and moves sigma by w1 * ulp(h): allowed for
+    at most 0.2 % of the samples (~1 in 1000 observed)."""
+    got = np.asarray(got, np.float32)
+    ref = np.asarray(ref, np.float32)
+    bad = ~(np.abs(got - ref) <= np.abs(ref) * 2.0 ** -9 + 2.0 ** -14)
+    return bad.sum() <= 2 + 2e-3 * bad.size
+
+
+def test_sigma_module_forward_backward(tc):
+    """NetworkWithInputEncoding (the sigma field): fp16 sigma and the flat-params gradient."""
+    m = tc.NetworkWithInputEncoding(n_input_dims=3, n_output_dims=1, encoding_config=SIGMA_ENC,
+                                    network_config=SIGMA_NET)
+    assert m.dtype == torch.half and m.n_output_dims == 1
+    assert m.params.numel() == 3072 + 7413760 and m.params.dtype == torch.float32
+    torch.manual_seed(0)
+    with torch.no_grad():  # non-trivial field for parity (tcnn's U(1e-4) table gives sigma ~ 0)
+        m.params[3072:].uniform_(-0.5, 0.5)
+        m.params[2048:3072].mul_(8.0)
+    rng = np.random.default_rng(1)
+    n = 3000
+    pos = rng.uniform(0, 1, (n, 3)).astype(np.float32)
+    x = torch.from_numpy(pos).cuda()
+    out = m(x)
+    assert out.shape == (n, 1) and out.dtype == torch.half
+    p16 = host(m.params).astype(np.float16)
+    w0, w1, table = p16[:2048].reshape(64, 32), p16[2048:3072].reshape(16, 64), p16[3072:].reshape(-1, 2)
+    lay = ohg.GridLayout(16, 2, 18, 16)
+    enc = ohg.encode(pos, table, lay)
+    ref, hid = omlp.forward(enc, [w0, w1])
+    assert sigma_close(host(out)[:, 0].astype(np.float32), ref[:, 0].astype(np.float32))
+    # backward through a torch loss, as the reference's compute_loss does
+    gs = torch.from_numpy(rng.normal(0, 1, (n, 1)).astype(np.float32)).cuda()
+    (out.float() * gs).sum().backward()
+    g = host(m.params.grad)
+    dout = np.zeros((n, 16))
+    dout[:, 0] = host(gs.half().float())[:, 0]  # autograd casts dL/dsigma to the fp16 output dtype
+    dx, dws = omlp.backward(enc, [w0, w1], hid, dout)
+    gt = ohg.encode_backward(pos, dx, lay).reshape(-1)
+    g_ref = np.concatenate([dws[0].reshape(-1), dws[1].reshape(-1), gt])
+    # table: fp32 records + int64 fixed-point sums; MLP weights: the dW0 MFMA takes fp16-rounded
+    # dsigma*enc operands (as tcnn's fp16 weight-gradient GEMM does), see DESIGN.md numerics
+    gt_err = np.linalg.norm(g[3072:] - g_ref[3072:]) / np.linalg.norm(g_ref[3072:])
+    gw_err = np.linalg.norm(g[:3072] - g_ref[:3072]) / np.linalg.norm(g_ref[:3072])
+    assert gt_err < 1e-4 and gw_err < 3e-3, (gt_err, gw_err)
+
+
+def test_encoding_hashgrid_2_19(tc):
+    """Encoding(HashGrid T=2^19) — the colour head's grid — forward AoS fp16 and backward."""
+    cfg = NERF_CFG["pos_encoding_intensity"]
+    e = tc.Encoding(3, cfg)
+    assert e.n_output_dims == 32 and e.params.numel() == 2 * 7114752
+    with torch.no_grad():
+        e.params.uniform_(-1, 1)
+    rng = np.random.default_rng(2)
+    n = 2000
+    pos = rng.uniform(0, 1, (n, 3)).astype(np.float32)
+    out = e(torch.from_numpy(pos).cuda())
+    lay = ohg.GridLayout(16, 2, 19, 16)
+    table = host(e.params).astype(np.float16).reshape(-1, 2)
+    ref = ohg.encode(pos, table, lay)
+    assert f16_close(host(out), ref).mean() > 0.999
+    gd = rng.normal(0, 1, (n, 32)).astype(np.float32)
+    (out.float() * torch.from_numpy(gd).cuda()).sum().backward()
+    g = host(e.params.grad)
+    g_ref = ohg.encode_backward(pos, gd.astype(np.float16).astype(np.float64), lay).reshape(-1)
+    assert np.linalg.norm(g - g_ref) / np.linalg.norm(g_ref) < 1e-4
+
+
+def test_spherical_harmonics_degree4(tc):
+    e = tc.Encoding(3, NERF_CFG["dir_encoding_intensity"])
+    assert e.n_output_dims == 16
+    rng = np.random.default_rng(3)
+    d = rng.normal(size=(500, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    d01 = ((d + 1) / 2).astype(np.float32)
+    out = host(e(torch.from_numpy(d01).cuda())).astype(np.float64)
+    x, y, z = (d01 * 2 - 1).astype(np.float64).T
+    ref = np.stack([np.full_like(x, 0.28209479177387814), -0.48860251190291987 * y, 0.48860251190291987 * z,
+                    -0.48860251190291987 * x, 1.0925484305920792 * x * y, -1.0925484305920792 * y * z,
+                    0.94617469575755997 * z * z - 0.31539156525251999, -1.0925484305920792 * x * z,
+                    0.54627421529603959 * (x * x - y * y), 0.59004358992664352 * y * (-3 * x * x + y * y),
+                    2.8906114426405538 * x * y * z, 0.45704579946446572 * y * (1 - 5 * z * z),
+                    0.3731763325901154 * z * (5 * z * z - 3), 0.45704579946446572 * x * (1 - 5 * z * z),
+                    1.4453057213202769 * z * (x * x - y * y), 0.59004358992664352 * x * (-x * x + 3 * y * y)], 1)
+    np.testing.assert_allclose(out, ref, rtol=2e-3, atol=2e-3)
+
+
+def test_network_generic_matches_fp32(tc):
+    net = tc.Network(48, 3, NERF_CFG["intensity_network"])
+    assert net.params.numel() == 64 * 48 + 3 * 64 * 64 + 16 * 64
+    rng = np.random.default_rng(4)
+    x = rng.normal(0, 1, (700, 48)).astype(np.float16)
+    out = host(net(torch.from_numpy(x).cuda())).astype(np.float32)
+    p = host(net.params).astype(np.float16).astype(np.float64)
+    shapes = [(64, 48), (64, 64), (64, 64), (64, 64), (16, 64)]
+    h, off = x.astype(np.float64), 0
+    for k, (o, i) in enumerate(shapes):
+        W = p[off:off + o * i].reshape(o, i)
+        off += o * i
+        h = h @ W.T
+        if k < len(shapes) - 1:
+            h = np.maximum(h, 0).astype(np.float16).astype(np.float64)
+    np.testing.assert_allclose(out, h[:, :3], rtol=2e-2, atol=2e-3)
+
+
+def test_unsupported_configs_raise(tc):
+    with pytest.raises(RuntimeError):
+        tc.Network(32, 1, dict(otype="FullyFusedMLP", activation="ReLU", n_neurons=48, n_hidden_layers=1))
+    with pytest.raises(RuntimeError):
+        tc.Encoding(3, dict(otype="Frequency", n_frequencies=4))
+    m = tc.NetworkWithInputEncoding(3, 1, SIGMA_ENC, SIGMA_NET)
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(4, 3))  # CPU input: no CPU path
+
+
+# ----------------------------------------------------------------- compositing autograd
+def _torch_raw2outputs(sig, z, rays_d, noise, far, adjusted):
+    """rendering_tcnn.py:219-295 / :70-214 restated in torch float64 (autograd reference)."""
+    deltas = torch.cat([z[:, 1:] - z[:, :-1], 1e10 * torch.ones_like(z[:, :1])], -1)
+    deltas = deltas * torch.norm(rays_d.unsqueeze(1), dim=-1)
+    x = sig + (0 if adjusted else noise)
+    alphas = 1 - torch.exp(-deltas * torch.relu(x))
+    sh = torch.cat([torch.ones_like(alphas[:, :1]), 1. - alphas + 1e-10], -1)
+    T = torch.cumprod(sh, -1)[:, :-1]
+    w = alphas * T
+    op = w.sum(-1)
+    if adjusted:
+        Tsh = torch.cat([torch.ones_like(T[:, :1]), T[:, :-1]], 1)
+        hit = (~(T > 0.5)) & (Tsh > 0.5)
+        depth = torch.where(hit.any(-1), z.gather(1, hit.float().argmax(-1, keepdim=True))[:, 0],
+                            torch.zeros_like(op))
+    else:
+        depth = torch.sum(torch.cat([w, 1 - w.sum(1, keepdim=True)], 1) * torch.cat([z, far], -1), -1)
+    var = (w * (depth.view(-1, 1) - z) ** 2).sum(1)
+    return w, depth, op, var
+
+
+@pytest.mark.parametrize("adjusted", [False, True])
+def test_raw2outputs_autograd(tc, adjusted):
+    from loner_amd import random as lr
+    from loner_amd import rendering
+    from loner_amd import _lib as L
+    rng = np.random.default_rng(5)
+    R_, S = 37, 512
+    z = np.sort(rng.uniform(0.01, 0.6, (R_, S)), 1).astype(np.float32)
+    sig = rng.normal(0, 30, (R_, S)).astype(np.float16).astype(np.float32)
+    d = rng.normal(size=(R_, 3))
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    far = (z[:, -1:] + 0.05).astype(np.float32)
+    lr.manual_seed(11)
+    key = L.step_key(11, 0)
+    s_t = torch.from_numpy(sig).cuda().requires_grad_(True)
+    fn = rendering.raw2outputs_adjusted if adjusted else rendering.raw2outputs
+    if adjusted:
+        _, depth, w, op, var = fn(s_t[..., None], torch.from_numpy(z).cuda(), torch.zeros(R_, 3).cuda(),
+                                  torch.from_numpy(d).cuda(), 1.0, sigma_only=True, ret_var=True)
+        noise = np.zeros((R_, S), np.float32)
+    else:
+        _, depth, w, op, var = fn(s_t[..., None], torch.from_numpy(z).cuda(), torch.from_numpy(d).cuda(), 1.0,
+                                  sigma_only=True, far=torch.from_numpy(far).cuda(), ret_var=True)
+        a, b = orng.ray_sample_grid(np.arange(R_), S)
+        noise = orng.normal(key, orng.STREAM_NOISE, a, b).astype(np.float32)
+    gw = rng.normal(0, 1, (R_, S))
+    gd, go, gv = rng.normal(0, 1, R_), rng.normal(0, 1, R_), rng.normal(0, 1, R_)
+    loss = (w * torch.from_numpy(gw).float().cuda()).sum() + (depth * torch.from_numpy(gd).float().cuda()).sum() \
+        + (op * torch.from_numpy(go).float().cuda()).sum() + (var * torch.from_numpy(gv).float().cuda()).sum()
+    loss.backward()
+    # float64 torch reference
+    st = torch.from_numpy(sig.astype(np.float64)).requires_grad_(True)
+    w2, d2, o2, v2 = _torch_raw2outputs(st, torch.from_numpy(z.astype(np.float64)), torch.from_numpy(d.astype(np.float64)),
+                                        torch.from_numpy(noise.astype(np.float64)),
+                                        torch.from_numpy(far.astype(np.float64)), adjusted)
+    np.testing.assert_allclose(host(w), w2.detach().numpy(), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(host(depth), d2.detach().numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(host(op), o2.detach().numpy(), rtol=1e-5, atol=1e-6)
+    l2 = (w2 * torch.from_numpy(gw)).sum() + (d2 * torch.from_numpy(gd)).sum() + (o2 * torch.from_numpy(go)).sum() \
+        + (v2 * torch.from_numpy(gv)).sum()
+    l2.backward()
+    g = host(s_t.grad)
+    gr = st.grad.numpy()
+    assert np.linalg.norm(g - gr) / np.linalg.norm(gr) < 1e-4
+
+
+# ----------------------------------------------------------------- render_rays end to end
+def test_render_rays_sigma_only_vs_oracle(tc):
+    """Model.forward(camera=False) = OGM sampler + sigma field + default compositing, against the
+    oracle on the same draws (keys from loner_amd.random)."""
+    from loner_amd import model as M
+    from loner_amd import random as lr
+    from loner_amd import ray_sampling
+    from loner_amd import synthetic as syn
+    from loner_amd import _lib as L
+    cfg = dict(model_type="nerf_decoupled", num_colors=3, nerf_config=NERF_CFG, ray_range=[1, 75],
+               render=dict(N_samples_train=512, N_samples_test=2048, retraw=True, perturb=1.0, raw_noise_std=1.0,
+                           chunk=16384, netchunk=0))
+    model = M.Model(cfg)
+    sig_params = model.get_sigma_parameters()[0]
+    torch.manual_seed(1)
+    with torch.no_grad():
+        sig_params[3072:].uniform_(-0.5, 0.5)
+        sig_params[2048:3072].mul_(8.0)
+    occ = M.OccupancyGridModel(dict(voxel_size=100), device="cuda")
+    with torch.no_grad():
+        occ.occupancy_grid.normal_(0, 2)
+    sampler = ray_sampling.OccGridRaySampler()
+    sampler.update_occ_grid(occ.occupancy_grid.detach())
+    win = syn.make_window("quad", 1, seed=2)
+    rays, dgt = syn.build_batch(win, "quad", 24, 0, "RANDOM", seed=4)
+    lr.manual_seed(21)
+    res = model(rays.cuda(), sampler, torch.tensor([121.426537]), camera=False, return_variance=True)
+    assert set(res) >= {"rgb_fine", "depth_fine", "weights_fine", "opacity_fine", "variance", "samples_fine",
+                        "points_fine", "raw_fine"}
+    rn = rays.numpy()
+    Rn, S = rn.shape[0], 512
+    a, b = orng.ray_sample_grid(np.arange(Rn), S // 2)
+    k0, k1 = L.step_key(21, 0), L.step_key(21, 1)
+    uj, up = orng.uniform(k0, orng.STREAM_JITTER, a, b), orng.uniform(k0, orng.STREAM_PDF, a, b)
+    z_ref = orender.ogm_samples(rn, S, host(occ.occupancy_grid).reshape(100, 100, 100), uj, up)
+    z = host(res["samples_fine"])
+    # inverse-CDF depths: t = (u - cdf)/denom amplifies cumsum rounding where denom is small, so
+    # depths differ by up to a few ulp (bound 4e-6 normalised = 0.5 mm at this scale).  Where
+    # sample_pdf's `denom < eps -> 1` rule applies (rendering_tcnn.py:60-62) z is discontinuous
+    # in u at the bin edge, and a draw within rounding distance of a cdf value may land one bin
+    # over in either implementation: allowed for 0.1 % of the samples.
+    dz = np.abs(z - z_ref)
+    assert (dz > 4e-6).sum() <= 2 + 1e-3 * dz.size and np.all(np.diff(z, axis=1) >= 0)
+    # field + compositing on the GPU's samples
+    p16 = host(sig_params).astype(np.float16)
+    w0, w1, table = p16[:2048].reshape(64, 32), p16[2048:3072].reshape(16, 64), p16[3072:].reshape(-1, 2)
+    xyz = (rn[:, None, 0:3] + rn[:, None, 3:6] * z[:, :, None]).astype(np.float32)
+    pos = ((xyz + np.float32(1)) / np.float32(2)).astype(np.float32).reshape(-1, 3)
+    enc = ohg.encode(pos, table, ohg.GridLayout(16, 2, 18, 16))
+    out16, _ = omlp.forward(enc, [w0, w1])
+    sig = out16[:, 0].astype(np.float32).reshape(Rn, S)
+    a2, b2 = orng.ray_sample_grid(np.arange(Rn), S)
+    noise = orng.normal(k1, orng.STREAM_NOISE, a2, b2).astype(np.float32)
+    ro = orender.raw2outputs(sig, z, rn[:, 3:6], noise, rn[:, -1:])
+    np.testing.assert_array_equal(host(res["points_fine"]), xyz)
+    assert sigma_close(host(res["raw_fine"])[..., 0], sig)
+    np.testing.assert_allclose(host(res["depth_fine"]), ro["depth"], rtol=2e-4, atol=1e-6)
+    # rendered-depth L1 in metres (BASELINE.json metric), GPU vs oracle on identical rays/draws
+    l1 = np.abs(host(res["depth_fine"]) - ro["depth"]).mean() * 121.426537
+    assert l1 < 1e-3, l1
