@@ -83,9 +83,9 @@ int lnr_hashgrid_fwd_rays(const lnr_grid_desc* d, const float* rays, const float
                           int32_t n_samples, const uint16_t* table, uint32_t* enc, int64_t enc_stride,
                           void* bwd_ws, int64_t bwd_ws_bytes, void* stream);
 /* Backward: d_table (n_entries,2) fp32 = scatter of corner weights * d_enc, as an atomic-free
- * binned scatter with int64 fixed-point accumulation.  d_table must be zero on entry
- * (chunks spanning several work slices add into it); `workspace` holds at least
- * lnr_hashgrid_bwd_workspace_bytes(d, N) bytes. */
+ * binned scatter with int64 fixed-point accumulation.  d_table is OVERWRITTEN (every
+ * entry, zero where no sample touches it) and the result is bitwise reproducible; `workspace`
+ * holds at least lnr_hashgrid_bwd_workspace_bytes(d, N) bytes. */
 #define LNR_BWD_COUNTS_READY 1
 int64_t lnr_hashgrid_bwd_workspace_bytes(const lnr_grid_desc* d, int64_t n);
 int lnr_hashgrid_bwd(const lnr_grid_desc* d, const float* pos01, int64_t n, const float* d_enc,

@@ -166,7 +166,7 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
   if (bwd_ws) {
     LNR_REQUIRE(bwd_ws_bytes >= bwd_workspace_bytes(d, n), "%s: backward workspace too small", who);
     LNR_REQUIRE(a.n_buckets <= (uint32_t)kMaxBuckets, "%s: too many table chunks (%u)", who, a.n_buckets);
-    BwdWorkspace w = carve_workspace(bwd_ws, a, n);
+    BwdWorkspace w = carve_workspace(bwd_ws, a, d, n);
     hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, true>), grid, dim3(256), 0, st, a, pos, n,
                        reinterpret_cast<const uint32_t*>(table), enc, enc_stride, w);
   } else {

@@ -20,7 +20,11 @@ constexpr int kChunkLog2 = 12;
 constexpr int kChunk = 1 << kChunkLog2;
 constexpr int kMaxChunksPerLevel = 128;
 constexpr int kMaxBuckets = 2048;
-constexpr int64_t kSliceRecords = 1 << 20;  // records per accumulation work item
+// Records per accumulation work item.  Buckets with more records are split into slices whose int64
+// fixed-point partial chunks (one scale per bucket) k_bwd_finalize sums exactly: which records
+// land in which slice depends on LDS-atomic order, the integer sum does not;
+// 2^18 gives ~3 rounds of work items over the 512 resident 64 KB-LDS workgroups at C2/C4 sizes.
+constexpr int64_t kSliceRecords = 1 << 18;
 
 struct GridArgs {
   LevelParams lv[LNR_MAX_LEVELS];
@@ -150,6 +154,19 @@ __device__ __forceinline__ void run_sum(const RunInfo& ri, float& v0, float& v1)
   }
 }
 
+// The same in int64 (exact and associative: the result does not depend on the record order).
+__device__ __forceinline__ void run_sum_i64(const RunInfo& ri, long long& v0, long long& v1) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long q0 = __shfl_up(v0, o, 64), q1 = __shfl_up(v1, o, 64);
+    if (lane - o >= ri.head_lane) {
+      v0 += q0;
+      v1 += q1;
+    }
+  }
+}
+
 // Rank of this lane's record among the block's records of the same bucket (LDS counters).
 // Coherent levels put most of a wave's records into one or two buckets: there each distinct
 // bucket of the wave does one atomic (ballot + popcount) instead of 64 same-address atomics.
@@ -179,10 +196,18 @@ struct BwdWorkspace {
   float* level_max;      // [LNR_MAX_LEVELS]
   uint32_t* counts;      // [kMaxBuckets]
   uint64_t* seg_start;   // [kMaxBuckets + 1]
-  uint32_t* slice_pre;   // [kMaxBuckets + 1]
+  uint32_t* slice_pre;   // [kMaxBuckets + 1] work-item prefix over buckets
+  uint32_t* part_pre;    // [kMaxBuckets + 1] partial-chunk prefix (multi-slice buckets only)
+  long long* partial;    // [max_partials][2 * kChunk] int64 fixed-point partial sums of split buckets
   uint64_t* records;     // [8 * N * L] {idx in chunk (13b), g0 (fp25), g1 (fp25)}
   int64_t n_bx;
 };
+
+// Upper bound on the partial chunks: a split bucket holds c > kSliceRecords records in
+// ceil(c / kSliceRecords) <= 2c / kSliceRecords slices, and sum(c) <= 8 N L.
+inline int64_t bwd_max_partials(const lnr_grid_desc* d, int64_t n) {
+  return 2 * (8 * n * (int64_t)d->n_levels) / kSliceRecords + 1;
+}
 
 inline int64_t bwd_n_bx(int64_t n) { return (n + 255) / 256; }
 
@@ -198,11 +223,13 @@ inline int64_t bwd_workspace_bytes(const lnr_grid_desc* d, int64_t n) {
   b += align256(kMaxBuckets * 4);
   b += align256((kMaxBuckets + 1) * 8);
   b += align256((kMaxBuckets + 1) * 4);
+  b += align256((kMaxBuckets + 1) * 4);
+  b += align256(bwd_max_partials(d, n) * 2 * kChunk * 8);
   b += align256(8 * n * (int64_t)d->n_levels * 8);
   return b;
 }
 
-inline BwdWorkspace carve_workspace(void* base, const GridArgs& a, int64_t n) {
+inline BwdWorkspace carve_workspace(void* base, const GridArgs& a, const lnr_grid_desc* d, int64_t n) {
   BwdWorkspace w{};
   char* p = reinterpret_cast<char*>(base);
   w.n_bx = bwd_n_bx(n);
@@ -218,6 +245,10 @@ inline BwdWorkspace carve_workspace(void* base, const GridArgs& a, int64_t n) {
   p += align256((kMaxBuckets + 1) * 8);
   w.slice_pre = reinterpret_cast<uint32_t*>(p);
   p += align256((kMaxBuckets + 1) * 4);
+  w.part_pre = reinterpret_cast<uint32_t*>(p);
+  p += align256((kMaxBuckets + 1) * 4);
+  w.partial = reinterpret_cast<long long*>(p);
+  p += align256(bwd_max_partials(d, n) * 2 * kChunk * 8);
   w.records = reinterpret_cast<uint64_t*>(p);
   return w;
 }

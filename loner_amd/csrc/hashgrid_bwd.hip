@@ -9,8 +9,9 @@
 //   scatter records {idx in chunk, g0, g1 as fp25} staged in LDS in bucket order and written
 //           as coalesced runs; per-block max |g| for the fixed-point scale
 //   accum   one workgroup per (bucket, slice): int64 fixed-point sums in a 64 KB LDS chunk with
-//           ds_add_u64, converted back to fp32 and stored (float atomic adds only when a bucket
-//           spans several slices)
+//           ds_add_u64, converted back to fp32 and stored; a bucket split over several slices
+//           stores per-slice int64 partial chunks that k_bwd_finalize adds exactly
+// No float atomics anywhere: the result is bitwise reproducible, and d_table is overwritten.
 // Coherent coarse levels merge runs of equal corner indices across lanes before emitting.
 #include "hashgrid.hpp"
 
@@ -71,24 +72,29 @@ __global__ void __launch_bounds__(1024) k_bwd_scan_columns(BwdWorkspace ws) {
 __global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint32_t n_buckets) {
   __shared__ uint64_t s_seg[kMaxBuckets + 1];
   __shared__ uint32_t s_sl[kMaxBuckets + 1];
+  __shared__ uint32_t s_pp[kMaxBuckets + 1];
   if (threadIdx.x == 0) {
     uint64_t acc = 0;
-    uint32_t sl = 0;
+    uint32_t sl = 0, pp = 0;
     for (uint32_t b = 0; b < n_buckets; ++b) {
       s_seg[b] = acc;
       s_sl[b] = sl;
+      s_pp[b] = pp;
       const uint32_t c = ws.counts[b];
       acc += c;
       const uint32_t k = (uint32_t)((c + kSliceRecords - 1) / kSliceRecords);
       sl += k > 0 ? k : 1;
+      pp += k > 1 ? k : 0;
     }
     s_seg[n_buckets] = acc;
     s_sl[n_buckets] = sl;
+    s_pp[n_buckets] = pp;
   }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b <= n_buckets; b += blockDim.x) {
     ws.seg_start[b] = s_seg[b];
     ws.slice_pre[b] = s_sl[b];
+    ws.part_pre[b] = s_pp[b];
   }
 }
 
@@ -207,10 +213,12 @@ __global__ void __launch_bounds__(512) k_bwd_accum(GridArgs a, BwdWorkspace ws, 
     const uint32_t chunk = b - a.bucket_base[l];
     const uint32_t ent0 = chunk * kChunk;
     const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
-    // fixed-point scale: |v| < 2^E, at most `cnt` records -> |sum| < 2^62
+    // fixed-point scale: |v| < 2^E, at most `cnt` records in the whole bucket -> |sum| < 2^62
+    // (one scale per bucket, so split buckets' int64 partials add exactly)
     int E;
     frexpf(ws.level_max[l], &E);
-    const uint64_t cnt = end > beg ? end - beg : 1;
+    const uint64_t bcnt = ws.seg_start[b + 1] - ws.seg_start[b];
+    const uint64_t cnt = bcnt > 0 ? bcnt : 1;
     const int lg = 64 - __clzll((long long)cnt);  // ceil-ish log2(cnt + 1)
     int k2 = 62 - lg - E;
     k2 = k2 > 120 ? 120 : (k2 < -120 ? -120 : k2);
@@ -231,32 +239,57 @@ __global__ void __launch_bounds__(512) k_bwd_accum(GridArgs a, BwdWorkspace ws, 
       for (int u = 0; u < 4; ++u) {
         const bool ok = q[u] != ~0ull;
         const uint32_t ee = ok ? (uint32_t)(q[u] & (kChunk - 1)) : 0xFFFFFFFFu;
-        float v0 = ok ? f25_to_f32((uint32_t)(q[u] >> 13) & 0x1FFFFFFu) : 0.f;
-        float v1 = ok ? f25_to_f32((uint32_t)(q[u] >> 38) & 0x1FFFFFFu) : 0.f;
+        const float v0 = ok ? f25_to_f32((uint32_t)(q[u] >> 13) & 0x1FFFFFFu) : 0.f;
+        const float v1 = ok ? f25_to_f32((uint32_t)(q[u] >> 38) & 0x1FFFFFFu) : 0.f;
+        long long i0 = __float2ll_rn(v0 * scale), i1 = __float2ll_rn(v1 * scale);
         bool emit = ok;
-        if (coherent) {  // records of coherent levels arrive in runs of equal entries
-          const RunInfo ri = lane_runs(ee);
-          run_sum(ri, v0, v1);
+        if (coherent) {  // records of coherent levels arrive in runs of equal entries; merged in
+          const RunInfo ri = lane_runs(ee);  // int64 so the sum does not depend on record order
+          run_sum_i64(ri, i0, i1);
           emit = ok && ri.tail;
         }
         if (emit) {
-          atomicAdd(&acc[2 * ee + 0], (unsigned long long)__float2ll_rn(v0 * scale));
-          atomicAdd(&acc[2 * ee + 1], (unsigned long long)__float2ll_rn(v1 * scale));
+          atomicAdd(&acc[2 * ee + 0], (unsigned long long)i0);
+          atomicAdd(&acc[2 * ee + 1], (unsigned long long)i1);
         }
       }
     }
     __syncthreads();
-    const float inv = ldexpf(1.f, -k2);
-    float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0);
-    if (nsl == 1) {
+    if (nsl == 1) {  // the final values
+      const float inv = ldexpf(1.f, -k2);
+      float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0);
       for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) dst[t] = (float)(long long)acc[t] * inv;
-    } else {
-      for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) {
-        const float v = (float)(long long)acc[t] * inv;
-        if (v != 0.f) atomicAdd(&dst[t], v);
-      }
+    } else {  // this slice's int64 partial chunk
+      long long* dst = ws.partial + (int64_t)(ws.part_pre[b] + j) * (2 * kChunk);
+      for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) dst[t] = (long long)acc[t];
     }
     __syncthreads();
+  }
+}
+
+// Split buckets: d_table = sum of the slices' partial chunks, in slice order (deterministic).
+__global__ void __launch_bounds__(256) k_bwd_finalize(GridArgs a, BwdWorkspace ws, float* __restrict__ d_table) {
+  const uint32_t b = blockIdx.x;
+  const uint32_t nsl = ws.part_pre[b + 1] - ws.part_pre[b];
+  if (nsl == 0) return;
+  uint32_t l = 0;
+  while (l + 1 < a.n_levels && a.bucket_base[l + 1] <= b) ++l;
+  const uint32_t ent0 = (b - a.bucket_base[l]) * kChunk;
+  const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
+  // the accumulate kernel's per-bucket scale
+  int E;
+  frexpf(ws.level_max[l], &E);
+  const uint64_t bcnt = ws.seg_start[b + 1] - ws.seg_start[b];
+  const int lg = 64 - __clzll((long long)(bcnt > 0 ? bcnt : 1));
+  int k2 = 62 - lg - E;
+  k2 = k2 > 120 ? 120 : (k2 < -120 ? -120 : k2);
+  const float inv = ldexpf(1.f, -k2);
+  const long long* src = ws.partial + (int64_t)ws.part_pre[b] * (2 * kChunk);
+  float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0);
+  for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) {
+    long long v = 0;
+    for (uint32_t k = 0; k < nsl; ++k) v += src[(int64_t)k * (2 * kChunk) + t];
+    dst[t] = (float)v * inv;
   }
 }
 
@@ -272,7 +305,7 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
   LNR_REQUIRE(workspace != nullptr && ws_bytes >= bwd_workspace_bytes(d, n),
               "%s: workspace too small (%lld < %lld bytes)", who, (long long)ws_bytes,
               (long long)bwd_workspace_bytes(d, n));
-  BwdWorkspace w = carve_workspace(workspace, a, n);
+  BwdWorkspace w = carve_workspace(workspace, a, d, n);
   dim3 grid((unsigned)w.n_bx, d->n_levels);
   if (!(flags & LNR_BWD_COUNTS_READY)) hipLaunchKernelGGL(k_bwd_count<PosFn>, grid, dim3(256), 0, st, a, pos, n, w);
   hipLaunchKernelGGL(k_bwd_scan_columns, dim3(a.n_buckets), dim3(1024), 0, st, w);
@@ -283,6 +316,7 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
   const int64_t max_slices = a.n_buckets + (8 * n * (int64_t)d->n_levels) / kSliceRecords + 1;
   const unsigned g = (unsigned)(max_slices < 4096 ? max_slices : 4096);
   hipLaunchKernelGGL(k_bwd_accum, dim3(g), dim3(512), 2 * kChunk * sizeof(unsigned long long), st, a, w, d_table);
+  hipLaunchKernelGGL(k_bwd_finalize, dim3(a.n_buckets), dim3(256), 0, st, a, w, d_table);
   LNR_RETURN_LAUNCH(who);
 }
 

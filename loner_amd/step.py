@@ -238,7 +238,7 @@ class StepEngine:
                self.bwd_ws, self.bwd_ws_bytes, s)
         m(prof, "encode")
         # 4. fused field + loss + backward through compositing and MLP
-        st.grad.zero_()
+        st.grad_mlp.zero_()  # the MLP gradient accumulates; the table gradient is overwritten below
         m(prof, "field")
         L.call("lnr_field_train", st.mlp_f16, self.enc, N, rays, self.z, depth_gt, R, S, cfg.raw_noise_std, noise, key,
                self.ray_offset, L.ctypes.byref(lp), self.d_enc, st.grad_mlp, self.ws, self.stats, self.depth,

@@ -95,9 +95,9 @@ class _GridSpec:
 def _grid_backward(spec, pos01, d_enc, n):
     """d_enc (L, n, 2) fp32 level-major -> d_table (n_params) fp32 (binned HIP backward)."""
     dev = pos01.device
-    d_table = torch.zeros(spec.n_params, dtype=torch.float32, device=dev)
     if n == 0:
-        return d_table
+        return torch.zeros(spec.n_params, dtype=torch.float32, device=dev)
+    d_table = torch.empty(spec.n_params, dtype=torch.float32, device=dev)  # overwritten by the backward
     nbytes = int(L.lib().lnr_hashgrid_bwd_workspace_bytes(ctypes.byref(spec.desc), n))
     ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     L.call("lnr_hashgrid_bwd", ctypes.byref(spec.desc), pos01, n, d_enc, n, d_table, ws, nbytes, 0, L.stream(dev))

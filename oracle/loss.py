@@ -67,11 +67,17 @@ def get_weights_gt(s, g, eps, norm=True):
     return wgt
 
 
-def lidar_loss(weights, z, depth, opacity, depth_gt, far, scale, cfg, global_step, iteration_idx=0):
+def lidar_loss(weights, z, depth, opacity, depth_gt, far, scale, cfg, global_step, iteration_idx=0,
+               n_opaque=None, n_total=None, far_ref=None):
     """Returns dict(loss, terms..., g_w (R,S), g_depth (R,), g_opacity (R,), eps (R,), js (R,)).
 
     weights/z (R,S) fp32 normalised units, depth/opacity (R,), depth_gt/far (R,) normalised.
     cfg: the ``loss`` section of the model config (``cfg/model_config/default_model_config.yaml:40-60``).
+
+    Data-parallel shards pass the GLOBAL normalisers: ``n_opaque`` (opaque rays
+    over all shards), ``n_total`` (rays x samples over all shards) and ``far_ref`` (far bound of
+    global ray 0, see below); the returned loss and gradients are then this shard's share, and
+    summing them over shards gives the single-batch values.
     """
     R, S = weights.shape
     scale = F32(scale)
@@ -80,9 +86,11 @@ def lidar_loss(weights, z, depth, opacity, depth_gt, far, scale, cfg, global_ste
     g = (depth_gt.reshape(-1, 1) * scale).astype(F32)
     # optimizer.py:724: ``(lidar_depths.view(-1,1) > far)[...,0]`` broadcasts (R,1) against (R,) and
     # keeps column 0, i.e. every ray is compared with the far bound of ray 0.  Reproduced as is.
-    transparent = depth_gt.reshape(-1) > far.reshape(-1)[0]
+    f0 = far.reshape(-1)[0] if far_ref is None else F32(far_ref)
+    transparent = depth_gt.reshape(-1) > f0
     opaque = (depth_gt.reshape(-1) > 0) & ~transparent
-    n_op = int(opaque.sum())
+    n_op = int(opaque.sum()) if n_opaque is None else int(n_opaque)
+    n_rs = R * S if n_total is None else int(n_total)
     wsum = w.astype(np.float64).sum(1, keepdims=True).astype(F32)
     mean = ((s * w).astype(np.float64).sum(1, keepdims=True).astype(F32) / (wsum + F32(1e-10))).astype(F32)
     var = (((s - mean) ** 2 * w).astype(np.float64).sum(1, keepdims=True).astype(F32) / (wsum + F32(1e-10)) + F32(1e-10)).astype(F32)
@@ -104,16 +112,16 @@ def lidar_loss(weights, z, depth, opacity, depth_gt, far, scale, cfg, global_ste
     dscaled = (depth.reshape(-1) * scale).astype(F32)
     lam = los_lambda(cfg, global_step)
     diff_d = (dscaled - g.reshape(-1)).astype(np.float64)
-    depth_loss = float((diff_d[opaque] ** 2).mean()) if n_op else float("nan")
+    depth_loss = float((diff_d[opaque] ** 2).sum() / n_op) if n_op else float("nan")
     dw = (w - wgt).astype(np.float64)
     if sel.startswith("L1"):
-        los = float(np.abs(dw).mean())
-        g_w = lam * np.sign(dw) / (R * S)
+        los = float(np.abs(dw).sum() / n_rs)
+        g_w = lam * np.sign(dw) / n_rs
     else:
-        los = float((dw ** 2).mean())
-        g_w = lam * 2.0 * dw / (R * S)
+        los = float((dw ** 2).sum() / n_rs)
+        g_w = lam * 2.0 * dw / n_rs
     op_err = opacity.reshape(-1).astype(np.float64) - 1.0
-    op_loss = float(np.abs(op_err[opaque]).mean()) if n_op else float("nan")
+    op_loss = float(np.abs(op_err[opaque]).sum() / n_op) if n_op else float("nan")
     dl_lambda = cfg["depthloss_lambda"]
     loss = dl_lambda * depth_loss + lam * los + op_loss
     inv = 1.0 / max(n_op, 1)

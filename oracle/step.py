@@ -39,13 +39,19 @@ class OracleField:
 
 
 def train_step(field, rays, depth_gt, scale, loss_cfg, global_step, n_samples=512, key=0, ray_offset=0, lr=0.01,
-               occ_lr=1e-4, n_iters_acc=10, noise_std=1.0, z=None):
+               occ_lr=1e-4, n_iters_acc=10, noise_std=1.0, z=None, allreduce=None, n_rays_global=None,
+               far_ref=None):
     """One step; returns (loss, z, grad).  Draws come from oracle.rng with the HIP path's keys.
 
     ``z`` (R, n_samples) replaces the sampler's output when given: the finest hash levels have
     cells of ~2e-6 (scale 16*2^15), so a 1-ulp difference in a sample depth moves its trilinear
     weights by percents; a checker that wants to isolate the field/backward from the sampler
-    feeds the sampler's GPU output back in here (the sampler is checked on its own)."""
+    feeds the sampler's GPU output back in here (the sampler is checked on its own).
+
+    Data-parallel shard: ``ray_offset`` = global index of this shard's first
+    ray (keys the draws), ``n_rays_global``, ``far_ref`` = far bound of global ray 0, and
+    ``allreduce(np.ndarray) -> np.ndarray`` summing over shards: the opaque count and the
+    gradient are exchanged before the loss and before Adam.  Returns this shard's loss share."""
     R = rays.shape[0]
     H = n_samples // 2
     if z is None:
@@ -63,13 +69,23 @@ def train_step(field, rays, depth_gt, scale, loss_cfg, global_step, n_samples=51
     sig = out16[:, 0].astype(F32).reshape(R, n_samples)
     far = rays[:, -1:]
     ro = orender.raw2outputs(sig, z, rays[:, 3:6], noise, far)
-    res = oloss.lidar_loss(ro["weights"], z, ro["depth"], ro["opacity"], depth_gt, far, scale, loss_cfg, global_step)
+    n_op = n_tot = None
+    if allreduce is not None:
+        f0 = np.float32(far[0, 0] if far_ref is None else far_ref)
+        cnt = np.array([float(((depth_gt > 0) & ~(depth_gt > f0)).sum())])
+        n_op = int(allreduce(cnt)[0])
+        n_tot = (R if n_rays_global is None else n_rays_global) * n_samples
+    res = oloss.lidar_loss(ro["weights"], z, ro["depth"], ro["opacity"], depth_gt, far, scale, loss_cfg, global_step,
+                           n_opaque=n_op, n_total=n_tot, far_ref=far_ref)
     ds = orender.composite_backward(sig, z, rays[:, 3:6], noise, far, res["g_w"], res["g_depth"], res["g_opacity"])
     dout = np.zeros((R * n_samples, 16))
     dout[:, 0] = ds.reshape(-1)
     dx, dws = omlp.backward(x, [w0, w1], hid, dout)
     g_table = ohg.encode_backward(pos, dx, field.layout).reshape(-1)
-    grad = np.concatenate([dws[0].reshape(-1), dws[1].reshape(-1), g_table]).astype(F32)
+    grad = np.concatenate([dws[0].reshape(-1), dws[1].reshape(-1), g_table])
+    if allreduce is not None:
+        grad = allreduce(grad)
+    grad = grad.astype(F32)
     field.adam_step += 1
     ooptim.adam_step(field.params, grad, field.m, field.v, field.adam_step, lr)
     if global_step % n_iters_acc == 0:
