@@ -14,7 +14,7 @@
 namespace lnr {
 
 template <class PosFn, bool COUNT>
-__global__ void __launch_bounds__(256) k_hashgrid_fwd(GridArgs a, PosFn pos, int64_t n, const uint32_t* __restrict__ table,
+__global__ void __launch_bounds__(1024) k_hashgrid_fwd(GridArgs a, PosFn pos, int64_t n, const uint32_t* __restrict__ table,
                                                       uint32_t* __restrict__ enc, int64_t stride, BwdWorkspace ws) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t l = blockIdx.y;
@@ -162,12 +162,24 @@ template <class PosFn>
 static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16_t* table, uint32_t* enc,
                       int64_t enc_stride, void* bwd_ws, int64_t bwd_ws_bytes, hipStream_t st, const char* who) {
   GridArgs a = make_args(d);
+  LNR_REQUIRE(n < (int64_t(1) << 31), "%s: n=%lld samples exceeds 2^31", who, (long long)n);
   dim3 grid((unsigned)((n + 255) / 256), d->n_levels);
   if (bwd_ws) {
     LNR_REQUIRE(bwd_ws_bytes >= bwd_workspace_bytes(d, n), "%s: backward workspace too small", who);
     LNR_REQUIRE(a.n_buckets <= (uint32_t)kMaxBuckets, "%s: too many table chunks (%u)", who, a.n_buckets);
+    for (uint32_t l = 0; l < d->n_levels; ++l)
+      LNR_REQUIRE(a.bucket_base[l + 1] - a.bucket_base[l] <= (uint32_t)kMaxChunksPerLevel,
+                  "%s: level %u has more than %d table chunks", who, l, kMaxChunksPerLevel);
     BwdWorkspace w = carve_workspace(bwd_ws, a, d, n);
-    hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, true>), grid, dim3(256), 0, st, a, pos, n,
+    int64_t off, bytes;
+    chunk_sum_range(d, n, &off, &bytes);
+    if (hipMemsetAsync(reinterpret_cast<char*>(bwd_ws) + off, 0, bytes, st) != hipSuccess) {
+      set_error("%s: hipMemsetAsync failed", who);
+      return LNR_ERR_HIP;
+    }
+    // one workgroup per histogram row (kSB samples) so the row is written whole
+    dim3 gridc((unsigned)w.n_sb, d->n_levels);
+    hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, true>), gridc, dim3(kSB), 0, st, a, pos, n,
                        reinterpret_cast<const uint32_t*>(table), enc, enc_stride, w);
   } else {
     hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, false>), grid, dim3(256), 0, st, a, pos, n,

@@ -94,7 +94,7 @@ struct PosFromRays {
   const float* zs;
   int32_t n_samples;
   __device__ __forceinline__ void operator()(int64_t n, float& x, float& y, float& z) const {
-    const int64_t r = n / n_samples;
+    const uint32_t r = (uint32_t)n / (uint32_t)n_samples;  // N < 2^31 (checked at the C ABI)
     const float* ry = rays + 13 * r;
     const float t = zs[n];
     x = (ry[0] + ry[3] * t + 1.0f) * 0.5f;
@@ -190,9 +190,16 @@ __device__ __forceinline__ uint32_t wave_bucket_rank(uint32_t* hist, uint32_t bu
 }
 
 // Backward workspace (device), carved from one caller-provided buffer.
+// Records are binned per "super-block" of kSB consecutive samples (one histogram row per
+// (level, super-block), one scatter workgroup per row): rows are written and read coalesced, and
+// each block's run of records in a bucket averages kSB * 8 / buckets-per-level entries.
+constexpr int kSB = 1024;           // samples per histogram row / count / scatter workgroup
+constexpr int kRowsPerChunk = 256;  // histogram rows per scan chunk
+
 struct BwdWorkspace {
-  uint32_t* hist;        // [n_buckets][n_bx] records per (bucket, 256-sample block) -> exclusive offsets
-  float* blockmax;       // [n_levels][n_bx] max |record value| per block
+  uint32_t* hist;        // per level l: [n_sb][nb_l] record counts -> exclusive offsets within bucket
+  uint32_t* chunk_sum;   // [L][n_chunks][kMaxChunksPerLevel] per-chunk column sums (zeroed by the producer)
+  float* blockmax;       // [L][n_sb] max |record value| per row
   float* level_max;      // [LNR_MAX_LEVELS]
   uint32_t* counts;      // [kMaxBuckets]
   uint64_t* seg_start;   // [kMaxBuckets + 1]
@@ -200,8 +207,12 @@ struct BwdWorkspace {
   uint32_t* part_pre;    // [kMaxBuckets + 1] partial-chunk prefix (multi-slice buckets only)
   long long* partial;    // [max_partials][2 * kChunk] int64 fixed-point partial sums of split buckets
   uint64_t* records;     // [8 * N * L] {idx in chunk (13b), g0 (fp25), g1 (fp25)}
-  int64_t n_bx;
+  int64_t n_sb;
+  int64_t n_chunks;
 };
+
+inline int64_t bwd_n_sb(int64_t n) { return (n + kSB - 1) / kSB; }
+inline int64_t bwd_n_chunks(int64_t n) { return (bwd_n_sb(n) + kRowsPerChunk - 1) / kRowsPerChunk; }
 
 // Upper bound on the partial chunks: a split bucket holds c > kSliceRecords records in
 // ceil(c / kSliceRecords) <= 2c / kSliceRecords slices, and sum(c) <= 8 N L.
@@ -209,53 +220,67 @@ inline int64_t bwd_max_partials(const lnr_grid_desc* d, int64_t n) {
   return 2 * (8 * n * (int64_t)d->n_levels) / kSliceRecords + 1;
 }
 
-inline int64_t bwd_n_bx(int64_t n) { return (n + 255) / 256; }
-
 inline int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
 
-inline int64_t bwd_workspace_bytes(const lnr_grid_desc* d, int64_t n) {
-  GridArgs a = make_args(d);
-  const int64_t nbx = bwd_n_bx(n);
-  int64_t b = 0;
-  b += align256((int64_t)a.n_buckets * nbx * 4);
-  b += align256((int64_t)d->n_levels * nbx * 4);
-  b += align256(LNR_MAX_LEVELS * 4);
-  b += align256(kMaxBuckets * 4);
-  b += align256((kMaxBuckets + 1) * 8);
-  b += align256((kMaxBuckets + 1) * 4);
-  b += align256((kMaxBuckets + 1) * 4);
-  b += align256(bwd_max_partials(d, n) * 2 * kChunk * 8);
-  b += align256(8 * n * (int64_t)d->n_levels * 8);
-  return b;
-}
+struct WsLayout {
+  int64_t hist, chunk_sum, blockmax, level_max, counts, seg_start, slice_pre, part_pre, partial, records, total;
+};
 
-inline BwdWorkspace carve_workspace(void* base, const GridArgs& a, const lnr_grid_desc* d, int64_t n) {
-  BwdWorkspace w{};
-  char* p = reinterpret_cast<char*>(base);
-  w.n_bx = bwd_n_bx(n);
-  w.hist = reinterpret_cast<uint32_t*>(p);
-  p += align256((int64_t)a.n_buckets * w.n_bx * 4);
-  w.blockmax = reinterpret_cast<float*>(p);
-  p += align256((int64_t)a.n_levels * w.n_bx * 4);
-  w.level_max = reinterpret_cast<float*>(p);
-  p += align256(LNR_MAX_LEVELS * 4);
-  w.counts = reinterpret_cast<uint32_t*>(p);
-  p += align256(kMaxBuckets * 4);
-  w.seg_start = reinterpret_cast<uint64_t*>(p);
-  p += align256((kMaxBuckets + 1) * 8);
-  w.slice_pre = reinterpret_cast<uint32_t*>(p);
-  p += align256((kMaxBuckets + 1) * 4);
-  w.part_pre = reinterpret_cast<uint32_t*>(p);
-  p += align256((kMaxBuckets + 1) * 4);
-  w.partial = reinterpret_cast<long long*>(p);
-  p += align256(bwd_max_partials(d, n) * 2 * kChunk * 8);
-  w.records = reinterpret_cast<uint64_t*>(p);
+inline WsLayout ws_layout(const lnr_grid_desc* d, const GridArgs& a, int64_t n) {
+  const int64_t nsb = bwd_n_sb(n), nch = bwd_n_chunks(n);
+  WsLayout w{};
+  int64_t b = 0;
+  w.hist = b;      b += align256((int64_t)a.n_buckets * nsb * 4);
+  w.chunk_sum = b; b += align256((int64_t)d->n_levels * nch * kMaxChunksPerLevel * 4);
+  w.blockmax = b;  b += align256((int64_t)d->n_levels * nsb * 4);
+  w.level_max = b; b += align256(LNR_MAX_LEVELS * 4);
+  w.counts = b;    b += align256(kMaxBuckets * 4);
+  w.seg_start = b; b += align256((kMaxBuckets + 1) * 8);
+  w.slice_pre = b; b += align256((kMaxBuckets + 1) * 4);
+  w.part_pre = b;  b += align256((kMaxBuckets + 1) * 4);
+  w.partial = b;   b += align256(bwd_max_partials(d, n) * 2 * kChunk * 8);
+  w.records = b;   b += align256(8 * n * (int64_t)d->n_levels * 8);
+  w.total = b;
   return w;
 }
 
-// Per-(block, level) record histogram, written as column bx of the bucket-major hist array.
+inline int64_t bwd_workspace_bytes(const lnr_grid_desc* d, int64_t n) { return ws_layout(d, make_args(d), n).total; }
+
+inline BwdWorkspace carve_workspace(void* base, const GridArgs& a, const lnr_grid_desc* d, int64_t n) {
+  const WsLayout L = ws_layout(d, a, n);
+  char* p = reinterpret_cast<char*>(base);
+  BwdWorkspace w{};
+  w.hist = reinterpret_cast<uint32_t*>(p + L.hist);
+  w.chunk_sum = reinterpret_cast<uint32_t*>(p + L.chunk_sum);
+  w.blockmax = reinterpret_cast<float*>(p + L.blockmax);
+  w.level_max = reinterpret_cast<float*>(p + L.level_max);
+  w.counts = reinterpret_cast<uint32_t*>(p + L.counts);
+  w.seg_start = reinterpret_cast<uint64_t*>(p + L.seg_start);
+  w.slice_pre = reinterpret_cast<uint32_t*>(p + L.slice_pre);
+  w.part_pre = reinterpret_cast<uint32_t*>(p + L.part_pre);
+  w.partial = reinterpret_cast<long long*>(p + L.partial);
+  w.records = reinterpret_cast<uint64_t*>(p + L.records);
+  w.n_sb = bwd_n_sb(n);
+  w.n_chunks = bwd_n_chunks(n);
+  return w;
+}
+
+// Byte range of the chunk sums, which the counting producer accumulates into (zero it first).
+inline void chunk_sum_range(const lnr_grid_desc* d, int64_t n, int64_t* off, int64_t* bytes) {
+  const WsLayout L = ws_layout(d, make_args(d), n);
+  *off = L.chunk_sum;
+  *bytes = L.blockmax - L.chunk_sum;
+}
+
+__device__ __forceinline__ uint32_t* hist_row(const GridArgs& a, const BwdWorkspace& ws, uint32_t l, int64_t sb) {
+  const uint32_t nb = a.bucket_base[l + 1] - a.bucket_base[l];
+  return ws.hist + (int64_t)a.bucket_base[l] * ws.n_sb + sb * nb;
+}
+
+// Per-(super-block, level) record histogram: one kSB-thread workgroup, one sample per thread.
 // Shared by the forward (training mode) and the standalone count kernel: identical corners and
-// identical merge decisions as the scatter kernel, so counts and ranks agree exactly.
+// identical merge decisions as the scatter kernel, so counts and ranks agree exactly.  Writes the
+// histogram row and adds it into the row's scan-chunk sums.
 __device__ __forceinline__ void count_block_records(const GridArgs& a, uint32_t l, const Corners& c, bool in,
                                                     uint32_t* hist, const BwdWorkspace& ws) {
   const uint32_t nb = a.bucket_base[l + 1] - a.bucket_base[l];
@@ -271,8 +296,14 @@ __device__ __forceinline__ void count_block_records(const GridArgs& a, uint32_t 
     (void)wave_bucket_rank(hist, valid ? (idx - a.lv[l].offset) >> kChunkLog2 : 0u, valid, coherent);
   }
   __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x)
-    ws.hist[(int64_t)(a.bucket_base[l] + b) * ws.n_bx + blockIdx.x] = hist[b];
+  const int64_t sb = blockIdx.x;
+  uint32_t* row = hist_row(a, ws, l, sb);
+  uint32_t* cs = ws.chunk_sum + ((int64_t)l * ws.n_chunks + sb / kRowsPerChunk) * kMaxChunksPerLevel;
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
+    const uint32_t v = hist[b];
+    row[b] = v;
+    if (v) atomicAdd(&cs[b], v);
+  }
 }
 
 }  // namespace lnr

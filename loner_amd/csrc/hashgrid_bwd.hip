@@ -25,10 +25,10 @@ __device__ __forceinline__ uint32_t f32_to_f25(float f) {
 __device__ __forceinline__ float f25_to_f32(uint32_t v) { return __uint_as_float(v << 7); }
 
 template <class PosFn>
-__global__ void __launch_bounds__(256) k_bwd_count(GridArgs a, PosFn pos, int64_t n, BwdWorkspace ws) {
+__global__ void __launch_bounds__(kSB) k_bwd_count(GridArgs a, PosFn pos, int64_t n, BwdWorkspace ws) {
   __shared__ uint32_t hist[kMaxChunksPerLevel];
   const uint32_t l = blockIdx.y;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * kSB + threadIdx.x;
   const bool in = i < n;
   for (int b = threadIdx.x; b < kMaxChunksPerLevel; b += blockDim.x) hist[b] = 0;
   __syncthreads();
@@ -39,83 +39,123 @@ __global__ void __launch_bounds__(256) k_bwd_count(GridArgs a, PosFn pos, int64_
   count_block_records(a, l, c, in, hist, ws);
 }
 
-// Exclusive scan of one bucket's column (over blocks); total -> counts[bucket].
-__global__ void __launch_bounds__(1024) k_bwd_scan_columns(BwdWorkspace ws) {
-  __shared__ uint32_t wsum[16];
-  const uint32_t b = blockIdx.x;
-  uint32_t* col = ws.hist + (int64_t)b * ws.n_bx;
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  uint32_t carry = 0;
-  for (int64_t base = 0; base < ws.n_bx; base += 1024) {
-    const int64_t j = base + t;
-    const uint32_t v = j < ws.n_bx ? col[j] : 0u;
-    uint32_t inc = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t q = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += q;
-    }
-    if (lane == 63) wsum[wid] = inc;
-    __syncthreads();
-    uint32_t pre = 0, tot = 0;
-    for (int w = 0; w < 16; ++w) {
-      if (w < wid) pre += wsum[w];
-      tot += wsum[w];
-    }
-    if (j < ws.n_bx) col[j] = carry + pre + inc - v;
-    carry += tot;
-    __syncthreads();
+// Exclusive prefix of every bucket column over the histogram rows of one scan chunk, offset by
+// the preceding chunks' sums; chunk 0 also writes the bucket totals.  One thread per column,
+// rows read whole (coalesced); grid (n_chunks, L).
+__global__ void __launch_bounds__(kMaxChunksPerLevel) k_bwd_scan_rows(GridArgs a, BwdWorkspace ws) {
+  const uint32_t l = blockIdx.y, ch = blockIdx.x, c = threadIdx.x;
+  const uint32_t nb = a.bucket_base[l + 1] - a.bucket_base[l];
+  if (c >= nb) return;
+  const uint32_t* cs = ws.chunk_sum + (int64_t)l * ws.n_chunks * kMaxChunksPerLevel + c;
+  uint32_t base = 0;
+  for (uint32_t k = 0; k < ch; ++k) base += cs[(int64_t)k * kMaxChunksPerLevel];
+  if (ch == 0) {
+    uint32_t tot = 0;
+    for (int64_t k = 0; k < ws.n_chunks; ++k) tot += cs[k * kMaxChunksPerLevel];
+    ws.counts[a.bucket_base[l] + c] = tot;
   }
-  if (t == 0) ws.counts[b] = carry;
+  uint32_t* col = ws.hist + (int64_t)a.bucket_base[l] * ws.n_sb + c;
+  const int64_t r0 = (int64_t)ch * kRowsPerChunk;
+  const int64_t r1 = r0 + kRowsPerChunk < ws.n_sb ? r0 + kRowsPerChunk : ws.n_sb;
+  for (int64_t r = r0; r < r1; r += 16) {  // 16 row loads in flight
+    uint32_t v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = r + u < r1 ? col[(r + u) * nb] : 0u;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (r + u < r1) col[(r + u) * nb] = base;
+      base += v[u];
+    }
+  }
 }
 
+// Bucket segment starts, work-item (slice) prefix and split-bucket partial prefix.
 __global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint32_t n_buckets) {
-  __shared__ uint64_t s_seg[kMaxBuckets + 1];
-  __shared__ uint32_t s_sl[kMaxBuckets + 1];
-  __shared__ uint32_t s_pp[kMaxBuckets + 1];
-  if (threadIdx.x == 0) {
-    uint64_t acc = 0;
-    uint32_t sl = 0, pp = 0;
-    for (uint32_t b = 0; b < n_buckets; ++b) {
-      s_seg[b] = acc;
-      s_sl[b] = sl;
-      s_pp[b] = pp;
-      const uint32_t c = ws.counts[b];
-      acc += c;
-      const uint32_t k = (uint32_t)((c + kSliceRecords - 1) / kSliceRecords);
-      sl += k > 0 ? k : 1;
-      pp += k > 1 ? k : 0;
+  __shared__ uint64_t w_seg[16];
+  __shared__ uint32_t w_sl[16], w_pp[16];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  // two buckets per thread (n_buckets <= kMaxBuckets = 2048)
+  uint64_t seg[2];
+  uint32_t sl[2], pp[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const uint32_t b = 2 * t + q;
+    const uint32_t c = b < n_buckets ? ws.counts[b] : 0u;
+    const uint32_t k = (uint32_t)((c + kSliceRecords - 1) / kSliceRecords);
+    seg[q] = c;
+    sl[q] = b < n_buckets ? (k > 0 ? k : 1) : 0u;
+    pp[q] = b < n_buckets && k > 1 ? k : 0u;
+  }
+  uint64_t iseg = seg[0] + seg[1];
+  uint32_t isl = sl[0] + sl[1], ipp = pp[0] + pp[1];
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t a0 = __shfl_up(iseg, o, 64);
+    const uint32_t a1 = __shfl_up(isl, o, 64), a2 = __shfl_up(ipp, o, 64);
+    if (lane >= o) {
+      iseg += a0;
+      isl += a1;
+      ipp += a2;
     }
-    s_seg[n_buckets] = acc;
-    s_sl[n_buckets] = sl;
-    s_pp[n_buckets] = pp;
+  }
+  if (lane == 63) {
+    w_seg[wid] = iseg;
+    w_sl[wid] = isl;
+    w_pp[wid] = ipp;
   }
   __syncthreads();
-  for (uint32_t b = threadIdx.x; b <= n_buckets; b += blockDim.x) {
-    ws.seg_start[b] = s_seg[b];
-    ws.slice_pre[b] = s_sl[b];
-    ws.part_pre[b] = s_pp[b];
+  uint64_t bseg = 0;
+  uint32_t bsl = 0, bpp = 0;
+  for (int w = 0; w < wid; ++w) {
+    bseg += w_seg[w];
+    bsl += w_sl[w];
+    bpp += w_pp[w];
+  }
+  // exclusive values at this thread's first bucket
+  uint64_t e_seg = bseg + iseg - seg[0] - seg[1];
+  uint32_t e_sl = bsl + isl - sl[0] - sl[1], e_pp = bpp + ipp - pp[0] - pp[1];
+  if (t == 1023) {  // totals (n_buckets may equal 2 * blockDim)
+    ws.seg_start[n_buckets] = bseg + iseg;
+    ws.slice_pre[n_buckets] = bsl + isl;
+    ws.part_pre[n_buckets] = bpp + ipp;
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const uint32_t b = 2 * t + q;
+    if (b < n_buckets) {
+      ws.seg_start[b] = e_seg;
+      ws.slice_pre[b] = e_sl;
+      ws.part_pre[b] = e_pp;
+    }
+    e_seg += seg[q];
+    e_sl += sl[q];
+    e_pp += pp[q];
   }
 }
 
+// One workgroup per (histogram row, level): kSB samples, 8 records each, staged in LDS in bucket
+// order and written as one contiguous run per bucket.
 template <class PosFn>
-__global__ void __launch_bounds__(256) k_bwd_scatter(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ d_enc,
+__global__ void __launch_bounds__(kSB) k_bwd_scatter(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ d_enc,
                                                      int64_t stride, BwdWorkspace ws) {
-  __shared__ uint32_t hist[kMaxChunksPerLevel];
-  __shared__ uint32_t start[kMaxChunksPerLevel + 1];
-  __shared__ uint64_t gbase[kMaxChunksPerLevel];
-  __shared__ uint64_t stage[8 * 256];
-  __shared__ uint8_t sb[8 * 256];
-  __shared__ float wmax[4];
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint64_t* stage = reinterpret_cast<uint64_t*>(smem);                // [8 * kSB]
+  uint64_t* gbase = stage + 8 * kSB;                                  // [kMaxChunksPerLevel]
+  uint32_t* hist = reinterpret_cast<uint32_t*>(gbase + kMaxChunksPerLevel);  // [kMaxChunksPerLevel]
+  uint32_t* start = hist + kMaxChunksPerLevel;                        // [kMaxChunksPerLevel + 1]
+  float* wmax = reinterpret_cast<float*>(start + kMaxChunksPerLevel + 1);    // [kSB / 64]
+  uint8_t* sbk = reinterpret_cast<uint8_t*>(wmax + kSB / 64);         // [8 * kSB]
   const uint32_t l = blockIdx.y;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t sb = blockIdx.x;
+  const int64_t i = sb * kSB + threadIdx.x;
   const bool in = i < n;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t b0 = a.bucket_base[l];
   const uint32_t nb = a.bucket_base[l + 1] - b0;
-  for (uint32_t b = threadIdx.x; b < kMaxChunksPerLevel; b += 256) {
+  const uint32_t* row = hist_row(a, ws, l, sb);
+  for (uint32_t b = threadIdx.x; b < kMaxChunksPerLevel; b += kSB) {
     hist[b] = 0;
-    if (b < nb) gbase[b] = ws.seg_start[b0 + b] + ws.hist[(int64_t)(b0 + b) * ws.n_bx + blockIdx.x];
+    if (b < nb) gbase[b] = ws.seg_start[b0 + b] + row[b];
   }
   __syncthreads();
   float x = 0.f, y = 0.f, z = 0.f;
@@ -151,14 +191,21 @@ __global__ void __launch_bounds__(256) k_bwd_scatter(GridArgs a, PosFn pos, int6
   m = wave_max(m);
   if (lane == 0) wmax[wid] = m;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t acc = 0;
-    for (uint32_t b = 0; b < nb; ++b) {
-      start[b] = acc;
-      acc += hist[b];
+  if (wid == 0) {  // exclusive prefix of the (<= 128) bucket counts: 2 per lane + a wave scan
+    const uint32_t c0 = 2 * lane < nb ? hist[2 * lane] : 0u;
+    const uint32_t c1 = 2 * lane + 1 < nb ? hist[2 * lane + 1] : 0u;
+    uint32_t inc = c0 + c1;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t q = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += q;
     }
-    start[nb] = acc;
-    ws.blockmax[(int64_t)l * ws.n_bx + blockIdx.x] = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+    const uint32_t ex = inc - c0 - c1;
+    if (2 * lane <= nb) start[2 * lane] = ex;
+    if (2 * lane + 1 <= nb) start[2 * lane + 1] = ex + c0;
+    float mm = lane < kSB / 64 ? wmax[lane] : 0.f;
+    mm = wave_max(mm);
+    if (lane == 0) ws.blockmax[(int64_t)l * ws.n_sb + sb] = mm;
   }
   __syncthreads();
 #pragma unroll
@@ -167,22 +214,25 @@ __global__ void __launch_bounds__(256) k_bwd_scatter(GridArgs a, PosFn pos, int6
       const uint32_t ch = e[k] >> kChunkLog2;
       const uint32_t slot = start[ch] + rank[k];
       stage[slot] = rec[k];
-      sb[slot] = (uint8_t)ch;
+      sbk[slot] = (uint8_t)ch;
     }
   }
   __syncthreads();
   const uint32_t total = start[nb];
-  for (uint32_t t = threadIdx.x; t < total; t += 256) {
-    const uint32_t ch = sb[t];
-    ws.records[gbase[ch] + (t - start[ch])] = stage[t];
+  for (uint32_t t = threadIdx.x; t < total; t += kSB) {
+    const uint32_t ch = sbk[t];
+    __builtin_nontemporal_store(stage[t], &ws.records[gbase[ch] + (t - start[ch])]);  // read once, later
   }
 }
 
+constexpr size_t kScatterLds = 8 * kSB * 8 + kMaxChunksPerLevel * 8 + kMaxChunksPerLevel * 4 +
+                               (kMaxChunksPerLevel + 1) * 4 + (kSB / 64) * 4 + 8 * kSB;
+
 __global__ void __launch_bounds__(256) k_bwd_level_max(BwdWorkspace ws) {
   __shared__ float red[4];
-  const float* col = ws.blockmax + (int64_t)blockIdx.x * ws.n_bx;
+  const float* col = ws.blockmax + (int64_t)blockIdx.x * ws.n_sb;
   float m = 0.f;
-  for (int64_t j = threadIdx.x; j < ws.n_bx; j += 256) m = fmaxf(m, col[j]);
+  for (int64_t j = threadIdx.x; j < ws.n_sb; j += 256) m = fmaxf(m, col[j]);
   m = wave_max(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
@@ -233,7 +283,7 @@ __global__ void __launch_bounds__(512) k_bwd_accum(GridArgs a, BwdWorkspace ws, 
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const uint64_t rr = r + (uint64_t)u * blockDim.x;
-        q[u] = rr < end ? rec[rr] : ~0ull;
+        q[u] = rr < end ? __builtin_nontemporal_load(&rec[rr]) : ~0ull;
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -305,13 +355,31 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
   LNR_REQUIRE(workspace != nullptr && ws_bytes >= bwd_workspace_bytes(d, n),
               "%s: workspace too small (%lld < %lld bytes)", who, (long long)ws_bytes,
               (long long)bwd_workspace_bytes(d, n));
+  LNR_REQUIRE(n < (int64_t(1) << 31), "%s: n=%lld samples exceeds 2^31", who, (long long)n);
   BwdWorkspace w = carve_workspace(workspace, a, d, n);
-  dim3 grid((unsigned)w.n_bx, d->n_levels);
-  if (!(flags & LNR_BWD_COUNTS_READY)) hipLaunchKernelGGL(k_bwd_count<PosFn>, grid, dim3(256), 0, st, a, pos, n, w);
-  hipLaunchKernelGGL(k_bwd_scan_columns, dim3(a.n_buckets), dim3(1024), 0, st, w);
+  static bool lds_attr = false;  // scatter stages 8 records per sample of its row in LDS (> 64 KB)
+  if (!lds_attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bwd_scatter<PosFn>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScatterLds) != hipSuccess) {
+      set_error("%s: cannot raise the scatter kernel's LDS limit to %zu bytes", who, kScatterLds);
+      return LNR_ERR_HIP;
+    }
+    lds_attr = true;
+  }
+  dim3 grid((unsigned)w.n_sb, d->n_levels);
+  if (!(flags & LNR_BWD_COUNTS_READY)) {
+    int64_t off, bytes;
+    chunk_sum_range(d, n, &off, &bytes);
+    if (hipMemsetAsync(reinterpret_cast<char*>(workspace) + off, 0, bytes, st) != hipSuccess) {
+      set_error("%s: hipMemsetAsync failed", who);
+      return LNR_ERR_HIP;
+    }
+    hipLaunchKernelGGL(k_bwd_count<PosFn>, grid, dim3(kSB), 0, st, a, pos, n, w);
+  }
+  hipLaunchKernelGGL(k_bwd_scan_rows, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
   hipLaunchKernelGGL(k_bwd_scan_buckets, dim3(1), dim3(1024), 0, st, w, a.n_buckets);
-  hipLaunchKernelGGL(k_bwd_scatter<PosFn>, grid, dim3(256), 0, st, a, pos, n, reinterpret_cast<const float2*>(d_enc),
-                     stride, w);
+  hipLaunchKernelGGL(k_bwd_scatter<PosFn>, grid, dim3(kSB), kScatterLds, st, a, pos, n,
+                     reinterpret_cast<const float2*>(d_enc), stride, w);
   hipLaunchKernelGGL(k_bwd_level_max, dim3(d->n_levels), dim3(256), 0, st, w);
   const int64_t max_slices = a.n_buckets + (8 * n * (int64_t)d->n_levels) / kSliceRecords + 1;
   const unsigned g = (unsigned)(max_slices < 4096 ? max_slices : 4096);
