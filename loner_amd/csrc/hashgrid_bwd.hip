@@ -239,7 +239,10 @@ __global__ void __launch_bounds__(256) k_bwd_level_max(BwdWorkspace ws) {
   if (threadIdx.x == 0) ws.level_max[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
-__global__ void __launch_bounds__(512) k_bwd_accum(GridArgs a, BwdWorkspace ws, float* __restrict__ d_table) {
+constexpr int kAccumThreads = 1024;
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
+__global__ void __launch_bounds__(kAccumThreads) k_bwd_accum(GridArgs a, BwdWorkspace ws, float* __restrict__ d_table) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [kChunk][2] int64 fixed point
   const uint32_t nbk = a.n_buckets;
@@ -276,21 +279,29 @@ __global__ void __launch_bounds__(512) k_bwd_accum(GridArgs a, BwdWorkspace ws, 
     for (int t = threadIdx.x; t < 2 * kChunk; t += blockDim.x) acc[t] = 0ull;
     __syncthreads();
     const bool coherent = l < a.merge_levels;
+#ifdef LNR_EXP_NO_LDS_ATOMICS
+    long long dummy = 0;
+#endif
     const uint64_t* rec = ws.records;
-    for (uint64_t rb = beg + (threadIdx.x & ~63u); rb < end; rb += 4 * blockDim.x) {  // wave-uniform trips
-      const uint64_t r = rb + lane;
-      uint64_t q[4];
+    // 16-B loads (2 records per lane), 4 in flight: 8 KB per wave trip; a lane's two records are
+    // handled as two lane-ordered streams (merging of equal entries is an optimisation only)
+    const uint64_t beg2 = beg & ~1ull;
+    for (uint64_t rb = beg2 + 2 * (threadIdx.x & ~63u); rb < end; rb += 8 * kAccumThreads) {  // wave-uniform
+      u64x2 q[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const uint64_t rr = r + (uint64_t)u * blockDim.x;
-        q[u] = rr < end ? __builtin_nontemporal_load(&rec[rr]) : ~0ull;
+        const uint64_t rr = rb + 2 * lane + (uint64_t)u * 2 * kAccumThreads;
+        q[u] = rr < end ? __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(&rec[rr])) : u64x2{~0ull, ~0ull};
+        if (rr < beg) q[u].x = ~0ull;
+        if (rr + 1 >= end) q[u].y = ~0ull;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const bool ok = q[u] != ~0ull;
-        const uint32_t ee = ok ? (uint32_t)(q[u] & (kChunk - 1)) : 0xFFFFFFFFu;
-        const float v0 = ok ? f25_to_f32((uint32_t)(q[u] >> 13) & 0x1FFFFFFu) : 0.f;
-        const float v1 = ok ? f25_to_f32((uint32_t)(q[u] >> 38) & 0x1FFFFFFu) : 0.f;
+      for (int u = 0; u < 8; ++u) {
+        const uint64_t v = (u & 1) ? q[u >> 1].y : q[u >> 1].x;
+        const bool ok = v != ~0ull;
+        const uint32_t ee = ok ? (uint32_t)(v & (kChunk - 1)) : 0xFFFFFFFFu;
+        const float v0 = ok ? f25_to_f32((uint32_t)(v >> 13) & 0x1FFFFFFu) : 0.f;
+        const float v1 = ok ? f25_to_f32((uint32_t)(v >> 38) & 0x1FFFFFFu) : 0.f;
         long long i0 = __float2ll_rn(v0 * scale), i1 = __float2ll_rn(v1 * scale);
         bool emit = ok;
         if (coherent) {  // records of coherent levels arrive in runs of equal entries; merged in
@@ -298,12 +309,19 @@ __global__ void __launch_bounds__(512) k_bwd_accum(GridArgs a, BwdWorkspace ws, 
           run_sum_i64(ri, i0, i1);
           emit = ok && ri.tail;
         }
+#ifdef LNR_EXP_NO_LDS_ATOMICS
+        if (emit) dummy += i0 + i1 + ee;
+#else
         if (emit) {
           atomicAdd(&acc[2 * ee + 0], (unsigned long long)i0);
           atomicAdd(&acc[2 * ee + 1], (unsigned long long)i1);
         }
+#endif
       }
     }
+#ifdef LNR_EXP_NO_LDS_ATOMICS
+    if (dummy == 0x123456789LL) acc[threadIdx.x] = dummy;
+#endif
     __syncthreads();
     if (nsl == 1) {  // the final values
       const float inv = ldexpf(1.f, -k2);
@@ -383,7 +401,7 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
   hipLaunchKernelGGL(k_bwd_level_max, dim3(d->n_levels), dim3(256), 0, st, w);
   const int64_t max_slices = a.n_buckets + (8 * n * (int64_t)d->n_levels) / kSliceRecords + 1;
   const unsigned g = (unsigned)(max_slices < 4096 ? max_slices : 4096);
-  hipLaunchKernelGGL(k_bwd_accum, dim3(g), dim3(512), 2 * kChunk * sizeof(unsigned long long), st, a, w, d_table);
+  hipLaunchKernelGGL(k_bwd_accum, dim3(g), dim3(kAccumThreads), 2 * kChunk * sizeof(unsigned long long), st, a, w, d_table);
   hipLaunchKernelGGL(k_bwd_finalize, dim3(a.n_buckets), dim3(256), 0, st, a, w, d_table);
   LNR_RETURN_LAUNCH(who);
 }
