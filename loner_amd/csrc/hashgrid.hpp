@@ -239,7 +239,7 @@ inline WsLayout ws_layout(const lnr_grid_desc* d, const GridArgs& a, int64_t n) 
   w.slice_pre = b; b += align256((kMaxBuckets + 1) * 4);
   w.part_pre = b;  b += align256((kMaxBuckets + 1) * 4);
   w.partial = b;   b += align256(bwd_max_partials(d, n) * 2 * kChunk * 8);
-  w.records = b;   b += align256(8 * n * (int64_t)d->n_levels * 8);
+  w.records = b;   b += align256(8 * n * (int64_t)d->n_levels * 8 + 16);  // +16: the accumulate's paired loads
   w.total = b;
   return w;
 }

@@ -203,6 +203,7 @@ __global__ void __launch_bounds__(kSB) k_bwd_scatter(GridArgs a, PosFn pos, int6
     const uint32_t ex = inc - c0 - c1;
     if (2 * lane <= nb) start[2 * lane] = ex;
     if (2 * lane + 1 <= nb) start[2 * lane + 1] = ex + c0;
+    if (lane == 63) start[nb] = inc;  // the total (nb = 128 has no lane whose pair reaches it)
     float mm = lane < kSB / 64 ? wmax[lane] : 0.f;
     mm = wave_max(mm);
     if (lane == 0) ws.blockmax[(int64_t)l * ws.n_sb + sb] = mm;
@@ -213,12 +214,14 @@ __global__ void __launch_bounds__(kSB) k_bwd_scatter(GridArgs a, PosFn pos, int6
     if (valid[k]) {
       const uint32_t ch = e[k] >> kChunkLog2;
       const uint32_t slot = start[ch] + rank[k];
-      stage[slot] = rec[k];
-      sbk[slot] = (uint8_t)ch;
+      if (slot < 8 * kSB) {  // always true when counts and ranks agree; guards the LDS stage
+        stage[slot] = rec[k];
+        sbk[slot] = (uint8_t)ch;
+      }
     }
   }
   __syncthreads();
-  const uint32_t total = start[nb];
+  const uint32_t total = start[nb] < 8u * kSB ? start[nb] : 8u * kSB;
   for (uint32_t t = threadIdx.x; t < total; t += kSB) {
     const uint32_t ch = sbk[t];
     __builtin_nontemporal_store(stage[t], &ws.records[gbase[ch] + (t - start[ch])]);  // read once, later
