@@ -13,6 +13,8 @@ import os
 import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libloner_amd.so")
+# Kernel experiments load an alternative in-tree build (tools/exp_variants.py); unset in production.
+LIB_PATH = os.environ.get("LONER_AMD_LIB", LIB_PATH)
 MAX_LEVELS = 32
 RAY_STATS = 5
 SIGMA_MLP_PARAMS = 64 * 32 + 16 * 64

@@ -34,39 +34,44 @@ def _deps():
     return sorted(glob.glob(os.path.join(CSRC, "*.hpp")) + [os.path.join(ROOT, "include", "loner_amd.h")])
 
 
-def _compile(src):
-    obj = os.path.join(OBJDIR, os.path.basename(src).replace(".hip", ".o"))
+def _compile(src, objdir=OBJDIR, extra=()):
+    obj = os.path.join(objdir, os.path.basename(src).replace(".hip", ".o"))
     newest_dep = max(os.path.getmtime(p) for p in _deps() + [src])
     if os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
         return obj, ""
-    cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
+    cmd = [HIPCC, *FLAGS, *extra, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
     return obj, r.stderr
 
 
-def build(jobs=8, force=False, verbose=False):
-    os.makedirs(OBJDIR, exist_ok=True)
-    os.makedirs(LIBDIR, exist_ok=True)
+def build(jobs=8, force=False, verbose=False, defines=(), out=None):
+    """Build the library.  ``defines``/``out``: an experiment variant (-D flags) linked to ``out``
+    with its own object directory (tools/exp_variants.py); the default build has neither."""
+    lib_path = out or LIB
+    objdir = OBJDIR if not defines else os.path.join(ROOT, "build", "obj_" + "_".join(sorted(defines)).lower())
+    extra = [f"-D{d}" for d in defines]
+    os.makedirs(objdir, exist_ok=True)
+    os.makedirs(os.path.dirname(lib_path), exist_ok=True)
     if force:
-        for o in glob.glob(os.path.join(OBJDIR, "*.o")):
+        for o in glob.glob(os.path.join(objdir, "*.o")):
             os.remove(o)
     srcs = _sources()
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        results = list(ex.map(_compile, srcs))
+        results = list(ex.map(lambda s: _compile(s, objdir, extra), srcs))
     objs = [o for o, _ in results]
     if verbose:
         for o, err in results:
             if err.strip():
                 print(f"[{os.path.basename(o)}]\n{err}", file=sys.stderr)
-    if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
-        return LIB
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+    if os.path.exists(lib_path) and os.path.getmtime(lib_path) >= max(os.path.getmtime(o) for o in objs):
+        return lib_path
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib_path, *objs]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
-    return LIB
+    return lib_path
 
 
 def main():

@@ -19,3 +19,4 @@ void set_error(const char* fmt, ...) {
 
 extern "C" const char* lnr_last_error(void) { return lnr::g_err.c_str(); }
 extern "C" int lnr_version(void) { return 1; }
+

@@ -70,6 +70,16 @@ __device__ __forceinline__ float2 half2_to_float2(uint32_t v) {
   return make_float2(h2f((uint16_t)(v & 0xFFFFu)), h2f((uint16_t)(v >> 16)));
 }
 
+// ------------------------------------------------------------------ barriers
+// Workgroup barrier that orders LDS only: waits for this wave's LDS operations (lgkmcnt), not for
+// its global loads and stores (vmcnt), which __syncthreads' full fence would drain.  For barriers
+// that only publish LDS data, so global loads issued before them stay in flight across them.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // ------------------------------------------------------------------ wave / block reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -104,5 +114,33 @@ __device__ __forceinline__ void block_sum(float (&v)[K], float* scratch) {
   }
   __syncthreads();
 }
+
+// ------------------------------------------------------------------ diagnostic phase stamps
+// Experiment builds only (-DLNR_EXP_STAMPS, tools/exp_variants.py): thread 0 of each workgroup adds
+// the s_memtime cycles of phase k to this translation unit's g_phase[k];
+// LNR_PHASE_EXPORT(tu) defines lnr_debug_phases_<tu>() to read and clear them.
+#ifdef LNR_EXP_STAMPS
+static __device__ unsigned long long g_phase[32];
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define LNR_STAMP(var) unsigned long long var = (threadIdx.x == 0) ? ::lnr::stamp() : 0ull
+#define LNR_PHASE(k, t1, t0) \
+  if (threadIdx.x == 0 && (blockIdx.x & 63) == 0) atomicAdd(&::lnr::g_phase[k], (t1) - (t0))  // 1/64 sampled
+#define LNR_PHASE_EXPORT(tu)                                                                      \
+  extern "C" int lnr_debug_phases_##tu(unsigned long long* out32) {                              \
+    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(::lnr::g_phase), 32 * 8) != hipSuccess) return -1; \
+    unsigned long long z[32] = {};                                                                \
+    return hipMemcpyToSymbol(HIP_SYMBOL(::lnr::g_phase), z, sizeof(z)) == hipSuccess ? 0 : -1;    \
+  }
+#else
+#define LNR_STAMP(var)
+#define LNR_PHASE(k, t1, t0)
+#define LNR_PHASE_EXPORT(tu)
+#endif
 
 }  // namespace lnr

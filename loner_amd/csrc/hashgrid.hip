@@ -20,10 +20,42 @@ __global__ void __launch_bounds__(1024) k_hashgrid_fwd(GridArgs a, PosFn pos, in
   const uint32_t l = blockIdx.y;
   const bool in = i < n;
   if (!COUNT && !in) return;
+  __shared__ uint32_t hist[COUNT ? kMaxChunksPerLevel : 1];
+  if (COUNT) {
+    for (int b = threadIdx.x; b < kMaxChunksPerLevel; b += blockDim.x) hist[b] = 0;
+  }
   float x = 0.f, y = 0.f, z = 0.f;
   if (in) pos(i, x, y, z);
+  const LevelParams& lv = a.lv[l];
+  if (lv.fine) {  // block-uniform
+    FineCell c;
+    fine_cell(lv, x, y, z, c);
+    if (in) {
+      const uint32_t* tl = table + lv.offset;
+      uint32_t v[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[2 * j] = tl[c.e[j]];
+        v[2 * j + 1] = tl[c.e[j] ^ c.d];
+      }
+      float f0 = 0.f, f1 = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float w = fine_weight(c, k >> 1, k & 1);
+        const float2 t = half2_to_float2(v[k]);
+        f0 = fmaf(w, t.x, f0);
+        f1 = fmaf(w, t.y, f1);
+      }
+      enc[(int64_t)l * stride + i] = (uint32_t)f2h(f0) | ((uint32_t)f2h(f1) << 16);
+    }
+    if (COUNT) {
+      lds_barrier();
+      count_block_records_fine(a, l, c, in, hist, ws);
+    }
+    return;
+  }
   Corners c;
-  level_corners(a.lv[l], x, y, z, c);
+  level_corners(lv, x, y, z, c);
   if (in) {
     uint32_t v[8];
 #pragma unroll
@@ -38,9 +70,7 @@ __global__ void __launch_bounds__(1024) k_hashgrid_fwd(GridArgs a, PosFn pos, in
     enc[(int64_t)l * stride + i] = (uint32_t)f2h(f0) | ((uint32_t)f2h(f1) << 16);
   }
   if (COUNT) {
-    __shared__ uint32_t hist[kMaxChunksPerLevel];
-    for (int b = threadIdx.x; b < kMaxChunksPerLevel; b += blockDim.x) hist[b] = 0;
-    __syncthreads();
+    lds_barrier();
     count_block_records(a, l, c, in, hist, ws);
   }
 }

@@ -12,6 +12,7 @@ struct LevelParams {
   uint32_t size_mask;  // size - 1 when size is a power of two, else 0
   uint32_t offset;
   uint32_t hashed;     // stride walk exceeded size -> coherent prime hash
+  uint32_t fine;       // hashed, power-of-two size, not coherent: FineCell fast path
 };
 
 // Backward buckets: each level's table slice is cut into chunks of 2^kChunkLog2 entries; one
@@ -66,6 +67,8 @@ inline GridArgs make_args(const lnr_grid_desc* d) {
   a.bucket_base[d->n_levels] = b;
   a.n_buckets = b;
   a.merge_levels = merge_levels_for(d);
+  for (uint32_t l = 0; l < d->n_levels; ++l)
+    a.lv[l].fine = (a.lv[l].hashed && a.lv[l].size_mask && l >= a.merge_levels) ? 1u : 0u;
   return a;
 }
 
@@ -106,6 +109,7 @@ struct PosFromRays {
 struct Corners {
   uint32_t idx[8];
   float w[8];
+  float tx, ty, tz;  // cell fractions (the backward's x-pair records split by tx)
 };
 
 __device__ __forceinline__ void level_corners(const LevelParams& p, float x, float y, float z, Corners& c) {
@@ -114,6 +118,9 @@ __device__ __forceinline__ void level_corners(const LevelParams& p, float x, flo
   float fx = floorf(px), fy = floorf(py), fz = floorf(pz);
   uint32_t cx = (uint32_t)(int)fx, cy = (uint32_t)(int)fy, cz = (uint32_t)(int)fz;
   float tx = px - fx, ty = py - fy, tz = pz - fz;
+  c.tx = tx;
+  c.ty = ty;
+  c.tz = tz;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int bx = k & 1, by = (k >> 1) & 1, bz = (k >> 2) & 1;
@@ -123,6 +130,39 @@ __device__ __forceinline__ void level_corners(const LevelParams& p, float x, flo
     c.w[k] = w;
     c.idx[k] = p.offset + grid_index(p, cx + bx, cy + by, cz + bz);
   }
+}
+
+// Hashed levels with a power-of-two table (every level finer than 256^3 cells when log2 T <= 24).
+// The cell's four y/z edges share the x-neighbour mask: corner 2j+1 = corner 2j ^ d with
+// d = (x ^ (x + 1)) & (size - 1), a mask of the form 2^p - 1.  Entries are relative to the level
+// offset; the y/z prime products are formed once per cell.
+struct FineCell {
+  uint32_t e[4];  // entry of corner 2j (bx = 0, by = j & 1, bz = j >> 1)
+  uint32_t d;     // x-pair mask
+  float tx, ty, tz;
+};
+__device__ __forceinline__ void fine_cell(const LevelParams& p, float x, float y, float z, FineCell& c) {
+  const float px = fmaf(p.scale, x, 0.5f), py = fmaf(p.scale, y, 0.5f), pz = fmaf(p.scale, z, 0.5f);
+  const float fx = floorf(px), fy = floorf(py), fz = floorf(pz);
+  const uint32_t cx = (uint32_t)(int)fx, cy = (uint32_t)(int)fy, cz = (uint32_t)(int)fz;
+  c.tx = px - fx;
+  c.ty = py - fy;
+  c.tz = pz - fz;
+  const uint32_t hy0 = cy * 2654435761u, hy1 = (cy + 1u) * 2654435761u;
+  const uint32_t hz0 = cz * 805459861u, hz1 = (cz + 1u) * 805459861u;
+  const uint32_t m = p.size_mask;
+  c.e[0] = (cx ^ hy0 ^ hz0) & m;
+  c.e[1] = (cx ^ hy1 ^ hz0) & m;
+  c.e[2] = (cx ^ hy0 ^ hz1) & m;
+  c.e[3] = (cx ^ hy1 ^ hz1) & m;
+  c.d = (cx ^ (cx + 1u)) & m;
+}
+// level_corners' weight of corner k = 2j + bx: ((wx * wy) * wz), same rounding
+__device__ __forceinline__ float fine_weight(const FineCell& c, int j, int bx) {
+  float w = bx ? c.tx : 1.0f - c.tx;
+  w *= (j & 1) ? c.ty : 1.0f - c.ty;
+  w *= (j & 2) ? c.tz : 1.0f - c.tz;
+  return w;
 }
 
 // Runs of equal keys across consecutive lanes: head/tail flags and the lane of the run head.
@@ -152,6 +192,46 @@ __device__ __forceinline__ void run_sum(const RunInfo& ri, float& v0, float& v1)
       v1 += q1;
     }
   }
+}
+
+// DPP forms of the above (gfx9 DPP: row_shr within 16-lane rows, row_bcast across rows): VALU
+// data movement instead of ds_bpermute round trips through the LDS unit.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xF, false));
+}
+__device__ __forceinline__ RunInfo lane_runs_dpp(uint32_t key) {
+  const int lane = threadIdx.x & 63;
+  // wave_shr:1 (0x138): lane i reads lane i - 1; lane 0 keeps the "old" operand (~key: a head)
+  const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp((int)~key, (int)key, 0x138, 0xF, 0xF, false);
+  const bool head = (lane == 0) || (prev != key);
+  RunInfo ri;
+  ri.heads = __ballot(head);
+  ri.head_lane = 63 - __clzll(ri.heads & ((2ull << lane) - 1ull));
+  ri.tail = (lane == 63) || ((ri.heads >> (lane + 1)) & 1ull);
+  return ri;
+}
+// Segmented inclusive sum over runs (head_lane per lane): within-row shifts, then row 15 / 31
+// broadcasts, each added only where the run reaches back that far.
+__device__ __forceinline__ void run_sum_dpp(const RunInfo& ri, float& v0, float& v1) {
+  const int lane = threadIdx.x & 63;
+  const int h = ri.head_lane;
+#define LNR_SEG_STEP(CTRL, RMASK, COND)        \
+  {                                           \
+    const float q0 = dpp_f32<CTRL, RMASK>(v0); \
+    const float q1 = dpp_f32<CTRL, RMASK>(v1); \
+    if (COND) {                               \
+      v0 += q0;                               \
+      v1 += q1;                               \
+    }                                         \
+  }
+  LNR_SEG_STEP(0x111, 0xF, lane - 1 >= h)                        // row_shr:1
+  LNR_SEG_STEP(0x112, 0xF, lane - 2 >= h)                        // row_shr:2
+  LNR_SEG_STEP(0x114, 0xF, lane - 4 >= h)                        // row_shr:4
+  LNR_SEG_STEP(0x118, 0xF, lane - 8 >= h)                        // row_shr:8
+  LNR_SEG_STEP(0x142, 0xA, (lane & 16) && h < (lane & ~15))      // row_bcast:15 -> rows 1, 3
+  LNR_SEG_STEP(0x143, 0xC, lane >= 32 && h < 32)                 // row_bcast:31 -> rows 2, 3
+#undef LNR_SEG_STEP
 }
 
 // The same in int64 (exact and associative: the result does not depend on the record order).
@@ -193,7 +273,10 @@ __device__ __forceinline__ uint32_t wave_bucket_rank(uint32_t* hist, uint32_t bu
 // Records are binned per "super-block" of kSB consecutive samples (one histogram row per
 // (level, super-block), one scatter workgroup per row): rows are written and read coalesced, and
 // each block's run of records in a bucket averages kSB * 8 / buckets-per-level entries.
-constexpr int kSB = 1024;           // samples per histogram row / count / scatter workgroup
+#ifndef LNR_KSB
+#define LNR_KSB 512
+#endif
+constexpr int kSB = LNR_KSB;        // samples per histogram row / count / scatter workgroup
 constexpr int kRowsPerChunk = 256;  // histogram rows per scan chunk
 
 struct BwdWorkspace {
@@ -206,7 +289,8 @@ struct BwdWorkspace {
   uint32_t* slice_pre;   // [kMaxBuckets + 1] work-item prefix over buckets
   uint32_t* part_pre;    // [kMaxBuckets + 1] partial-chunk prefix (multi-slice buckets only)
   long long* partial;    // [max_partials][2 * kChunk] int64 fixed-point partial sums of split buckets
-  uint64_t* records;     // [8 * N * L] {idx in chunk (13b), g0 (fp25), g1 (fp25)}
+  uint32_t* rec_w;       // [8 * N * L] record words (see "Backward records")
+  float2* rec_v;         // [8 * N * L] record values
   int64_t n_sb;
   int64_t n_chunks;
 };
@@ -223,7 +307,7 @@ inline int64_t bwd_max_partials(const lnr_grid_desc* d, int64_t n) {
 inline int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
 
 struct WsLayout {
-  int64_t hist, chunk_sum, blockmax, level_max, counts, seg_start, slice_pre, part_pre, partial, records, total;
+  int64_t hist, chunk_sum, blockmax, level_max, counts, seg_start, slice_pre, part_pre, partial, rec_w, rec_v, total;
 };
 
 inline WsLayout ws_layout(const lnr_grid_desc* d, const GridArgs& a, int64_t n) {
@@ -239,7 +323,9 @@ inline WsLayout ws_layout(const lnr_grid_desc* d, const GridArgs& a, int64_t n) 
   w.slice_pre = b; b += align256((kMaxBuckets + 1) * 4);
   w.part_pre = b;  b += align256((kMaxBuckets + 1) * 4);
   w.partial = b;   b += align256(bwd_max_partials(d, n) * 2 * kChunk * 8);
-  w.records = b;   b += align256(8 * n * (int64_t)d->n_levels * 8 + 16);  // +16: the accumulate's paired loads
+  // +2 records: the accumulate loads records in pairs
+  w.rec_w = b;     b += align256((8 * n * (int64_t)d->n_levels + 2) * 4);
+  w.rec_v = b;     b += align256((8 * n * (int64_t)d->n_levels + 2) * 8);
   w.total = b;
   return w;
 }
@@ -259,7 +345,8 @@ inline BwdWorkspace carve_workspace(void* base, const GridArgs& a, const lnr_gri
   w.slice_pre = reinterpret_cast<uint32_t*>(p + L.slice_pre);
   w.part_pre = reinterpret_cast<uint32_t*>(p + L.part_pre);
   w.partial = reinterpret_cast<long long*>(p + L.partial);
-  w.records = reinterpret_cast<uint64_t*>(p + L.records);
+  w.rec_w = reinterpret_cast<uint32_t*>(p + L.rec_w);
+  w.rec_v = reinterpret_cast<float2*>(p + L.rec_v);
   w.n_sb = bwd_n_sb(n);
   w.n_chunks = bwd_n_chunks(n);
   return w;
@@ -277,25 +364,39 @@ __device__ __forceinline__ uint32_t* hist_row(const GridArgs& a, const BwdWorksp
   return ws.hist + (int64_t)a.bucket_base[l] * ws.n_sb + sb * nb;
 }
 
+// Backward records.  12 bytes, stored SoA: a word w = entry within its 4096-entry chunk (bits 0-11)
+// | pair code p (bits 12-15) | tx as unorm16 (bits 16-31), and a float2 of values.
+//   p = 0  one corner; the values are its (g0, g1) contribution (coherent levels: summed over the
+//          run of lanes that share the corner).
+//   p > 0  the two x-adjacent corners e0 and e1 = e0 ^ (2^p - 1) of one y/z edge, in one chunk; the
+//          values are wy*wz*(g0, g1), split (1 - tx, tx) when accumulated.  The x-neighbour of a
+//          hashed corner, (x + 1) ^ h against x ^ h, flips the trailing ones of x and one more bit;
+//          a dense level's neighbour is idx + 1: both are an XOR with 2^p - 1.
+// Slots per (sample, level): coherent levels: slot k = corner k after the lane-run merge.  Other
+// levels: slot j < 4 = the x-pair (2j, 2j+1), or corner 2j when the pair spans two chunks; slot
+// 4 + j = corner 2j+1 of such a split pair.  So fine levels emit 4 records per sample, not 8.
+constexpr uint32_t kRecNone = 0xFFFFFFFFu;  // never a valid word (p <= 12)
+
+__device__ __forceinline__ bool pairable(uint32_t e0, uint32_t e1) {
+  const uint32_t d = e0 ^ e1;
+  return d != 0u && (d >> kChunkLog2) == 0u && (d & (d + 1u)) == 0u;
+}
+__device__ __forceinline__ uint32_t pair_word(uint32_t e0, uint32_t e1, uint32_t txq) {
+  return (e0 & (kChunk - 1)) | ((uint32_t)__popc(e0 ^ e1) << kChunkLog2) | (txq << 16);
+}
+__device__ __forceinline__ uint32_t tx_unorm16(float tx) {
+  const float q = fminf(fmaxf(tx, 0.f), 1.f) * 65535.f + 0.5f;
+  return (uint32_t)q;
+}
+constexpr float kInvU16 = 1.0f / 65535.0f;
+
 // Per-(super-block, level) record histogram: one kSB-thread workgroup, one sample per thread.
-// Shared by the forward (training mode) and the standalone count kernel: identical corners and
-// identical merge decisions as the scatter kernel, so counts and ranks agree exactly.  Writes the
+// Shared by the forward (training mode) and the standalone count kernel: identical corners, merge
+// and pairing decisions as the scatter kernel, so counts and ranks agree exactly.  Writes the
 // histogram row and adds it into the row's scan-chunk sums.
-__device__ __forceinline__ void count_block_records(const GridArgs& a, uint32_t l, const Corners& c, bool in,
-                                                    uint32_t* hist, const BwdWorkspace& ws) {
+__device__ __forceinline__ void publish_block_counts(const GridArgs& a, uint32_t l, const uint32_t* hist,
+                                                     const BwdWorkspace& ws) {
   const uint32_t nb = a.bucket_base[l + 1] - a.bucket_base[l];
-  const bool coherent = l < a.merge_levels;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const uint32_t idx = in ? c.idx[k] : 0xFFFFFFFFu;
-    bool valid = in;
-    if (coherent) {
-      const RunInfo ri = lane_runs(idx);  // every lane must take part in the shuffles/ballot
-      valid = in && ri.tail;
-    }
-    (void)wave_bucket_rank(hist, valid ? (idx - a.lv[l].offset) >> kChunkLog2 : 0u, valid, coherent);
-  }
-  __syncthreads();
   const int64_t sb = blockIdx.x;
   uint32_t* row = hist_row(a, ws, l, sb);
   uint32_t* cs = ws.chunk_sum + ((int64_t)l * ws.n_chunks + sb / kRowsPerChunk) * kMaxChunksPerLevel;
@@ -304,6 +405,43 @@ __device__ __forceinline__ void count_block_records(const GridArgs& a, uint32_t 
     row[b] = v;
     if (v) atomicAdd(&cs[b], v);
   }
+}
+
+// Fine levels: one record per x-pair, two when the pair spans two chunks (d >= kChunk).
+__device__ __forceinline__ void count_block_records_fine(const GridArgs& a, uint32_t l, const FineCell& c, bool in,
+                                                         uint32_t* hist, const BwdWorkspace& ws) {
+  if (in) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      atomicAdd(&hist[c.e[j] >> kChunkLog2], 1u);
+      if (c.d >= (uint32_t)kChunk) atomicAdd(&hist[(c.e[j] ^ c.d) >> kChunkLog2], 1u);
+    }
+  }
+  lds_barrier();
+  publish_block_counts(a, l, hist, ws);
+}
+
+__device__ __forceinline__ void count_block_records(const GridArgs& a, uint32_t l, const Corners& c, bool in,
+                                                    uint32_t* hist, const BwdWorkspace& ws) {
+  const uint32_t off = a.lv[l].offset;
+  if (l < a.merge_levels) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t idx = in ? c.idx[k] : 0xFFFFFFFFu;
+      const RunInfo ri = lane_runs_dpp(idx);  // every lane must take part in the ballot
+      const bool valid = in && ri.tail;
+      (void)wave_bucket_rank(hist, valid ? (idx - off) >> kChunkLog2 : 0u, valid, true);
+    }
+  } else if (in) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t e0 = c.idx[2 * j] - off, e1 = c.idx[2 * j + 1] - off;
+      atomicAdd(&hist[e0 >> kChunkLog2], 1u);
+      if (!pairable(e0, e1)) atomicAdd(&hist[e1 >> kChunkLog2], 1u);
+    }
+  }
+  lds_barrier();
+  publish_block_counts(a, l, hist, ws);
 }
 
 }  // namespace lnr

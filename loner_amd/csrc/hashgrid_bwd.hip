@@ -2,27 +2,20 @@
 //
 // Measured on MI355X: scattered fp32 global atomics run at ~20 G lane-ops/s (memory-side
 // execution) and LDS ds_add_f32 at only 0.33 lanes/clk/CU whatever the address pattern, while
-// ds_add_u64 runs at 4.8 lanes/clk/CU (scratch/ubench_*.hip).  So the backward is
-//   count   per (256-sample block, level) record histogram per 4096-entry table chunk
+// ds_add_u64 runs at 4.8 lanes/clk/CU.  So the backward is
+//   count   per (kSB-sample row, level) record histogram per 4096-entry table chunk
 //           (emitted by the training forward, or by k_bwd_count)
-//   scan    column prefix over blocks -> exact record offsets (no global atomics, no capacity guess)
-//   scatter records {idx in chunk, g0, g1 as fp25} staged in LDS in bucket order and written
-//           as coalesced runs; per-block max |g| for the fixed-point scale
+//   scan    column prefix over rows -> exact record offsets (no global atomics, no capacity guess)
+//   scatter 12-byte records (hashgrid.hpp: one per x-pair of corners at fine levels, one per
+//           merged corner at coherent levels) staged in LDS in bucket order and written as
+//           coalesced runs; per-row max |value| for the fixed-point scale
 //   accum   one workgroup per (bucket, slice): int64 fixed-point sums in a 64 KB LDS chunk with
 //           ds_add_u64, converted back to fp32 and stored; a bucket split over several slices
 //           stores per-slice int64 partial chunks that k_bwd_finalize adds exactly
 // No float atomics anywhere: the result is bitwise reproducible, and d_table is overwritten.
-// Coherent coarse levels merge runs of equal corner indices across lanes before emitting.
 #include "hashgrid.hpp"
 
 namespace lnr {
-
-__device__ __forceinline__ uint32_t f32_to_f25(float f) {
-  uint32_t u = __float_as_uint(f);
-  u += 0x3Fu + ((u >> 7) & 1u);
-  return u >> 7;
-}
-__device__ __forceinline__ float f25_to_f32(uint32_t v) { return __uint_as_float(v << 7); }
 
 template <class PosFn>
 __global__ void __launch_bounds__(kSB) k_bwd_count(GridArgs a, PosFn pos, int64_t n, BwdWorkspace ws) {
@@ -31,12 +24,18 @@ __global__ void __launch_bounds__(kSB) k_bwd_count(GridArgs a, PosFn pos, int64_
   const int64_t i = (int64_t)blockIdx.x * kSB + threadIdx.x;
   const bool in = i < n;
   for (int b = threadIdx.x; b < kMaxChunksPerLevel; b += blockDim.x) hist[b] = 0;
-  __syncthreads();
   float x = 0.f, y = 0.f, z = 0.f;
   if (in) pos(i, x, y, z);
-  Corners c;
-  level_corners(a.lv[l], x, y, z, c);
-  count_block_records(a, l, c, in, hist, ws);
+  lds_barrier();
+  if (a.lv[l].fine) {
+    FineCell c;
+    fine_cell(a.lv[l], x, y, z, c);
+    count_block_records_fine(a, l, c, in, hist, ws);
+  } else {
+    Corners c;
+    level_corners(a.lv[l], x, y, z, c);
+    count_block_records(a, l, c, in, hist, ws);
+  }
 }
 
 // Exclusive prefix of every bucket column over the histogram rows of one scan chunk, offset by
@@ -103,7 +102,7 @@ __global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint
     w_sl[wid] = isl;
     w_pp[wid] = ipp;
   }
-  __syncthreads();
+  lds_barrier();
   uint64_t bseg = 0;
   uint32_t bsl = 0, bpp = 0;
   for (int w = 0; w < wid; ++w) {
@@ -133,64 +132,237 @@ __global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint
   }
 }
 
-// One workgroup per (histogram row, level): kSB samples, 8 records each, staged in LDS in bucket
-// order and written as one contiguous run per bucket.
-template <class PosFn>
-__global__ void __launch_bounds__(kSB) k_bwd_scatter(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ d_enc,
-                                                     int64_t stride, BwdWorkspace ws) {
+// One workgroup per (histogram row, level): kSB samples, up to 8 records each (hashgrid.hpp).
+// Records are appended to an LDS buffer in arrival order (wave-compacted), ranked within their
+// bucket by LDS atomics, and an inverse permutation (bucket order -> arrival slot) lets every wave
+// copy whole bucket runs to global memory, coalesced.  A thread keeps one packed word per record
+// {arrival slot, bucket, rank}, not the record, so the kernel stays small enough for 4 workgroups
+// per CU.  Records beyond the buffer (rows whose coherent levels did not merge) go straight to
+// their global slot, which is known as soon as the rank is.
+constexpr int kStage = 8 * kSB;           // record slots per row (bucket-order positions)
+constexpr int kArr = 4 * kSB + 256;       // arrival buffer: 4 per sample (fine levels) + slack
+constexpr uint32_t kArrNone = 0x1FFFu;    // "not in the arrival buffer"
+static_assert(kArr < (int)kArrNone && kStage <= 4096 && kMaxChunksPerLevel <= 128, "packed record word");
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pack_rec(uint32_t slot, uint32_t bk, uint32_t rank) {
+  return slot | (bk << 13) | (rank << 20);
+}
+
+#ifndef LNR_SCATTER_WAVES_PER_EU
+#define LNR_SCATTER_WAVES_PER_EU 1
+#endif
+// KIND: the levels one launch covers, so each gets only its own code and registers.
+enum : int { kLevelsCoherent = 0, kLevelsFine = 1, kLevelsGeneric = 2 };
+
+template <class PosFn, int KIND>
+__global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ d_enc,
+                                                     int64_t stride, BwdWorkspace ws, uint32_t l0) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint64_t* stage = reinterpret_cast<uint64_t*>(smem);                // [8 * kSB]
-  uint64_t* gbase = stage + 8 * kSB;                                  // [kMaxChunksPerLevel]
-  uint32_t* hist = reinterpret_cast<uint32_t*>(gbase + kMaxChunksPerLevel);  // [kMaxChunksPerLevel]
-  uint32_t* start = hist + kMaxChunksPerLevel;                        // [kMaxChunksPerLevel + 1]
-  float* wmax = reinterpret_cast<float*>(start + kMaxChunksPerLevel + 1);    // [kSB / 64]
-  uint8_t* sbk = reinterpret_cast<uint8_t*>(wmax + kSB / 64);         // [8 * kSB]
-  const uint32_t l = blockIdx.y;
+  float2* arr_v = reinterpret_cast<float2*>(smem);                         // [kArr]
+  uint64_t* gbase = reinterpret_cast<uint64_t*>(arr_v + kArr);             // [kMaxChunksPerLevel]
+  uint32_t* arr_w = reinterpret_cast<uint32_t*>(gbase + kMaxChunksPerLevel);  // [kArr]
+  uint32_t* hist = arr_w + kArr;                                           // [kMaxChunksPerLevel]
+  uint32_t* start = hist + kMaxChunksPerLevel;                             // [kMaxChunksPerLevel + 1]
+  float* wmax = reinterpret_cast<float*>(start + kMaxChunksPerLevel + 1);  // [kSB / 64]
+  uint32_t* arr_n = reinterpret_cast<uint32_t*>(wmax + kSB / 64);          // [1]
+  uint16_t* inv = reinterpret_cast<uint16_t*>(arr_n + 1);                  // [kStage]
+  const uint32_t l = l0 + blockIdx.y;
   const int64_t sb = blockIdx.x;
   const int64_t i = sb * kSB + threadIdx.x;
   const bool in = i < n;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t b0 = a.bucket_base[l];
   const uint32_t nb = a.bucket_base[l + 1] - b0;
-  const uint32_t* row = hist_row(a, ws, l, sb);
-  for (uint32_t b = threadIdx.x; b < kMaxChunksPerLevel; b += kSB) {
-    hist[b] = 0;
-    if (b < nb) gbase[b] = ws.seg_start[b0 + b] + row[b];
-  }
-  __syncthreads();
+  const LevelParams& lv = a.lv[l];
+  LNR_STAMP(t0);
+  static_assert(kMaxChunksPerLevel <= kSB, "one bucket per thread");
+  const uint32_t tb = threadIdx.x;
+  uint64_t gb = 0;  // this row's first slot in bucket tb; first needed after the ranking
+  if (tb < nb) gb = ws.seg_start[b0 + tb] + hist_row(a, ws, l, sb)[tb];
   float x = 0.f, y = 0.f, z = 0.f;
   float2 g = make_float2(0.f, 0.f);
   if (in) {
     pos(i, x, y, z);
     g = d_enc[(int64_t)l * stride + i];
   }
-  Corners c;
-  level_corners(a.lv[l], x, y, z, c);
-  const bool coherent = l < a.merge_levels;
-  const uint32_t off = a.lv[l].offset;
-  uint32_t e[8], rank[8];
-  uint64_t rec[8];
-  bool valid[8];
-  float m = 0.f;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
+  if (tb < kMaxChunksPerLevel) hist[tb] = 0;
+  if (tb == 0) *arr_n = 0;
+  lds_barrier();
+  LNR_STAMP(t1);
+
+  // Coherent levels: corner k summed over the run of lanes that share it (one record per run).
+  auto coh_record = [&](const Corners& c, int k, uint32_t& word, uint32_t& bk, float2& val, bool& valid) {
     const uint32_t idx = in ? c.idx[k] : 0xFFFFFFFFu;
     float v0 = c.w[k] * g.x, v1 = c.w[k] * g.y;
-    valid[k] = in;
-    if (coherent) {
-      const RunInfo ri = lane_runs(idx);
-      run_sum(ri, v0, v1);
-      valid[k] = in && ri.tail;
+    const RunInfo ri = lane_runs_dpp(idx);
+    run_sum_dpp(ri, v0, v1);
+    valid = in && ri.tail;
+    const uint32_t e = valid ? idx - lv.offset : 0u;
+    word = e & (kChunk - 1);
+    bk = e >> kChunkLog2;
+    val = make_float2(v0, v1);
+  };
+  // The (sample, level)'s records in slots 0-7 (hashgrid.hpp "Backward records"); deterministic,
+  // so the rare overflow path below can recompute them.
+  auto records = [&](uint32_t* word, uint32_t* bk, float2* val, bool* valid) {
+    if constexpr (KIND == kLevelsFine) {
+      FineCell c;
+      fine_cell(lv, x, y, z, c);
+      const bool split = c.d >= (uint32_t)kChunk;
+      const uint32_t code = ((uint32_t)__popc(c.d) << kChunkLog2) | (tx_unorm16(c.tx) << 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t e0 = c.e[j], e1 = c.e[j] ^ c.d;
+        const float wyz = ((j & 1) ? c.ty : 1.0f - c.ty) * ((j & 2) ? c.tz : 1.0f - c.tz);
+        const float w0 = split ? fine_weight(c, j, 0) : wyz;
+        const float w1 = fine_weight(c, j, 1);
+        valid[j] = in;
+        word[j] = (e0 & (kChunk - 1)) | (split ? 0u : code);
+        bk[j] = e0 >> kChunkLog2;
+        val[j] = make_float2(w0 * g.x, w0 * g.y);
+        valid[4 + j] = in && split;
+        word[4 + j] = e1 & (kChunk - 1);
+        bk[4 + j] = e1 >> kChunkLog2;
+        val[4 + j] = make_float2(w1 * g.x, w1 * g.y);
+      }
+      return;
     }
-    e[k] = valid[k] ? idx - off : 0u;
-    rank[k] = wave_bucket_rank(hist, e[k] >> kChunkLog2, valid[k], coherent);
-    const uint32_t q0 = f32_to_f25(v0), q1 = f32_to_f25(v1);
-    rec[k] = (uint64_t)(e[k] & (kChunk - 1)) | ((uint64_t)q0 << 13) | ((uint64_t)q1 << 38);
-    if (valid[k]) m = fmaxf(m, fmaxf(fabsf(f25_to_f32(q0)), fabsf(f25_to_f32(q1))));
+    Corners c;
+    level_corners(lv, x, y, z, c);
+    const uint32_t off = lv.offset;
+    if constexpr (KIND == kLevelsCoherent) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) coh_record(c, k, word[k], bk[k], val[k], valid[k]);
+      return;
+    }
+    const uint32_t txq = tx_unorm16(c.tx);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t e0 = c.idx[2 * j] - off, e1 = c.idx[2 * j + 1] - off;
+      const bool pair = pairable(e0, e1);
+      const float wyz = ((j & 1) ? c.ty : 1.0f - c.ty) * ((j & 2) ? c.tz : 1.0f - c.tz);
+      const float w0 = pair ? wyz : c.w[2 * j];
+      valid[j] = in;
+      word[j] = pair ? pair_word(e0, e1, txq) : (e0 & (kChunk - 1));
+      bk[j] = e0 >> kChunkLog2;
+      val[j] = make_float2(w0 * g.x, w0 * g.y);
+      valid[4 + j] = in && !pair;
+      word[4 + j] = e1 & (kChunk - 1);
+      bk[4 + j] = e1 >> kChunkLog2;
+      val[4 + j] = make_float2(c.w[2 * j + 1] * g.x, c.w[2 * j + 1] * g.y);
+    }
+  };
+
+  constexpr bool coherent = KIND == kLevelsCoherent;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  uint32_t packed[8];
+  float m = 0.f;
+  if constexpr (coherent) {  // one corner at a time: record, rank, arrival slot (few live registers)
+    Corners c;
+    level_corners(lv, x, y, z, c);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      uint32_t word, bk;
+      float2 val;
+      bool valid;
+      coh_record(c, k, word, bk, val, valid);
+      packed[k] = 0xFFFFFFFFu;
+      const unsigned long long vm = __ballot(valid);
+      if (!vm) continue;
+      const uint32_t rank = wave_bucket_rank(hist, bk, valid, true);
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(arr_n, (uint32_t)__popcll(vm));
+      base = __shfl(base, 0, 64);
+      const uint32_t slot = base + (uint32_t)__popcll(vm & lt);
+      if (valid) {
+        m = fmaxf(m, fmaxf(fabsf(val.x), fabsf(val.y)));
+        if (slot < (uint32_t)kArr) {
+          arr_w[slot] = word;
+          arr_v[slot] = val;
+          packed[k] = pack_rec(slot, bk, rank);
+        } else {
+          packed[k] = pack_rec(kArrNone, bk, rank);  // written by the overflow path below
+        }
+      }
+    }
+  } else {
+    uint32_t word[8], bk[8];
+    float2 val[8];
+    bool valid[8];
+    records(word, bk, val, valid);
+    // wave-compacted arrival slots: one LDS atomic per wave for all its records
+    uint32_t wave_total = 0;
+    unsigned long long vm[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      vm[k] = __ballot(valid[k]);
+      wave_total += (uint32_t)__popcll(vm[k]);
+    }
+    uint32_t base = 0;
+    if (lane == 0 && wave_total) base = atomicAdd(arr_n, wave_total);
+    base = __shfl(base, 0, 64);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      packed[k] = 0xFFFFFFFFu;
+      if (!vm[k]) continue;  // wave-uniform (fine levels: slots 4-7 only for split pairs)
+      uint32_t rank = 0;
+      if constexpr (coherent) {
+        rank = wave_bucket_rank(hist, bk[k], valid[k], true);
+      } else if (valid[k]) {
+        rank = atomicAdd(&hist[bk[k]], 1u);
+      }
+      const uint32_t slot = base + (uint32_t)__popcll(vm[k] & lt);
+      base += (uint32_t)__popcll(vm[k]);
+      if (valid[k]) {
+        m = fmaxf(m, fmaxf(fabsf(val[k].x), fabsf(val[k].y)));
+        if (slot < (uint32_t)kArr) {
+          arr_w[slot] = word[k];
+          arr_v[slot] = val[k];
+          packed[k] = pack_rec(slot, bk[k], rank);
+        } else {
+          packed[k] = pack_rec(kArrNone, bk[k], rank);  // written by the overflow path below
+        }
+      }
+    }
   }
   m = wave_max(m);
   if (lane == 0) wmax[wid] = m;
-  __syncthreads();
+  if (tb < nb) gbase[tb] = gb;
+  LNR_STAMP(t2);
+  lds_barrier();
+  LNR_STAMP(t3);
+  if (*arr_n > (uint32_t)kArr) {  // block-uniform and rare (rows whose coherent levels did not merge)
+    auto direct = [&](int k, uint32_t word, uint32_t bk, float2 val) {
+      const uint32_t pk = packed[k];
+      if (pk != 0xFFFFFFFFu && (pk & 0x1FFFu) == kArrNone) {
+        const uint64_t dst = gbase[bk] + (pk >> 20);
+        ws.rec_w[dst] = word;
+        ws.rec_v[dst] = val;
+      }
+    };
+    if constexpr (coherent) {
+      Corners c;
+      level_corners(lv, x, y, z, c);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        uint32_t word, bk;
+        float2 val;
+        bool valid;
+        coh_record(c, k, word, bk, val, valid);
+        direct(k, word, bk, val);
+      }
+    } else {
+      uint32_t word[8], bk[8];
+      float2 val[8];
+      bool valid[8];
+      records(word, bk, val, valid);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) direct(k, word[k], bk[k], val[k]);
+    }
+  }
   if (wid == 0) {  // exclusive prefix of the (<= 128) bucket counts: 2 per lane + a wave scan
     const uint32_t c0 = 2 * lane < nb ? hist[2 * lane] : 0u;
     const uint32_t c1 = 2 * lane + 1 < nb ? hist[2 * lane + 1] : 0u;
@@ -208,28 +380,47 @@ __global__ void __launch_bounds__(kSB) k_bwd_scatter(GridArgs a, PosFn pos, int6
     mm = wave_max(mm);
     if (lane == 0) ws.blockmax[(int64_t)l * ws.n_sb + sb] = mm;
   }
-  __syncthreads();
+  lds_barrier();
+  LNR_STAMP(t4);
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    if (valid[k]) {
-      const uint32_t ch = e[k] >> kChunkLog2;
-      const uint32_t slot = start[ch] + rank[k];
-      if (slot < 8 * kSB) {  // always true when counts and ranks agree; guards the LDS stage
-        stage[slot] = rec[k];
-        sbk[slot] = (uint8_t)ch;
+    const uint32_t pk = packed[k];
+    if (pk != 0xFFFFFFFFu) {
+      const uint32_t t = start[(pk >> 13) & 127u] + (pk >> 20);
+      if (t < (uint32_t)kStage) inv[t] = (uint16_t)(pk & 0x1FFFu);
+    }
+  }
+  lds_barrier();
+  LNR_STAMP(t5);
+  // one bucket run at a time per wave (runs average 4 * kSB / buckets-per-level records)
+  for (uint32_t b = wid; b < nb; b += kSB / 64) {
+    const uint32_t r0 = start[b], r1 = start[b + 1] < (uint32_t)kStage ? start[b + 1] : (uint32_t)kStage;
+    const uint64_t dst0 = gbase[b] - r0;
+    for (uint32_t t = r0 + lane; t < r1; t += 64) {
+      const uint32_t sl = inv[t];
+      if (sl < (uint32_t)kArr) {
+#ifndef LNR_EXP_SKIP_STORE
+        ws.rec_w[dst0 + t] = arr_w[sl];
+        ws.rec_v[dst0 + t] = arr_v[sl];
+#else
+        if (arr_w[sl] == 0x12345678u) ws.rec_w[dst0 + t] = 0;
+#endif
       }
     }
   }
-  __syncthreads();
-  const uint32_t total = start[nb] < 8u * kSB ? start[nb] : 8u * kSB;
-  for (uint32_t t = threadIdx.x; t < total; t += kSB) {
-    const uint32_t ch = sbk[t];
-    __builtin_nontemporal_store(stage[t], &ws.records[gbase[ch] + (t - start[ch])]);  // read once, later
-  }
+  LNR_STAMP(t6);
+  LNR_PHASE(0, t1, t0);
+  LNR_PHASE(1, t2, t1);
+  LNR_PHASE(2, t3, t2);
+  LNR_PHASE(3, t4, t3);
+  LNR_PHASE(4, t5, t4);
+  LNR_PHASE(5, t6, t5);
+  LNR_PHASE(6, 1ull, 0ull);
 }
 
-constexpr size_t kScatterLds = 8 * kSB * 8 + kMaxChunksPerLevel * 8 + kMaxChunksPerLevel * 4 +
-                               (kMaxChunksPerLevel + 1) * 4 + (kSB / 64) * 4 + 8 * kSB;
+constexpr size_t kScatterLds = (size_t)kArr * 8 + kMaxChunksPerLevel * 8 + (size_t)kArr * 4 + kMaxChunksPerLevel * 4 +
+                               (kMaxChunksPerLevel + 1) * 4 + (kSB / 64) * 4 + 4 + (size_t)kStage * 2;
+static_assert(kScatterLds <= 65536, "scatter LDS within the default dynamic limit");
 
 __global__ void __launch_bounds__(256) k_bwd_level_max(BwdWorkspace ws) {
   __shared__ float red[4];
@@ -238,12 +429,11 @@ __global__ void __launch_bounds__(256) k_bwd_level_max(BwdWorkspace ws) {
   for (int64_t j = threadIdx.x; j < ws.n_sb; j += 256) m = fmaxf(m, col[j]);
   m = wave_max(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
+  lds_barrier();
   if (threadIdx.x == 0) ws.level_max[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
 constexpr int kAccumThreads = 1024;
-typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
 __global__ void __launch_bounds__(kAccumThreads) k_bwd_accum(GridArgs a, BwdWorkspace ws, float* __restrict__ d_table) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -279,53 +469,65 @@ __global__ void __launch_bounds__(kAccumThreads) k_bwd_accum(GridArgs a, BwdWork
     int k2 = 62 - lg - E;
     k2 = k2 > 120 ? 120 : (k2 < -120 ? -120 : k2);
     const float scale = ldexpf(1.f, k2);
+    LNR_STAMP(t0);
     for (int t = threadIdx.x; t < 2 * kChunk; t += blockDim.x) acc[t] = 0ull;
-    __syncthreads();
+    lds_barrier();
+    LNR_STAMP(t1);
     const bool coherent = l < a.merge_levels;
-#ifdef LNR_EXP_NO_LDS_ATOMICS
-    long long dummy = 0;
-#endif
-    const uint64_t* rec = ws.records;
-    // 16-B loads (2 records per lane), 4 in flight: 8 KB per wave trip; a lane's two records are
-    // handled as two lane-ordered streams (merging of equal entries is an optimisation only)
+    // 2 records per lane per load (8-B words, 16-B values), 4 loads in flight: 4 K records per
+    // workgroup trip; a lane's two records are handled as two lane-ordered streams (merging
+    // equal entries of coherent levels is an optimisation only: the int64 sums are exact)
     const uint64_t beg2 = beg & ~1ull;
     for (uint64_t rb = beg2 + 2 * (threadIdx.x & ~63u); rb < end; rb += 8 * kAccumThreads) {  // wave-uniform
-      u64x2 q[4];
+      uint2 qw[4];
+      float4 qv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const uint64_t rr = rb + 2 * lane + (uint64_t)u * 2 * kAccumThreads;
-        q[u] = rr < end ? __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(&rec[rr])) : u64x2{~0ull, ~0ull};
-        if (rr < beg) q[u].x = ~0ull;
-        if (rr + 1 >= end) q[u].y = ~0ull;
+        if (rr < end) {
+          const u32x2 w2 = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(&ws.rec_w[rr]));
+          const f32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(&ws.rec_v[rr]));
+          qw[u] = make_uint2(w2.x, w2.y);
+          qv[u] = make_float4(v4.x, v4.y, v4.z, v4.w);
+        } else {
+          qw[u] = make_uint2(kRecNone, kRecNone);
+          qv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if (rr < beg) qw[u].x = kRecNone;
+        if (rr + 1 >= end) qw[u].y = kRecNone;
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const uint64_t v = (u & 1) ? q[u >> 1].y : q[u >> 1].x;
-        const bool ok = v != ~0ull;
-        const uint32_t ee = ok ? (uint32_t)(v & (kChunk - 1)) : 0xFFFFFFFFu;
-        const float v0 = ok ? f25_to_f32((uint32_t)(v >> 13) & 0x1FFFFFFu) : 0.f;
-        const float v1 = ok ? f25_to_f32((uint32_t)(v >> 38) & 0x1FFFFFFu) : 0.f;
-        long long i0 = __float2ll_rn(v0 * scale), i1 = __float2ll_rn(v1 * scale);
-        bool emit = ok;
-        if (coherent) {  // records of coherent levels arrive in runs of equal entries; merged in
-          const RunInfo ri = lane_runs(ee);  // int64 so the sum does not depend on record order
+        const uint32_t w = (u & 1) ? qw[u >> 1].y : qw[u >> 1].x;
+        const float v0 = (u & 1) ? qv[u >> 1].z : qv[u >> 1].x;
+        const float v1 = (u & 1) ? qv[u >> 1].w : qv[u >> 1].y;
+        const bool ok = w != kRecNone;
+        const uint32_t e0 = ok ? (w & (kChunk - 1)) : 0xFFFFFFFFu;
+        if (coherent) {  // single-corner records arriving in runs of equal entries
+          long long i0 = ok ? __float2ll_rn(v0 * scale) : 0, i1 = ok ? __float2ll_rn(v1 * scale) : 0;
+          const RunInfo ri = lane_runs(e0);
           run_sum_i64(ri, i0, i1);
-          emit = ok && ri.tail;
+          if (ok && ri.tail) {
+            atomicAdd(&acc[2 * e0 + 0], (unsigned long long)i0);
+            atomicAdd(&acc[2 * e0 + 1], (unsigned long long)i1);
+          }
+        } else if (ok) {
+          const uint32_t p = (w >> kChunkLog2) & 15u;
+          const float tx = (float)(w >> 16) * kInvU16;  // 0 for single-corner records
+          const float s0 = 1.0f - tx;
+          atomicAdd(&acc[2 * e0 + 0], (unsigned long long)__float2ll_rn(s0 * v0 * scale));
+          atomicAdd(&acc[2 * e0 + 1], (unsigned long long)__float2ll_rn(s0 * v1 * scale));
+          if (p) {
+            const uint32_t e1 = e0 ^ ((1u << p) - 1u);
+            atomicAdd(&acc[2 * e1 + 0], (unsigned long long)__float2ll_rn(tx * v0 * scale));
+            atomicAdd(&acc[2 * e1 + 1], (unsigned long long)__float2ll_rn(tx * v1 * scale));
+          }
         }
-#ifdef LNR_EXP_NO_LDS_ATOMICS
-        if (emit) dummy += i0 + i1 + ee;
-#else
-        if (emit) {
-          atomicAdd(&acc[2 * ee + 0], (unsigned long long)i0);
-          atomicAdd(&acc[2 * ee + 1], (unsigned long long)i1);
-        }
-#endif
       }
     }
-#ifdef LNR_EXP_NO_LDS_ATOMICS
-    if (dummy == 0x123456789LL) acc[threadIdx.x] = dummy;
-#endif
-    __syncthreads();
+    LNR_STAMP(t2);
+    lds_barrier();
+    LNR_STAMP(t3);
     if (nsl == 1) {  // the final values
       const float inv = ldexpf(1.f, -k2);
       float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0);
@@ -334,7 +536,14 @@ __global__ void __launch_bounds__(kAccumThreads) k_bwd_accum(GridArgs a, BwdWork
       long long* dst = ws.partial + (int64_t)(ws.part_pre[b] + j) * (2 * kChunk);
       for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) dst[t] = (long long)acc[t];
     }
-    __syncthreads();
+    lds_barrier();
+    LNR_STAMP(t4);
+    LNR_PHASE(8, t1, t0);
+    LNR_PHASE(9, t2, t1);
+    LNR_PHASE(10, t3, t2);
+    LNR_PHASE(11, t4, t3);
+    LNR_PHASE(12, 1ull, 0ull);
+    LNR_PHASE(13, end - beg, 0ull);
   }
 }
 
@@ -378,15 +587,6 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
               (long long)bwd_workspace_bytes(d, n));
   LNR_REQUIRE(n < (int64_t(1) << 31), "%s: n=%lld samples exceeds 2^31", who, (long long)n);
   BwdWorkspace w = carve_workspace(workspace, a, d, n);
-  static bool lds_attr = false;  // scatter stages 8 records per sample of its row in LDS (> 64 KB)
-  if (!lds_attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bwd_scatter<PosFn>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScatterLds) != hipSuccess) {
-      set_error("%s: cannot raise the scatter kernel's LDS limit to %zu bytes", who, kScatterLds);
-      return LNR_ERR_HIP;
-    }
-    lds_attr = true;
-  }
   dim3 grid((unsigned)w.n_sb, d->n_levels);
   if (!(flags & LNR_BWD_COUNTS_READY)) {
     int64_t off, bytes;
@@ -399,8 +599,23 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
   }
   hipLaunchKernelGGL(k_bwd_scan_rows, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
   hipLaunchKernelGGL(k_bwd_scan_buckets, dim3(1), dim3(1024), 0, st, w, a.n_buckets);
-  hipLaunchKernelGGL(k_bwd_scatter<PosFn>, grid, dim3(kSB), kScatterLds, st, a, pos, n,
-                     reinterpret_cast<const float2*>(d_enc), stride, w);
+  {
+    const float2* de = reinterpret_cast<const float2*>(d_enc);
+    const uint32_t m = a.merge_levels, L = d->n_levels;
+    bool all_fine = true;
+    for (uint32_t l = m; l < L; ++l) all_fine = all_fine && a.lv[l].fine;
+    if (m > 0)
+      hipLaunchKernelGGL((k_bwd_scatter<PosFn, kLevelsCoherent>), dim3((unsigned)w.n_sb, m), dim3(kSB), kScatterLds, st,
+                         a, pos, n, de, stride, w, 0u);
+    if (L > m) {
+      if (all_fine)
+        hipLaunchKernelGGL((k_bwd_scatter<PosFn, kLevelsFine>), dim3((unsigned)w.n_sb, L - m), dim3(kSB), kScatterLds,
+                           st, a, pos, n, de, stride, w, m);
+      else
+        hipLaunchKernelGGL((k_bwd_scatter<PosFn, kLevelsGeneric>), dim3((unsigned)w.n_sb, L - m), dim3(kSB),
+                           kScatterLds, st, a, pos, n, de, stride, w, m);
+    }
+  }
   hipLaunchKernelGGL(k_bwd_level_max, dim3(d->n_levels), dim3(256), 0, st, w);
   const int64_t max_slices = a.n_buckets + (8 * n * (int64_t)d->n_levels) / kSliceRecords + 1;
   const unsigned g = (unsigned)(max_slices < 4096 ? max_slices : 4096);
@@ -446,3 +661,5 @@ extern "C" int lnr_hashgrid_bwd_rays(const lnr_grid_desc* d, const float* rays, 
   return launch_bwd_bucketed(d, PosFromRays{rays, z, n_samples}, n, d_enc, enc_stride, d_table, workspace,
                              workspace_bytes, flags, as_stream(stream), "lnr_hashgrid_bwd_rays");
 }
+
+LNR_PHASE_EXPORT(hashgrid_bwd)
