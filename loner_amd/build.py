@@ -26,6 +26,12 @@ FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-ffp-contract=
          "-Wno-unused-function", "-I", os.path.join(ROOT, "include")]
 
 
+# Per-file flags.  The hash-grid kernels keep global loads in flight across LDS-only barriers;
+# SLP-packed f32 math (v_pk_*) needs its loaded operands copied into register pairs, and those
+# copies wait for the loads before the barrier.
+FILE_FLAGS = {"hashgrid_bwd.hip": ["-fno-slp-vectorize"]}
+
+
 def _sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
 
@@ -39,7 +45,7 @@ def _compile(src, objdir=OBJDIR, extra=()):
     newest_dep = max(os.path.getmtime(p) for p in _deps() + [src])
     if os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
         return obj, ""
-    cmd = [HIPCC, *FLAGS, *extra, "-c", src, "-o", obj]
+    cmd = [HIPCC, *FLAGS, *FILE_FLAGS.get(os.path.basename(src), []), *extra, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")

@@ -74,10 +74,14 @@ __device__ __forceinline__ float2 half2_to_float2(uint32_t v) {
 // Workgroup barrier that orders LDS only: waits for this wave's LDS operations (lgkmcnt), not for
 // its global loads and stores (vmcnt), which __syncthreads' full fence would drain.  For barriers
 // that only publish LDS data, so global loads issued before them stay in flight across them.
+// The scheduling barriers keep register copies of in-flight loads from being hoisted above it
+// (such a copy waits for its load).
 __device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 // ------------------------------------------------------------------ wave / block reductions

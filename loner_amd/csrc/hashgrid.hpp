@@ -84,26 +84,39 @@ __device__ __forceinline__ uint32_t grid_index(const LevelParams& p, uint32_t x,
 
 // Sample position in [0,1]^3.  From rays: xyz = o + d*z (rendering_tcnn.py:390), pos = (xyz+1)/2
 // (nerf_tcnn.py:63); compiled with -ffp-contract=off so the op order matches torch.
+// load() issues the global loads, eval() does the arithmetic: kernels that must not wait for the
+// loads before a barrier call them on either side of it.
 struct PosFromArray {
   const float* pos;
-  __device__ __forceinline__ void operator()(int64_t n, float& x, float& y, float& z) const {
-    x = pos[3 * n + 0];
-    y = pos[3 * n + 1];
-    z = pos[3 * n + 2];
+  struct Raw {
+    float x, y, z;
+  };
+  __device__ __forceinline__ Raw load(int64_t n) const { return {pos[3 * n + 0], pos[3 * n + 1], pos[3 * n + 2]}; }
+  __device__ __forceinline__ void eval(const Raw& r, float& x, float& y, float& z) const {
+    x = r.x;
+    y = r.y;
+    z = r.z;
   }
+  __device__ __forceinline__ void operator()(int64_t n, float& x, float& y, float& z) const { eval(load(n), x, y, z); }
 };
 struct PosFromRays {
   const float* rays;
   const float* zs;
   int32_t n_samples;
-  __device__ __forceinline__ void operator()(int64_t n, float& x, float& y, float& z) const {
+  struct Raw {
+    float ox, oy, oz, dx, dy, dz, t;
+  };
+  __device__ __forceinline__ Raw load(int64_t n) const {
     const uint32_t r = (uint32_t)n / (uint32_t)n_samples;  // N < 2^31 (checked at the C ABI)
     const float* ry = rays + 13 * r;
-    const float t = zs[n];
-    x = (ry[0] + ry[3] * t + 1.0f) * 0.5f;
-    y = (ry[1] + ry[4] * t + 1.0f) * 0.5f;
-    z = (ry[2] + ry[5] * t + 1.0f) * 0.5f;
+    return {ry[0], ry[1], ry[2], ry[3], ry[4], ry[5], zs[n]};
   }
+  __device__ __forceinline__ void eval(const Raw& r, float& x, float& y, float& z) const {
+    x = (r.ox + r.dx * r.t + 1.0f) * 0.5f;
+    y = (r.oy + r.dy * r.t + 1.0f) * 0.5f;
+    z = (r.oz + r.dz * r.t + 1.0f) * 0.5f;
+  }
+  __device__ __forceinline__ void operator()(int64_t n, float& x, float& y, float& z) const { eval(load(n), x, y, z); }
 };
 
 struct Corners {

@@ -133,42 +133,34 @@ __global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint
 }
 
 // One workgroup per (histogram row, level): kSB samples, up to 8 records each (hashgrid.hpp).
-// Records are appended to an LDS buffer in arrival order (wave-compacted), ranked within their
-// bucket by LDS atomics, and an inverse permutation (bucket order -> arrival slot) lets every wave
-// copy whole bucket runs to global memory, coalesced.  A thread keeps one packed word per record
-// {arrival slot, bucket, rank}, not the record, so the kernel stays small enough for 4 workgroups
-// per CU.  Records beyond the buffer (rows whose coherent levels did not merge) go straight to
-// their global slot, which is known as soon as the rank is.
-constexpr int kStage = 8 * kSB;           // record slots per row (bucket-order positions)
-constexpr int kArr = 4 * kSB + 256;       // arrival buffer: 4 per sample (fine levels) + slack
-constexpr uint32_t kArrNone = 0x1FFFu;    // "not in the arrival buffer"
-static_assert(kArr < (int)kArrNone && kStage <= 4096 && kMaxChunksPerLevel <= 128, "packed record word");
+// The row's per-bucket record counts are known before it starts (the forward's histogram, scanned
+// into per-row offsets), so every record's place is known the moment its bucket rank is: staged
+// rows write records in bucket order into LDS and copy whole bucket runs out, coalesced.  Rows with
+// more than kCap records (coherent levels whose runs did not merge) write each record straight
+// to its global slot instead.
+constexpr int kCap = 4 * kSB + 256;  // 4 records per sample at fine levels, plus slack
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ uint32_t pack_rec(uint32_t slot, uint32_t bk, uint32_t rank) {
-  return slot | (bk << 13) | (rank << 20);
-}
+// KIND: the levels one launch covers, so each gets only its own code and registers.
+enum : int { kLevelsCoherent = 0, kLevelsFine = 1, kLevelsGeneric = 2 };
 
 #ifndef LNR_SCATTER_WAVES_PER_EU
 #define LNR_SCATTER_WAVES_PER_EU 1
 #endif
-// KIND: the levels one launch covers, so each gets only its own code and registers.
-enum : int { kLevelsCoherent = 0, kLevelsFine = 1, kLevelsGeneric = 2 };
-
 template <class PosFn, int KIND>
-__global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ d_enc,
-                                                     int64_t stride, BwdWorkspace ws, uint32_t l0) {
+__global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(GridArgs a, PosFn pos, int64_t n,
+                                                                             const float2* __restrict__ d_enc,
+                                                                             int64_t stride, BwdWorkspace ws, uint32_t l0) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float2* arr_v = reinterpret_cast<float2*>(smem);                         // [kArr]
-  uint64_t* gbase = reinterpret_cast<uint64_t*>(arr_v + kArr);             // [kMaxChunksPerLevel]
-  uint32_t* arr_w = reinterpret_cast<uint32_t*>(gbase + kMaxChunksPerLevel);  // [kArr]
-  uint32_t* hist = arr_w + kArr;                                           // [kMaxChunksPerLevel]
-  uint32_t* start = hist + kMaxChunksPerLevel;                             // [kMaxChunksPerLevel + 1]
-  float* wmax = reinterpret_cast<float*>(start + kMaxChunksPerLevel + 1);  // [kSB / 64]
-  uint32_t* arr_n = reinterpret_cast<uint32_t*>(wmax + kSB / 64);          // [1]
-  uint16_t* inv = reinterpret_cast<uint16_t*>(arr_n + 1);                  // [kStage]
+  float2* stage_v = reinterpret_cast<float2*>(smem);                         // [kCap]
+  uint64_t* gbase = reinterpret_cast<uint64_t*>(stage_v + kCap);             // [kMaxChunksPerLevel]
+  uint32_t* stage_w = reinterpret_cast<uint32_t*>(gbase + kMaxChunksPerLevel);  // [kCap]
+  uint32_t* rank_ctr = stage_w + kCap;                                       // [kMaxChunksPerLevel]
+  uint32_t* start = rank_ctr + kMaxChunksPerLevel;                           // [kMaxChunksPerLevel + 1]
+  float* wmax = reinterpret_cast<float*>(start + kMaxChunksPerLevel + 1);    // [kSB / 64]
+  uint8_t* sbk = reinterpret_cast<uint8_t*>(wmax + kSB / 64);                // [kCap] bucket of each staged record
   const uint32_t l = l0 + blockIdx.y;
   const int64_t sb = blockIdx.x;
   const int64_t i = sb * kSB + threadIdx.x;
@@ -177,195 +169,32 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
   const uint32_t b0 = a.bucket_base[l];
   const uint32_t nb = a.bucket_base[l + 1] - b0;
   const LevelParams& lv = a.lv[l];
+  static_assert(kMaxChunksPerLevel <= 128, "two buckets per lane of wave 0");
   LNR_STAMP(t0);
-  static_assert(kMaxChunksPerLevel <= kSB, "one bucket per thread");
-  const uint32_t tb = threadIdx.x;
-  uint64_t gb = 0;  // this row's first slot in bucket tb; first needed after the ranking
-  if (tb < nb) gb = ws.seg_start[b0 + tb] + hist_row(a, ws, l, sb)[tb];
-  float x = 0.f, y = 0.f, z = 0.f;
-  float2 g = make_float2(0.f, 0.f);
-  if (in) {
-    pos(i, x, y, z);
-    g = d_enc[(int64_t)l * stride + i];
-  }
-  if (tb < kMaxChunksPerLevel) hist[tb] = 0;
-  if (tb == 0) *arr_n = 0;
-  lds_barrier();
-  LNR_STAMP(t1);
-
-  // Coherent levels: corner k summed over the run of lanes that share it (one record per run).
-  auto coh_record = [&](const Corners& c, int k, uint32_t& word, uint32_t& bk, float2& val, bool& valid) {
-    const uint32_t idx = in ? c.idx[k] : 0xFFFFFFFFu;
-    float v0 = c.w[k] * g.x, v1 = c.w[k] * g.y;
-    const RunInfo ri = lane_runs_dpp(idx);
-    run_sum_dpp(ri, v0, v1);
-    valid = in && ri.tail;
-    const uint32_t e = valid ? idx - lv.offset : 0u;
-    word = e & (kChunk - 1);
-    bk = e >> kChunkLog2;
-    val = make_float2(v0, v1);
-  };
-  // The (sample, level)'s records in slots 0-7 (hashgrid.hpp "Backward records"); deterministic,
-  // so the rare overflow path below can recompute them.
-  auto records = [&](uint32_t* word, uint32_t* bk, float2* val, bool* valid) {
-    if constexpr (KIND == kLevelsFine) {
-      FineCell c;
-      fine_cell(lv, x, y, z, c);
-      const bool split = c.d >= (uint32_t)kChunk;
-      const uint32_t code = ((uint32_t)__popc(c.d) << kChunkLog2) | (tx_unorm16(c.tx) << 16);
+  // 1. Global loads, all unconditional (clamped indices) so nothing waits for them before it must:
+  //    the sample's position inputs and d_enc, and (wave 0) the row's offsets.
+  const int64_t ic = in ? i : n - 1;
+  const typename PosFn::Raw raw = pos.load(ic);
+  const float2 g_raw = d_enc[(int64_t)l * stride + ic];
+  uint32_t h0[2] = {0u, 0u}, h1[2] = {0u, 0u};
+  uint64_t seg[2] = {0ull, 0ull};
+  const bool last = sb + 1 >= ws.n_sb;
+  {  // every wave loads (L2 hits): a branch around the loads would make its exit wait for them
+    const uint32_t* row = hist_row(a, ws, l, sb);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t e0 = c.e[j], e1 = c.e[j] ^ c.d;
-        const float wyz = ((j & 1) ? c.ty : 1.0f - c.ty) * ((j & 2) ? c.tz : 1.0f - c.tz);
-        const float w0 = split ? fine_weight(c, j, 0) : wyz;
-        const float w1 = fine_weight(c, j, 1);
-        valid[j] = in;
-        word[j] = (e0 & (kChunk - 1)) | (split ? 0u : code);
-        bk[j] = e0 >> kChunkLog2;
-        val[j] = make_float2(w0 * g.x, w0 * g.y);
-        valid[4 + j] = in && split;
-        word[4 + j] = e1 & (kChunk - 1);
-        bk[4 + j] = e1 >> kChunkLog2;
-        val[4 + j] = make_float2(w1 * g.x, w1 * g.y);
-      }
-      return;
-    }
-    Corners c;
-    level_corners(lv, x, y, z, c);
-    const uint32_t off = lv.offset;
-    if constexpr (KIND == kLevelsCoherent) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) coh_record(c, k, word[k], bk[k], val[k], valid[k]);
-      return;
-    }
-    const uint32_t txq = tx_unorm16(c.tx);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t e0 = c.idx[2 * j] - off, e1 = c.idx[2 * j + 1] - off;
-      const bool pair = pairable(e0, e1);
-      const float wyz = ((j & 1) ? c.ty : 1.0f - c.ty) * ((j & 2) ? c.tz : 1.0f - c.tz);
-      const float w0 = pair ? wyz : c.w[2 * j];
-      valid[j] = in;
-      word[j] = pair ? pair_word(e0, e1, txq) : (e0 & (kChunk - 1));
-      bk[j] = e0 >> kChunkLog2;
-      val[j] = make_float2(w0 * g.x, w0 * g.y);
-      valid[4 + j] = in && !pair;
-      word[4 + j] = e1 & (kChunk - 1);
-      bk[4 + j] = e1 >> kChunkLog2;
-      val[4 + j] = make_float2(c.w[2 * j + 1] * g.x, c.w[2 * j + 1] * g.y);
-    }
-  };
-
-  constexpr bool coherent = KIND == kLevelsCoherent;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  uint32_t packed[8];
-  float m = 0.f;
-  if constexpr (coherent) {  // one corner at a time: record, rank, arrival slot (few live registers)
-    Corners c;
-    level_corners(lv, x, y, z, c);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      uint32_t word, bk;
-      float2 val;
-      bool valid;
-      coh_record(c, k, word, bk, val, valid);
-      packed[k] = 0xFFFFFFFFu;
-      const unsigned long long vm = __ballot(valid);
-      if (!vm) continue;
-      const uint32_t rank = wave_bucket_rank(hist, bk, valid, true);
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(arr_n, (uint32_t)__popcll(vm));
-      base = __shfl(base, 0, 64);
-      const uint32_t slot = base + (uint32_t)__popcll(vm & lt);
-      if (valid) {
-        m = fmaxf(m, fmaxf(fabsf(val.x), fabsf(val.y)));
-        if (slot < (uint32_t)kArr) {
-          arr_w[slot] = word;
-          arr_v[slot] = val;
-          packed[k] = pack_rec(slot, bk, rank);
-        } else {
-          packed[k] = pack_rec(kArrNone, bk, rank);  // written by the overflow path below
-        }
-      }
-    }
-  } else {
-    uint32_t word[8], bk[8];
-    float2 val[8];
-    bool valid[8];
-    records(word, bk, val, valid);
-    // wave-compacted arrival slots: one LDS atomic per wave for all its records
-    uint32_t wave_total = 0;
-    unsigned long long vm[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      vm[k] = __ballot(valid[k]);
-      wave_total += (uint32_t)__popcll(vm[k]);
-    }
-    uint32_t base = 0;
-    if (lane == 0 && wave_total) base = atomicAdd(arr_n, wave_total);
-    base = __shfl(base, 0, 64);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      packed[k] = 0xFFFFFFFFu;
-      if (!vm[k]) continue;  // wave-uniform (fine levels: slots 4-7 only for split pairs)
-      uint32_t rank = 0;
-      if constexpr (coherent) {
-        rank = wave_bucket_rank(hist, bk[k], valid[k], true);
-      } else if (valid[k]) {
-        rank = atomicAdd(&hist[bk[k]], 1u);
-      }
-      const uint32_t slot = base + (uint32_t)__popcll(vm[k] & lt);
-      base += (uint32_t)__popcll(vm[k]);
-      if (valid[k]) {
-        m = fmaxf(m, fmaxf(fabsf(val[k].x), fabsf(val[k].y)));
-        if (slot < (uint32_t)kArr) {
-          arr_w[slot] = word[k];
-          arr_v[slot] = val[k];
-          packed[k] = pack_rec(slot, bk[k], rank);
-        } else {
-          packed[k] = pack_rec(kArrNone, bk[k], rank);  // written by the overflow path below
-        }
-      }
+    for (int q = 0; q < 2; ++q) {
+      const uint32_t b = min(2u * lane + q, nb - 1u);
+      h0[q] = row[b];
+      h1[q] = (last ? ws.counts + b0 : row + nb)[b];  // next row's offset, or the bucket total
+      seg[q] = ws.seg_start[b0 + b];
     }
   }
-  m = wave_max(m);
-  if (lane == 0) wmax[wid] = m;
-  if (tb < nb) gbase[tb] = gb;
-  LNR_STAMP(t2);
-  lds_barrier();
-  LNR_STAMP(t3);
-  if (*arr_n > (uint32_t)kArr) {  // block-uniform and rare (rows whose coherent levels did not merge)
-    auto direct = [&](int k, uint32_t word, uint32_t bk, float2 val) {
-      const uint32_t pk = packed[k];
-      if (pk != 0xFFFFFFFFu && (pk & 0x1FFFu) == kArrNone) {
-        const uint64_t dst = gbase[bk] + (pk >> 20);
-        ws.rec_w[dst] = word;
-        ws.rec_v[dst] = val;
-      }
-    };
-    if constexpr (coherent) {
-      Corners c;
-      level_corners(lv, x, y, z, c);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        uint32_t word, bk;
-        float2 val;
-        bool valid;
-        coh_record(c, k, word, bk, val, valid);
-        direct(k, word, bk, val);
-      }
-    } else {
-      uint32_t word[8], bk[8];
-      float2 val[8];
-      bool valid[8];
-      records(word, bk, val, valid);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) direct(k, word[k], bk[k], val[k]);
-    }
-  }
-  if (wid == 0) {  // exclusive prefix of the (<= 128) bucket counts: 2 per lane + a wave scan
-    const uint32_t c0 = 2 * lane < nb ? hist[2 * lane] : 0u;
-    const uint32_t c1 = 2 * lane + 1 < nb ? hist[2 * lane + 1] : 0u;
+  // wave 0 turns the offsets into the row's bucket starts and global bases (called where its loads
+  // have had the most time to land)
+  auto row_starts = [&]() {
+    if (wid != 0) return;
+    const uint32_t c0 = 2 * lane < nb ? h1[0] - h0[0] : 0u;
+    const uint32_t c1 = 2 * lane + 1 < nb ? h1[1] - h0[1] : 0u;
     uint32_t inc = c0 + c1;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -373,53 +202,142 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
       if (lane >= o) inc += q;
     }
     const uint32_t ex = inc - c0 - c1;
-    if (2 * lane <= nb) start[2 * lane] = ex;
-    if (2 * lane + 1 <= nb) start[2 * lane + 1] = ex + c0;
-    if (lane == 63) start[nb] = inc;  // the total (nb = 128 has no lane whose pair reaches it)
+    if (2 * lane < nb) {
+      start[2 * lane] = ex;
+      gbase[2 * lane] = seg[0] + h0[0];
+    }
+    if (2 * lane + 1 < nb) {
+      start[2 * lane + 1] = ex + c0;
+      gbase[2 * lane + 1] = seg[1] + h0[1];
+    }
+    if (lane == 63) start[nb] = inc;
+  };
+  if (threadIdx.x < kMaxChunksPerLevel) rank_ctr[threadIdx.x] = 0;
+  if constexpr (KIND == kLevelsCoherent) row_starts();  // coherent rows place as they rank
+  lds_barrier();
+  LNR_STAMP(t1);
+  float x = 0.f, y = 0.f, z = 0.f;
+  pos.eval(raw, x, y, z);
+  const float2 g = in ? g_raw : make_float2(0.f, 0.f);
+  float m = 0.f;
+  bool staged = true;
+  auto place = [&](bool valid, uint32_t bk, uint32_t rank, uint32_t word, float2 val) {
+    if (!valid) return;
+    m = fmaxf(m, fmaxf(fabsf(val.x), fabsf(val.y)));
+    if (staged) {
+      const uint32_t t = start[bk] + rank;
+      stage_w[t] = word;
+      stage_v[t] = val;
+      sbk[t] = (uint8_t)bk;
+    } else {
+      const uint64_t dst = gbase[bk] + rank;
+      ws.rec_w[dst] = word;
+      ws.rec_v[dst] = val;
+    }
+  };
+  // 2. records: rank, then place (hashgrid.hpp "Backward records")
+  if constexpr (KIND == kLevelsFine) {
+    // ranks first (LDS counters only), placement after wave 0 has published the starts
+    FineCell c;
+    fine_cell(lv, x, y, z, c);
+    const bool split = c.d >= (uint32_t)kChunk;
+    const uint32_t code = ((uint32_t)__popc(c.d) << kChunkLog2) | (tx_unorm16(c.tx) << 16);
+    uint32_t rank[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rank[j] = in ? atomicAdd(&rank_ctr[c.e[j] >> kChunkLog2], 1u) : 0u;
+    row_starts();
+    LNR_STAMP(t1b);
+    lds_barrier();
+    LNR_PHASE(5 * KIND + 4, t1b, t1);
+    staged = start[nb] <= (uint32_t)kCap;  // block-uniform
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t e0 = c.e[j];
+      const float wyz = ((j & 1) ? c.ty : 1.0f - c.ty) * ((j & 2) ? c.tz : 1.0f - c.tz);
+      const float w0 = split ? fine_weight(c, j, 0) : wyz;
+      place(in, e0 >> kChunkLog2, rank[j], (e0 & (kChunk - 1)) | (split ? 0u : code), make_float2(w0 * g.x, w0 * g.y));
+    }
+    if (__ballot(in && split)) {  // pairs spanning two chunks: the second corners on their own
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t e1 = c.e[j] ^ c.d;
+        const float w1 = fine_weight(c, j, 1);
+        const bool v = in && split;
+        const uint32_t r = v ? atomicAdd(&rank_ctr[e1 >> kChunkLog2], 1u) : 0u;
+        place(v, e1 >> kChunkLog2, r, e1 & (kChunk - 1), make_float2(w1 * g.x, w1 * g.y));
+      }
+    }
+  } else {
+    Corners c;
+    level_corners(lv, x, y, z, c);
+    const uint32_t off = lv.offset;
+    if constexpr (KIND == kLevelsCoherent) {  // corner k summed over the run of lanes that share it
+      staged = start[nb] <= (uint32_t)kCap;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t idx = in ? c.idx[k] : 0xFFFFFFFFu;
+        float v0 = c.w[k] * g.x, v1 = c.w[k] * g.y;
+        const RunInfo ri = lane_runs_dpp(idx);
+        run_sum_dpp(ri, v0, v1);
+        const bool valid = in && ri.tail;
+        const uint32_t e = valid ? idx - off : 0u;
+        const uint32_t bk = e >> kChunkLog2;
+        const uint32_t rank = wave_bucket_rank(rank_ctr, bk, valid, true);
+        place(valid, bk, rank, e & (kChunk - 1), make_float2(v0, v1));
+      }
+    } else {  // generic non-coherent levels (configurations without power-of-two hashed tables)
+      row_starts();
+      lds_barrier();
+      staged = start[nb] <= (uint32_t)kCap;
+      const uint32_t txq = tx_unorm16(c.tx);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t e0 = c.idx[2 * j] - off, e1 = c.idx[2 * j + 1] - off;
+        const bool pair = pairable(e0, e1);
+        const float wyz = ((j & 1) ? c.ty : 1.0f - c.ty) * ((j & 2) ? c.tz : 1.0f - c.tz);
+        const float w0 = pair ? wyz : c.w[2 * j];
+        const uint32_t r0 = in ? atomicAdd(&rank_ctr[e0 >> kChunkLog2], 1u) : 0u;
+        place(in, e0 >> kChunkLog2, r0, pair ? pair_word(e0, e1, txq) : (e0 & (kChunk - 1)),
+              make_float2(w0 * g.x, w0 * g.y));
+        const bool v1 = in && !pair;
+        const uint32_t r1 = v1 ? atomicAdd(&rank_ctr[e1 >> kChunkLog2], 1u) : 0u;
+        place(v1, e1 >> kChunkLog2, r1, e1 & (kChunk - 1), make_float2(c.w[2 * j + 1] * g.x, c.w[2 * j + 1] * g.y));
+      }
+    }
+  }
+  m = wave_max(m);
+  if (lane == 0) wmax[wid] = m;
+  LNR_STAMP(t2);
+  lds_barrier();
+  LNR_STAMP(t3);
+  if (wid == 0) {
     float mm = lane < kSB / 64 ? wmax[lane] : 0.f;
     mm = wave_max(mm);
     if (lane == 0) ws.blockmax[(int64_t)l * ws.n_sb + sb] = mm;
   }
-  lds_barrier();
-  LNR_STAMP(t4);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const uint32_t pk = packed[k];
-    if (pk != 0xFFFFFFFFu) {
-      const uint32_t t = start[(pk >> 13) & 127u] + (pk >> 20);
-      if (t < (uint32_t)kStage) inv[t] = (uint16_t)(pk & 0x1FFFu);
-    }
-  }
-  lds_barrier();
-  LNR_STAMP(t5);
-  // one bucket run at a time per wave (runs average 4 * kSB / buckets-per-level records)
-  for (uint32_t b = wid; b < nb; b += kSB / 64) {
-    const uint32_t r0 = start[b], r1 = start[b + 1] < (uint32_t)kStage ? start[b + 1] : (uint32_t)kStage;
-    const uint64_t dst0 = gbase[b] - r0;
-    for (uint32_t t = r0 + lane; t < r1; t += 64) {
-      const uint32_t sl = inv[t];
-      if (sl < (uint32_t)kArr) {
+  // 3. copy the staged row out in bucket order (consecutive lanes -> consecutive slots of a run)
+  if (staged) {
+    const uint32_t total = start[nb];
+    for (uint32_t t = threadIdx.x; t < total; t += kSB) {
+      const uint32_t bk = sbk[t];
+      const uint64_t dst = gbase[bk] + (t - start[bk]);
 #ifndef LNR_EXP_SKIP_STORE
-        ws.rec_w[dst0 + t] = arr_w[sl];
-        ws.rec_v[dst0 + t] = arr_v[sl];
+      ws.rec_w[dst] = stage_w[t];
+      ws.rec_v[dst] = stage_v[t];
 #else
-        if (arr_w[sl] == 0x12345678u) ws.rec_w[dst0 + t] = 0;
+      if (stage_w[t] == 0x12345678u) ws.rec_w[dst] = 0;
 #endif
-      }
     }
   }
-  LNR_STAMP(t6);
-  LNR_PHASE(0, t1, t0);
-  LNR_PHASE(1, t2, t1);
-  LNR_PHASE(2, t3, t2);
-  LNR_PHASE(3, t4, t3);
-  LNR_PHASE(4, t5, t4);
-  LNR_PHASE(5, t6, t5);
-  LNR_PHASE(6, 1ull, 0ull);
+  LNR_STAMP(t4);
+  LNR_PHASE(5 * KIND + 0, t1, t0);
+  LNR_PHASE(5 * KIND + 1, t2, t1);
+  LNR_PHASE(5 * KIND + 2, t3, t2);
+  LNR_PHASE(5 * KIND + 3, t4, t3);
 }
 
-constexpr size_t kScatterLds = (size_t)kArr * 8 + kMaxChunksPerLevel * 8 + (size_t)kArr * 4 + kMaxChunksPerLevel * 4 +
-                               (kMaxChunksPerLevel + 1) * 4 + (kSB / 64) * 4 + 4 + (size_t)kStage * 2;
+constexpr size_t kScatterLds = (size_t)kCap * 8 + kMaxChunksPerLevel * 8 + (size_t)kCap * 4 + kMaxChunksPerLevel * 4 +
+                               (kMaxChunksPerLevel + 1) * 4 + (kSB / 64) * 4 + kCap;
 static_assert(kScatterLds <= 65536, "scatter LDS within the default dynamic limit");
 
 __global__ void __launch_bounds__(256) k_bwd_level_max(BwdWorkspace ws) {
@@ -538,12 +456,12 @@ __global__ void __launch_bounds__(kAccumThreads) k_bwd_accum(GridArgs a, BwdWork
     }
     lds_barrier();
     LNR_STAMP(t4);
-    LNR_PHASE(8, t1, t0);
-    LNR_PHASE(9, t2, t1);
-    LNR_PHASE(10, t3, t2);
-    LNR_PHASE(11, t4, t3);
-    LNR_PHASE(12, 1ull, 0ull);
-    LNR_PHASE(13, end - beg, 0ull);
+    LNR_PHASE(16, t1, t0);
+    LNR_PHASE(17, t2, t1);
+    LNR_PHASE(18, t3, t2);
+    LNR_PHASE(19, t4, t3);
+    LNR_PHASE(20, 1ull, 0ull);
+    LNR_PHASE(21, end - beg, 0ull);
   }
 }
 
