@@ -260,28 +260,6 @@ __device__ __forceinline__ void run_sum_i64(const RunInfo& ri, long long& v0, lo
   }
 }
 
-// Rank of this lane's record among the block's records of the same bucket (LDS counters).
-// Coherent levels put most of a wave's records into one or two buckets: there each distinct
-// bucket of the wave does one atomic (ballot + popcount) instead of 64 same-address atomics.
-__device__ __forceinline__ uint32_t wave_bucket_rank(uint32_t* hist, uint32_t bucket, bool valid, bool coherent) {
-  if (!coherent) return valid ? atomicAdd(&hist[bucket], 1u) : 0u;
-  const int lane = threadIdx.x & 63;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  unsigned long long todo = __ballot(valid);
-  uint32_t rank = 0;
-  while (todo) {
-    const int leader = __ffsll((long long)todo) - 1;
-    const uint32_t b = __shfl(bucket, leader, 64);
-    const unsigned long long m = __ballot(valid && bucket == b);
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(&hist[b], (uint32_t)__popcll(m));
-    base = __shfl(base, leader, 64);
-    if (valid && bucket == b) rank = base + (uint32_t)__popcll(m & lt);
-    todo &= ~m;
-  }
-  return rank;
-}
-
 // Backward workspace (device), carved from one caller-provided buffer.
 // Records are binned per "super-block" of kSB consecutive samples (one histogram row per
 // (level, super-block), one scatter workgroup per row): rows are written and read coalesced, and
@@ -442,8 +420,7 @@ __device__ __forceinline__ void count_block_records(const GridArgs& a, uint32_t 
     for (int k = 0; k < 8; ++k) {
       const uint32_t idx = in ? c.idx[k] : 0xFFFFFFFFu;
       const RunInfo ri = lane_runs_dpp(idx);  // every lane must take part in the ballot
-      const bool valid = in && ri.tail;
-      (void)wave_bucket_rank(hist, valid ? (idx - off) >> kChunkLog2 : 0u, valid, true);
+      if (in && ri.tail) atomicAdd(&hist[(idx - off) >> kChunkLog2], 1u);  // run tails only: few lanes
     }
   } else if (in) {
 #pragma unroll

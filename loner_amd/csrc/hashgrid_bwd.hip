@@ -282,7 +282,7 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
         const bool valid = in && ri.tail;
         const uint32_t e = valid ? idx - off : 0u;
         const uint32_t bk = e >> kChunkLog2;
-        const uint32_t rank = wave_bucket_rank(rank_ctr, bk, valid, true);
+        const uint32_t rank = valid ? atomicAdd(&rank_ctr[bk], 1u) : 0u;  // run tails only: few lanes
         place(valid, bk, rank, e & (kChunk - 1), make_float2(v0, v1));
       }
     } else {  // generic non-coherent levels (configurations without power-of-two hashed tables)
@@ -353,9 +353,16 @@ __global__ void __launch_bounds__(256) k_bwd_level_max(BwdWorkspace ws) {
 
 constexpr int kAccumThreads = 1024;
 
-__global__ void __launch_bounds__(kAccumThreads) k_bwd_accum(GridArgs a, BwdWorkspace ws, float* __restrict__ d_table) {
+#ifndef LNR_ACCUM_WAVES_PER_EU
+#define LNR_ACCUM_WAVES_PER_EU 8
+#endif
+#ifndef LNR_ACCUM_LOADS
+#define LNR_ACCUM_LOADS 2
+#endif
+__global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_accum(GridArgs a, BwdWorkspace ws, float* __restrict__ d_table) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [kChunk][2] int64 fixed point
+  unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [2][kChunk] int64 fixed point
+  // (one array per feature: 8-B atomics on random entries spread over twice the bank pairs)
   const uint32_t nbk = a.n_buckets;
   const uint32_t total = ws.slice_pre[nbk];
   const int lane = threadIdx.x & 63;
@@ -396,26 +403,20 @@ __global__ void __launch_bounds__(kAccumThreads) k_bwd_accum(GridArgs a, BwdWork
     // workgroup trip; a lane's two records are handled as two lane-ordered streams (merging
     // equal entries of coherent levels is an optimisation only: the int64 sums are exact)
     const uint64_t beg2 = beg & ~1ull;
-    for (uint64_t rb = beg2 + 2 * (threadIdx.x & ~63u); rb < end; rb += 8 * kAccumThreads) {  // wave-uniform
-      uint2 qw[4];
-      float4 qv[4];
+    for (uint64_t rb = beg2 + 2 * (threadIdx.x & ~63u); rb < end; rb += 2 * LNR_ACCUM_LOADS * kAccumThreads) {
+      uint2 qw[LNR_ACCUM_LOADS];
+      float4 qv[LNR_ACCUM_LOADS];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < LNR_ACCUM_LOADS; ++u) {
         const uint64_t rr = rb + 2 * lane + (uint64_t)u * 2 * kAccumThreads;
-        if (rr < end) {
-          const u32x2 w2 = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(&ws.rec_w[rr]));
-          const f32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(&ws.rec_v[rr]));
-          qw[u] = make_uint2(w2.x, w2.y);
-          qv[u] = make_float4(v4.x, v4.y, v4.z, v4.w);
-        } else {
-          qw[u] = make_uint2(kRecNone, kRecNone);
-          qv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        if (rr < beg) qw[u].x = kRecNone;
-        if (rr + 1 >= end) qw[u].y = kRecNone;
+        const uint64_t rc = rr < end ? rr : beg2;  // unconditional loads: no branch to wait at
+        const u32x2 w2 = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(&ws.rec_w[rc]));
+        const f32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(&ws.rec_v[rc]));
+        qw[u] = make_uint2(rr < beg || rr >= end ? kRecNone : w2.x, rr + 1 >= end ? kRecNone : w2.y);
+        qv[u] = make_float4(v4.x, v4.y, v4.z, v4.w);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 2 * LNR_ACCUM_LOADS; ++u) {
         const uint32_t w = (u & 1) ? qw[u >> 1].y : qw[u >> 1].x;
         const float v0 = (u & 1) ? qv[u >> 1].z : qv[u >> 1].x;
         const float v1 = (u & 1) ? qv[u >> 1].w : qv[u >> 1].y;
@@ -426,19 +427,19 @@ __global__ void __launch_bounds__(kAccumThreads) k_bwd_accum(GridArgs a, BwdWork
           const RunInfo ri = lane_runs(e0);
           run_sum_i64(ri, i0, i1);
           if (ok && ri.tail) {
-            atomicAdd(&acc[2 * e0 + 0], (unsigned long long)i0);
-            atomicAdd(&acc[2 * e0 + 1], (unsigned long long)i1);
+            atomicAdd(&acc[e0], (unsigned long long)i0);
+            atomicAdd(&acc[1 * kChunk + e0], (unsigned long long)i1);
           }
         } else if (ok) {
           const uint32_t p = (w >> kChunkLog2) & 15u;
           const float tx = (float)(w >> 16) * kInvU16;  // 0 for single-corner records
           const float s0 = 1.0f - tx;
-          atomicAdd(&acc[2 * e0 + 0], (unsigned long long)__float2ll_rn(s0 * v0 * scale));
-          atomicAdd(&acc[2 * e0 + 1], (unsigned long long)__float2ll_rn(s0 * v1 * scale));
+          atomicAdd(&acc[e0], (unsigned long long)__float2ll_rn(s0 * v0 * scale));
+          atomicAdd(&acc[1 * kChunk + e0], (unsigned long long)__float2ll_rn(s0 * v1 * scale));
           if (p) {
             const uint32_t e1 = e0 ^ ((1u << p) - 1u);
-            atomicAdd(&acc[2 * e1 + 0], (unsigned long long)__float2ll_rn(tx * v0 * scale));
-            atomicAdd(&acc[2 * e1 + 1], (unsigned long long)__float2ll_rn(tx * v1 * scale));
+            atomicAdd(&acc[e1], (unsigned long long)__float2ll_rn(tx * v0 * scale));
+            atomicAdd(&acc[1 * kChunk + e1], (unsigned long long)__float2ll_rn(tx * v1 * scale));
           }
         }
       }
@@ -449,10 +450,11 @@ __global__ void __launch_bounds__(kAccumThreads) k_bwd_accum(GridArgs a, BwdWork
     if (nsl == 1) {  // the final values
       const float inv = ldexpf(1.f, -k2);
       float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0);
-      for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) dst[t] = (float)(long long)acc[t] * inv;
+      for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x)
+        dst[t] = (float)(long long)acc[(t & 1) * kChunk + (t >> 1)] * inv;
     } else {  // this slice's int64 partial chunk
       long long* dst = ws.partial + (int64_t)(ws.part_pre[b] + j) * (2 * kChunk);
-      for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) dst[t] = (long long)acc[t];
+      for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) dst[t] = (long long)acc[(t & 1) * kChunk + (t >> 1)];
     }
     lds_barrier();
     LNR_STAMP(t4);
