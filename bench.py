@@ -61,6 +61,18 @@ LOSS_PRESETS = {
 }
 
 
+def pmc_traffic(cfg_name):
+    """HBM bytes per launch of the hash-grid backward stage, from the newest committed PMC pass of
+    this bench command (profiles/<round>_traffic_<cfg>.json, written by tools/refresh_profiles.py
+    from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs); None if there is none."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_traffic_{cfg_name}.json")))
+    if not files:
+        return None, None
+    rec = json.load(open(files[-1]))
+    return rec["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(cfg_name, n_rays, n_steps):
     """The numpy oracle on a bounded sample of the same workload (rank 0, N=1 only)."""
     from oracle import step as ostep
@@ -155,6 +167,7 @@ def main():
     value = world * N * args.steps / elapsed
     bwd_ms = stage_ms["grid_bwd"]
     achieved = 1024.0 * N / (bwd_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(args.config)
     line = {
         "metric": "ray-samples/sec per optimizer step",
         "value": value,
@@ -173,7 +186,7 @@ def main():
                    "rays_per_gpu": R, "samples_per_ray": n_samples, "global_rays": R * world,
                    "parallelism": f"dp{world}" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "hash-grid backward stage (k_bwd_scan_*, k_bwd_scatter, k_bwd_level_max, k_bwd_accum)",
                      "algorithmic_bytes_per_launch": 1024 * N, "ms_per_launch": bwd_ms},
         "stage_ms": stage_ms,
