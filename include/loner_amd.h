@@ -180,8 +180,12 @@ int lnr_composite_bwd(const float* rays, const float* z, const float* sigma, int
                       int32_t strategy, float noise_std, const float* noise, uint32_t key, int64_t ray_offset,
                       const float* g_weights, const float* g_depth, const float* g_opacity, const float* g_variance,
                       float* d_sigma, void* stream);
+/* Workspace (fp32 words) lnr_field_train needs: the dW slabs, then an (n_rays, n_samples) d_sigma
+ * buffer between its ray phase and its tile-parallel MLP backward. */
+int64_t lnr_field_train_workspace_words(int64_t n_rays, int32_t n_samples);
 /* Fused: sigma MLP forward from enc, compositing, loss, compositing backward, MLP backward.
- * Writes d_enc (level-major float2), accumulates d_w (3072 fp32), per-ray stats; optional outputs NULL. */
+ * Writes d_enc (level-major float2), accumulates d_w (3072 fp32), per-ray stats; optional outputs NULL.
+ * workspace: lnr_field_train_workspace_words(n_rays, n_samples) fp32 words. */
 int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, const float* rays, const float* z,
                     const float* depth_gt, int64_t n_rays, int32_t n_samples, float noise_std, const float* noise,
                     uint32_t key, int64_t ray_offset, const lnr_loss_params* lp, float* d_enc, float* d_w,

@@ -66,6 +66,7 @@ _SIGNATURES = {
     "lnr_sh_encode": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_p]),
     "lnr_sigma_mlp_fwd": (ctypes.c_int, [c_p, c_p, c_i64, c_i64, c_p, c_p]),
     "lnr_dw_workspace_words": (c_i64, [c_i64]),
+    "lnr_field_train_workspace_words": (c_i64, [c_i64, c_i32]),
     "lnr_sigma_mlp_bwd": (ctypes.c_int, [c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p]),
     "lnr_step_key": (c_u32, [c_u32, c_u32]),
     "lnr_sample_ogm": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i32, c_f, c_p, c_p, c_u32, c_i64, c_p, c_p]),

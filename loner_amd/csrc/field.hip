@@ -505,6 +505,293 @@ __global__ void __launch_bounds__(NT) k_field(FieldArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- wave-per-ray training kernel
+// The training hot path (lnr_field_train: sigma MLP, default compositing, LiDAR loss, backward)
+// with ONE WAVE PER RAY: S = 64 * C samples, lane l holds samples [C*l, C*l + C).  Scans and sums
+// are wave-level shuffles, so a ray needs no workgroup barrier; the 4 waves of a workgroup work on
+// 4 rays independently and meet once, at the end, to reduce their dW slabs.  Same arithmetic as
+// composite_ray<C, true, false> (the block version), reassociated only in the cross-lane sums.
+constexpr int kWavesPerBlock = NT / 64;
+
+__device__ __forceinline__ double wave_excl_prod(double p) {
+  const int lane = threadIdx.x & 63;
+  double inc = p;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double q = __shfl_up(inc, o, 64);
+    if (lane >= o) inc *= q;
+  }
+  const double ex = __shfl_up(inc, 1, 64);
+  return lane == 0 ? 1.0 : ex;
+}
+
+// X_t = (F_{t+1} o ... o F_63)(0) for per-lane affine maps F(x) = A x + B.
+__device__ __forceinline__ float wave_suffix_affine(float A, float B) {
+  const int lane = threadIdx.x & 63;
+  float qa = A, qb = B;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float na = __shfl_down(qa, o, 64), nb = __shfl_down(qb, o, 64);
+    if (lane + o < 64) {
+      qb = qa * nb + qb;
+      qa = qa * na;
+    }
+  }
+  const float na = __shfl_down(qa, 1, 64), nb = __shfl_down(qb, 1, 64);
+  return (lane == 63) ? 0.f : na * 0.f + nb;
+}
+
+__device__ __forceinline__ void wave_lds_handoff() {
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int C>
+__device__ void composite_loss_wave(const FieldArgs& a, float* sig, int64_t r) {
+  const int lane = threadIdx.x & 63;
+  const int S = a.S;
+  const int i0 = lane * C;
+  const float* ry = a.rays + 13 * r;
+  const float dx = ry[3], dy = ry[4], dz = ry[5];
+  const float far = ry[12];
+  const float dnorm = sqrtf(dx * dx + dy * dy + dz * dz);
+  const float* zr = a.z + r * S;
+  const int64_t gr = a.ray_offset + r;
+  const lnr_loss_params& lp = a.lp;
+
+  float z[C], alpha[C], s[C], delta[C], x[C], T[C], w[C];
+  double tl[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) z[c] = zr[i0 + c];
+  const float z_next = __shfl_down(z[0], 1, 64);  // first sample of the next lane
+  double P = 1.0;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int i = i0 + c;
+    const float zn = (c + 1 < C) ? z[c + 1] : z_next;
+    const float dl = (i + 1 < S) ? (zn - z[c]) : 1e10f;
+    delta[c] = dl * dnorm;
+    float nz = 0.f;
+    if (a.noise) nz = a.noise[r * S + i] * a.noise_std;
+    else if (a.noise_std > 0.f) nz = rand_normal(a.key, kStreamNoise, (uint32_t)gr, (uint32_t)i) * a.noise_std;
+    x[c] = sig[i] + nz;
+    const float sr = fmaxf(x[c], 0.f);
+    alpha[c] = 1.0f - expf(-(delta[c] * sr));
+    s[c] = (1.0f - alpha[c]) + 1e-10f;
+    tl[c] = P;
+    P *= (double)s[c];
+  }
+  const double T0 = wave_excl_prod(P);
+  double acc_w = 0.0, acc_wz = 0.0, acc_wzs = 0.0;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    T[c] = (float)(T0 * tl[c]);
+    w[c] = alpha[c] * T[c];
+    acc_w += (double)w[c];
+    acc_wz += (double)(w[c] * z[c]);
+    acc_wzs += (double)((z[c] * lp.scale) * w[c]);
+  }
+  const float wsum = wave_sum((float)acc_w);
+  const float wzsum = wave_sum((float)acc_wz);
+  const float wzssum = wave_sum((float)acc_wzs);
+  const float tail = (1.0f - wsum) * far;
+  const float depth = (float)((double)wzsum + (double)tail);
+  const float opacity = wsum;
+  const float wden = wsum + 1e-10f;
+  const float mean = wzssum / wden;
+  double acc_lv = 0.0;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const float e = z[c] * lp.scale - mean;
+    acc_lv += (double)((e * e) * w[c]);
+  }
+  const float lvsum = wave_sum((float)acc_lv);
+  if (lane == 0) {
+    if (a.depth) a.depth[r] = depth;
+    if (a.opacity) a.opacity[r] = opacity;
+  }
+  // ------------------------------------------------ loss (optimizer.py:718-844)
+  const float inv_nop = lp.dev_n_opaque ? 1.0f / fmaxf(lp.dev_n_opaque[0], 1.0f) : lp.inv_n_opaque;
+  const float dgt = a.depth_gt[r];
+  const float g = dgt * lp.scale;
+  const bool opaque = (dgt > 0.f) && !(dgt > lp.far_ref);
+  const float lvar = lvsum / wden + 1e-10f;
+  const float stdv = sqrtf(lvar);
+  float eps;
+  if (lp.kind == LNR_LOSS_L1_JS || lp.kind == LNR_LOSS_L2_JS) {
+    const float s1 = lp.min_depth_eps / 3.0f;
+    const float mm = 0.5f * (g + mean);
+    const float smv = 0.5f * sqrtf(s1 * s1 + stdv * stdv);
+    const float v2 = smv * smv;
+    const float kl1 = logf(smv / s1) + (s1 * s1 + (g - mm) * (g - mm)) / (2.0f * v2) - 0.5f;
+    const float kl2 = logf(smv / stdv) + (stdv * stdv + (mean - mm) * (mean - mm)) / (2.0f * v2) - 0.5f;
+    float js = 0.5f * kl1 + 0.5f * kl2;
+    if (js < lp.min_js) js = 0.f;
+    if (js > lp.max_js) js = lp.max_js;
+    eps = lp.min_depth_eps * (1.0f + lp.js_alpha * js);
+  } else {
+    eps = lp.los_eps;
+  }
+  // truncated Gaussian target (losses.py:29-51)
+  const float sg = eps / 9.0f;
+  const float clip_a = ((g - eps) - g) / sg;
+  const float clip_b = ((g + eps) - g) / sg;
+  const float cdf_a = 0.5f * (1.0f + erff(clip_a / 1.4142135623730951f));
+  const float cdf_b = 0.5f * (1.0f + erff(clip_b / 1.4142135623730951f));
+  const float zden = cdf_b - cdf_a;
+  float wgt[C];
+  double acc_gt = 0.0;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const float sm = z[c] * lp.scale;
+    const float xx = (sm - g) / sg;
+    const float pdf = 0.3989422804014327f * expf(-0.5f * (xx * xx));
+    const float v = pdf / sg / zden;
+    const bool inside = ((sm - (g - eps)) > 0.f) && (((g + eps) - sm) > 0.f);
+    wgt[c] = inside ? v : 0.f;
+    acc_gt += (double)wgt[c];
+  }
+  const float gt_den = wave_sum((float)acc_gt) + 1e-6f;
+  const bool l1 = (lp.kind == LNR_LOSS_L1_JS || lp.kind == LNR_LOSS_L1_LOS);
+  const float d_euc = depth * lp.scale;
+  const float ddiff = d_euc - g;
+  const float g_depth = opaque ? lp.depthloss_lambda * 2.0f * ddiff * lp.scale * inv_nop : 0.f;
+  const float operr = opacity - 1.0f;
+  const float g_op = opaque ? ((operr > 0.f) ? 1.f : (operr < 0.f ? -1.f : 0.f)) * inv_nop : 0.f;
+  float G[C];
+  double acc_los = 0.0;
+  float FA = 1.f, FB = 0.f;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const float wg = opaque ? wgt[c] / gt_den : 0.f;
+    const float dw = w[c] - wg;
+    float gw;
+    if (l1) {
+      gw = lp.los_lambda * ((dw > 0.f) ? 1.f : (dw < 0.f ? -1.f : 0.f)) * lp.inv_rs;
+      acc_los += (double)fabsf(dw);
+    } else {
+      gw = lp.los_lambda * 2.0f * dw * lp.inv_rs;
+      acc_los += (double)(dw * dw);
+    }
+    G[c] = gw + g_depth * (z[c] - far) + g_op;
+  }
+#pragma unroll
+  for (int c = C - 1; c >= 0; --c) {
+    FB = G[c] * alpha[c] + s[c] * FB;
+    FA = s[c] * FA;
+  }
+  const float los = wave_sum((float)acc_los);
+  float X = wave_suffix_affine(FA, FB);
+#pragma unroll
+  for (int c = C - 1; c >= 0; --c) {
+    const float dA = T[c] * (G[c] - X);
+    X = G[c] * alpha[c] + s[c] * X;
+    const float sr = fmaxf(x[c], 0.f);
+    sig[i0 + c] = (x[c] > 0.f) ? dA * (delta[c] * expf(-(delta[c] * sr))) : 0.f;
+  }
+  if (a.weights)
+#pragma unroll
+    for (int c = 0; c < C; ++c) a.weights[r * S + i0 + c] = w[c];
+  if (lane == 0) {
+    float* st = a.ray_stats + r * LNR_RAY_STATS;
+    st[0] = opaque ? ddiff * ddiff : 0.f;
+    st[1] = los;
+    st[2] = opaque ? fabsf(operr) : 0.f;
+    st[3] = eps;
+    st[4] = opaque ? 1.f : 0.f;
+  }
+}
+
+// Phase 1, one wave per ray: sigma MLP forward -> compositing -> loss -> compositing backward;
+// writes dL/dsigma (R, S) fp32 for phase 2.
+template <int C>
+__global__ void __launch_bounds__(NT) k_field_wave(FieldArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+  constexpr int S = 64 * C;  // == a.S (checked at launch)
+  float* sig = reinterpret_cast<float*>(smem) + wid * S;  // this wave's ray: sigma, then dL/dsigma
+  SigmaWeights sw;
+  load_sigma_weights(a.w, sw);
+  for (int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + wid; r < a.n_rays; r += (int64_t)gridDim.x * kWavesPerBlock) {
+#pragma unroll 8
+    for (int tb = 0; tb < S; tb += 16) {
+      float h[16];
+      const float sgm = sigma_tile_fwd(sw, load_enc_operand(a.enc, a.enc_stride, r * S + tb + c, true), h);
+      if (g == 0) sig[tb + c] = sigma_to_f16(sgm);
+    }
+    wave_lds_handoff();
+    composite_loss_wave<C>(a, sig, r);
+    wave_lds_handoff();
+#pragma unroll
+    for (int k = 0; k < C; ++k) a.d_sigma[r * S + 64 * k + lane] = sig[64 * k + lane];  // coalesced
+    wave_lds_handoff();  // sig is rewritten by the next ray
+  }
+}
+
+// Phase 2, tile-parallel: sigma MLP backward over 32-sample tile pairs (no per-ray structure):
+// d_enc (level-major float2) and the per-block dW slab.
+__global__ void __launch_bounds__(NT) k_mlp_bwd_tiles(FieldArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+  _Float16* lds = reinterpret_cast<_Float16*>(smem) + wid * (64 * 32 + 32 * 32);
+  SigmaWeights sw;
+  load_sigma_weights(a.w, sw);
+  DW0Acc acc;
+  float dw1[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) dw1[k] = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc.v[t][m][q] = 0.f;
+  float2* denc = reinterpret_cast<float2*>(a.d_enc);
+  const int64_t N = a.n_rays * (int64_t)a.S;  // a multiple of 64
+  for (int64_t n0 = ((int64_t)blockIdx.x * kWavesPerBlock + wid) * 32; n0 < N;
+       n0 += (int64_t)gridDim.x * kWavesPerBlock * 32) {
+    float h0[16], h1[16];
+    const half8_t e0 = load_enc_operand(a.enc, a.enc_stride, n0 + c, true);
+    const half8_t e1 = load_enc_operand(a.enc, a.enc_stride, n0 + 16 + c, true);
+    const float ds0 = a.d_sigma[n0 + c], ds1 = a.d_sigma[n0 + 16 + c];
+    (void)sigma_tile_fwd(sw, e0, h0);
+    (void)sigma_tile_fwd(sw, e1, h1);
+    float mx = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      dw1[k] = fmaf(ds0, h0[k], dw1[k]);
+      dw1[k] = fmaf(ds1, h1[k], dw1[k]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fmaxf(fabsf((float)e0[j] * ds0), fabsf((float)e1[j] * ds1)));
+    const float scale = grad_scale(wave_max(mx));
+    float d[2][4];
+    sigma_tile_bwd_denc(sw, h0, d);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int lvl = 8 * m + 2 * g;
+      denc[(int64_t)lvl * a.enc_stride + n0 + c] = make_float2(d[m][0] * ds0, d[m][1] * ds0);
+      denc[(int64_t)(lvl + 1) * a.enc_stride + n0 + c] = make_float2(d[m][2] * ds0, d[m][3] * ds0);
+    }
+    sigma_tile_bwd_denc(sw, h1, d);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int lvl = 8 * m + 2 * g;
+      denc[(int64_t)lvl * a.enc_stride + n0 + 16 + c] = make_float2(d[m][0] * ds1, d[m][1] * ds1);
+      denc[(int64_t)(lvl + 1) * a.enc_stride + n0 + 16 + c] = make_float2(d[m][2] * ds1, d[m][3] * ds1);
+    }
+    dw0_pair(lds, sw, h0, h1, e0, e1, ds0, ds1, scale, acc);
+  }
+  __syncthreads();
+  write_dw_slab<NT>(reinterpret_cast<float*>(smem), acc, dw1, a.dw_slab + (int64_t)blockIdx.x * LNR_SIGMA_MLP_PARAMS);
+}
+
+static size_t wave_smem_bytes(int S) { return (size_t)kWavesPerBlock * S * 4; }
+static size_t bwd_tiles_smem_bytes() {
+  const size_t b = (size_t)kWavesPerBlock * (64 * 32 + 32 * 32) * 2;
+  return b < LNR_SIGMA_MLP_PARAMS * 4 ? LNR_SIGMA_MLP_PARAMS * 4 : b;
+}
+
 // dW[i] += sum_b slab[b][i]  (fixed order: deterministic)
 // dW[i] += sum_b slab[b][i]: blockIdx.y splits the slabs into groups of 32 (one atomic per group).
 __global__ void k_reduce_slabs(const float* __restrict__ slab, int nb, float* __restrict__ dw) {
@@ -584,6 +871,11 @@ extern "C" int64_t lnr_dw_workspace_words(int64_t n_rows) {
   int64_t nb = n_rows < 1024 ? n_rows : 1024;
   if (nb < 1) nb = 1;
   return nb * LNR_SIGMA_MLP_PARAMS;
+}
+
+extern "C" int64_t lnr_field_train_workspace_words(int64_t n_rays, int32_t n_samples) {
+  if (n_rays < 0 || n_samples < 0) return -1;
+  return lnr_dw_workspace_words(n_rays) + n_rays * (int64_t)n_samples;
 }
 
 static int check_rays(const float* rays, const float* z, int64_t n_rays, int32_t S, const char* who) {
@@ -669,10 +961,32 @@ extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t e
   a.n_rays = n_rays; a.S = n_samples; a.noise_std = noise_std; a.noise = noise; a.key = key;
   a.ray_offset = ray_offset; a.lp = *lp; a.d_enc = d_enc; a.dw_slab = workspace; a.ray_stats = ray_stats;
   a.depth = depth; a.opacity = opacity; a.weights = weights;
-  const int nb = field_blocks(n_rays);
   hipStream_t st = as_stream(stream);
-  int e = launch_field<true, false, kSigmaMLP>(a, nb, st, "lnr_field_train");
-  if (e) return e;
+  int nb;
+  const int C = n_samples / 64;
+  float* dsig_ws = workspace + lnr_dw_workspace_words(n_rays);
+  if ((C == 1 || C == 2 || C == 4 || C == 8) && dsig_ws) {
+    // one wave per ray (the reference's 512 samples: C = 8), then the tile-parallel MLP backward
+    a.d_sigma = dsig_ws;
+    const int64_t want = (n_rays + kWavesPerBlock - 1) / kWavesPerBlock;
+    const int nr = (int)(want < 2048 ? want : 2048);
+    const size_t sm = wave_smem_bytes(n_samples);
+    switch (C) {
+      case 1: hipLaunchKernelGGL(k_field_wave<1>, dim3(nr), dim3(NT), sm, st, a); break;
+      case 2: hipLaunchKernelGGL(k_field_wave<2>, dim3(nr), dim3(NT), sm, st, a); break;
+      case 4: hipLaunchKernelGGL(k_field_wave<4>, dim3(nr), dim3(NT), sm, st, a); break;
+      default: hipLaunchKernelGGL(k_field_wave<8>, dim3(nr), dim3(NT), sm, st, a); break;
+    }
+    const int64_t pairs = (n_rays * (int64_t)n_samples) / 32;
+    const int64_t wantb = (pairs + kWavesPerBlock - 1) / kWavesPerBlock;
+    const int64_t slabs = lnr_dw_workspace_words(n_rays) / LNR_SIGMA_MLP_PARAMS;  // one dW slab per block
+    nb = (int)(wantb < slabs ? wantb : slabs);
+    hipLaunchKernelGGL(k_mlp_bwd_tiles, dim3(nb), dim3(NT), bwd_tiles_smem_bytes(), st, a);
+  } else {
+    nb = field_blocks(n_rays);
+    int e = launch_field<true, false, kSigmaMLP>(a, nb, st, "lnr_field_train");
+    if (e) return e;
+  }
   hipLaunchKernelGGL(k_reduce_slabs, dim3((LNR_SIGMA_MLP_PARAMS + 255) / 256, (nb + 31) / 32), dim3(256), 0, st, workspace, nb, d_w);
   LNR_RETURN_LAUNCH("lnr_field_train(reduce)");
 }

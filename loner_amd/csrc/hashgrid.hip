@@ -33,11 +33,31 @@ __global__ void __launch_bounds__(1024) k_hashgrid_fwd(GridArgs a, PosFn pos, in
     if (in) {
       const uint32_t* tl = table + lv.offset;
       uint32_t v[8];
+#ifdef LNR_FWD_X4
+      // one 16-B load per x-pair: the partner e ^ d lies in the same aligned 4-entry group when
+      // d <= 3 (x even or x = 1 mod 4); the rest take a second, sparser gather
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 q[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) q[j] = *reinterpret_cast<const u32x4*>(tl + (c.e[j] & ~3u));
+      const bool near = c.d <= 3u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t s0 = c.e[j] & 3u, s1 = (c.e[j] ^ c.d) & 3u;
+        v[2 * j] = s0 == 0 ? q[j].x : s0 == 1 ? q[j].y : s0 == 2 ? q[j].z : q[j].w;
+        v[2 * j + 1] = s1 == 0 ? q[j].x : s1 == 1 ? q[j].y : s1 == 2 ? q[j].z : q[j].w;
+      }
+      if (!near) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[2 * j + 1] = tl[c.e[j] ^ c.d];
+      }
+#else
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         v[2 * j] = tl[c.e[j]];
         v[2 * j + 1] = tl[c.e[j] ^ c.d];
       }
+#endif
       float f0 = 0.f, f1 = 0.f;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {

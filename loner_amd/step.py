@@ -169,7 +169,7 @@ class StepEngine:
         self.z = torch.empty(n_rays, self.S, dtype=torch.float32, device=dev)
         self.enc = torch.empty(self.cfg.n_levels, self.N, dtype=torch.int32, device=dev)
         self.d_enc = torch.empty(self.cfg.n_levels, self.N, 2, dtype=torch.float32, device=dev)
-        self.ws = torch.empty(L.lib().lnr_dw_workspace_words(n_rays), dtype=torch.float32, device=dev)
+        self.ws = torch.empty(L.lib().lnr_field_train_workspace_words(n_rays, self.S), dtype=torch.float32, device=dev)
         self.bwd_ws_bytes = int(L.lib().lnr_hashgrid_bwd_workspace_bytes(L.ctypes.byref(state.desc), self.N))
         self.bwd_ws = torch.empty(self.bwd_ws_bytes, dtype=torch.uint8, device=dev)
         self.stats = torch.zeros(n_rays, L.RAY_STATS, dtype=torch.float32, device=dev)

@@ -88,7 +88,7 @@ def test_field_train_matches_oracle(L):
     lp = _lp(L, L2JS, g["scale"], 40, rays[0, -1], n_op, R, S)
     d_enc = torch.empty(16, R * S, 2, dtype=torch.float32, device="cuda")
     d_w = torch.zeros(3072, dtype=torch.float32, device="cuda")
-    ws = torch.empty(L.lib().lnr_dw_workspace_words(R), dtype=torch.float32, device="cuda")
+    ws = torch.empty(L.lib().lnr_field_train_workspace_words(R, S), dtype=torch.float32, device="cuda")
     stats = torch.empty(R, L.RAY_STATS, dtype=torch.float32, device="cuda")
     depth = torch.empty(R, dtype=torch.float32, device="cuda")
     op = torch.empty(R, dtype=torch.float32, device="cuda")
@@ -109,7 +109,9 @@ def test_field_train_matches_oracle(L):
     d2 = torch.empty(R, dtype=torch.float32, device="cuda")
     L.call("lnr_field_render", cu(wflat), cu(x_lm), R * S, cu(rays), cu(z), R, S, 0, 1.0, cu(noise), 0, 0, d2, None,
            None, None, L.stream())
-    np.testing.assert_allclose(host(d2), host(depth), rtol=0, atol=0)
+    # the training kernel (one wave per ray) and the render kernel (one workgroup per ray) sum the
+    # ray in different association orders: equal to a few fp32 ulps
+    np.testing.assert_allclose(host(d2), host(depth), rtol=4e-6, atol=0)
 
 
 def test_composite_inkernel_noise_matches_oracle_rng(L):
