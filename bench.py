@@ -8,7 +8,9 @@ on one ray batch: OGM sampling -> hash-grid encode -> sigma MLP -> compositing -
 backward -> [all-reduce] -> Adam (+ the OGM update every N_iters_acc=10 global steps, which falls
 inside the timed region as in the reference).  Default workload: BASELINE.json configs[1],
 Newer College quad-easy: 16 keyframes x 512 rays = 8192 rays x 512 samples, L=16 hash grid +
-64-wide MLP, synthetic analytic scene (no datasets reachable), rays resident in HBM before timing.
+64-wide MLP, synthetic analytic scene (no datasets reachable).  By default every step also selects
+and builds its rays on the device from the keyframe window's scans, which are resident in HBM
+before timing (optimizer.py:363-424; ``--rays resident`` instead cycles prebuilt ray batches).
 
 Multi-GPU (torchrun): one process per GPU, each rank optimises its own 8192-ray shard of a global
 batch of 8192*N rays (weak scaling) and the sigma gradients (7.4 M params, 29.7 MB fp32) plus the
@@ -40,7 +42,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="C2", choices=["C1", "C2", "C4"])
-    ap.add_argument("--batches", type=int, default=4, help="distinct resident ray batches cycled per rank")
+    ap.add_argument("--rays", default="device", choices=["device", "resident"],
+                    help="device: select + build each step's rays on the GPU from the resident window; "
+                         "resident: cycle prebuilt ray batches")
+    ap.add_argument("--batches", type=int, default=4, help="--rays resident: distinct batches cycled per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rays", type=int, default=64, help="rays per CPU-baseline step (x512 samples)")
     ap.add_argument("--cpu-steps", type=int, default=16)
@@ -112,15 +117,27 @@ def main():
     kind, nkf, rpk, spk, strat, n_samples, preset = syn.CONFIGS[args.config]
     scale = syn.CUBES[kind][0]
 
-    # ---- workload: distinct resident batches for this rank's shard
-    batches = []
-    for b in range(args.batches):
-        win = syn.make_window(kind, nkf, seed=1000 * rank + b, start=17 * b + 5 * rank)
-        rays, dgt = syn.build_batch(win, kind, rpk, spk, strat, seed=31 * b + rank)
-        batches.append((rays.to(dev), dgt.to(dev)))
-    R = batches[0][0].shape[0]
-    assert all(b[0].shape[0] == R for b in batches)
-    far_ref = [float(b[0][0, -1]) for b in batches]
+    # ---- workload
+    if args.rays == "device":
+        # one global keyframe window (nkf keyframes per rank), resident on every rank; rank r builds
+        # the slots of its own nkf keyframes each step (a contiguous R/g slice)
+        from loner_amd.rays import RayWindow
+        scans = syn.make_window(kind, nkf * world, seed=1000)
+        window = RayWindow(scans, syn.world_cube(kind), syn.SENSORS[kind]["ray_range"], n_lidar=rpk, n_sky=spk,
+                           strategy=strat, device=dev)
+        del scans
+        if not window.all_valid or window.n_slots % world:
+            raise RuntimeError("bench window must give a fixed, evenly sharded batch")
+        R = window.n_slots // world
+    else:
+        batches = []
+        for b in range(args.batches):
+            win = syn.make_window(kind, nkf, seed=1000 * rank + b, start=17 * b + 5 * rank)
+            rays, dgt = syn.build_batch(win, kind, rpk, spk, strat, seed=31 * b + rank)
+            batches.append((rays.to(dev), dgt.to(dev)))
+        R = batches[0][0].shape[0]
+        assert all(b[0].shape[0] == R for b in batches)
+        far_ref = [float(b[0][0, -1]) for b in batches]
 
     cfg = S_.StepConfig(n_samples=n_samples, occ_lr=1e-3 if preset == "haveri" else 1e-4,
                         loss=S_.LossConfig.from_dict(LOSS_PRESETS[preset]))
@@ -132,6 +149,8 @@ def main():
     eng = S_.StepEngine(state, R, seed=12345, allreduce=allreduce, ray_offset=rank * R)
 
     def run(i, prof=None):
+        if args.rays == "device":
+            return eng.step_window(window, global_step=i, n_rays_global=R * world, prof=prof)
         rays, dgt = batches[i % len(batches)]
         return eng.step(rays, dgt, global_step=i, scale=scale, far_ref=far_ref[i % len(batches)],
                         n_rays_global=R * world, prof=prof)
@@ -180,7 +199,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp16 params/activations, fp32 accumulate+optimizer",
-        "data": f"synthetic {kind} LiDAR scene (analytic ray-cast), rays resident in HBM; random-init sigma field",
+        "data": f"synthetic {kind} LiDAR scene (analytic ray-cast), "
+                + ("keyframe scans resident in HBM, rays selected + built on the GPU every step"
+                   if args.rays == "device" else "prebuilt rays resident in HBM") + "; random-init sigma field",
         "config": {"workload": f"{args.config}: {nkf} KF x ({rpk} + {spk} sky) rays x {n_samples} samples per GPU, "
                                f"L=16 T=2^18 hash grid + 64-wide sigma MLP, {preset} loss (L1_JS)",
                    "rays_per_gpu": R, "samples_per_ray": n_samples, "global_rays": R * world,

@@ -18,6 +18,9 @@
  *   lnr_loss_finalize             scalar loss / mean depth-eps from per-ray partials (optimizer.py:767,838-844)
  *   lnr_adam_step                 torch.optim.Adam step on the flat params  src/mapping/optimizer.py:255-265,460
  *   lnr_ogm_update                Optimizer._step_occupancy_grid  src/mapping/optimizer.py:897-908
+ *   lnr_build_lidar_rays          per-step ray selection (RANDOM / MASK / sky) + KeyFrame.build_lidar_rays
+ *                                 src/mapping/optimizer.py:363-424, src/mapping/keyframe.py:75-105,
+ *                                 src/common/ray_utils.py:31-60,269-322
  *
  * Conventions:
  *   - all data pointers are DEVICE pointers owned by the caller (PyTorch); no allocation, no host
@@ -157,6 +160,8 @@ typedef struct lnr_loss_params {
   float inv_rs;            /* 1 / (global rays * samples) */
   const float* dev_n_opaque; /* optional DEVICE scalar: global opaque count (e.g. after an all-reduce);
                                 when non-NULL it overrides inv_n_opaque (= 1/max(count,1)) */
+  const float* dev_far_ref;  /* optional DEVICE scalar overriding far_ref (rays built on the device:
+                                lnr_build_lidar_rays writes it) */
 } lnr_loss_params;
 
 /* Per-ray partial sums written by the loss kernels: [depth_sq_err, los_sum, opacity_abs_err, eps, opaque] */
@@ -199,8 +204,46 @@ int lnr_field_render(const uint16_t* w, const uint32_t* enc, int64_t enc_stride,
  * from (R, LNR_RAY_STATS). */
 int lnr_loss_finalize(const float* ray_stats, int64_t n_rays, const lnr_loss_params* lp, float* out, void* stream);
 
-/* out[0] = number of opaque rays: depth_gt > 0 && !(depth_gt > far_ref) (optimizer.py:724-727). */
-int lnr_count_opaque(const float* depth_gt, int64_t n_rays, float far_ref, float* out, void* stream);
+/* out[0] = number of opaque rays: depth_gt > 0 && !(depth_gt > far_ref) (optimizer.py:724-727).
+ * dev_far_ref: optional DEVICE scalar overriding far_ref. */
+int lnr_count_opaque(const float* depth_gt, int64_t n_rays, float far_ref, const float* dev_far_ref, float* out,
+                     void* stream);
+
+/* ---------------------------------------------------------------- ray selection + building */
+#define LNR_SELECT_RANDOM 0 /* torch.randint over each scan (optimizer.py:365-366) */
+#define LNR_SELECT_MASK 1   /* int(0.75 n) trunk points (0.5 < z_sensor < 8 m) + the rest from the other points,
+                               each without replacement (optimizer.py:367-379) */
+#define LNR_SELECT_ALL 2    /* every point of every scan, in order (LidarRayDirections.fetch_chunk_rays) */
+#define LNR_SELECT_GIVEN 3  /* caller-supplied scan-local indices, one per slot (parity tests) */
+
+/* The active keyframe window, resident on the device for the whole window.  All pointers are
+ * DEVICE pointers; counts are validated by the caller (loner_amd.rays.RayWindow). */
+typedef struct lnr_ray_window {
+  int32_t n_kf;
+  float scale;                /* WorldCube.scale_factor */
+  float shift[3];             /* WorldCube.shift */
+  float r_min, r_max;         /* ray_range (metres) */
+  const float* poses;         /* [K][12]: the 3x4 [R | t] rows of each keyframe's lidar pose (world) */
+  const float* dirs;          /* [P][3] sensor-frame ray directions (LidarScan.ray_directions, transposed) */
+  const float* dists;         /* [P] ranges (metres) */
+  const int32_t* scan_off;    /* [K+1] point offsets of each keyframe's scan in dirs / dists */
+  const int32_t* order;       /* MASK: [P] per keyframe, scan-local indices of its trunk points, then the rest */
+  const int32_t* n_trunk;     /* MASK: [K] trunk points per keyframe */
+  const float* sky_dirs;      /* [Q][3] sky directions (LidarScan.sky_rays), or NULL without sky rays */
+  const int32_t* sky_off;     /* [K+1] offsets into sky_dirs, or NULL */
+  const int32_t* ray_off;     /* [K+1] output slots of each keyframe: its LiDAR rays, then its sky rays */
+  const int32_t* n_sel;       /* [K] LiDAR slots per keyframe (slots beyond them are sky rays) */
+  const int32_t* n_sel_trunk; /* MASK: [K] LiDAR slots drawn from the trunk points */
+} lnr_ray_window;
+
+/* Build output slots [slot0, slot0 + n_slots) of the window's ray batch: rays (n_slots, 13), depth
+ * (n_slots) normalised, valid (n_slots) = far > near + 1 m / scale (the reference drops invalid rays;
+ * NULL allowed), point_index (n_slots) scan-local point of each slot (NULL allowed), far_ref (1) =
+ * far bound of the first valid slot of the WHOLE batch (NULL allowed).  Draws keyed by
+ * (key, keyframe, slot-in-keyframe): a sharded build reproduces the unsharded one slot for slot. */
+int lnr_build_lidar_rays(const lnr_ray_window* window, int32_t select, const int32_t* given, uint32_t key,
+                         int64_t slot0, int64_t n_slots, float* rays, float* depth, uint8_t* valid,
+                         int32_t* point_index, float* far_ref, void* stream);
 
 /* ---------------------------------------------------------------- optimiser */
 /* torch.optim.Adam (no weight decay); step is 1-based.  shadow (fp16) may be NULL. */

@@ -43,7 +43,18 @@ class LossParams(ctypes.Structure):
                 ("depthloss_lambda", ctypes.c_float), ("min_depth_eps", ctypes.c_float),
                 ("min_js", ctypes.c_float), ("max_js", ctypes.c_float), ("js_alpha", ctypes.c_float),
                 ("los_eps", ctypes.c_float), ("far_ref", ctypes.c_float), ("inv_n_opaque", ctypes.c_float),
-                ("inv_rs", ctypes.c_float), ("dev_n_opaque", ctypes.c_void_p)]
+                ("inv_rs", ctypes.c_float), ("dev_n_opaque", ctypes.c_void_p), ("dev_far_ref", ctypes.c_void_p)]
+
+
+SELECT = {"RANDOM": 0, "MASK": 1, "ALL": 2, "GIVEN": 3}
+
+
+class RayWindowDesc(ctypes.Structure):
+    """``lnr_ray_window``: device pointers of a resident keyframe window (loner_amd.rays.RayWindow)."""
+    _fields_ = [("n_kf", ctypes.c_int32), ("scale", ctypes.c_float), ("shift", ctypes.c_float * 3),
+                ("r_min", ctypes.c_float), ("r_max", ctypes.c_float), ("poses", c_p), ("dirs", c_p), ("dists", c_p),
+                ("scan_off", c_p), ("order", c_p), ("n_trunk", c_p), ("sky_dirs", c_p), ("sky_off", c_p),
+                ("ray_off", c_p), ("n_sel", c_p), ("n_sel_trunk", c_p)]
 
 
 _SIGNATURES = {
@@ -82,7 +93,9 @@ _SIGNATURES = {
     "lnr_field_render": (ctypes.c_int, [c_p, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_i32, c_f, c_p, c_u32, c_i64, c_p,
                                         c_p, c_p, c_p, c_p]),
     "lnr_loss_finalize": (ctypes.c_int, [c_p, c_i64, ctypes.POINTER(LossParams), c_p, c_p]),
-    "lnr_count_opaque": (ctypes.c_int, [c_p, c_i64, c_f, c_p, c_p]),
+    "lnr_count_opaque": (ctypes.c_int, [c_p, c_i64, c_f, c_p, c_p, c_p]),
+    "lnr_build_lidar_rays": (ctypes.c_int, [ctypes.POINTER(RayWindowDesc), c_i32, c_p, c_u32, c_i64, c_i64, c_p, c_p,
+                                            c_p, c_p, c_p, c_p]),
     "lnr_adam_step": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i32, c_f, c_f, c_f, c_f, c_p]),
     "lnr_ogm_update": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_f, c_f, c_p, c_p, c_i32, c_p]),
     "lnr_ogm_grad": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_i32, c_p]),

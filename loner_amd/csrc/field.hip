@@ -274,7 +274,8 @@ __device__ void composite_ray(const FieldArgs& a, const RayShared& sh, int64_t r
   const float inv_nop = lp.dev_n_opaque ? 1.0f / fmaxf(lp.dev_n_opaque[0], 1.0f) : lp.inv_n_opaque;
   const float dgt = a.depth_gt[r];
   const float g = dgt * lp.scale;
-  const bool opaque = (dgt > 0.f) && !(dgt > lp.far_ref);
+  const float far_ref = lp.dev_far_ref ? lp.dev_far_ref[0] : lp.far_ref;
+  const bool opaque = (dgt > 0.f) && !(dgt > far_ref);
   const float lvar = redB[1] / wden + 1e-10f;
   const float stdv = sqrtf(lvar);
   float eps;
@@ -614,7 +615,8 @@ __device__ void composite_loss_wave(const FieldArgs& a, float* sig, int64_t r) {
   const float inv_nop = lp.dev_n_opaque ? 1.0f / fmaxf(lp.dev_n_opaque[0], 1.0f) : lp.inv_n_opaque;
   const float dgt = a.depth_gt[r];
   const float g = dgt * lp.scale;
-  const bool opaque = (dgt > 0.f) && !(dgt > lp.far_ref);
+  const float far_ref = lp.dev_far_ref ? lp.dev_far_ref[0] : lp.far_ref;
+  const bool opaque = (dgt > 0.f) && !(dgt > far_ref);
   const float lvar = lvsum / wden + 1e-10f;
   const float stdv = sqrtf(lvar);
   float eps;
@@ -792,15 +794,9 @@ static size_t bwd_tiles_smem_bytes() {
   return b < LNR_SIGMA_MLP_PARAMS * 4 ? LNR_SIGMA_MLP_PARAMS * 4 : b;
 }
 
-// dW[i] += sum_b slab[b][i]  (fixed order: deterministic)
-// dW[i] += sum_b slab[b][i]: blockIdx.y splits the slabs into groups of 32 (one atomic per group).
-__global__ void k_reduce_slabs(const float* __restrict__ slab, int nb, float* __restrict__ dw) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= LNR_SIGMA_MLP_PARAMS) return;
-  const int b0 = blockIdx.y * 32, b1 = b0 + 32 < nb ? b0 + 32 : nb;
-  float s = 0.f;
-  for (int b = b0; b < b1; ++b) s += slab[(int64_t)b * LNR_SIGMA_MLP_PARAMS + i];
-  atomicAdd(&dw[i], s);
+// dW += the per-workgroup slabs, fixed summation order (mlp.hpp reduce_slabs_fixed)
+__global__ void __launch_bounds__(64 * kSlabWaves) k_reduce_slabs(const float* __restrict__ slab, int nb, float* __restrict__ dw) {
+  reduce_slabs_fixed(slab, nb, dw);
 }
 
 __global__ void k_loss_finalize(const float* __restrict__ st, int64_t n, lnr_loss_params lp, float* out) {
@@ -987,7 +983,7 @@ extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t e
     int e = launch_field<true, false, kSigmaMLP>(a, nb, st, "lnr_field_train");
     if (e) return e;
   }
-  hipLaunchKernelGGL(k_reduce_slabs, dim3((LNR_SIGMA_MLP_PARAMS + 255) / 256, (nb + 31) / 32), dim3(256), 0, st, workspace, nb, d_w);
+  hipLaunchKernelGGL(k_reduce_slabs, dim3((LNR_SIGMA_MLP_PARAMS + 63) / 64), dim3(64 * kSlabWaves), 0, st, workspace, nb, d_w);
   LNR_RETURN_LAUNCH("lnr_field_train(reduce)");
 }
 
@@ -1012,7 +1008,9 @@ extern "C" int lnr_field_render(const uint16_t* w, const uint32_t* enc, int64_t 
   return launch_field<false, false, kSigmaMLP>(a, nb, as_stream(stream), "lnr_field_render");
 }
 
-__global__ void k_count_opaque(const float* __restrict__ dgt, int64_t n, float far_ref, float* out) {
+__global__ void k_count_opaque(const float* __restrict__ dgt, int64_t n, float far_ref_h, const float* dev_far_ref,
+                               float* out) {
+  const float far_ref = dev_far_ref ? dev_far_ref[0] : far_ref_h;
   __shared__ float red[4];
   float c = 0.f;
   for (int64_t i = threadIdx.x; i < n; i += blockDim.x) c += (dgt[i] > 0.f && !(dgt[i] > far_ref)) ? 1.f : 0.f;
@@ -1021,10 +1019,11 @@ __global__ void k_count_opaque(const float* __restrict__ dgt, int64_t n, float f
   if (threadIdx.x == 0) out[0] = v[0];
 }
 
-extern "C" int lnr_count_opaque(const float* depth_gt, int64_t n_rays, float far_ref, float* out, void* stream) {
+extern "C" int lnr_count_opaque(const float* depth_gt, int64_t n_rays, float far_ref, const float* dev_far_ref,
+                                float* out, void* stream) {
   LNR_REQUIRE(n_rays >= 0 && out, "lnr_count_opaque: bad arguments");
   LNR_REQUIRE(n_rays == 0 || depth_gt, "lnr_count_opaque: null depth_gt");
-  hipLaunchKernelGGL(k_count_opaque, dim3(1), dim3(256), 0, as_stream(stream), depth_gt, n_rays, far_ref, out);
+  hipLaunchKernelGGL(k_count_opaque, dim3(1), dim3(256), 0, as_stream(stream), depth_gt, n_rays, far_ref, dev_far_ref, out);
   LNR_RETURN_LAUNCH("lnr_count_opaque");
 }
 

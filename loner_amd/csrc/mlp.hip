@@ -89,14 +89,9 @@ __global__ void __launch_bounds__(256) k_sigma_mlp_bwd(const uint16_t* __restric
   write_dw_slab<256>(reinterpret_cast<float*>(smem), acc, dw1, slab + (int64_t)blockIdx.x * LNR_SIGMA_MLP_PARAMS);
 }
 
-// dW[i] += sum_b slab[b][i]: blockIdx.y splits the slabs into groups of 32 (one atomic per group).
-__global__ void k_reduce_slabs_mlp(const float* __restrict__ slab, int nb, float* __restrict__ dw) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= LNR_SIGMA_MLP_PARAMS) return;
-  const int b0 = blockIdx.y * 32, b1 = b0 + 32 < nb ? b0 + 32 : nb;
-  float s = 0.f;
-  for (int b = b0; b < b1; ++b) s += slab[(int64_t)b * LNR_SIGMA_MLP_PARAMS + i];
-  atomicAdd(&dw[i], s);
+// dW += the per-workgroup slabs, fixed summation order (mlp.hpp reduce_slabs_fixed)
+__global__ void __launch_bounds__(64 * kSlabWaves) k_reduce_slabs_mlp(const float* __restrict__ slab, int nb, float* __restrict__ dw) {
+  reduce_slabs_fixed(slab, nb, dw);
 }
 
 static int mlp_blocks(int64_t n_rows) {
@@ -129,6 +124,6 @@ extern "C" int lnr_sigma_mlp_bwd(const uint16_t* w, const uint32_t* enc, int64_t
   const int nb = mlp_blocks((pairs + 3) / 4);
   hipStream_t st = as_stream(stream);
   hipLaunchKernelGGL(k_sigma_mlp_bwd, dim3(nb), dim3(256), 0, st, w, enc, enc_stride, n, d_sigma, d_enc, workspace);
-  hipLaunchKernelGGL(k_reduce_slabs_mlp, dim3((LNR_SIGMA_MLP_PARAMS + 255) / 256, (nb + 31) / 32), dim3(256), 0, st, workspace, nb, d_w);
+  hipLaunchKernelGGL(k_reduce_slabs_mlp, dim3((LNR_SIGMA_MLP_PARAMS + 63) / 64), dim3(64 * kSlabWaves), 0, st, workspace, nb, d_w);
   LNR_RETURN_LAUNCH("lnr_sigma_mlp_bwd");
 }

@@ -207,4 +207,37 @@ __device__ __forceinline__ void write_dw_slab(float* __restrict__ red, const DW0
   for (int i = threadIdx.x; i < LNR_SIGMA_MLP_PARAMS; i += NT) slab[i] = red[i];
 }
 
+
+// dW[i] += sum over the nb per-workgroup slabs of slab[b][i], in a FIXED order (bitwise
+// reproducible): workgroup x owns 64 consecutive i, each of its kSlabWaves waves sums a contiguous
+// range of slabs (256-B coalesced rows), then the wave partials are added in wave order.
+constexpr int kSlabWaves = 16;
+__device__ __forceinline__ void reduce_slabs_fixed(const float* __restrict__ slab, int nb, float* __restrict__ dw) {
+  __shared__ float part[kSlabWaves][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  const int per = (nb + kSlabWaves - 1) / kSlabWaves;
+  const int b0 = wid * per, b1 = b0 + per < nb ? b0 + per : nb;
+  float s = 0.f;
+  if (i < LNR_SIGMA_MLP_PARAMS) {
+    int b = b0;
+    for (; b + 8 <= b1; b += 8) {  // 8 rows in flight
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = slab[(int64_t)(b + u) * LNR_SIGMA_MLP_PARAMS + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; b < b1; ++b) s += slab[(int64_t)b * LNR_SIGMA_MLP_PARAMS + i];
+  }
+  part[wid][lane] = s;
+  __syncthreads();
+  if (wid == 0 && i < LNR_SIGMA_MLP_PARAMS) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < kSlabWaves; ++w) t += part[w][lane];
+    dw[i] += t;
+  }
+}
+
 }  // namespace lnr

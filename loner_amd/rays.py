@@ -88,3 +88,138 @@ def build_keyframe_rays(scan, lidar_pose, lidar_indices, ray_range, world_cube, 
         rays = torch.cat((rays, srays))
         depths = torch.cat((depths, sdepths))
     return rays, depths
+
+
+class RayWindow:
+    """The active keyframe window, resident on the GPU, from which every optimiser step selects and
+    builds its LiDAR rays on the device (``lnr_build_lidar_rays``) instead of on the CPU
+    (``Optimizer._do_iterate_optimizer``, src/mapping/optimizer.py:363-424, with
+    ``data_prep_on_cpu``).
+
+    ``scans``: one dict per keyframe with ``directions`` (3,P) sensor frame, ``distances`` (P,) metres,
+    optional ``sky_directions`` (3,Q) and ``pose`` (4,4) lidar pose (or pass ``poses``).  The
+    per-keyframe slot counts follow the reference exactly: MASK takes min(int(0.75 n), #trunk)
+    trunk points and min(n - int(0.75 n), #other) others (randperm prefixes), RANDOM takes n, and
+    ``n_sky`` sky rays are drawn when the scan has sky directions (optimizer.py:383-386).
+
+    The reference asserts that every ray origin lies inside the world cube (ray_utils.py:301-303)
+    and drops rays with far <= near + 1 m / scale (:319-322).  The first is checked here, once per
+    window; for the second the window checks once whether ANY point can be invalid (``all_valid``).
+    When none can, a step's batch has a fixed size and needs no host synchronisation."""
+
+    def __init__(self, scans, world_cube, ray_range, n_lidar=512, n_sky=0, strategy="RANDOM", poses=None,
+                 device="cuda"):
+        from . import _lib as L
+        if strategy not in ("RANDOM", "MASK"):
+            raise ValueError(f"unsupported ray selection strategy {strategy!r} (optimizer.py:363-381)")
+        self.device = torch.device(device)
+        self.strategy = strategy
+        self.n_lidar = int(n_lidar)
+        self.n_sky = int(n_sky)
+        K = len(scans)
+        if K == 0:
+            raise ValueError("empty keyframe window")
+        poses = torch.stack([s["pose"] for s in scans]) if poses is None else torch.as_tensor(poses)
+        poses = poses.detach().to("cpu", torch.float32)
+        scale = float(world_cube.scale_factor.reshape(-1)[0])
+        shift = [float(v) for v in world_cube.shift.reshape(-1)]
+        origins = (poses[:, :3, 3] + world_cube.shift.reshape(1, 3).float()) / world_cube.scale_factor.reshape(1, 1)
+        assert (origins.abs().max(dim=1)[0] > 1).sum() == 0, \
+            f"{int((origins.abs().max(dim=1)[0] > 1).sum())} ray origins are outside the world cube"
+        dirs, dists, order, n_trunk, sky, scan_off, sky_off = [], [], [], [], [], [0], [0]
+        n_sel, n_sel_trunk, n_sky_k = [], [], []
+        nt_want = int(self.n_lidar * 0.75)
+        for s in scans:
+            d = s["directions"].detach().to("cpu", torch.float32)
+            r = s["distances"].detach().to("cpu", torch.float32).reshape(-1)
+            P = r.shape[0]
+            if P == 0:
+                raise ValueError("a keyframe scan has no points")
+            dirs.append(d.T.contiguous())
+            dists.append(r)
+            scan_off.append(scan_off[-1] + P)
+            if strategy == "MASK":
+                z = (d * r)[2]  # xyz = ray_directions * distances (optimizer.py:372)
+                trunk = (0.5 < z) & (z < 8)
+                idx = torch.arange(P, dtype=torch.int32)
+                order.append(torch.cat([idx[trunk], idx[~trunk]]))
+                nt = int(trunk.sum())
+                n_trunk.append(nt)
+                ts = min(nt_want, nt)
+                n_sel_trunk.append(ts)
+                n_sel.append(ts + min(self.n_lidar - nt_want, P - nt))
+            else:
+                n_sel.append(self.n_lidar)
+            sd = s.get("sky_directions")
+            q = 0 if sd is None else int(sd.shape[1])
+            if q > 0:
+                sky.append(sd.detach().to("cpu", torch.float32).T.contiguous())
+            sky_off.append(sky_off[-1] + q)
+            n_sky_k.append(self.n_sky if (self.n_sky > 0 and q > 0) else 0)
+        dev = self.device
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.poses = poses[:, :3, :4].reshape(K, 12).contiguous().to(dev)
+        self.dirs = torch.cat(dirs).contiguous().to(dev)
+        self.dists = torch.cat(dists).contiguous().to(dev)
+        self.scan_off = torch.tensor(scan_off, **i32)
+        self.sky_dirs = torch.cat(sky).contiguous().to(dev) if sky else None
+        self.sky_off = torch.tensor(sky_off, **i32)
+        self.order = torch.cat(order).contiguous().to(dev) if order else None
+        self.n_trunk = torch.tensor(n_trunk, **i32) if order else None
+        self.n_sel_trunk = torch.tensor(n_sel_trunk, **i32) if order else None
+        self.n_sel = torch.tensor(n_sel, **i32)
+        counts = [a + b for a, b in zip(n_sel, n_sky_k)]
+        self.ray_off_host = [0]
+        for c in counts:
+            self.ray_off_host.append(self.ray_off_host[-1] + c)
+        self.ray_off = torch.tensor(self.ray_off_host, **i32)
+        self.n_slots = self.ray_off_host[-1]
+        self.n_kf = K
+        self.scale = scale
+        self.ray_range = (float(ray_range[0]), float(ray_range[1]))
+        self._L = L
+        self.desc = self._desc(self.ray_off, self.n_sel, shift)
+        # every point (and sky direction) once: can any ray of this window fail the 1 m filter?
+        all_sel = torch.tensor([scan_off[k + 1] - scan_off[k] for k in range(K)], **i32)
+        all_off = torch.tensor([scan_off[k] + sky_off[k] for k in range(K + 1)], **i32)
+        d_all = self._desc(all_off, all_sel, shift)
+        n_all = scan_off[-1] + sky_off[-1]
+        rays = torch.empty(n_all, 13, dtype=torch.float32, device=dev)
+        depth = torch.empty(n_all, dtype=torch.float32, device=dev)
+        valid = torch.empty(n_all, dtype=torch.uint8, device=dev)
+        L.call("lnr_build_lidar_rays", L.ctypes.byref(d_all), L.SELECT["ALL"], None, 0, 0, n_all, rays, depth, valid,
+               None, None, L.stream(dev))
+        self.all_valid = bool(valid.bool().all())  # the one host synchronisation per window
+
+    def _desc(self, ray_off, n_sel, shift):
+        L = self._L
+        d = L.RayWindowDesc()
+        d.n_kf = self.n_kf
+        d.scale = self.scale
+        for i in range(3):
+            d.shift[i] = shift[i]
+        d.r_min, d.r_max = self.ray_range
+        p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        d.poses, d.dirs, d.dists, d.scan_off = p(self.poses), p(self.dirs), p(self.dists), p(self.scan_off)
+        d.order, d.n_trunk, d.n_sel_trunk = p(self.order), p(self.n_trunk), p(self.n_sel_trunk)
+        d.sky_dirs, d.sky_off = p(self.sky_dirs), p(self.sky_off)
+        d.ray_off, d.n_sel = p(ray_off), p(n_sel)
+        d._keep = (ray_off, n_sel)
+        return d
+
+    def build(self, key, slot0=0, n=None, rays=None, depth=None, valid=None, point_index=None, far_ref=None,
+              given=None):
+        """Enqueue the build of slots [slot0, slot0 + n) for the step keyed by ``key``
+        (``lnr_step_key``).  Returns (rays, depth, valid, point_index, far_ref) device tensors; outputs
+        may be passed in (preallocated).  ``given``: int32 scan-local indices per slot (parity tests)."""
+        L = self._L
+        n = self.n_slots - slot0 if n is None else n
+        dev = self.device
+        rays = torch.empty(n, 13, dtype=torch.float32, device=dev) if rays is None else rays
+        depth = torch.empty(n, dtype=torch.float32, device=dev) if depth is None else depth
+        valid = torch.empty(n, dtype=torch.uint8, device=dev) if valid is None else valid
+        far_ref = torch.empty(1, dtype=torch.float32, device=dev) if far_ref is None else far_ref
+        sel = L.SELECT["GIVEN"] if given is not None else L.SELECT[self.strategy]
+        L.call("lnr_build_lidar_rays", L.ctypes.byref(self.desc), sel, given, int(key) & 0xFFFFFFFF, slot0, n, rays,
+               depth, valid, point_index, far_ref, L.stream(dev))
+        return rays, depth, valid, point_index, far_ref

@@ -177,8 +177,13 @@ class StepEngine:
         self.opacity = torch.empty(n_rays, dtype=torch.float32, device=dev)
         self.loss_out = torch.zeros(8, dtype=torch.float32, device=dev)
         self.n_opaque = torch.zeros(1, dtype=torch.float32, device=dev)
+        # on-device ray building (step_window)
+        self.rays = torch.empty(n_rays, 13, dtype=torch.float32, device=dev)
+        self.depth_gt = torch.empty(n_rays, dtype=torch.float32, device=dev)
+        self.ray_valid = torch.empty(n_rays, dtype=torch.uint8, device=dev)
+        self.far_ref = torch.empty(1, dtype=torch.float32, device=dev)
 
-    def loss_params(self, global_step, iteration_idx, scale, far_ref, n_rays_global):
+    def loss_params(self, global_step, iteration_idx, scale, far_ref, n_rays_global, dev_far_ref=None):
         lc = self.cfg.loss
         lp = L.LossParams()
         lp.kind = L.LOSS_KINDS[lc.loss_selection]
@@ -190,10 +195,11 @@ class StepEngine:
         lp.max_js = lc.max_js_score
         lp.js_alpha = lc.js_alpha
         lp.los_eps = float(lc.los_eps_at(iteration_idx))
-        lp.far_ref = float(far_ref)
+        lp.far_ref = 0.0 if far_ref is None else float(far_ref)
         lp.inv_n_opaque = 0.0
         lp.inv_rs = 1.0 / float(n_rays_global * self.S)
         lp.dev_n_opaque = self.n_opaque.data_ptr()
+        lp.dev_far_ref = None if dev_far_ref is None else dev_far_ref.data_ptr()
         return lp
 
     @staticmethod
@@ -206,24 +212,27 @@ class StepEngine:
 
     def step(self, rays, depth_gt, global_step, iteration_idx=0, scale=1.0, far_ref=None, n_rays_global=None,
              u_jitter=None, u_pdf=None, noise=None, update_ogm=None, prof=None):
-        """rays (R,13) fp32, depth_gt (R,) fp32 normalised, both on this GPU.  Returns the device loss
-        buffer [loss, mean_eps, depth_term, los_term, opacity_term, n_opaque] (no host sync).
-        ``prof``: optional dict collecting (begin, end) HIP event pairs per stage."""
+        """rays (R,13) fp32, depth_gt (R,) fp32 normalised, both on this GPU, R <= the engine's
+        capacity.  Returns the device loss buffer [loss, mean_eps, depth_term, los_term, opacity_term,
+        n_opaque] (no host sync).  ``far_ref``: the far bound of global ray 0, a float or a 1-element
+        device tensor.  ``prof``: optional dict collecting (begin, end) HIP event pairs per stage."""
         st = self.state
         cfg = self.cfg
-        R, S, N = self.n_rays, self.S, self.N
-        assert rays.shape == (R, 13) and depth_gt.shape == (R,)
+        R, S, N = rays.shape[0], self.S, self.N  # N: the level stride of enc / d_enc (capacity)
+        assert rays.shape == (R, 13) and depth_gt.shape == (R,) and R <= self.n_rays, (rays.shape, self.n_rays)
         s = L.stream(st.device)
         key = L.step_key(self.seed, global_step)
         if far_ref is None:
             raise ValueError("far_ref (far bound of global ray 0) is required; optimizer.py:724")
+        dev_far = far_ref if isinstance(far_ref, torch.Tensor) else None
+        far_h = None if dev_far is not None else float(far_ref)
         n_glob = R if n_rays_global is None else n_rays_global
         m = self._mark
         # 1. opaque count (global): local count + all-reduce
-        L.call("lnr_count_opaque", depth_gt, R, float(far_ref), self.n_opaque, s)
+        L.call("lnr_count_opaque", depth_gt, R, 0.0 if far_h is None else far_h, dev_far, self.n_opaque, s)
         if self.allreduce is not None:
             self.allreduce(self.n_opaque)
-        lp = self.loss_params(global_step, iteration_idx, scale, far_ref, n_glob)
+        lp = self.loss_params(global_step, iteration_idx, scale, far_h, n_glob, dev_far)
         # 2. sampling
         m(prof, "sample")
         if cfg.sampler == "OGM":
@@ -277,11 +286,36 @@ class StepEngine:
         st = self.state
         s = L.stream(st.device)
         if self.allreduce is None:
-            L.call("lnr_ogm_update", (rays), (self.z), (depth_gt), self.n_rays, self.S, float(scale),
+            L.call("lnr_ogm_update", (rays), (self.z), (depth_gt), rays.shape[0], self.S, float(scale),
                    self.cfg.occ_lr, (st.occ), (st.occ_ws), self.cfg.occ_res, s)
             return
         st.occ_ws.zero_()
-        L.call("lnr_ogm_grad", (rays), (self.z), (depth_gt), self.n_rays, self.S, float(scale),
+        L.call("lnr_ogm_grad", (rays), (self.z), (depth_gt), rays.shape[0], self.S, float(scale),
                (st.occ_ws), self.cfg.occ_res, s)
         self.allreduce(st.occ_ws)
         L.call("lnr_sgd_step", (st.occ), (st.occ_ws), st.occ.numel(), self.cfg.occ_lr, s)
+
+    def step_window(self, window, global_step, iteration_idx=0, n_rays_global=None, prof=None, **kw):
+        """One optimiser step whose rays are selected and built on the device from a resident
+        ``loner_amd.rays.RayWindow`` (optimizer.py:363-424 + the step above).  This rank builds the
+        window's slots [ray_offset, ray_offset + capacity).  When the window can produce invalid rays
+        (``window.all_valid`` False) they are dropped as the reference drops them, which needs the
+        batch size on the host: one synchronisation, only on such windows."""
+        key = L.step_key(self.seed, global_step)
+        m = self._mark
+        m(prof, "rays")
+        window.build(key, self.ray_offset, self.n_rays, self.rays, self.depth_gt, self.ray_valid, None, self.far_ref)
+        m(prof, "rays")
+        rays, dgt = self.rays, self.depth_gt
+        if n_rays_global is None:
+            n_rays_global = window.n_slots
+        if not window.all_valid:
+            keep = self.ray_valid.bool()
+            rays, dgt = rays[keep].contiguous(), dgt[keep].contiguous()
+            cnt = torch.tensor([float(rays.shape[0])], device=self.state.device)
+            if self.allreduce is not None:
+                self.allreduce(cnt)
+            n_rays_global = int(cnt.item())
+        return self.step(rays, dgt, global_step, iteration_idx, scale=window.scale, far_ref=self.far_ref,
+                         n_rays_global=n_rays_global, prof=prof, **kw)
+

@@ -1,0 +1,146 @@
+"""On-device ray selection + building (lnr_build_lidar_rays, loner_amd.rays.RayWindow) against the
+numpy oracle (oracle/rays.py), and the optimiser step driven by it (GPU only).
+
+Reference behaviour restated: Optimizer._do_iterate_optimizer's selection (src/mapping/optimizer.py:
+363-386), KeyFrame.build_lidar_rays (src/mapping/keyframe.py:75-105), LidarRayDirections.build_lidar_rays
++ get_far_val (src/common/ray_utils.py:31-60, 269-322)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import rays as orays
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from loner_amd import _lib
+    _lib.lib()
+    return _lib
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+def _window(kind, n_kf, seed):
+    from loner_amd import synthetic as syn
+    return syn.make_window(kind, n_kf, seed=seed), syn.world_cube(kind), syn.SENSORS[kind]["ray_range"]
+
+
+def _oracle(scans, wc, rr, strategy, n_lidar, n_sky, key):
+    sel = orays.select_window(scans, strategy, n_lidar, n_sky, key)
+    poses = [s["pose"].numpy() for s in scans]
+    rays, dep, valid = orays.build_window(scans, poses, sel, rr, float(wc.scale_factor[0]), wc.shift.numpy())
+    idx = np.concatenate([np.concatenate([li, si]) for li, si in sel])
+    return rays, dep, valid, idx
+
+
+@pytest.mark.parametrize("kind,strategy,n_sky", [("quad", "RANDOM", 0), ("forest", "MASK", 64), ("quad", "MASK", 16)])
+def test_build_matches_oracle(L, kind, strategy, n_sky):
+    from loner_amd.rays import RayWindow
+    scans, wc, rr = _window(kind, 3, seed=11)
+    win = RayWindow(scans, wc, rr, n_lidar=512, n_sky=n_sky, strategy=strategy)
+    key = L.step_key(5, 17)
+    pidx = torch.empty(win.n_slots, dtype=torch.int32, device="cuda")
+    rays, dep, valid, _, far = win.build(key, point_index=pidx)
+    o_rays, o_dep, o_valid, o_idx = _oracle(scans, wc, rr, strategy, 512, n_sky, key)
+    assert win.n_slots == len(o_idx)
+    np.testing.assert_array_equal(host(pidx), o_idx)              # selection: bit-exact
+    np.testing.assert_array_equal(host(valid).astype(bool), o_valid)
+    np.testing.assert_allclose(host(rays), o_rays, rtol=2e-6, atol=2e-7)  # fp32 matmul order (BLAS) only
+    np.testing.assert_array_equal(host(dep), o_dep)                # range / scale: one division
+    assert host(far)[0] == pytest.approx(o_rays[np.flatnonzero(o_valid)[0], 12], rel=1e-6)
+    if strategy == "MASK":  # distinct points per keyframe part (randperm prefix: no repeats)
+        off = win.ray_off_host
+        sel = host(win.n_sel)
+        for k in range(win.n_kf):
+            li = o_idx[off[k]:off[k] + sel[k]]
+            assert len(np.unique(li)) == len(li)
+
+
+def test_mask_short_trunk_counts(L):
+    """A keyframe with fewer trunk points than int(0.75 n) keeps all of them (randperm prefix of a
+    shorter list, optimizer.py:377-378): the batch shrinks exactly as the reference's does."""
+    from loner_amd.rays import RayWindow
+    scans, wc, rr = _window("quad", 2, seed=3)
+    s0 = dict(scans[0])
+    z = (s0["directions"] * s0["distances"])[2]
+    trunk = torch.nonzero((0.5 < z) & (z < 8)).reshape(-1)
+    other = torch.nonzero(~((0.5 < z) & (z < 8))).reshape(-1)
+    keep = torch.cat([trunk[:100], other[:2000]])
+    s0["directions"], s0["distances"] = s0["directions"][:, keep].contiguous(), s0["distances"][keep].contiguous()
+    scans = [s0, scans[1]]
+    win = RayWindow(scans, wc, rr, n_lidar=512, strategy="MASK")
+    assert host(win.n_sel)[0] == min(100, len(trunk)) + 128
+    key = L.step_key(1, 2)
+    pidx = torch.empty(win.n_slots, dtype=torch.int32, device="cuda")
+    win.build(key, point_index=pidx)
+    o_idx = _oracle(scans, wc, rr, "MASK", 512, 0, key)[3]
+    np.testing.assert_array_equal(host(pidx), o_idx)
+
+
+def test_sharded_build_equals_unsharded(L):
+    from loner_amd.rays import RayWindow
+    scans, wc, rr = _window("forest", 4, seed=2)
+    win = RayWindow(scans, wc, rr, n_lidar=512, n_sky=64, strategy="MASK")
+    key = L.step_key(9, 3)
+    full = [host(t) for t in win.build(key)[:3]]
+    half = win.n_slots // 2 + 7
+    a = [host(t) for t in win.build(key, 0, half)[:3]]
+    b = [host(t) for t in win.build(key, half, win.n_slots - half)[:3]]
+    for f, x, y in zip(full, a, b):
+        np.testing.assert_array_equal(f, np.concatenate([x, y]))
+
+
+def test_invalid_rays_are_dropped(L):
+    """A pose close to the world-cube face: rays leaving the cube within 1 m are invalid
+    (ray_utils.py:319-322); the window notices and step_window compacts them away."""
+    from loner_amd import step as S_
+    from loner_amd.rays import RayWindow
+    scans, wc, rr = _window("quad", 2, seed=4)
+    scale, shift = float(wc.scale_factor[0]), wc.shift.numpy()
+    s1 = dict(scans[1])
+    pose = s1["pose"].clone()
+    pose[0, 3] = float(0.9995 * scale - shift[0])  # origin x just inside the +x face
+    s1["pose"] = pose
+    scans = [scans[0], s1]
+    win = RayWindow(scans, wc, rr, n_lidar=256, strategy="RANDOM")
+    assert not win.all_valid
+    key = L.step_key(3, 1)
+    _, _, valid, _, _ = win.build(key)
+    o_valid = _oracle(scans, wc, rr, "RANDOM", 256, 0, key)[2]
+    np.testing.assert_array_equal(host(valid).astype(bool), o_valid)
+    assert 0 < o_valid.sum() < len(o_valid)
+    cfg = S_.StepConfig(n_samples=64)
+    st = S_.FieldState(cfg, device="cuda:0")
+    eng = S_.StepEngine(st, win.n_slots, seed=3)
+    out = host(eng.step_window(win, global_step=1))
+    assert np.isfinite(out[0])
+
+
+def test_step_window_equals_step_on_built_rays(L):
+    """The step driven by on-device ray building is the step on the same rays built outside it."""
+    from loner_amd import step as S_
+    from loner_amd.rays import RayWindow
+    scans, wc, rr = _window("forest", 2, seed=8)
+    win = RayWindow(scans, wc, rr, n_lidar=128, n_sky=16, strategy="MASK")
+    assert win.all_valid
+    cfg = S_.StepConfig(n_samples=128)
+    outs, grads = [], []
+    for mode in ("window", "rays"):
+        st = S_.FieldState(cfg, device="cuda:0", table_init=0.5)
+        eng = S_.StepEngine(st, win.n_slots, seed=21)
+        if mode == "window":
+            out = eng.step_window(win, global_step=4)
+        else:
+            rays, dgt, _, _, far = win.build(L.step_key(21, 4))
+            out = eng.step(rays, dgt, global_step=4, scale=win.scale, far_ref=float(host(far)[0]))
+        outs.append(host(out).copy())
+        grads.append(host(st.grad).copy())
+    np.testing.assert_array_equal(outs[0], outs[1])
+    np.testing.assert_array_equal(grads[0], grads[1])
