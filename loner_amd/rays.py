@@ -184,12 +184,21 @@ class RayWindow:
         all_off = torch.tensor([scan_off[k] + sky_off[k] for k in range(K + 1)], **i32)
         d_all = self._desc(all_off, all_sel, shift)
         n_all = scan_off[-1] + sky_off[-1]
-        rays = torch.empty(n_all, 13, dtype=torch.float32, device=dev)
-        depth = torch.empty(n_all, dtype=torch.float32, device=dev)
-        valid = torch.empty(n_all, dtype=torch.uint8, device=dev)
-        L.call("lnr_build_lidar_rays", L.ctypes.byref(d_all), L.SELECT["ALL"], None, 0, 0, n_all, rays, depth, valid,
-               None, None, L.stream(dev))
+        self._desc_all, self.n_all = d_all, n_all
+        rays, depth, valid = self.build_all()
         self.all_valid = bool(valid.bool().all())  # the one host synchronisation per window
+
+    def build_all(self):
+        """Every scan point (then every sky direction) of every keyframe, in order: the rays of
+        ``LidarRayDirections.fetch_chunk_rays`` over whole scans (ray_utils.py:262-267), unfiltered,
+        with their validity.  Returns (rays (n_all,13), depth (n_all,), valid (n_all,) uint8)."""
+        L, dev, n = self._L, self.device, self.n_all
+        rays = torch.empty(n, 13, dtype=torch.float32, device=dev)
+        depth = torch.empty(n, dtype=torch.float32, device=dev)
+        valid = torch.empty(n, dtype=torch.uint8, device=dev)
+        L.call("lnr_build_lidar_rays", L.ctypes.byref(self._desc_all), L.SELECT["ALL"], None, 0, 0, n, rays, depth,
+               valid, None, None, L.stream(dev))
+        return rays, depth, valid
 
     def _desc(self, ray_off, n_sel, shift):
         L = self._L

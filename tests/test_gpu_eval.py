@@ -1,0 +1,117 @@
+"""Inference path (loner_amd.evaluate): DepthRenderer = Model.forward(testing=True, camera=False) with
+N_samples_test = 2048 and compute_l1_depth (examples/fdt_optimize_implicit_map_utils.py:260-282),
+against the oracle on identical rays and draws (GPU only)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import hashgrid as ohg
+from oracle import mlp as omlp
+from oracle import rays as orays
+from oracle import render as orender
+from oracle import rng as orng
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from loner_amd import _lib
+    _lib.lib()
+    return _lib
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+def _state(S_):
+    st = S_.FieldState(S_.StepConfig(), device="cuda:0", table_init=0.5, seed=7)
+    torch.manual_seed(3)
+    with torch.no_grad():
+        st.params[2048:3072].mul_(8.0)  # a sigma head with contrast: surfaces along the rays
+        st.occ.normal_(0, 2)
+    st.refresh_shadow()
+    return st
+
+
+def _oracle_render(st, rays, z, key, strategy, noise_std=1.0):
+    p16 = host(st.params[:st.n_params]).astype(np.float16)
+    w0, w1, table = p16[:2048].reshape(64, 32), p16[2048:3072].reshape(16, 64), p16[3072:].reshape(-1, 2)
+    R, S = z.shape
+    xyz = (rays[:, None, 0:3] + rays[:, None, 3:6] * z[:, :, None]).astype(np.float32)
+    pos = ((xyz + np.float32(1)) / np.float32(2)).astype(np.float32).reshape(-1, 3)
+    out16, _ = omlp.forward(ohg.encode(pos, table, ohg.GridLayout(16, 2, 18, 16)), [w0, w1])
+    sig = out16[:, 0].astype(np.float32).reshape(R, S)
+    if strategy == "adjusted":  # noise forced to 0 (rendering_tcnn.py:104)
+        return orender.raw2outputs_adjusted(sig, z, rays[:, 3:6])
+    a, b = orng.ray_sample_grid(np.arange(R), S)
+    noise = orng.normal(key, orng.STREAM_NOISE, a, b) * np.float32(noise_std)
+    return orender.raw2outputs(sig, z, rays[:, 3:6], noise, rays[:, -1:])
+
+
+@pytest.mark.parametrize("strategy", ["default", "adjusted"])
+def test_depth_renderer_vs_oracle(L, strategy):
+    from loner_amd import evaluate as E
+    from loner_amd import step as S_
+    from loner_amd import synthetic as syn
+    st = _state(S_)
+    scan = syn.make_window("canteen", 1, seed=5)[0]
+    keep = torch.arange(0, scan["distances"].shape[0], 97)[:96]
+    scan = dict(directions=scan["directions"][:, keep].contiguous(), distances=scan["distances"][keep].contiguous(),
+                pose=scan["pose"])
+    win = E.scan_window(scan, scan["pose"], syn.world_cube("canteen"), syn.SENSORS["canteen"]["ray_range"], "cuda:0")
+    rays, _, _ = win.build_all()
+    rend = E.DepthRenderer(st, n_samples=2048, chunk=64)  # 2 chunks: ray offsets key the draws
+    key = L.step_key(99, 0)
+    depth, opacity, var = rend.render(rays, key, strategy)
+    rn = host(rays)
+    # the sampler at test time: no jitter, random importance draws (det=False)
+    a, b = orng.ray_sample_grid(np.arange(rn.shape[0]), 1024)
+    z_ref = orender.ogm_samples(rn, 2048, host(st.occ).reshape(100, 100, 100), None,
+                                orng.uniform(key, orng.STREAM_PDF, a, b))
+    zs = []
+    for r0 in range(0, rn.shape[0], 64):  # re-render chunk by chunk to read each chunk's z
+        n = min(64, rn.shape[0] - r0)
+        L.call("lnr_sample_ogm", rays[r0:r0 + n], n, 2048, st.occ, 100, 0.0, None, None, key, r0, rend.z,
+               L.stream(st.device))
+        zs.append(host(rend.z[:n]).copy())
+    z = np.concatenate(zs)
+    dz = np.abs(z - z_ref)
+    assert (dz > 4e-6).sum() <= 2 + 1e-3 * dz.size
+    ro = _oracle_render(st, rn, z, key, strategy)
+    d = host(depth)
+    if strategy == "default":
+        np.testing.assert_allclose(d, ro["depth"], rtol=2e-4, atol=1e-6)
+    else:  # peak depth is a sample position: equal, or one sample over where T crosses 0.5 within rounding
+        assert np.mean(d != ro["depth"]) <= 0.02
+    np.testing.assert_allclose(host(opacity), ro["opacity"], rtol=1e-4, atol=1e-5)
+    l1 = np.abs(d - ro["depth"]).mean() * win.scale
+    assert l1 < (1e-3 if strategy == "default" else 0.05), l1  # metres
+
+
+def test_compute_l1_depth(L):
+    from loner_amd import evaluate as E
+    from loner_amd import step as S_
+    from loner_amd import synthetic as syn
+    st = _state(S_)
+    scan = syn.make_window("quad", 1, seed=8)[0]
+    keep = torch.arange(0, scan["distances"].shape[0], 211)
+    scan = dict(directions=scan["directions"][:, keep].contiguous(), distances=scan["distances"][keep].contiguous(),
+                pose=scan["pose"])
+    wc, rr = syn.world_cube("quad"), syn.SENSORS["quad"]["ray_range"]
+    rend = E.DepthRenderer(st, n_samples=512, chunk=256)
+    key = L.step_key(4, 4)
+    l1 = float(host(E.compute_l1_depth(rend, scan, scan["pose"], wc, rr, key)))
+    # the same metric from the renderer's depths on the oracle-built rays
+    sel = [(np.arange(scan["distances"].shape[0]), np.array([], np.int64))]
+    rays, _, valid = orays.build_window([scan], [scan["pose"].numpy()], sel, rr, float(wc.scale_factor[0]),
+                                        wc.shift.numpy())
+    depth, _, _ = rend.render(torch.from_numpy(rays).cuda(), key)
+    dist = scan["distances"].numpy()
+    good = (dist > rr[0]) & (dist < rr[1] - 0.25) & valid
+    ref = np.abs(host(depth) * np.float32(wc.scale_factor[0]) - dist)[good].mean()
+    assert l1 == pytest.approx(ref, rel=1e-4, abs=1e-3)
