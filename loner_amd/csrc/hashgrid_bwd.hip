@@ -138,7 +138,18 @@ __global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint
 // rows write records in bucket order into LDS and copy whole bucket runs out, coalesced.  Rows with
 // more than kCap records (coherent levels whose runs did not merge) write each record straight
 // to its global slot instead.
-constexpr int kCap = 4 * kSB + 256;  // 4 records per sample at fine levels, plus slack
+constexpr int kCap = 4 * kSB + 256;
+
+// Histogram row of scatter workgroup bx.  Workgroups are dealt round-robin over the 8 XCDs
+// (MI355X_MICROARCH.md, workgroup dispatch), so row r+1 would run on the XCD after row r's.  Rows r
+// and r+1 write adjacent runs in every bucket: their boundary lines are completed in one XCD's L2
+// only if both rows run there.  So XCD x takes the contiguous rows [x n/8, (x+1) n/8), in order.
+__device__ __forceinline__ int64_t xcd_row(uint32_t bx, uint32_t n) {
+#ifndef LNR_EXP_NO_XCD_ROWS
+  if ((n & 7u) == 0) return (int64_t)(bx & 7u) * (n >> 3) + (bx >> 3);
+#endif
+  return bx;
+}  // 4 records per sample at fine levels, plus slack
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -162,7 +173,7 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
   float* wmax = reinterpret_cast<float*>(start + kMaxChunksPerLevel + 1);    // [kSB / 64]
   uint8_t* sbk = reinterpret_cast<uint8_t*>(wmax + kSB / 64);                // [kCap] bucket of each staged record
   const uint32_t l = l0 + blockIdx.y;
-  const int64_t sb = blockIdx.x;
+  const int64_t sb = xcd_row(blockIdx.x, gridDim.x);
   const int64_t i = sb * kSB + threadIdx.x;
   const bool in = i < n;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;

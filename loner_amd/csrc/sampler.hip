@@ -197,6 +197,165 @@ __global__ void __launch_bounds__(SNT) k_sampler(SamplerArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// OGM sampler, one wave per ray (S/2 a multiple of 64, next power of two of S <= 2048): no
+// workgroup barriers.  Lane l owns the stratified indices [l*Q, (l+1)*Q) (Q = S/128); the cdf and
+// the bins live in this wave's LDS slice; the S depths are sorted by a bitonic network in registers
+// (E = P2/64 per lane, lane l holding sorted positions [l*E, (l+1)*E)): in-lane exchanges for
+// distances < E, __shfl_xor across lanes for the rest.  Same arithmetic as k_sampler<true>.
+template <int E>
+__device__ __forceinline__ void wave_bitonic_sort(float (&v)[E]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 2; k <= 64 * E; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j >= E) {  // partner in lane ^ (j / E), same register
+        const int dl = j / E;
+        const bool lower = (lane & dl) == 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int pos = lane * E + e;
+          const bool up = (pos & k) == 0;
+          const float o = __shfl_xor(v[e], dl, 64);
+          // the lower position keeps the min when ascending
+          v[e] = (lower == up) ? fminf(v[e], o) : fmaxf(v[e], o);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          if ((e & j) == 0) {
+            const int pos = lane * E + e;
+            const bool up = (pos & k) == 0;
+            const float x = v[e], y = v[e + j];
+            v[e] = up ? fminf(x, y) : fmaxf(x, y);
+            v[e + j] = up ? fmaxf(x, y) : fminf(x, y);
+          }
+        }
+      }
+    }
+  }
+}
+
+constexpr int kSamplerWaves = 4;
+
+template <int E>
+__global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_wave(SamplerArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int QMAX = E / 2;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int H = a.H, S = a.S, Q = H / 64, M = H - 2;
+  float* base = reinterpret_cast<float*>(smem) + (size_t)wid * (64 * E + 2 * H);
+  float* buf = base;              // [P2] stratified, then importance, then +inf padding
+  float* cdf = base + 64 * E;     // [H - 1]
+  float* bins = cdf + H;          // [H - 1]
+  for (int64_t r = (int64_t)blockIdx.x * kSamplerWaves + wid; r < a.n_rays; r += (int64_t)gridDim.x * kSamplerWaves) {
+    const float* ry = a.rays + 13 * r;
+    const float near = ry[11], far = ry[12];
+    const float ox = ry[0], oy = ry[1], oz = ry[2], dx = ry[3], dy = ry[4], dz = ry[5];
+    const uint32_t gr = (uint32_t)(a.ray_offset + r);
+    // 1. linspace + jitter (ray_sampling.py:59-72); neighbours recomputed, not exchanged
+    float zq[QMAX], pq[QMAX];
+    double wl = 0.0;
+#pragma unroll
+    for (int q = 0; q < QMAX; ++q) {
+      if (q >= Q) break;
+      const int i = lane * Q + q;
+      const float tt = linspace01(i, H);
+      float z = near * (1.0f - tt) + far * tt;
+      if (a.perturb > 0.f) {
+        const float tl = linspace01(i > 0 ? i - 1 : 0, H), tu = linspace01(i + 1 < H ? i + 1 : H - 1, H);
+        const float zl = near * (1.0f - tl) + far * tl, zu = near * (1.0f - tu) + far * tu;
+        const float upper = (i + 1 < H) ? 0.5f * (z + zu) : z;
+        const float lower = (i > 0) ? 0.5f * (zl + z) : z;
+        const float u = a.u_jitter ? a.u_jitter[r * H + i] : rand_uniform(a.key, kStreamJitter, gr, (uint32_t)i);
+        z = lower + (upper - lower) * (a.perturb * u);
+      }
+      zq[q] = z;
+      buf[i] = z;
+      // 2. occupancy probability (ray_sampling.py:74-81)
+      const float l = grid_sample(a.occ, a.occ_res, ox + dx * z, oy + dy * z, oz + dz * z);
+      float p = 1.0f / (1.0f + expf(-l));
+      p = 2.0f * (fminf(fmaxf(p, 0.5f), 1.0f) - 0.5f);
+      pq[q] = p;
+      if (i >= 1 && i <= M) wl += (double)(p + 1e-5f);  // weights = prob[1:-1] + eps
+    }
+    // 3. sample_pdf (rendering_tcnn.py:19-68): wtot, cdf = cumsum(pdf) in double
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) wl += __shfl_xor(wl, o, 64);
+    const float wtot = (float)wl;
+    double loc = 0.0;
+#pragma unroll
+    for (int q = 0; q < QMAX; ++q) {
+      if (q >= Q) break;
+      const int i = lane * Q + q;
+      if (i >= 1 && i <= M) loc += (double)((pq[q] + 1e-5f) / wtot);
+    }
+    double inc = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    double run = inc - loc;
+#pragma unroll
+    for (int q = 0; q < QMAX; ++q) {
+      if (q >= Q) break;
+      const int i = lane * Q + q;
+      if (i >= 1 && i <= M) {
+        run += (double)((pq[q] + 1e-5f) / wtot);
+        cdf[i] = (float)run;
+      }
+    }
+    if (lane == 0) cdf[0] = 0.f;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    // bins = midpoints of the jittered stratified depths (needs the next lane's first depth)
+#pragma unroll
+    for (int q = 0; q < QMAX; ++q) {
+      if (q >= Q) break;
+      const int i = lane * Q + q;
+      if (i < H - 1) bins[i] = 0.5f * (zq[q] + buf[i + 1]);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");
+    // 4. inverse CDF, searchsorted(cdf, u, right=True)
+    for (int i = lane; i < H; i += 64) {
+      const float u = a.u_pdf ? a.u_pdf[r * H + i] : rand_uniform(a.key, kStreamPdf, gr, (uint32_t)i);
+      int lo = 0, hi = H - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cdf[mid] <= u) lo = mid + 1;
+        else hi = mid;
+      }
+      const int below = lo - 1 > 0 ? lo - 1 : 0;
+      const int above = lo < M ? lo : M;
+      const float c0 = cdf[below], c1 = cdf[above];
+      const float b0 = bins[below], b1 = bins[above];
+      float denom = c1 - c0;
+      if (denom < 1e-5f) denom = 1.0f;
+      buf[H + i] = b0 + (u - c0) / denom * (b1 - b0);
+    }
+    for (int i = S + lane; i < 64 * E; i += 64) buf[i] = INFINITY;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");
+    // 5. sort (torch.sort, ray_sampling.py:90) and store
+    float v[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] = buf[lane * E + e];
+    wave_bitonic_sort<E>(v);
+    float* zr = a.z + r * S;
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (lane * E + e < S) zr[lane * E + e] = v[e];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");  // buf is rewritten by the next ray
+  }
+}
+
+static size_t sampler_wave_smem(int E, int H) { return (size_t)kSamplerWaves * (64 * E + 2 * H) * 4; }
+
 static size_t sampler_smem(int H, int P2) { return ((size_t)3 * H + P2 + 2) * 4 + (SNT / 64 + 2) * 8 + 16; }
 
 }  // namespace lnr
@@ -221,6 +380,20 @@ extern "C" int lnr_sample_ogm(const float* rays, int64_t n_rays, int32_t n_sampl
   while (p2 < n_samples) p2 <<= 1;
   a.P2 = p2;
   LNR_REQUIRE(a.H <= 8 * SNT, "lnr_sample_ogm: too many samples");
+  if (a.H % 64 == 0 && p2 >= 128 && p2 <= 2048) {  // one wave per ray
+    const int E = p2 / 64;
+    const int64_t nbw = (n_rays + kSamplerWaves - 1) / kSamplerWaves;
+    const dim3 g((unsigned)(nbw < 8192 ? nbw : 8192)), b(64 * kSamplerWaves);
+    const size_t sm = sampler_wave_smem(E, a.H);
+    switch (E) {
+      case 2: hipLaunchKernelGGL(k_sampler_wave<2>, g, b, sm, as_stream(stream), a); break;
+      case 4: hipLaunchKernelGGL(k_sampler_wave<4>, g, b, sm, as_stream(stream), a); break;
+      case 8: hipLaunchKernelGGL(k_sampler_wave<8>, g, b, sm, as_stream(stream), a); break;
+      case 16: hipLaunchKernelGGL(k_sampler_wave<16>, g, b, sm, as_stream(stream), a); break;
+      default: hipLaunchKernelGGL(k_sampler_wave<32>, g, b, sm, as_stream(stream), a); break;
+    }
+    LNR_RETURN_LAUNCH("lnr_sample_ogm");
+  }
   const int nb = (int)(n_rays < 4096 ? n_rays : 4096);
   hipLaunchKernelGGL(k_sampler<true>, dim3(nb), dim3(SNT), sampler_smem(a.H, p2), as_stream(stream), a);
   LNR_RETURN_LAUNCH("lnr_sample_ogm");
