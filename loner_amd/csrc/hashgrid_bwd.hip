@@ -155,7 +155,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // KIND: the levels one launch covers, so each gets only its own code and registers.
-enum : int { kLevelsCoherent = 0, kLevelsFine = 1, kLevelsGeneric = 2 };
+// kLevelsAny: one launch over every level, grid.x = rows x levels with the level fastest, so each CU
+// interleaves VALU-heavy coherent-level rows with store-heavy fine-level rows; consecutive rows of
+// one level are L blocks apart, i.e. on the same XCD when L is a multiple of 8 (see xcd_row).
+enum : int { kLevelsCoherent = 0, kLevelsFine = 1, kLevelsGeneric = 2, kLevelsAny = 3 };
 
 #ifndef LNR_SCATTER_WAVES_PER_EU
 #define LNR_SCATTER_WAVES_PER_EU 1
@@ -172,8 +175,12 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
   uint32_t* start = rank_ctr + kMaxChunksPerLevel;                           // [kMaxChunksPerLevel + 1]
   float* wmax = reinterpret_cast<float*>(start + kMaxChunksPerLevel + 1);    // [kSB / 64]
   uint8_t* sbk = reinterpret_cast<uint8_t*>(wmax + kSB / 64);                // [kCap] bucket of each staged record
-  const uint32_t l = l0 + blockIdx.y;
-  const int64_t sb = xcd_row(blockIdx.x, gridDim.x);
+  const uint32_t l = KIND == kLevelsAny ? blockIdx.x % a.n_levels : l0 + blockIdx.y;
+  const int64_t sb = KIND == kLevelsAny ? (int64_t)(blockIdx.x / a.n_levels) : xcd_row(blockIdx.x, gridDim.x);
+  const int kind = KIND != kLevelsAny ? KIND
+                   : a.lv[l].fine           ? kLevelsFine
+                   : l < a.merge_levels     ? kLevelsCoherent
+                                            : kLevelsGeneric;
   const int64_t i = sb * kSB + threadIdx.x;
   const bool in = i < n;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -224,7 +231,7 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
     if (lane == 63) start[nb] = inc;
   };
   if (threadIdx.x < kMaxChunksPerLevel) rank_ctr[threadIdx.x] = 0;
-  if constexpr (KIND == kLevelsCoherent) row_starts();  // coherent rows place as they rank
+  if (kind == kLevelsCoherent) row_starts();  // coherent rows place as they rank
   lds_barrier();
   LNR_STAMP(t1);
   float x = 0.f, y = 0.f, z = 0.f;
@@ -247,7 +254,7 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
     }
   };
   // 2. records: rank, then place (hashgrid.hpp "Backward records")
-  if constexpr (KIND == kLevelsFine) {
+  if (kind == kLevelsFine) {
     // ranks first (LDS counters only), placement after wave 0 has published the starts
     FineCell c;
     fine_cell(lv, x, y, z, c);
@@ -259,7 +266,7 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
     row_starts();
     LNR_STAMP(t1b);
     lds_barrier();
-    LNR_PHASE(5 * KIND + 4, t1b, t1);
+    LNR_PHASE(5 * kind + 4, t1b, t1);
     staged = start[nb] <= (uint32_t)kCap;  // block-uniform
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -282,7 +289,7 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
     Corners c;
     level_corners(lv, x, y, z, c);
     const uint32_t off = lv.offset;
-    if constexpr (KIND == kLevelsCoherent) {  // corner k summed over the run of lanes that share it
+    if (kind == kLevelsCoherent) {  // corner k summed over the run of lanes that share it
       staged = start[nb] <= (uint32_t)kCap;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -341,10 +348,10 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
     }
   }
   LNR_STAMP(t4);
-  LNR_PHASE(5 * KIND + 0, t1, t0);
-  LNR_PHASE(5 * KIND + 1, t2, t1);
-  LNR_PHASE(5 * KIND + 2, t3, t2);
-  LNR_PHASE(5 * KIND + 3, t4, t3);
+  LNR_PHASE(5 * kind + 0, t1, t0);
+  LNR_PHASE(5 * kind + 1, t2, t1);
+  LNR_PHASE(5 * kind + 2, t3, t2);
+  LNR_PHASE(5 * kind + 3, t4, t3);
 }
 
 constexpr size_t kScatterLds = (size_t)kCap * 8 + kMaxChunksPerLevel * 8 + (size_t)kCap * 4 + kMaxChunksPerLevel * 4 +
@@ -535,6 +542,12 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
     const uint32_t m = a.merge_levels, L = d->n_levels;
     bool all_fine = true;
     for (uint32_t l = m; l < L; ++l) all_fine = all_fine && a.lv[l].fine;
+#ifndef LNR_EXP_SPLIT_SCATTER
+    (void)m;
+    (void)all_fine;
+    hipLaunchKernelGGL((k_bwd_scatter<PosFn, kLevelsAny>), dim3((unsigned)(w.n_sb * L)), dim3(kSB), kScatterLds, st, a,
+                       pos, n, de, stride, w, 0u);
+#else
     if (m > 0)
       hipLaunchKernelGGL((k_bwd_scatter<PosFn, kLevelsCoherent>), dim3((unsigned)w.n_sb, m), dim3(kSB), kScatterLds, st,
                          a, pos, n, de, stride, w, 0u);
@@ -546,6 +559,7 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
         hipLaunchKernelGGL((k_bwd_scatter<PosFn, kLevelsGeneric>), dim3((unsigned)w.n_sb, L - m), dim3(kSB),
                            kScatterLds, st, a, pos, n, de, stride, w, m);
     }
+#endif
   }
   hipLaunchKernelGGL(k_bwd_level_max, dim3(d->n_levels), dim3(256), 0, st, w);
   const int64_t max_slices = a.n_buckets + (8 * n * (int64_t)d->n_levels) / kSliceRecords + 1;
