@@ -750,12 +750,37 @@ __global__ void __launch_bounds__(NT) k_mlp_bwd_tiles(FieldArgs a) {
       for (int q = 0; q < 4; ++q) acc.v[t][m][q] = 0.f;
   float2* denc = reinterpret_cast<float2*>(a.d_enc);
   const int64_t N = a.n_rays * (int64_t)a.S;  // a multiple of 64
-  for (int64_t n0 = ((int64_t)blockIdx.x * kWavesPerBlock + wid) * 32; n0 < N;
-       n0 += (int64_t)gridDim.x * kWavesPerBlock * 32) {
+  // software-pipelined: the next tile pair's enc / dsigma loads are in flight while this one computes
+  // (2 waves per SIMD at this register count: latency is hidden by ILP, not by occupancy)
+  const int64_t step = (int64_t)gridDim.x * kWavesPerBlock * 32;
+  int64_t n0 = ((int64_t)blockIdx.x * kWavesPerBlock + wid) * 32;
+  const int gq = g;
+  uint32_t nx0[4], nx1[4];
+  float nds0 = 0.f, nds1 = 0.f;
+  auto prefetch = [&](int64_t m) {
+    const bool v = m < N;
+    const int64_t mm = v ? m : 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      nx0[q] = a.enc[(int64_t)(4 * gq + q) * a.enc_stride + mm + c];
+      nx1[q] = a.enc[(int64_t)(4 * gq + q) * a.enc_stride + mm + 16 + c];
+    }
+    nds0 = a.d_sigma[mm + c];
+    nds1 = a.d_sigma[mm + 16 + c];
+  };
+  prefetch(n0);
+  for (; n0 < N; n0 += step) {
     float h0[16], h1[16];
-    const half8_t e0 = load_enc_operand(a.enc, a.enc_stride, n0 + c, true);
-    const half8_t e1 = load_enc_operand(a.enc, a.enc_stride, n0 + 16 + c, true);
-    const float ds0 = a.d_sigma[n0 + c], ds1 = a.d_sigma[n0 + 16 + c];
+    half8_t e0, e1;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      e0[2 * q + 0] = __builtin_bit_cast(_Float16, (uint16_t)(nx0[q] & 0xFFFFu));
+      e0[2 * q + 1] = __builtin_bit_cast(_Float16, (uint16_t)(nx0[q] >> 16));
+      e1[2 * q + 0] = __builtin_bit_cast(_Float16, (uint16_t)(nx1[q] & 0xFFFFu));
+      e1[2 * q + 1] = __builtin_bit_cast(_Float16, (uint16_t)(nx1[q] >> 16));
+    }
+    const float ds0 = nds0, ds1 = nds1;
+    prefetch(n0 + step);
     (void)sigma_tile_fwd(sw, e0, h0);
     (void)sigma_tile_fwd(sw, e1, h1);
     float mx = 0.f;
@@ -799,8 +824,11 @@ __global__ void __launch_bounds__(64 * kSlabWaves) k_reduce_slabs(const float* _
   reduce_slabs_fixed(slab, nb, dw);
 }
 
-__global__ void k_loss_finalize(const float* __restrict__ st, int64_t n, lnr_loss_params lp, float* out) {
-  __shared__ float red[5 * 4];
+constexpr int kReduceThreads = 1024;  // single-workgroup reductions over rays: latency, not bandwidth
+
+__global__ void __launch_bounds__(kReduceThreads) k_loss_finalize(const float* __restrict__ st, int64_t n,
+                                                                  lnr_loss_params lp, float* out) {
+  __shared__ float red[5 * kReduceThreads / 64];
   double a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0;
   for (int64_t r = threadIdx.x; r < n; r += blockDim.x) {
     const float* s = st + r * LNR_RAY_STATS;
@@ -811,7 +839,7 @@ __global__ void k_loss_finalize(const float* __restrict__ st, int64_t n, lnr_los
     a4 += s[4];
   }
   float v[5] = {(float)a0, (float)a1, (float)a2, (float)a3, (float)a4};
-  block_sum<256, 5>(v, red);
+  block_sum<kReduceThreads, 5>(v, red);
   if (threadIdx.x == 0) {
     const float inv_nop = lp.dev_n_opaque ? 1.0f / fmaxf(lp.dev_n_opaque[0], 1.0f) : lp.inv_n_opaque;
     const float dterm = v[0] * inv_nop;
@@ -1008,14 +1036,14 @@ extern "C" int lnr_field_render(const uint16_t* w, const uint32_t* enc, int64_t 
   return launch_field<false, false, kSigmaMLP>(a, nb, as_stream(stream), "lnr_field_render");
 }
 
-__global__ void k_count_opaque(const float* __restrict__ dgt, int64_t n, float far_ref_h, const float* dev_far_ref,
-                               float* out) {
+__global__ void __launch_bounds__(kReduceThreads) k_count_opaque(const float* __restrict__ dgt, int64_t n,
+                                                                 float far_ref_h, const float* dev_far_ref, float* out) {
   const float far_ref = dev_far_ref ? dev_far_ref[0] : far_ref_h;
-  __shared__ float red[4];
+  __shared__ float red[kReduceThreads / 64];
   float c = 0.f;
   for (int64_t i = threadIdx.x; i < n; i += blockDim.x) c += (dgt[i] > 0.f && !(dgt[i] > far_ref)) ? 1.f : 0.f;
   float v[1] = {c};
-  block_sum<256, 1>(v, red);
+  block_sum<kReduceThreads, 1>(v, red);
   if (threadIdx.x == 0) out[0] = v[0];
 }
 
@@ -1023,7 +1051,7 @@ extern "C" int lnr_count_opaque(const float* depth_gt, int64_t n_rays, float far
                                 float* out, void* stream) {
   LNR_REQUIRE(n_rays >= 0 && out, "lnr_count_opaque: bad arguments");
   LNR_REQUIRE(n_rays == 0 || depth_gt, "lnr_count_opaque: null depth_gt");
-  hipLaunchKernelGGL(k_count_opaque, dim3(1), dim3(256), 0, as_stream(stream), depth_gt, n_rays, far_ref, dev_far_ref, out);
+  hipLaunchKernelGGL(k_count_opaque, dim3(1), dim3(kReduceThreads), 0, as_stream(stream), depth_gt, n_rays, far_ref, dev_far_ref, out);
   LNR_RETURN_LAUNCH("lnr_count_opaque");
 }
 
@@ -1031,6 +1059,6 @@ extern "C" int lnr_loss_finalize(const float* ray_stats, int64_t n_rays, const l
                                  void* stream) {
   if (int e = check_lp(lp, "lnr_loss_finalize")) return e;
   LNR_REQUIRE(ray_stats && out, "lnr_loss_finalize: null pointer");
-  hipLaunchKernelGGL(k_loss_finalize, dim3(1), dim3(256), 0, as_stream(stream), ray_stats, n_rays, *lp, out);
+  hipLaunchKernelGGL(k_loss_finalize, dim3(1), dim3(kReduceThreads), 0, as_stream(stream), ray_stats, n_rays, *lp, out);
   LNR_RETURN_LAUNCH("lnr_loss_finalize");
 }

@@ -25,7 +25,10 @@ constexpr int kMaxBuckets = 2048;
 // fixed-point partial chunks (one scale per bucket) k_bwd_finalize sums exactly: which records
 // land in which slice depends on LDS-atomic order, the integer sum does not;
 // 2^18 gives ~3 rounds of work items over the 512 resident 64 KB-LDS workgroups at C2/C4 sizes.
-constexpr int64_t kSliceRecords = 1 << 18;
+#ifndef LNR_SLICE_LOG2
+#define LNR_SLICE_LOG2 18
+#endif
+constexpr int64_t kSliceRecords = int64_t(1) << LNR_SLICE_LOG2;
 
 struct GridArgs {
   LevelParams lv[LNR_MAX_LEVELS];
