@@ -103,14 +103,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # LONER_DIST_BACKEND=gloo rehearses the multi-rank path on fewer GPUs than ranks (ranks share
+    # devices round-robin); the driver's N-GPU runs use RCCL ("nccl"), one rank per GPU.
+    backend = os.environ.get("LONER_DIST_BACKEND", "nccl")
+    gpu = local % max(torch.cuda.device_count(), 1) if backend == "gloo" else local
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
     else:
         dist = None
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", gpu)
 
     from loner_amd import step as S_
     from loner_amd import synthetic as syn
@@ -144,8 +151,8 @@ def main():
     state = S_.FieldState(cfg, device=dev)
     allreduce = None
     if dist is not None:
-        def allreduce(t):
-            dist.all_reduce(t)
+        def allreduce(t, async_op=False):
+            return dist.all_reduce(t, async_op=async_op)
     eng = S_.StepEngine(state, R, seed=12345, allreduce=allreduce, ray_offset=rank * R)
 
     def run(i, prof=None):

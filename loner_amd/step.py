@@ -164,7 +164,9 @@ class StepEngine:
         self.N = n_rays * self.S
         self.seed = seed
         self.ray_offset = ray_offset
-        self.allreduce = allreduce  # callable(tensor) summing in place across ranks, or None
+        # callable(tensor[, async_op]) summing in place across ranks (torch.distributed.all_reduce
+        # semantics), or None
+        self.allreduce = allreduce
         dev = state.device
         self.z = torch.empty(n_rays, self.S, dtype=torch.float32, device=dev)
         self.enc = torch.empty(self.cfg.n_levels, self.N, dtype=torch.int32, device=dev)
@@ -202,6 +204,16 @@ class StepEngine:
         lp.dev_far_ref = None if dev_far_ref is None else dev_far_ref.data_ptr()
         return lp
 
+    def _allreduce_async(self, t):
+        """``allreduce(t, async_op=True)`` when the hook supports it (torch.distributed's
+        all_reduce does: the returned work's wait() makes the current stream wait), else a
+        blocking call."""
+        try:
+            return self.allreduce(t, async_op=True)
+        except TypeError:
+            self.allreduce(t)
+            return None
+
     @staticmethod
     def _mark(prof, stage):
         """Record a HIP event on the current stream (the stream every kernel here is launched on)."""
@@ -230,8 +242,8 @@ class StepEngine:
         m = self._mark
         # 1. opaque count (global): local count + all-reduce
         L.call("lnr_count_opaque", depth_gt, R, 0.0 if far_h is None else far_h, dev_far, self.n_opaque, s)
-        if self.allreduce is not None:
-            self.allreduce(self.n_opaque)
+        # the count is first needed by the field kernel: its all-reduce overlaps sampling + encode
+        pending = self._allreduce_async(self.n_opaque) if self.allreduce is not None else None
         lp = self.loss_params(global_step, iteration_idx, scale, far_h, n_glob, dev_far)
         # 2. sampling
         m(prof, "sample")
@@ -248,6 +260,8 @@ class StepEngine:
         m(prof, "encode")
         # 4. fused field + loss + backward through compositing and MLP
         st.grad_mlp.zero_()  # the MLP gradient accumulates; the table gradient is overwritten below
+        if pending is not None:
+            pending.wait()  # orders the current stream after the collective (no host sync)
         m(prof, "field")
         L.call("lnr_field_train", st.mlp_f16, self.enc, N, rays, self.z, depth_gt, R, S, cfg.raw_noise_std, noise, key,
                self.ray_offset, L.ctypes.byref(lp), self.d_enc, st.grad_mlp, self.ws, self.stats, self.depth,
