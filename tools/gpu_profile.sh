@@ -1,0 +1,21 @@
+# GPU box: the committed profile set for one config (tools/refresh_profiles.py turns it into profiles/):
+#   bench.json (plain run, with cpu_baseline), prof/ (rocprofv3 --kernel-trace --stats of the same
+#   bench command), pmc/FETCH_SIZE and pmc/WRITE_SIZE (one --pmc pass each, kernel trace only).
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+CFG=${1:-C2}
+cd $R
+mkdir -p gpurun_out
+timeout -k 10 300 python bench.py --config $CFG > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -20 gpurun_out/bench.err; exit 1; }
+cat gpurun_out/bench.json
+cd /tmp && export TMPDIR=/tmp
+rm -rf $R/gpurun_out/prof $R/gpurun_out/pmc
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- \
+  python3 $R/bench.py --config $CFG --no-cpu-baseline > $R/gpurun_out/bench_prof.json 2> $R/gpurun_out/bench_prof.err \
+  || { tail -20 $R/gpurun_out/bench_prof.err; exit 1; }
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $R/gpurun_out/pmc/$c -o run -- \
+    python3 $R/bench.py --config $CFG --no-cpu-baseline --steps 10 --warmup 3 > $R/gpurun_out/pmc/$c.out 2>&1 \
+    || { echo "pmc $c failed"; tail -5 $R/gpurun_out/pmc/$c.out; exit 1; }
+done
+echo profiles done
