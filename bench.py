@@ -41,7 +41,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="C2", choices=["C1", "C2", "C4"])
+    ap.add_argument("--config", default="C2", choices=["C1", "C2", "C3", "C4"],
+                    help="C1/C2/C4: optimiser step; C3: inference render (peak depth, N_samples_test=2048)")
     ap.add_argument("--rays", default="device", choices=["device", "resident"],
                     help="device: select + build each step's rays on the GPU from the resident window; "
                          "resident: cycle prebuilt ray batches")
@@ -98,8 +99,111 @@ def cpu_baseline(cfg_name, n_rays, n_steps):
                       f"numpy oracle (oracle/step.py), {dt:.1f} s"}
 
 
+def cpu_baseline_render(kind, n_rays, S):
+    """Oracle forward render (OGM sampler, sigma field, peak compositing) on a bounded sample."""
+    from oracle import hashgrid as ohg
+    from oracle import mlp as omlp
+    from oracle import render as orender
+    from oracle import rng as orng
+    from oracle import step as ostep
+    from loner_amd import synthetic as syn
+    win = syn.make_window(kind, 1, seed=99)
+    rays, _ = syn.build_batch(win, kind, n_rays, 0, "RANDOM", seed=7)
+    rays = rays.numpy()
+    field = ostep.OracleField()
+    w0, w1, table = field.split16()
+    t0 = time.perf_counter()
+    a, b = orng.ray_sample_grid(np.arange(n_rays), S // 2)
+    z = orender.ogm_samples(rays, S, field.occ, None, orng.uniform(1, orng.STREAM_PDF, a, b))
+    xyz = (rays[:, None, 0:3] + rays[:, None, 3:6] * z[:, :, None]).astype(np.float32)
+    pos = ((xyz + np.float32(1)) / np.float32(2)).astype(np.float32).reshape(-1, 3)
+    out16, _ = omlp.forward(ohg.encode(pos, table, field.layout), [w0, w1])
+    orender.raw2outputs_adjusted(out16[:, 0].astype(np.float32).reshape(n_rays, S), z, rays[:, 3:6])
+    dt = time.perf_counter() - t0
+    return {"value": n_rays * S / dt, "unit": "ray-samples/s", "cores": 1, "kind": "port",
+            "sample": f"one render of {n_rays} rays x {S} samples (C3 scene), numpy oracle, {dt:.1f} s"}
+
+
+def bench_render(args):
+    """C3 (BASELINE.json configs[2]): inference rendering, Model.forward(testing=True) shape -- 4096 rays
+    (one chunk, analysis/fdt_analysis_render_trajectory.py:40) x 2048 samples, peak ('adjusted')
+    depth.  Sigma head only: the colour head is not on the fused path."""
+    from loner_amd import evaluate as E
+    from loner_amd import step as S_
+    from loner_amd import synthetic as syn
+    from loner_amd import _lib as L
+    from loner_amd.rays import RayWindow
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    kind, nkf, rpk, spk, strat, S, preset = syn.CONFIGS["C3"]
+    window = RayWindow(syn.make_window(kind, nkf, seed=1000), syn.world_cube(kind), syn.SENSORS[kind]["ray_range"],
+                       n_lidar=rpk, strategy=strat, device=dev)
+    R = window.n_slots
+    state = S_.FieldState(S_.StepConfig(n_samples=S), device=dev)
+    rend = E.DepthRenderer(state, n_samples=S, chunk=R)
+    rays = torch.empty(R, 13, dtype=torch.float32, device=dev)
+    dgt = torch.empty(R, dtype=torch.float32, device=dev)
+    outs = [torch.empty(R, dtype=torch.float32, device=dev) for _ in range(3)]
+    st = L.stream(dev)
+    ev = {}
+
+    def mark(k):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        ev.setdefault(k, []).append(e)
+
+    def run(i, prof):
+        key = L.step_key(7, i)
+        window.build(key, 0, R, rays, dgt)
+        if prof:
+            mark("sample")
+        L.call("lnr_sample_ogm", rays, R, S, state.occ, 100, 0.0, None, None, key, 0, rend.z, st)
+        if prof:
+            mark("sample")
+            mark("encode")
+        L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(state.desc), rays, rend.z, R, S, state.table_f16, rend.enc,
+               R * S, None, 0, st)
+        if prof:
+            mark("encode")
+            mark("render")
+        L.call("lnr_field_render", state.mlp_f16, rend.enc, R * S, rays, rend.z, R, S, 1, 1.0, None, key, 0, outs[0],
+               outs[1], outs[2], None, st)
+        if prof:
+            mark("render")
+
+    for i in range(args.warmup):
+        run(i, False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        run(args.warmup + i, True)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    stage_ms = {k: float(np.mean([v[j].elapsed_time(v[j + 1]) for j in range(0, len(v), 2)])) for k, v in ev.items()}
+    N = R * S
+    enc_ms = stage_ms["encode"]
+    achieved = 512.0 * N / (enc_ms * 1e-3) / 1e9
+    line = {"metric": "ray-samples/sec per render (inference)", "value": N * args.steps / elapsed,
+            "unit": "ray-samples/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp16 params/activations, fp32 compositing",
+            "data": f"synthetic {kind} LiDAR scene, rays built on the GPU per render; random-init sigma field",
+            "config": {"workload": f"C3: {R} rays x {S} samples, peak rendering, sigma head (L=16 T=2^18 + 64-wide MLP)",
+                       "rays": R, "samples_per_ray": S, "parallelism": "single"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "hash-grid forward (k_hashgrid_fwd), 512 B/sample of gathers",
+                         "algorithmic_bytes_per_launch": 512 * N, "ms_per_launch": enc_ms},
+            "stage_ms": stage_ms}
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_render(kind, 512, S)
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
+    if args.config == "C3":
+        return bench_render(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
