@@ -121,13 +121,15 @@ def cpu_baseline_render(kind, n_rays, S):
     orender.raw2outputs_adjusted(out16[:, 0].astype(np.float32).reshape(n_rays, S), z, rays[:, 3:6])
     dt = time.perf_counter() - t0
     return {"value": n_rays * S / dt, "unit": "ray-samples/s", "cores": 1, "kind": "port",
-            "sample": f"one render of {n_rays} rays x {S} samples (C3 scene), numpy oracle, {dt:.1f} s"}
+            "sample": f"one render of {n_rays} rays x {S} samples (C3 scene), sigma head + peak depth only, "
+                      f"numpy oracle, {dt:.1f} s"}
 
 
 def bench_render(args):
     """C3 (BASELINE.json configs[2]): inference rendering, Model.forward(testing=True) shape -- 4096 rays
     (one chunk, analysis/fdt_analysis_render_trajectory.py:40) x 2048 samples, peak ('adjusted')
-    depth.  Sigma head only: the colour head is not on the fused path."""
+    depth and the colour map (sigma head + colour head: SH4 + 2^19 HashGrid + 48->64x4->3 MLP).
+    Algorithmic bytes: 512 B/sample of sigma-grid gathers + 512 B/sample of colour-grid gathers."""
     from loner_amd import evaluate as E
     from loner_amd import step as S_
     from loner_amd import synthetic as syn
@@ -140,7 +142,9 @@ def bench_render(args):
                        n_lidar=rpk, strategy=strat, device=dev)
     R = window.n_slots
     state = S_.FieldState(S_.StepConfig(n_samples=S), device=dev)
-    rend = E.DepthRenderer(state, n_samples=S, chunk=R)
+    color = E.ColorHead.init(4, device=dev)  # nerf_config intensity_network: 4 hidden layers of 64
+    rend = E.DepthRenderer(state, n_samples=S, chunk=R, color=color)
+    rgb = torch.empty(R, 3, dtype=torch.float32, device=dev)
     rays = torch.empty(R, 13, dtype=torch.float32, device=dev)
     dgt = torch.empty(R, dtype=torch.float32, device=dev)
     outs = [torch.empty(R, dtype=torch.float32, device=dev) for _ in range(3)]
@@ -167,9 +171,18 @@ def bench_render(args):
             mark("encode")
             mark("render")
         L.call("lnr_field_render", state.mlp_f16, rend.enc, R * S, rays, rend.z, R, S, 1, 1.0, None, key, 0, outs[0],
-               outs[1], outs[2], None, st)
+               outs[1], outs[2], rend.weights, st)
         if prof:
             mark("render")
+            mark("encode_rgb")
+        L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(color.desc), rays, rend.z, R, S, color.table, rend.enc_rgb,
+               R * S, None, 0, st)
+        if prof:
+            mark("encode_rgb")
+            mark("rgb")
+        L.call("lnr_rgb_render", color.mlp, 4, rend.enc_rgb, R * S, rays, rend.weights, R, S, rgb, st)
+        if prof:
+            mark("rgb")
 
     for i in range(args.warmup):
         run(i, False)
@@ -181,19 +194,20 @@ def bench_render(args):
     elapsed = time.perf_counter() - t0
     stage_ms = {k: float(np.mean([v[j].elapsed_time(v[j + 1]) for j in range(0, len(v), 2)])) for k, v in ev.items()}
     N = R * S
-    enc_ms = stage_ms["encode"]
-    achieved = 512.0 * N / (enc_ms * 1e-3) / 1e9
+    enc_ms = stage_ms["encode"] + stage_ms["encode_rgb"]
+    achieved = 1024.0 * N / (enc_ms * 1e-3) / 1e9
     line = {"metric": "ray-samples/sec per render (inference)", "value": N * args.steps / elapsed,
             "unit": "ray-samples/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "fp16 params/activations, fp32 compositing",
             "data": f"synthetic {kind} LiDAR scene, rays built on the GPU per render; random-init sigma field",
-            "config": {"workload": f"C3: {R} rays x {S} samples, peak rendering, sigma head (L=16 T=2^18 + 64-wide MLP)",
+            "config": {"workload": f"C3: {R} rays x {S} samples, peak rendering, sigma head (L=16 T=2^18 + 64-wide "
+                                   f"MLP) + colour head (SH4 + L=16 T=2^19 + 48->64x4->3 MLP)",
                        "rays": R, "samples_per_ray": S, "parallelism": "single"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "hash-grid forward (k_hashgrid_fwd), 512 B/sample of gathers",
-                         "algorithmic_bytes_per_launch": 512 * N, "ms_per_launch": enc_ms},
+                         "kernel": "hash-grid forwards (k_hashgrid_fwd, sigma + colour grids), 1024 B/sample of gathers",
+                         "algorithmic_bytes_per_launch": 1024 * N, "ms_per_launch": enc_ms},
             "stage_ms": stage_ms}
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_render(kind, 512, S)

@@ -18,6 +18,8 @@
  *   lnr_loss_finalize             scalar loss / mean depth-eps from per-ray partials (optimizer.py:767,838-844)
  *   lnr_adam_step                 torch.optim.Adam step on the flat params  src/mapping/optimizer.py:255-265,460
  *   lnr_ogm_update                Optimizer._step_occupancy_grid  src/mapping/optimizer.py:897-908
+ *   lnr_rgb_render                colour head (SH4 + 2^19 HashGrid + FullyFusedMLP) + colour map
+ *                                 src/models/nerf_tcnn.py:80-95, src/models/rendering_tcnn.py:283-289
  *   lnr_build_lidar_rays          per-step ray selection (RANDOM / MASK / sky) + KeyFrame.build_lidar_rays
  *                                 src/mapping/optimizer.py:363-424, src/mapping/keyframe.py:75-105,
  *                                 src/common/ray_utils.py:31-60,269-322
@@ -200,6 +202,14 @@ int lnr_field_render(const uint16_t* w, const uint32_t* enc, int64_t enc_stride,
                      int64_t n_rays, int32_t n_samples, int32_t strategy, float noise_std, const float* noise,
                      uint32_t key, int64_t ray_offset, float* depth, float* opacity, float* variance,
                      float* weights, void* stream);
+/* Colour head forward + colour map (DecoupledNeRF colour branch nerf_tcnn.py:80-95, raw2outputs
+ * rendering_tcnn.py:283-289): w_rgb = tcnn flat fp16 params of the 48 -> 64 x n_hidden_layers -> 3
+ * FullyFusedMLP (1..4 hidden layers), enc_rgb = level-major colour hash-grid encodings (16 levels x 2),
+ * weights (R,S) = the sigma pass's compositing weights (lnr_field_render).  Directions = rays[:, 6:9]
+ * (SH degree 4 of (viewdir + 1) / 2).  rgb (R,3) = sum_i w_i sigmoid(c_i) + 1 - sum_i w_i. */
+int lnr_rgb_render(const uint16_t* w_rgb, int32_t n_hidden_layers, const uint32_t* enc_rgb, int64_t enc_stride,
+                   const float* rays, const float* weights, int64_t n_rays, int32_t n_samples, float* rgb,
+                   void* stream);
 /* out[0] = loss, out[1] = mean eps, out[2..4] = depth/los/opacity terms, out[5] = opaque count,
  * from (R, LNR_RAY_STATS). */
 int lnr_loss_finalize(const float* ray_stats, int64_t n_rays, const lnr_loss_params* lp, float* out, void* stream);

@@ -92,6 +92,7 @@ _SIGNATURES = {
                                        ctypes.POINTER(LossParams), c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "lnr_field_render": (ctypes.c_int, [c_p, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_i32, c_f, c_p, c_u32, c_i64, c_p,
                                         c_p, c_p, c_p, c_p]),
+    "lnr_rgb_render": (ctypes.c_int, [c_p, c_i32, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_p, c_p]),
     "lnr_loss_finalize": (ctypes.c_int, [c_p, c_i64, ctypes.POINTER(LossParams), c_p, c_p]),
     "lnr_count_opaque": (ctypes.c_int, [c_p, c_i64, c_f, c_p, c_p, c_p]),
     "lnr_build_lidar_rays": (ctypes.c_int, [ctypes.POINTER(RayWindowDesc), c_i32, c_p, c_u32, c_i64, c_i64, c_p, c_p,

@@ -28,10 +28,48 @@ from .rays import RayWindow
 _STRATEGY = {"default": 0, "adjusted": 1}
 
 
-class DepthRenderer:
-    """Forward-only depth rendering of a ``loner_amd.step.FieldState``."""
+class ColorHead:
+    """The colour branch of DecoupledNeRF (nerf_tcnn.py:40-52,80-95) for rendering: the T=2^19
+    colour HashGrid table and the 48 -> 64 x n_hidden_layers -> 3 FullyFusedMLP, both fp16 on the
+    GPU in tcnn's flat layouts.  ``table`` / ``mlp`` are the ``params`` of the reference's
+    ``_pos_encoding`` and ``_model_intensity`` modules (or of loner_amd.tcnn's), in any float dtype."""
 
-    def __init__(self, state, n_samples=2048, chunk=8192, raw_noise_std=1.0, sampler="OGM"):
+    def __init__(self, table, mlp, n_hidden_layers=4, n_levels=16, log2_hashmap_size=19, base_resolution=16,
+                 device="cuda"):
+        self.desc = L.grid_desc(n_levels, 2, log2_hashmap_size, base_resolution, 2.0)
+        self.n_hidden_layers = int(n_hidden_layers)
+        n_mlp = 64 * 48 + (self.n_hidden_layers - 1) * 64 * 64 + 16 * 64
+        if table.numel() != 2 * self.desc.n_entries or mlp.numel() != n_mlp:
+            raise RuntimeError(f"colour head sizes: table {table.numel()} (want {2 * self.desc.n_entries}), "
+                               f"mlp {mlp.numel()} (want {n_mlp})")
+        self.table = table.detach().reshape(-1).to(device, torch.float16).contiguous()
+        self.mlp = mlp.detach().reshape(-1).to(device, torch.float16).contiguous()
+        self.n_levels = n_levels
+
+    @staticmethod
+    def init(n_hidden_layers=4, seed=1337, device="cuda"):
+        """tcnn-style initialisation: table U(-1e-4, 1e-4), Xavier-uniform layers (counter-based draws)."""
+        import math
+        desc = L.grid_desc(16, 2, 19, 16, 2.0)
+        dev = torch.device(device)
+        s = L.stream(dev)
+        table = torch.empty(2 * desc.n_entries, dtype=torch.float32, device=dev)
+        L.call("lnr_fill_uniform", table, table.numel(), seed, -1e-4, 1e-4, 0, s)
+        shapes = [(64, 48)] + [(64, 64)] * (n_hidden_layers - 1) + [(16, 64)]
+        parts = []
+        for k, (o, i) in enumerate(shapes):
+            a = math.sqrt(6.0 / (o + i))
+            w = torch.empty(o * i, dtype=torch.float32, device=dev)
+            L.call("lnr_fill_uniform", w, o * i, seed + 1 + k, -a, a, 0, s)
+            parts.append(w)
+        return ColorHead(table, torch.cat(parts), n_hidden_layers, device=dev)
+
+
+class DepthRenderer:
+    """Forward-only rendering of a ``loner_amd.step.FieldState``: depth / opacity / variance, and
+    the colour map when a ``ColorHead`` is given (Model.forward(testing=True, camera=True))."""
+
+    def __init__(self, state, n_samples=2048, chunk=8192, raw_noise_std=1.0, sampler="OGM", color=None):
         if n_samples % 64:
             raise ValueError(f"n_samples={n_samples} must be a multiple of 64")
         self.state = state
@@ -42,9 +80,17 @@ class DepthRenderer:
         dev = state.device
         self.z = torch.empty(self.chunk, self.S, dtype=torch.float32, device=dev)
         self.enc = torch.empty(state.cfg.n_levels, self.chunk * self.S, dtype=torch.int32, device=dev)
+        self.color = color
+        if color is not None:
+            if self.S % 16:
+                raise ValueError("colour rendering needs n_samples % 16 == 0")
+            self.enc_rgb = torch.empty(color.n_levels, self.chunk * self.S, dtype=torch.int32, device=dev)
+            self.weights = torch.empty(self.chunk, self.S, dtype=torch.float32, device=dev)
 
-    def render(self, rays, key, strategy="default", depth=None, opacity=None, variance=None, ray_offset=0):
-        """rays (R,13) on the GPU -> depth, opacity, variance (R,) normalised units (device)."""
+    def render(self, rays, key, strategy="default", depth=None, opacity=None, variance=None, ray_offset=0,
+               rgb=None):
+        """rays (R,13) on the GPU -> depth, opacity, variance (R,) normalised units (device).  With a
+        colour head, ``rgb`` (R,3) receives the white-background colour map."""
         if strategy not in _STRATEGY:
             raise ValueError(f"Unknown render strategy: {strategy}")  # rendering_tcnn.py:404
         st = self.state
@@ -65,8 +111,16 @@ class DepthRenderer:
                 L.call("lnr_sample_uniform", rc, n, self.S, 0.0, None, key, off, self.z, s)
             L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(st.desc), rc, self.z, n, self.S, st.table_f16, self.enc,
                    stride, None, 0, s)
+            cw = self.color is not None and rgb is not None
             L.call("lnr_field_render", st.mlp_f16, self.enc, stride, rc, self.z, n, self.S, _STRATEGY[strategy],
-                   self.noise_std, None, key, off, depth[r0:r0 + n], opacity[r0:r0 + n], variance[r0:r0 + n], None, s)
+                   self.noise_std, None, key, off, depth[r0:r0 + n], opacity[r0:r0 + n], variance[r0:r0 + n],
+                   self.weights if cw else None, s)
+            if cw:
+                c = self.color
+                L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(c.desc), rc, self.z, n, self.S, c.table, self.enc_rgb,
+                       stride, None, 0, s)
+                L.call("lnr_rgb_render", c.mlp, c.n_hidden_layers, self.enc_rgb, stride, rc, self.weights, n, self.S,
+                       rgb[r0:r0 + n], s)
         return depth, opacity, variance
 
 

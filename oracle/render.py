@@ -200,3 +200,17 @@ def composite_backward(sigma, z, rays_d, noise, far, g_w, g_depth, g_opacity):
     with np.errstate(over="ignore", invalid="ignore"):
         dadsig = np.where(sig > 0, dl * np.exp(-dl * sr), 0.0)
     return dA * dadsig
+
+
+def sh4(dir01):
+    """tiny-cuda-nn SphericalHarmonics degree 4 of directions in [0,1]^3 (mapped back with 2x-1),
+    fp64 arithmetic -> fp16 (the colour head's direction encoding, nerf_tcnn.py:43,86)."""
+    x, y, z = (np.asarray(dir01, np.float32).astype(np.float64) * 2 - 1).T
+    o = np.stack([np.full_like(x, 0.28209479177387814), -0.48860251190291987 * y, 0.48860251190291987 * z,
+                  -0.48860251190291987 * x, 1.0925484305920792 * x * y, -1.0925484305920792 * y * z,
+                  0.94617469575755997 * z * z - 0.31539156525251999, -1.0925484305920792 * x * z,
+                  0.54627421529603959 * (x * x - y * y), 0.59004358992664352 * y * (-3 * x * x + y * y),
+                  2.8906114426405538 * x * y * z, 0.45704579946446572 * y * (1 - 5 * z * z),
+                  0.3731763325901154 * z * (5 * z * z - 3), 0.45704579946446572 * x * (1 - 5 * z * z),
+                  1.4453057213202769 * z * (x * x - y * y), 0.59004358992664352 * x * (-x * x + 3 * y * y)], 1)
+    return o.astype(np.float16)

@@ -115,3 +115,47 @@ def test_compute_l1_depth(L):
     good = (dist > rr[0]) & (dist < rr[1] - 0.25) & valid
     ref = np.abs(host(depth) * np.float32(wc.scale_factor[0]) - dist)[good].mean()
     assert l1 == pytest.approx(ref, rel=1e-4, abs=1e-3)
+
+
+@pytest.mark.parametrize("strategy", ["default", "adjusted"])
+def test_color_render_vs_oracle(L, strategy):
+    """Model.forward(testing=True, camera=True): the colour map from the fused colour head
+    (lnr_rgb_render) against SH4 + colour HashGrid + 48->64x4->3 MLP + sigmoid + white background
+    restated in numpy on the same samples and weights (rendering_tcnn.py:283-289)."""
+    from loner_amd import evaluate as E
+    from loner_amd import step as S_
+    from loner_amd import synthetic as syn
+    st = _state(S_)
+    color = E.ColorHead.init(4, seed=11)
+    torch.manual_seed(5)
+    with torch.no_grad():  # a colour table with structure, so colours vary along the rays
+        color.table.uniform_(-0.5, 0.5)
+    scan = syn.make_window("canteen", 1, seed=6)[0]
+    keep = torch.arange(0, scan["distances"].shape[0], 331)[:48]
+    scan = dict(directions=scan["directions"][:, keep].contiguous(), distances=scan["distances"][keep].contiguous(),
+                pose=scan["pose"])
+    win = E.scan_window(scan, scan["pose"], syn.world_cube("canteen"), syn.SENSORS["canteen"]["ray_range"], "cuda:0")
+    rays, _, _ = win.build_all()
+    R, S = rays.shape[0], 512
+    rend = E.DepthRenderer(st, n_samples=S, chunk=R, color=color)
+    key = L.step_key(12, 0)
+    rgb = torch.empty(R, 3, dtype=torch.float32, device="cuda")
+    rend.render(rays, key, strategy, rgb=rgb)
+    z, w = host(rend.z[:R]).copy(), host(rend.weights[:R]).copy()
+    rn = host(rays)
+    ro = _oracle_render(st, rn, z, key, strategy)
+    # sigma is fp16: a hidden-layer rounding flip (MFMA fp32 sum vs the oracle's fp64) moves a few weights
+    assert np.mean(np.abs(w - ro["weights"]) > 1e-6 + 1e-4 * np.abs(ro["weights"])) < 1e-3
+    xyz = (rn[:, None, 0:3] + rn[:, None, 3:6] * z[:, :, None]).astype(np.float32)
+    pos = ((xyz + np.float32(1)) / np.float32(2)).astype(np.float32).reshape(-1, 3)
+    h_x = ohg.encode(pos, host(color.table).reshape(-1, 2), ohg.GridLayout(16, 2, 19, 16))
+    d01 = ((rn[:, 6:9] + np.float32(1)) / np.float32(2)).astype(np.float32)
+    h_d = np.repeat(orender.sh4(d01), S, axis=0)
+    mats = omlp.unflatten(host(color.mlp), omlp.layer_shapes(48, 3, 64, 4))
+    out16, _ = omlp.forward(np.concatenate([h_x, h_d], 1), mats)
+    col = (1 / (1 + np.exp(-out16[:, :3].astype(np.float32)))).astype(np.float16).astype(np.float64).reshape(R, S, 3)
+    ref = (w[..., None].astype(np.float64) * col).sum(1) + (1 - w.astype(np.float64).sum(1, keepdims=True))
+    got = host(rgb)
+    assert np.abs(got - ref).max() < 5e-3, np.abs(got - ref).max()
+    assert np.abs(got - ref).mean() < 5e-4
+    assert got.std() > 1e-3  # the colours are not trivially constant
