@@ -19,7 +19,7 @@ loss normaliser are all-reduced over RCCL once per step.
 Rank 0 prints one JSON line (contract in the task statement), including
   roofline      hash-grid backward stage (the dominant stage) against HBM peak, algorithmic bytes
                 1024 B/sample, duration from HIP events on the launch stream
-  cpu_baseline  the numpy oracle (oracle/step.py) on a bounded sample, single host thread
+  cpu_baseline  the pure-PyTorch CPU restatement (oracle/torch_step.py) on a bounded sample, host threads
 """
 import argparse
 import json
@@ -48,8 +48,8 @@ def parse():
                          "resident: cycle prebuilt ray batches")
     ap.add_argument("--batches", type=int, default=4, help="--rays resident: distinct batches cycled per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rays", type=int, default=64, help="rays per CPU-baseline step (x512 samples)")
-    ap.add_argument("--cpu-steps", type=int, default=16)
+    ap.add_argument("--cpu-rays", type=int, default=256, help="rays per CPU-baseline step (x512 samples)")
+    ap.add_argument("--cpu-steps", type=int, default=12)
     return ap.parse_args()
 
 
@@ -80,24 +80,33 @@ def pmc_traffic(cfg_name):
 
 
 def cpu_baseline(cfg_name, n_rays, n_steps):
-    """The numpy oracle on a bounded sample of the same workload (rank 0, N=1 only)."""
-    from oracle import step as ostep
+    """The pure-PyTorch CPU restatement of the step (oracle/torch_step.py) on a bounded sample of the
+    same workload, on the host threads this job may use (rank 0, N=1 only)."""
+    from oracle import torch_step as ts
     from loner_amd import synthetic as syn
     kind, nkf, rpk, spk, strat, S, preset = syn.CONFIGS[cfg_name]
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
     win = syn.make_window(kind, 2, seed=99)
     rays, dgt = syn.build_batch(win, kind, n_rays // 2, 0, strat, seed=7)
-    rays, dgt = rays.numpy(), dgt.numpy()
-    field = ostep.OracleField()
+    field = ts.TorchField()
     scale = syn.CUBES[kind][0]
-    ostep.train_step(field, rays, dgt, scale, LOSS_PRESETS[preset], 1, n_samples=S)  # warm-up (discarded)
+    ts.train_step(field, rays, dgt, scale, LOSS_PRESETS[preset], 1, S=S)  # warm-up (discarded)
     t0 = time.perf_counter()
     for it in range(n_steps):
-        ostep.train_step(field, rays, dgt, scale, LOSS_PRESETS[preset], 2 + it, n_samples=S, key=it)
+        ts.train_step(field, rays, dgt, scale, LOSS_PRESETS[preset], 2 + it, S=S)
     dt = time.perf_counter() - t0
-    return {"value": rays.shape[0] * S * n_steps / dt, "unit": "ray-samples/s", "cores": 1, "kind": "port",
-            "sample": f"{n_steps} optimiser steps of {rays.shape[0]} rays x {S} samples ({cfg_name} scene), "
-                      f"numpy oracle (oracle/step.py), {dt:.1f} s"}
-
+    torch.set_num_threads(prev)
+    cpu = ""
+    try:
+        cpu = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    return {"value": rays.shape[0] * S * n_steps / dt, "unit": "ray-samples/s", "cores": threads, "kind": "port",
+            "sample": f"{n_steps} optimiser steps of {rays.shape[0]} rays x {S} samples ({cfg_name} scene), pure-PyTorch "
+                      f"CPU restatement (oracle/torch_step.py: forward + autograd backward + Adam), {threads} threads "
+                      f"on {cpu or 'host CPU'}, {dt:.1f} s"}
 
 def cpu_baseline_render(kind, n_rays, S):
     """Oracle forward render (OGM sampler, sigma field, peak compositing) on a bounded sample."""
