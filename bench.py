@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--batches", type=int, default=4, help="--rays resident: distinct batches cycled per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rays", type=int, default=256, help="rays per CPU-baseline step (x512 samples)")
-    ap.add_argument("--cpu-steps", type=int, default=12)
+    ap.add_argument("--cpu-steps", type=int, default=36)
     return ap.parse_args()
 
 

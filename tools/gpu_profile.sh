@@ -13,9 +13,5 @@ rm -rf $R/gpurun_out/prof $R/gpurun_out/pmc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- \
   python3 $R/bench.py --config $CFG --no-cpu-baseline > $R/gpurun_out/bench_prof.json 2> $R/gpurun_out/bench_prof.err \
   || { tail -20 $R/gpurun_out/bench_prof.err; exit 1; }
-for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $R/gpurun_out/pmc/$c -o run -- \
-    python3 $R/bench.py --config $CFG --no-cpu-baseline --steps 10 --warmup 3 > $R/gpurun_out/pmc/$c.out 2>&1 \
-    || { echo "pmc $c failed"; tail -5 $R/gpurun_out/pmc/$c.out; exit 1; }
-done
+bash $R/tools/pmc_hbm.sh || exit 1
 echo profiles done
