@@ -259,15 +259,17 @@ int lnr_build_lidar_rays(const lnr_ray_window* window, int32_t select, const int
 /* torch.optim.Adam (no weight decay); step is 1-based.  shadow (fp16) may be NULL. */
 int lnr_adam_step(float* param, uint16_t* shadow, const float* grad, float* m, float* v, int64_t n, int32_t step,
                   float lr, float beta1, float beta2, float eps, void* stream);
-/* OGM update: occ (res^3) -= lr * grid_sample^T(logits_grad(z*scale - depth_gt*scale)). grad_ws (res^3) fp32
- * is zeroed and used as accumulation workspace. */
+/* OGM update: occ (res^3) -= lr * grid_sample^T(logits_grad(z*scale - depth_gt*scale)).  grad_ws is
+ * workspace of ws_words fp32 (lnr_ogm_workspace_words(occ_res) for full speed: replicas of the grid
+ * that spread same-voxel atomics; any ws_words >= res^3 works).  It is zeroed by the call. */
+int64_t lnr_ogm_workspace_words(int32_t occ_res);
 int lnr_ogm_update(const float* rays, const float* z, const float* depth_gt, int64_t n_rays, int32_t n_samples,
-                   float scale, float lr, float* occ, float* grad_ws, int32_t occ_res, void* stream);
+                   float scale, float lr, float* occ, float* grad_ws, int64_t ws_words, int32_t occ_res, void* stream);
 
-/* Split form for data-parallel runs: grad_ws += grid_sample^T(logits_grad) (caller zeroes), then
- * occ -= lr * grad_ws after the caller has all-reduced grad_ws. */
+/* Split form for data-parallel runs: grad_ws[0:res^3] = grid_sample^T(logits_grad) (the call zeroes the
+ * workspace), then occ -= lr * grad_ws[0:res^3] after the caller has all-reduced that slice. */
 int lnr_ogm_grad(const float* rays, const float* z, const float* depth_gt, int64_t n_rays, int32_t n_samples,
-                 float scale, float* grad_ws, int32_t occ_res, void* stream);
+                 float scale, float* grad_ws, int64_t ws_words, int32_t occ_res, void* stream);
 int lnr_sgd_step(float* param, const float* grad, int64_t n, float lr, void* stream);
 
 /* ---------------------------------------------------------------- utilities */

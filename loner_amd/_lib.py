@@ -98,8 +98,9 @@ _SIGNATURES = {
     "lnr_build_lidar_rays": (ctypes.c_int, [ctypes.POINTER(RayWindowDesc), c_i32, c_p, c_u32, c_i64, c_i64, c_p, c_p,
                                             c_p, c_p, c_p, c_p]),
     "lnr_adam_step": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i32, c_f, c_f, c_f, c_f, c_p]),
-    "lnr_ogm_update": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_f, c_f, c_p, c_p, c_i32, c_p]),
-    "lnr_ogm_grad": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_i32, c_p]),
+    "lnr_ogm_workspace_words": (c_i64, [c_i32]),
+    "lnr_ogm_update": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_f, c_f, c_p, c_p, c_i64, c_i32, c_p]),
+    "lnr_ogm_grad": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_i64, c_i32, c_p]),
     "lnr_sgd_step": (ctypes.c_int, [c_p, c_p, c_i64, c_f, c_p]),
     "lnr_fill_uniform": (ctypes.c_int, [c_p, c_i64, c_u32, c_f, c_f, c_i64, c_p]),
     "lnr_f32_to_f16": (ctypes.c_int, [c_p, c_p, c_i64, c_p]),

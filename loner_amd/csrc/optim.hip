@@ -63,10 +63,15 @@ __device__ __forceinline__ float logits_grad(float x) {
   return 0.25f * fr - 2.5f * oc;
 }
 
+constexpr int32_t kOgmReplicas = 8;
+
 __global__ void __launch_bounds__(256) k_ogm_grad(const float* __restrict__ rays, const float* __restrict__ z,
                                                   const float* __restrict__ dgt, int64_t n_rays, int32_t S,
-                                                  float scale, float* __restrict__ grad, int32_t R) {
+                                                  float scale, float* __restrict__ grad, int32_t R, int32_t n_rep) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // replica of the grid this workgroup adds into: the rays of one keyframe share their first
+  // voxels, so one copy would serialise hundreds of same-address atomics at the memory side
+  grad += (int64_t)(blockIdx.x % (uint32_t)n_rep) * R * R * R;
   const int lane = threadIdx.x & 63;
   const bool valid = i < n_rays * (int64_t)S;
   float gval = 0.f, px = 0.f, py = 0.f, pz = 0.f;
@@ -107,6 +112,37 @@ __global__ void __launch_bounds__(256) k_ogm_grad(const float* __restrict__ rays
     const bool tail = (lane == 63) || ((heads >> (lane + 1)) & 1ull);
     if (tail && idx >= 0) atomicAdd(&grad[idx], p);
   }
+}
+
+// replica 0 += replicas 1..n_rep-1 (fixed order)
+__global__ void k_sum_replicas(float* __restrict__ g, int64_t nv, int32_t n_rep) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nv) return;
+  float s = g[i];
+  for (int k = 1; k < n_rep; ++k) s += g[(int64_t)k * nv + i];
+  g[i] = s;
+}
+
+static int ogm_grad_launch(const float* rays, const float* z, const float* depth_gt, int64_t n_rays, int32_t n_samples,
+                           float scale, float* grad_ws, int64_t ws_words, int32_t occ_res, hipStream_t st,
+                           const char* who) {
+  const int64_t nv = (int64_t)occ_res * occ_res * occ_res;
+  LNR_REQUIRE(ws_words >= nv, "%s: grad_ws holds %lld words, needs >= %lld", who, (long long)ws_words, (long long)nv);
+  int64_t rep = ws_words / nv;
+  const int32_t n_rep = (int32_t)(rep > kOgmReplicas ? kOgmReplicas : rep);
+  if (hipMemsetAsync(grad_ws, 0, (size_t)n_rep * nv * sizeof(float), st) != hipSuccess) {
+    set_error("%s: hipMemsetAsync failed", who);
+    return LNR_ERR_HIP;
+  }
+  const int64_t n = n_rays * (int64_t)n_samples;
+  if (n > 0) {
+    LNR_REQUIRE(rays && z && depth_gt, "%s: null pointer", who);
+    hipLaunchKernelGGL(k_ogm_grad, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rays, z, depth_gt, n_rays,
+                       n_samples, scale, grad_ws, occ_res, n_rep);
+  }
+  if (n_rep > 1)
+    hipLaunchKernelGGL(k_sum_replicas, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, grad_ws, nv, n_rep);
+  return LNR_OK;
 }
 
 __global__ void k_sgd(float* __restrict__ p, const float* __restrict__ g, int64_t n, float lr) {
@@ -162,35 +198,32 @@ extern "C" int lnr_adam_step(float* param, uint16_t* shadow, const float* grad, 
   LNR_RETURN_LAUNCH("lnr_adam_step");
 }
 
+extern "C" int64_t lnr_ogm_workspace_words(int32_t occ_res) {
+  if (occ_res < 1) return -1;
+  return (int64_t)kOgmReplicas * occ_res * occ_res * occ_res;
+}
+
 extern "C" int lnr_ogm_update(const float* rays, const float* z, const float* depth_gt, int64_t n_rays,
-                              int32_t n_samples, float scale, float lr, float* occ, float* grad_ws, int32_t occ_res,
-                              void* stream) {
+                              int32_t n_samples, float scale, float lr, float* occ, float* grad_ws, int64_t ws_words,
+                              int32_t occ_res, void* stream) {
   LNR_REQUIRE(n_rays >= 0 && n_samples >= 1 && occ_res >= 1, "lnr_ogm_update: bad sizes");
   LNR_REQUIRE(occ && grad_ws, "lnr_ogm_update: null grid");
   const int64_t nv = (int64_t)occ_res * occ_res * occ_res;
   hipStream_t st = as_stream(stream);
-  if (hipMemsetAsync(grad_ws, 0, nv * sizeof(float), st) != hipSuccess) {
-    set_error("lnr_ogm_update: hipMemsetAsync failed");
-    return LNR_ERR_HIP;
-  }
-  const int64_t n = n_rays * (int64_t)n_samples;
-  if (n > 0) {
-    LNR_REQUIRE(rays && z && depth_gt, "lnr_ogm_update: null pointer");
-    hipLaunchKernelGGL(k_ogm_grad, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rays, z, depth_gt, n_rays,
-                       n_samples, scale, grad_ws, occ_res);
-  }
+  if (int e = ogm_grad_launch(rays, z, depth_gt, n_rays, n_samples, scale, grad_ws, ws_words, occ_res, st,
+                              "lnr_ogm_update"))
+    return e;
   hipLaunchKernelGGL(k_sgd, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, occ, grad_ws, nv, lr);
   LNR_RETURN_LAUNCH("lnr_ogm_update");
 }
 
 extern "C" int lnr_ogm_grad(const float* rays, const float* z, const float* depth_gt, int64_t n_rays,
-                            int32_t n_samples, float scale, float* grad_ws, int32_t occ_res, void* stream) {
+                            int32_t n_samples, float scale, float* grad_ws, int64_t ws_words, int32_t occ_res,
+                            void* stream) {
   LNR_REQUIRE(n_rays >= 0 && n_samples >= 1 && occ_res >= 1 && grad_ws, "lnr_ogm_grad: bad arguments");
-  const int64_t n = n_rays * (int64_t)n_samples;
-  if (n == 0) return LNR_OK;
-  LNR_REQUIRE(rays && z && depth_gt, "lnr_ogm_grad: null pointer");
-  hipLaunchKernelGGL(k_ogm_grad, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), rays, z, depth_gt,
-                     n_rays, n_samples, scale, grad_ws, occ_res);
+  if (int e = ogm_grad_launch(rays, z, depth_gt, n_rays, n_samples, scale, grad_ws, ws_words, occ_res,
+                              as_stream(stream), "lnr_ogm_grad"))
+    return e;
   LNR_RETURN_LAUNCH("lnr_ogm_grad");
 }
 

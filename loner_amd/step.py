@@ -96,7 +96,7 @@ class FieldState:
         self.v = torch.zeros_like(self.params)
         self.shadow = torch.zeros(self.n_padded, dtype=torch.float16, device=dev)
         self.occ = torch.zeros(cfg.occ_res ** 3, dtype=torch.float32, device=dev)
-        self.occ_ws = torch.zeros_like(self.occ)
+        self.occ_ws = torch.zeros(int(L.lib().lnr_ogm_workspace_words(cfg.occ_res)), dtype=torch.float32, device=dev)
         self.adam_step = 0
         self.init_params(seed, table_init)
 
@@ -301,13 +301,13 @@ class StepEngine:
         s = L.stream(st.device)
         if self.allreduce is None:
             L.call("lnr_ogm_update", (rays), (self.z), (depth_gt), rays.shape[0], self.S, float(scale),
-                   self.cfg.occ_lr, (st.occ), (st.occ_ws), self.cfg.occ_res, s)
+                   self.cfg.occ_lr, (st.occ), (st.occ_ws), st.occ_ws.numel(), self.cfg.occ_res, s)
             return
-        st.occ_ws.zero_()
         L.call("lnr_ogm_grad", (rays), (self.z), (depth_gt), rays.shape[0], self.S, float(scale),
-               (st.occ_ws), self.cfg.occ_res, s)
-        self.allreduce(st.occ_ws)
-        L.call("lnr_sgd_step", (st.occ), (st.occ_ws), st.occ.numel(), self.cfg.occ_lr, s)
+               (st.occ_ws), st.occ_ws.numel(), self.cfg.occ_res, s)
+        g = st.occ_ws[:st.occ.numel()]
+        self.allreduce(g)
+        L.call("lnr_sgd_step", (st.occ), g, st.occ.numel(), self.cfg.occ_lr, s)
 
     def step_window(self, window, global_step, iteration_idx=0, n_rays_global=None, prof=None, **kw):
         """One optimiser step whose rays are selected and built on the device from a resident

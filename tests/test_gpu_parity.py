@@ -293,15 +293,17 @@ def test_composite_loss_bwd_golden(L, tag):
     assert err < 1e-4, err
 
 
-def test_ogm_update_golden(L):
+@pytest.mark.parametrize("replicas", [False, True])
+def test_ogm_update_golden(L, replicas):
     g = np.load("tests/golden/loss_l1js_default.npz")
     occ = np.load("tests/golden/samplers.npz")["occ"]
     rays, z, dgt = g["rays"], g["z"], g["depth_gt"]
     R, S = z.shape
     grid = cu(occ.reshape(-1).copy())
-    ws = torch.empty_like(grid)
+    words = int(L.lib().lnr_ogm_workspace_words(100)) if replicas else grid.numel()
+    ws = torch.full((words,), 7.0, device="cuda")  # garbage: the call zeroes its workspace
     L.call("lnr_ogm_update", (cu(rays)), (cu(z)), (cu(dgt)), R, S, float(g["scale"]),
-           float(g["occ_lr"]), (grid), (ws), 100, L.stream())
+           float(g["occ_lr"]), (grid), (ws), words, 100, L.stream())
     delta = host(grid) - occ.reshape(-1)
     idx = g["occ_delta_idx"]
     np.testing.assert_allclose(delta[idx], g["occ_delta"], rtol=1e-3, atol=2e-7)
