@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(1024) k_hashgrid_fwd(GridArgs a, PosFn pos, in
   }
   if (COUNT) {
     lds_barrier();
-    count_block_records(a, l, c, in, hist, ws);
+    count_block_records(a, l, c, in, in, hist, ws);
   }
 }
 

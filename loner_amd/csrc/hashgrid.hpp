@@ -415,8 +415,11 @@ __device__ __forceinline__ void count_block_records_fine(const GridArgs& a, uint
   publish_block_counts(a, l, hist, ws);
 }
 
+// ``in``: the sample exists; ``act``: it has a non-zero gradient at this level (only the count
+// after the MLP backward knows; = in otherwise).  Coherent levels count every sample (zero lanes
+// merge into the runs harmlessly), the others only active ones: the scatter decides the same way.
 __device__ __forceinline__ void count_block_records(const GridArgs& a, uint32_t l, const Corners& c, bool in,
-                                                    uint32_t* hist, const BwdWorkspace& ws) {
+                                                    bool act, uint32_t* hist, const BwdWorkspace& ws) {
   const uint32_t off = a.lv[l].offset;
   if (l < a.merge_levels) {
 #pragma unroll
@@ -425,7 +428,7 @@ __device__ __forceinline__ void count_block_records(const GridArgs& a, uint32_t 
       const RunInfo ri = lane_runs_dpp(idx);  // every lane must take part in the ballot
       if (in && ri.tail) atomicAdd(&hist[(idx - off) >> kChunkLog2], 1u);  // run tails only: few lanes
     }
-  } else if (in) {
+  } else if (act) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t e0 = c.idx[2 * j] - off, e1 = c.idx[2 * j + 1] - off;

@@ -17,24 +17,33 @@
 
 namespace lnr {
 
+// Histogram after the MLP backward: samples whose d_enc is zero at a non-coherent level (ReLU'd
+// sigma: relu(sigma + noise) = 0 gives dL/dsigma = 0 exactly, typically half the samples) emit no
+// records there; the scatter skips them the same way (skip_zero).
 template <class PosFn>
-__global__ void __launch_bounds__(kSB) k_bwd_count(GridArgs a, PosFn pos, int64_t n, BwdWorkspace ws) {
+__global__ void __launch_bounds__(kSB) k_bwd_count(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ d_enc,
+                                                   int64_t stride, BwdWorkspace ws) {
   __shared__ uint32_t hist[kMaxChunksPerLevel];
   const uint32_t l = blockIdx.y;
   const int64_t i = (int64_t)blockIdx.x * kSB + threadIdx.x;
   const bool in = i < n;
   for (int b = threadIdx.x; b < kMaxChunksPerLevel; b += blockDim.x) hist[b] = 0;
   float x = 0.f, y = 0.f, z = 0.f;
-  if (in) pos(i, x, y, z);
+  bool act = false;
+  if (in) {
+    pos(i, x, y, z);
+    const float2 g = d_enc[(int64_t)l * stride + i];
+    act = g.x != 0.f || g.y != 0.f;
+  }
   lds_barrier();
   if (a.lv[l].fine) {
     FineCell c;
     fine_cell(a.lv[l], x, y, z, c);
-    count_block_records_fine(a, l, c, in, hist, ws);
+    count_block_records_fine(a, l, c, act, hist, ws);
   } else {
     Corners c;
     level_corners(a.lv[l], x, y, z, c);
-    count_block_records(a, l, c, in, hist, ws);
+    count_block_records(a, l, c, in, l < a.merge_levels ? in : act, hist, ws);
   }
 }
 
@@ -166,7 +175,8 @@ enum : int { kLevelsCoherent = 0, kLevelsFine = 1, kLevelsGeneric = 2, kLevelsAn
 template <class PosFn, int KIND>
 __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(GridArgs a, PosFn pos, int64_t n,
                                                                              const float2* __restrict__ d_enc,
-                                                                             int64_t stride, BwdWorkspace ws, uint32_t l0) {
+                                                                             int64_t stride, BwdWorkspace ws, uint32_t l0,
+                                                                             bool skip_zero) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float2* stage_v = reinterpret_cast<float2*>(smem);                         // [kCap]
   uint64_t* gbase = reinterpret_cast<uint64_t*>(stage_v + kCap);             // [kMaxChunksPerLevel]
@@ -237,6 +247,9 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
   float x = 0.f, y = 0.f, z = 0.f;
   pos.eval(raw, x, y, z);
   const float2 g = in ? g_raw : make_float2(0.f, 0.f);
+  // fine / generic levels: samples with a zero gradient emit nothing when the histogram was
+  // counted after the MLP backward (k_bwd_count, same predicate); coherent levels keep every lane
+  const bool act = in && (!skip_zero || g.x != 0.f || g.y != 0.f);
   float m = 0.f;
   bool staged = true;
   auto place = [&](bool valid, uint32_t bk, uint32_t rank, uint32_t word, float2 val) {
@@ -262,7 +275,7 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
     const uint32_t code = ((uint32_t)__popc(c.d) << kChunkLog2) | (tx_unorm16(c.tx) << 16);
     uint32_t rank[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) rank[j] = in ? atomicAdd(&rank_ctr[c.e[j] >> kChunkLog2], 1u) : 0u;
+    for (int j = 0; j < 4; ++j) rank[j] = act ? atomicAdd(&rank_ctr[c.e[j] >> kChunkLog2], 1u) : 0u;
     row_starts();
     LNR_STAMP(t1b);
     lds_barrier();
@@ -273,14 +286,14 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
       const uint32_t e0 = c.e[j];
       const float wyz = ((j & 1) ? c.ty : 1.0f - c.ty) * ((j & 2) ? c.tz : 1.0f - c.tz);
       const float w0 = split ? fine_weight(c, j, 0) : wyz;
-      place(in, e0 >> kChunkLog2, rank[j], (e0 & (kChunk - 1)) | (split ? 0u : code), make_float2(w0 * g.x, w0 * g.y));
+      place(act, e0 >> kChunkLog2, rank[j], (e0 & (kChunk - 1)) | (split ? 0u : code), make_float2(w0 * g.x, w0 * g.y));
     }
-    if (__ballot(in && split)) {  // pairs spanning two chunks: the second corners on their own
+    if (__ballot(act && split)) {  // pairs spanning two chunks: the second corners on their own
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint32_t e1 = c.e[j] ^ c.d;
         const float w1 = fine_weight(c, j, 1);
-        const bool v = in && split;
+        const bool v = act && split;
         const uint32_t r = v ? atomicAdd(&rank_ctr[e1 >> kChunkLog2], 1u) : 0u;
         place(v, e1 >> kChunkLog2, r, e1 & (kChunk - 1), make_float2(w1 * g.x, w1 * g.y));
       }
@@ -314,10 +327,10 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
         const bool pair = pairable(e0, e1);
         const float wyz = ((j & 1) ? c.ty : 1.0f - c.ty) * ((j & 2) ? c.tz : 1.0f - c.tz);
         const float w0 = pair ? wyz : c.w[2 * j];
-        const uint32_t r0 = in ? atomicAdd(&rank_ctr[e0 >> kChunkLog2], 1u) : 0u;
-        place(in, e0 >> kChunkLog2, r0, pair ? pair_word(e0, e1, txq) : (e0 & (kChunk - 1)),
+        const uint32_t r0 = act ? atomicAdd(&rank_ctr[e0 >> kChunkLog2], 1u) : 0u;
+        place(act, e0 >> kChunkLog2, r0, pair ? pair_word(e0, e1, txq) : (e0 & (kChunk - 1)),
               make_float2(w0 * g.x, w0 * g.y));
-        const bool v1 = in && !pair;
+        const bool v1 = act && !pair;
         const uint32_t r1 = v1 ? atomicAdd(&rank_ctr[e1 >> kChunkLog2], 1u) : 0u;
         place(v1, e1 >> kChunkLog2, r1, e1 & (kChunk - 1), make_float2(c.w[2 * j + 1] * g.x, c.w[2 * j + 1] * g.y));
       }
@@ -526,6 +539,7 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
   LNR_REQUIRE(n < (int64_t(1) << 31), "%s: n=%lld samples exceeds 2^31", who, (long long)n);
   BwdWorkspace w = carve_workspace(workspace, a, d, n);
   dim3 grid((unsigned)w.n_sb, d->n_levels);
+  const bool skip_zero = !(flags & LNR_BWD_COUNTS_READY);
   if (!(flags & LNR_BWD_COUNTS_READY)) {
     int64_t off, bytes;
     chunk_sum_range(d, n, &off, &bytes);
@@ -533,7 +547,8 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
       set_error("%s: hipMemsetAsync failed", who);
       return LNR_ERR_HIP;
     }
-    hipLaunchKernelGGL(k_bwd_count<PosFn>, grid, dim3(kSB), 0, st, a, pos, n, w);
+    hipLaunchKernelGGL(k_bwd_count<PosFn>, grid, dim3(kSB), 0, st, a, pos, n, reinterpret_cast<const float2*>(d_enc),
+                       stride, w);
   }
   hipLaunchKernelGGL(k_bwd_scan_rows, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
   hipLaunchKernelGGL(k_bwd_scan_buckets, dim3(1), dim3(1024), 0, st, w, a.n_buckets);
@@ -546,18 +561,18 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
     (void)m;
     (void)all_fine;
     hipLaunchKernelGGL((k_bwd_scatter<PosFn, kLevelsAny>), dim3((unsigned)(w.n_sb * L)), dim3(kSB), kScatterLds, st, a,
-                       pos, n, de, stride, w, 0u);
+                       pos, n, de, stride, w, 0u, skip_zero);
 #else
     if (m > 0)
       hipLaunchKernelGGL((k_bwd_scatter<PosFn, kLevelsCoherent>), dim3((unsigned)w.n_sb, m), dim3(kSB), kScatterLds, st,
-                         a, pos, n, de, stride, w, 0u);
+                         a, pos, n, de, stride, w, 0u, skip_zero);
     if (L > m) {
       if (all_fine)
         hipLaunchKernelGGL((k_bwd_scatter<PosFn, kLevelsFine>), dim3((unsigned)w.n_sb, L - m), dim3(kSB), kScatterLds,
-                           st, a, pos, n, de, stride, w, m);
+                           st, a, pos, n, de, stride, w, m, skip_zero);
       else
         hipLaunchKernelGGL((k_bwd_scatter<PosFn, kLevelsGeneric>), dim3((unsigned)w.n_sb, L - m), dim3(kSB),
-                           kScatterLds, st, a, pos, n, de, stride, w, m);
+                           kScatterLds, st, a, pos, n, de, stride, w, m, skip_zero);
     }
 #endif
   }
