@@ -221,12 +221,6 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
       LNR_REQUIRE(a.bucket_base[l + 1] - a.bucket_base[l] <= (uint32_t)kMaxChunksPerLevel,
                   "%s: level %u has more than %d table chunks", who, l, kMaxChunksPerLevel);
     BwdWorkspace w = carve_workspace(bwd_ws, a, d, n);
-    int64_t off, bytes;
-    chunk_sum_range(d, n, &off, &bytes);
-    if (hipMemsetAsync(reinterpret_cast<char*>(bwd_ws) + off, 0, bytes, st) != hipSuccess) {
-      set_error("%s: hipMemsetAsync failed", who);
-      return LNR_ERR_HIP;
-    }
     // one workgroup per histogram row (kSB samples) so the row is written whole
     dim3 gridc((unsigned)w.n_sb, d->n_levels);
     hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, true>), gridc, dim3(kSB), 0, st, a, pos, n,

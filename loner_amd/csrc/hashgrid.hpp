@@ -275,7 +275,7 @@ constexpr int kRowsPerChunk = 256;  // histogram rows per scan chunk
 
 struct BwdWorkspace {
   uint32_t* hist;        // per level l: [n_sb][nb_l] record counts -> exclusive offsets within bucket
-  uint32_t* chunk_sum;   // [L][n_chunks][kMaxChunksPerLevel] per-chunk column sums (zeroed by the producer)
+  uint32_t* chunk_sum;   // [L][n_chunks][kMaxChunksPerLevel] per-chunk column sums (k_bwd_chunk_sums)
   float* blockmax;       // [L][n_sb] max |record value| per row
   float* level_max;      // [LNR_MAX_LEVELS]
   uint32_t* counts;      // [kMaxBuckets]
@@ -346,12 +346,6 @@ inline BwdWorkspace carve_workspace(void* base, const GridArgs& a, const lnr_gri
   return w;
 }
 
-// Byte range of the chunk sums, which the counting producer accumulates into (zero it first).
-inline void chunk_sum_range(const lnr_grid_desc* d, int64_t n, int64_t* off, int64_t* bytes) {
-  const WsLayout L = ws_layout(d, make_args(d), n);
-  *off = L.chunk_sum;
-  *bytes = L.blockmax - L.chunk_sum;
-}
 
 __device__ __forceinline__ uint32_t* hist_row(const GridArgs& a, const BwdWorkspace& ws, uint32_t l, int64_t sb) {
   const uint32_t nb = a.bucket_base[l + 1] - a.bucket_base[l];
@@ -387,18 +381,12 @@ constexpr float kInvU16 = 1.0f / 65535.0f;
 // Per-(super-block, level) record histogram: one kSB-thread workgroup, one sample per thread.
 // Shared by the forward (training mode) and the standalone count kernel: identical corners, merge
 // and pairing decisions as the scatter kernel, so counts and ranks agree exactly.  Writes the
-// histogram row and adds it into the row's scan-chunk sums.
+// histogram row (k_bwd_chunk_sums then sums rows per scan chunk: no global atomics).
 __device__ __forceinline__ void publish_block_counts(const GridArgs& a, uint32_t l, const uint32_t* hist,
                                                      const BwdWorkspace& ws) {
   const uint32_t nb = a.bucket_base[l + 1] - a.bucket_base[l];
-  const int64_t sb = blockIdx.x;
-  uint32_t* row = hist_row(a, ws, l, sb);
-  uint32_t* cs = ws.chunk_sum + ((int64_t)l * ws.n_chunks + sb / kRowsPerChunk) * kMaxChunksPerLevel;
-  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
-    const uint32_t v = hist[b];
-    row[b] = v;
-    if (v) atomicAdd(&cs[b], v);
-  }
+  uint32_t* row = hist_row(a, ws, l, blockIdx.x);
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) row[b] = hist[b];
 }
 
 // Fine levels: one record per x-pair, two when the pair spans two chunks (d >= kChunk).

@@ -47,6 +47,25 @@ __global__ void __launch_bounds__(kSB) k_bwd_count(GridArgs a, PosFn pos, int64_
   }
 }
 
+// Column sums of the histogram rows of one scan chunk (kRowsPerChunk rows); grid (n_chunks, L).
+__global__ void __launch_bounds__(kMaxChunksPerLevel) k_bwd_chunk_sums(GridArgs a, BwdWorkspace ws) {
+  const uint32_t l = blockIdx.y, ch = blockIdx.x, c = threadIdx.x;
+  const uint32_t nb = a.bucket_base[l + 1] - a.bucket_base[l];
+  if (c >= nb) return;
+  const uint32_t* col = ws.hist + (int64_t)a.bucket_base[l] * ws.n_sb + c;
+  const int64_t r0 = (int64_t)ch * kRowsPerChunk;
+  const int64_t r1 = r0 + kRowsPerChunk < ws.n_sb ? r0 + kRowsPerChunk : ws.n_sb;
+  uint32_t s = 0;
+  for (int64_t r = r0; r < r1; r += 16) {  // 16 row loads in flight
+    uint32_t v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = r + u < r1 ? col[(r + u) * nb] : 0u;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) s += v[u];
+  }
+  ws.chunk_sum[((int64_t)l * ws.n_chunks + ch) * kMaxChunksPerLevel + c] = s;
+}
+
 // Exclusive prefix of every bucket column over the histogram rows of one scan chunk, offset by
 // the preceding chunks' sums; chunk 0 also writes the bucket totals.  One thread per column,
 // rows read whole (coalesced); grid (n_chunks, L).
@@ -541,15 +560,10 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
   dim3 grid((unsigned)w.n_sb, d->n_levels);
   const bool skip_zero = !(flags & LNR_BWD_COUNTS_READY);
   if (!(flags & LNR_BWD_COUNTS_READY)) {
-    int64_t off, bytes;
-    chunk_sum_range(d, n, &off, &bytes);
-    if (hipMemsetAsync(reinterpret_cast<char*>(workspace) + off, 0, bytes, st) != hipSuccess) {
-      set_error("%s: hipMemsetAsync failed", who);
-      return LNR_ERR_HIP;
-    }
     hipLaunchKernelGGL(k_bwd_count<PosFn>, grid, dim3(kSB), 0, st, a, pos, n, reinterpret_cast<const float2*>(d_enc),
                        stride, w);
   }
+  hipLaunchKernelGGL(k_bwd_chunk_sums, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
   hipLaunchKernelGGL(k_bwd_scan_rows, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
   hipLaunchKernelGGL(k_bwd_scan_buckets, dim3(1), dim3(1024), 0, st, w, a.n_buckets);
   {

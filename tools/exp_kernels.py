@@ -44,7 +44,7 @@ def main():
     R = rays.shape[0]
     cfg = S_.StepConfig(n_samples=n_samples, loss=S_.LossConfig.from_dict(bench.LOSS_PRESETS[preset]))
     st = S_.FieldState(cfg, device=dev)
-    eng = S_.StepEngine(st, R, seed=1, count_in_forward=os.environ.get("EXP_FWD_COUNT") == "1")
+    eng = S_.StepEngine(st, R, seed=1, count_in_forward=os.environ.get("EXP_FWD_COUNT", "1") == "1")
     scale = syn.CUBES[kind][0]
     far = float(rays[0, -1])
     for i in range(3):
