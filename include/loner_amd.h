@@ -20,6 +20,8 @@
  *   lnr_ogm_update                Optimizer._step_occupancy_grid  src/mapping/optimizer.py:897-908
  *   lnr_rgb_render                colour head (SH4 + 2^19 HashGrid + FullyFusedMLP) + colour map
  *                                 src/models/nerf_tcnn.py:80-95, src/models/rendering_tcnn.py:283-289
+ *   lnr_motion_compensate / lnr_sky_rays  per-keyframe scan preprocessing
+ *                                 src/common/sensors.py:169-231, examples/fdt_optimize_implicit_map_utils.py:38-77
  *   lnr_build_lidar_rays          per-step ray selection (RANDOM / MASK / sky) + KeyFrame.build_lidar_rays
  *                                 src/mapping/optimizer.py:363-424, src/mapping/keyframe.py:75-105,
  *                                 src/common/ray_utils.py:31-60,269-322
@@ -271,6 +273,36 @@ int lnr_ogm_update(const float* rays, const float* z, const float* depth_gt, int
 int lnr_ogm_grad(const float* rays, const float* z, const float* depth_gt, int64_t n_rays, int32_t n_samples,
                  float scale, float* grad_ws, int64_t ws_words, int32_t occ_res, void* stream);
 int lnr_sgd_step(float* param, const float* grad, int64_t n, float lr, void* stream);
+
+/* ---------------------------------------------------------------- per-keyframe scan preprocessing */
+/* LidarScan.motion_compensate (src/common/sensors.py:169-231).  Host-computed per scan: the start pose
+ * rotation (row-major) and translation, end - start translation, axis/angle of R_start^T R_end
+ * (identity = angle < 1e-9), timestamps t0/t1 of the two poses, and the first 3 rows of
+ * inv(T_world_to_target).  dirs (P,3) / dists (P) are rewritten in place. */
+typedef struct lnr_motion_comp {
+  float start_rot[9];
+  float start_t[3];
+  float delta_t[3];
+  float axis[3];
+  float angle;
+  float t0, t1;
+  float target_inv[12];
+  int32_t identity;
+} lnr_motion_comp;
+int lnr_motion_compensate(const lnr_motion_comp* mc, const float* timestamps, float* dirs, float* dists,
+                          int64_t n_points, void* stream);
+
+/* compute_sky_rays (examples/fdt_optimize_implicit_map_utils.py:38-77): sky directions (rotated by
+ * rot, the lidar pose rotation, row-major) of one scan's dirs (P,3), written as (count, 3) into out
+ * (capacity cap directions, lnr_sky_rays_capacity() is enough); count (1 int32, device) = number. */
+typedef struct lnr_sky_params {
+  float rot[9];
+  int32_t top_rows;     /* TOP_ROWS = 3 */
+  float horizon_deg;    /* HORIZON_OFFSET = 10 */
+} lnr_sky_params;
+int64_t lnr_sky_rays_capacity(void);
+int lnr_sky_rays(const float* dirs, int64_t n_points, const lnr_sky_params* params, float* out, int64_t cap,
+                 int32_t* count, void* stream);
 
 /* ---------------------------------------------------------------- utilities */
 /* dst[i] = lo + (hi-lo) * U(splitmix64(((uint64)seed << 32) + start + i)) */

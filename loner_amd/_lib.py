@@ -57,6 +57,18 @@ class RayWindowDesc(ctypes.Structure):
                 ("ray_off", c_p), ("n_sel", c_p), ("n_sel_trunk", c_p)]
 
 
+class MotionComp(ctypes.Structure):
+    """``lnr_motion_comp``."""
+    _fields_ = [("start_rot", ctypes.c_float * 9), ("start_t", ctypes.c_float * 3), ("delta_t", ctypes.c_float * 3),
+                ("axis", ctypes.c_float * 3), ("angle", ctypes.c_float), ("t0", ctypes.c_float), ("t1", ctypes.c_float),
+                ("target_inv", ctypes.c_float * 12), ("identity", ctypes.c_int32)]
+
+
+class SkyParams(ctypes.Structure):
+    """``lnr_sky_params``."""
+    _fields_ = [("rot", ctypes.c_float * 9), ("top_rows", ctypes.c_int32), ("horizon_deg", ctypes.c_float)]
+
+
 _SIGNATURES = {
     "lnr_version": (ctypes.c_int, []),
     "lnr_last_error": (ctypes.c_char_p, []),
@@ -93,6 +105,9 @@ _SIGNATURES = {
     "lnr_field_render": (ctypes.c_int, [c_p, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_i32, c_f, c_p, c_u32, c_i64, c_p,
                                         c_p, c_p, c_p, c_p]),
     "lnr_rgb_render": (ctypes.c_int, [c_p, c_i32, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_p, c_p]),
+    "lnr_motion_compensate": (ctypes.c_int, [ctypes.POINTER(MotionComp), c_p, c_p, c_p, c_i64, c_p]),
+    "lnr_sky_rays_capacity": (c_i64, []),
+    "lnr_sky_rays": (ctypes.c_int, [c_p, c_i64, ctypes.POINTER(SkyParams), c_p, c_i64, c_p, c_p]),
     "lnr_loss_finalize": (ctypes.c_int, [c_p, c_i64, ctypes.POINTER(LossParams), c_p, c_p]),
     "lnr_count_opaque": (ctypes.c_int, [c_p, c_i64, c_f, c_p, c_p, c_p]),
     "lnr_build_lidar_rays": (ctypes.c_int, [ctypes.POINTER(RayWindowDesc), c_i32, c_p, c_u32, c_i64, c_i64, c_p, c_p,
