@@ -94,6 +94,7 @@ int lnr_hashgrid_fwd_rays(const lnr_grid_desc* d, const float* rays, const float
  * entry, zero where no sample touches it) and the result is bitwise reproducible; `workspace`
  * holds at least lnr_hashgrid_bwd_workspace_bytes(d, N) bytes. */
 #define LNR_BWD_COUNTS_READY 1
+#define LNR_BWD_NO_ACCUM 2      /* stop after the scatter: lnr_hashgrid_bwd_accum then finishes level ranges */
 int64_t lnr_hashgrid_bwd_workspace_bytes(const lnr_grid_desc* d, int64_t n);
 int lnr_hashgrid_bwd(const lnr_grid_desc* d, const float* pos01, int64_t n, const float* d_enc,
                      int64_t enc_stride, float* d_table, void* workspace, int64_t workspace_bytes, int32_t flags,
@@ -101,6 +102,12 @@ int lnr_hashgrid_bwd(const lnr_grid_desc* d, const float* pos01, int64_t n, cons
 int lnr_hashgrid_bwd_rays(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
                           int32_t n_samples, const float* d_enc, int64_t enc_stride, float* d_table,
                           void* workspace, int64_t workspace_bytes, int32_t flags, void* stream);
+/* With flags & LNR_BWD_NO_ACCUM the two calls above stop after the scatter; this finishes the
+ * levels [level_begin, level_end) (n = samples of that call, same workspace): their slice of
+ * d_table is final on return, so a data-parallel caller can all-reduce it while the next range
+ * accumulates. */
+int lnr_hashgrid_bwd_accum(const lnr_grid_desc* d, int64_t n, void* workspace, int64_t workspace_bytes,
+                           uint32_t level_begin, uint32_t level_end, float* d_table, void* stream);
 /* Same result with one fp32 atomic pair per corner (coarse levels merged in-wave); d_table
  * accumulates.  Kept as an independent implementation for cross-checking and A/B timing. */
 int lnr_hashgrid_bwd_atomic(const lnr_grid_desc* d, const float* pos01, int64_t n, const float* d_enc,

@@ -22,6 +22,7 @@ SIGMA_MLP_PARAMS = 64 * 32 + 16 * 64
 LOSS_KINDS = {"L1_JS": 0, "L2_JS": 1, "L1_LOS": 2, "L2_LOS": 3}
 RENDER_STRATEGIES = {"default": 0, "adjusted": 1}
 BWD_COUNTS_READY = 1
+BWD_NO_ACCUM = 2
 
 c_p = ctypes.c_void_p
 c_i64 = ctypes.c_int64
@@ -81,6 +82,7 @@ _SIGNATURES = {
                                         c_p]),
     "lnr_hashgrid_bwd_rays": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_p,
                                              c_i64, c_i32, c_p]),
+    "lnr_hashgrid_bwd_accum": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_i64, c_p, c_i64, c_u32, c_u32, c_p, c_p]),
     "lnr_hashgrid_bwd_atomic": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_i64, c_p, c_i64, c_p, c_p]),
     "lnr_hashgrid_bwd_rays_atomic": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_i64, c_p,
                                                     c_p]),

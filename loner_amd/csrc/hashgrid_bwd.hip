@@ -409,14 +409,15 @@ constexpr int kAccumThreads = 1024;
 #ifndef LNR_ACCUM_LOADS
 #define LNR_ACCUM_LOADS 2
 #endif
-__global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_accum(GridArgs a, BwdWorkspace ws, float* __restrict__ d_table) {
+__global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_accum(GridArgs a, BwdWorkspace ws, float* __restrict__ d_table,
+                                                                                        uint32_t b_begin, uint32_t b_end) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [2][kChunk] int64 fixed point
   // (one array per feature: 8-B atomics on random entries spread over twice the bank pairs)
   const uint32_t nbk = a.n_buckets;
-  const uint32_t total = ws.slice_pre[nbk];
+  const uint32_t s_end = ws.slice_pre[b_end];  // work items of buckets [b_begin, b_end)
   const int lane = threadIdx.x & 63;
-  for (uint32_t s = blockIdx.x; s < total; s += gridDim.x) {
+  for (uint32_t s = ws.slice_pre[b_begin] + blockIdx.x; s < s_end; s += gridDim.x) {
     uint32_t lo = 0, hi = nbk;  // bucket b with slice_pre[b] <= s < slice_pre[b+1]
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) >> 1;
@@ -518,8 +519,9 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
 }
 
 // Split buckets: d_table = sum of the slices' partial chunks, in slice order (deterministic).
-__global__ void __launch_bounds__(256) k_bwd_finalize(GridArgs a, BwdWorkspace ws, float* __restrict__ d_table) {
-  const uint32_t b = blockIdx.x;
+__global__ void __launch_bounds__(256) k_bwd_finalize(GridArgs a, BwdWorkspace ws, float* __restrict__ d_table,
+                                                      uint32_t b_begin) {
+  const uint32_t b = b_begin + blockIdx.x;
   const uint32_t nsl = ws.part_pre[b + 1] - ws.part_pre[b];
   if (nsl == 0) return;
   uint32_t l = 0;
@@ -541,6 +543,18 @@ __global__ void __launch_bounds__(256) k_bwd_finalize(GridArgs a, BwdWorkspace w
     for (uint32_t k = 0; k < nsl; ++k) v += src[(int64_t)k * (2 * kChunk) + t];
     dst[t] = (float)v * inv;
   }
+}
+
+// Accumulate + finalize the buckets of levels [l0, l1): their slice of d_table becomes final.
+static void launch_accum(const GridArgs& a, const BwdWorkspace& w, const lnr_grid_desc* d, int64_t n, uint32_t l0,
+                         uint32_t l1, float* d_table, hipStream_t st) {
+  const uint32_t b0 = a.bucket_base[l0], b1 = a.bucket_base[l1];
+  if (b1 <= b0) return;
+  const int64_t max_slices = (b1 - b0) + (8 * n * (int64_t)(l1 - l0)) / kSliceRecords + 1;
+  const unsigned g = (unsigned)(max_slices < 4096 ? max_slices : 4096);
+  hipLaunchKernelGGL(k_bwd_accum, dim3(g), dim3(kAccumThreads), 2 * kChunk * sizeof(unsigned long long), st, a, w,
+                     d_table, b0, b1);
+  hipLaunchKernelGGL(k_bwd_finalize, dim3(b1 - b0), dim3(256), 0, st, a, w, d_table, b0);
 }
 
 template <class PosFn>
@@ -591,10 +605,8 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
 #endif
   }
   hipLaunchKernelGGL(k_bwd_level_max, dim3(d->n_levels), dim3(256), 0, st, w);
-  const int64_t max_slices = a.n_buckets + (8 * n * (int64_t)d->n_levels) / kSliceRecords + 1;
-  const unsigned g = (unsigned)(max_slices < 4096 ? max_slices : 4096);
-  hipLaunchKernelGGL(k_bwd_accum, dim3(g), dim3(kAccumThreads), 2 * kChunk * sizeof(unsigned long long), st, a, w, d_table);
-  hipLaunchKernelGGL(k_bwd_finalize, dim3(a.n_buckets), dim3(256), 0, st, a, w, d_table);
+  if (flags & LNR_BWD_NO_ACCUM) LNR_RETURN_LAUNCH(who);  // accumulate later, by level range
+  launch_accum(a, w, d, n, 0, d->n_levels, d_table, st);
   LNR_RETURN_LAUNCH(who);
 }
 
@@ -622,6 +634,18 @@ extern "C" int lnr_hashgrid_bwd(const lnr_grid_desc* d, const float* pos01, int6
   LNR_REQUIRE(pos01 && d_enc && d_table, "lnr_hashgrid_bwd: null pointer");
   return launch_bwd_bucketed(d, PosFromArray{pos01}, n, d_enc, enc_stride, d_table, workspace, workspace_bytes, flags,
                              as_stream(stream), "lnr_hashgrid_bwd");
+}
+
+extern "C" int lnr_hashgrid_bwd_accum(const lnr_grid_desc* d, int64_t n, void* workspace, int64_t workspace_bytes,
+                                      uint32_t level_begin, uint32_t level_end, float* d_table, void* stream) {
+  if (int e = check_desc_bwd(d, "lnr_hashgrid_bwd_accum")) return e;
+  LNR_REQUIRE(level_begin <= level_end && level_end <= d->n_levels, "lnr_hashgrid_bwd_accum: bad level range");
+  LNR_REQUIRE(n >= 0 && workspace && workspace_bytes >= bwd_workspace_bytes(d, n) && d_table,
+              "lnr_hashgrid_bwd_accum: bad workspace / pointers");
+  if (n == 0) return LNR_OK;
+  const GridArgs a = make_args(d);
+  launch_accum(a, carve_workspace(workspace, a, d, n), d, n, level_begin, level_end, d_table, as_stream(stream));
+  LNR_RETURN_LAUNCH("lnr_hashgrid_bwd_accum");
 }
 
 extern "C" int lnr_hashgrid_bwd_rays(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,

@@ -171,6 +171,11 @@ class StepEngine:
         # field has trained a few steps, and the extra count pass (d_enc reads) costs more than the
         # records it saves (3.35 vs 3.18 ms/step), so it is opt-in for sparse-gradient workloads.
         self.count_in_forward = count_in_forward
+        # level ranges of the bucketed gradient all-reduce, finest first (their records dominate the
+        # accumulation, so the first ranges' exchange overlaps the later ranges' accumulation)
+        nl = self.cfg.n_levels
+        cuts = sorted({nl, max(nl - 5, 1), max(nl - 10, 1), 0}, reverse=True)
+        self.ar_groups = [(cuts[i + 1], cuts[i]) for i in range(len(cuts) - 1)]
         # callable(tensor[, async_op]) summing in place across ranks (torch.distributed.all_reduce
         # semantics), or None
         self.allreduce = allreduce
@@ -280,13 +285,29 @@ class StepEngine:
         m(prof, "field")
         # 5. hash-grid backward
         m(prof, "grid_bwd")
-        L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(st.desc), rays, self.z, R, S, self.d_enc, N, st.grad_table,
-               self.bwd_ws, self.bwd_ws_bytes, L.BWD_COUNTS_READY if self.count_in_forward else 0, s)
-        m(prof, "grid_bwd")
-        # 6. data-parallel gradient exchange (one all-reduce of table + MLP grads)
-        if self.allreduce is not None:
+        flags = L.BWD_COUNTS_READY if self.count_in_forward else 0
+        if self.allreduce is None:
+            L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(st.desc), rays, self.z, R, S, self.d_enc, N, st.grad_table,
+                   self.bwd_ws, self.bwd_ws_bytes, flags, s)
+            m(prof, "grid_bwd")
+        else:
+            # 6. data-parallel gradient exchange, bucketed by level range: each range's slice of the
+            # gradient is all-reduced (async) while the next range accumulates; the MLP gradient
+            # travels with the last range
+            L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(st.desc), rays, self.z, R, S, self.d_enc, N, st.grad_table,
+                   self.bwd_ws, self.bwd_ws_bytes, flags | L.BWD_NO_ACCUM, s)
+            pending = []
+            for l0, l1 in self.ar_groups:
+                L.call("lnr_hashgrid_bwd_accum", L.ctypes.byref(st.desc), R * S, self.bwd_ws, self.bwd_ws_bytes, l0,
+                       l1, st.grad_table, s)
+                a0 = 0 if l0 == 0 else st.n_mlp + 2 * int(st.desc.offset[l0])
+                a1 = st.n_mlp + 2 * int(st.desc.offset[l1])
+                pending.append(self._allreduce_async(st.grad[a0:a1]))
+            m(prof, "grid_bwd")
             m(prof, "allreduce")
-            self.allreduce(st.grad)
+            for w in pending:
+                if w is not None:
+                    w.wait()
             m(prof, "allreduce")
         # 7. Adam (+ fp16 shadow)
         st.adam_step += 1
