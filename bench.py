@@ -41,8 +41,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="C2", choices=["C1", "C2", "C3", "C4"],
-                    help="C1/C2/C4: optimiser step; C3: inference render (peak depth, N_samples_test=2048)")
+    ap.add_argument("--config", default="C2", choices=["C1", "C2", "C3", "C4", "CAM"],
+                    help="C1/C2/C4: optimiser step; C3: inference render (peak depth, N_samples_test=2048); "
+                         "CAM: colour-head training iteration (camera phase)")
     ap.add_argument("--rays", default="device", choices=["device", "resident"],
                     help="device: select + build each step's rays on the GPU from the resident window; "
                          "resident: cycle prebuilt ray batches")
@@ -223,10 +224,160 @@ def bench_render(args):
     print(json.dumps(line), flush=True)
 
 
+def cpu_baseline_camera(n_rays, S, chunks):
+    """Oracle colour-head training (forward + L1 + MLP backward, oracle/camera.py) on a bounded
+    sample, from given colour-grid features (the hash-grid encode/backward are not included)."""
+    from oracle import camera as ocam
+    from oracle import mlp as omlp
+    rng = np.random.default_rng(0)
+    N = n_rays * S
+    enc = rng.uniform(-1, 1, (N, 32)).astype(np.float16)
+    o = rng.uniform(-0.5, 0.5, (n_rays, 3))
+    d = rng.normal(size=(n_rays, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([o, d, -d, np.zeros((n_rays, 4))], 1).astype(np.float32)
+    w = (rng.dirichlet(np.full(S, 0.3), n_rays) * 0.9).astype(np.float32)
+    gt = rng.uniform(0, 1, (n_rays, 3))
+    mats = [rng.uniform(-0.2, 0.2, s).astype(np.float16) for s in omlp.layer_shapes(48, 3, 64, 4)]
+    t0 = time.perf_counter()
+    for _ in range(chunks):  # the same chunk repeated: bounded memory, ~10 s of CPU work
+        ocam.rgb_train(enc, rays, w, gt, mats, S)
+    dt = time.perf_counter() - t0
+    threads = torch.get_num_threads()
+    return {"value": chunks * N / dt, "unit": "ray-samples/s", "cores": threads, "kind": "port",
+            "sample": f"colour forward + L1 + MLP backward of {chunks} x {n_rays} rays x {S} samples (numpy oracle, "
+                      f"fp64 GEMMs on up to {threads} BLAS threads), hash grids excluded, {dt:.1f} s"}
+
+
+def bench_camera(args):
+    """Camera phase (examples/fdt_optimize_implicit_map.py:826-873, optimizer.py:541-688): one colour
+    head iteration on a MAX_WINDOW_LENGTH_CAMERA = 6 keyframe window x num_samples.lidar = 512 rays
+    (the steady-state iterations; the first has 511) x N_samples_train = 512, 1280x720 images
+    (640x360 x IMAGE_UPSAMPLING 2) resident in HBM.  Per iteration: camera rays on the GPU, OGM
+    sampler, sigma encode + compositing weights (frozen, detached), colour encode, lnr_rgb_train,
+    colour hash-grid backward, Adam over the colour parameters."""
+    from loner_amd import camera as C
+    from loner_amd import step as S_
+    from loner_amd import synthetic as syn
+    from loner_amd import _lib as L
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    n_kf, per_kf, S, W, H = 6, 512, 512, 1280, 720
+    kind = "forest"
+    K = np.array([[640.0, 0, (W - 1) / 2], [0, 640.0, (H - 1) / 2], [0, 0, 1]])
+    dirs = C.pinhole_directions(W, H, K)
+    lidar_to_cam = np.array([[0, 0, 1], [-1, 0, 0], [0, -1, 0]], dtype=np.float64)  # camera z = lidar x
+    poses, imgs = [], []
+    yy, xx = np.mgrid[0:H, 0:W]
+    for k, P in enumerate(syn.keyframe_poses(kind, n_kf, np.random.default_rng(0))):
+        Pc = np.array(P, dtype=np.float64)
+        Pc[:3, :3] = Pc[:3, :3] @ lidar_to_cam
+        poses.append(Pc[:3])
+        imgs.append(np.stack([0.5 + 0.4 * np.sin(xx / 37.0 + k), 0.5 + 0.4 * np.cos(yy / 23.0),
+                              0.3 + 0.2 * np.sin((xx + yy) / 50.0)], -1).reshape(-1, 3).astype(np.float32))
+    fr = C.CameraFrames(dirs, W, H, imgs, poses, syn.world_cube(kind), syn.SENSORS[kind]["ray_range"],
+                        n_rays_per_kf=per_kf, seed=0, device=dev)
+    state = S_.FieldState(S_.StepConfig(n_samples=S), device=dev)
+    color = C.ColorState(4, device=dev)
+    R = n_kf * per_kf
+    eng = C.CameraStepEngine(state, color, n_rays=R, n_samples=S, seed=0)
+    rays = torch.empty(R, 13, dtype=torch.float32, device=dev)
+    inten = torch.empty(R, 3, dtype=torch.float32, device=dev)
+    ev = {}
+
+    def mark(k):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        ev.setdefault(k, []).append(e)
+
+    def run(i, prof):
+        it = 1 + i % (fr.n_iter - 1)  # steady-state iterations: 512 rays per keyframe
+        if prof:
+            mark("iteration")
+        n = fr.build(it, rays, inten)
+        eng.step(rays[:n], inten[:n])
+        if prof:
+            mark("iteration")
+        return n
+
+    for i in range(args.warmup):
+        run(i, False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n_tot = 0
+    for i in range(args.steps):
+        n_tot += run(args.warmup + i, True)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    # one extra profiled iteration split by stage (events between the engine's launches)
+    stage_ms = _camera_stages(eng, fr, rays, inten, L)
+    N = n_tot * S
+    bwd_ms = stage_ms["rgb_train"]
+    flop = 2 * 3 * (64 * 48 + 3 * 64 * 64 + 16 * 64) * R * S  # forward (x2: recomputed) + backward GEMMs
+    achieved = flop / (bwd_ms * 1e-3) / 1e12
+    line = {"metric": "ray-samples/sec per colour-head iteration", "value": N / elapsed, "unit": "ray-samples/s",
+            "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp16 params/activations, fp32 accumulate+optimizer",
+            "data": "synthetic 1280x720 images resident in HBM, camera rays built on the GPU each iteration; "
+                    "random-init sigma field (frozen) and colour head",
+            "config": {"workload": f"CAM: {n_kf} KF x {per_kf} camera rays x {S} samples, colour head SH4 + L=16 "
+                                   f"T=2^19 + 48->64x4->3 MLP, L1 loss, Adam",
+                       "rays": R, "samples_per_ray": S, "parallelism": "single"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": 2500.0, "unit": "TFLOP/s",
+                         "frac": achieved / 2500.0, "traffic": None,
+                         "kernel": "lnr_rgb_train (colour forward x2 + L1 + MLP backward, MFMA fp16)",
+                         "algorithmic_flop_per_launch": flop, "ms_per_launch": bwd_ms},
+            "stage_ms": stage_ms}
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_camera(256, S, 16)
+    print(json.dumps(line), flush=True)
+
+
+def _camera_stages(eng, fr, rays, inten, L):
+    """Per-stage HIP-event times of one camera iteration (same launches as CameraStepEngine.step)."""
+    fs, cs = eng.field, eng.color
+    s = L.stream(fs.device)
+    ev = []
+
+    def mark(name):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        ev.append((name, e))
+
+    R, S, N = eng.R, eng.S, eng.N
+    key = L.step_key(0, 12345)
+    mark("rays")
+    fr.build(1, rays, inten)
+    mark("sample")
+    L.call("lnr_sample_ogm", rays, R, S, fs.occ, fs.cfg.occ_res, 1.0, None, None, key, 0, eng.z, s)
+    mark("encode")
+    L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(fs.desc), rays, eng.z, R, S, fs.table_f16, eng.enc, N, None, 0, s)
+    mark("weights")
+    L.call("lnr_field_render", fs.mlp_f16, eng.enc, N, rays, eng.z, R, S, 0, 1.0, None, key, 0, eng.depth,
+           eng.opacity, None, eng.weights, s)
+    mark("encode_rgb")
+    L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(cs.desc), rays, eng.z, R, S, cs.table_f16, eng.enc_rgb, N,
+           eng.bwd_ws, eng.bwd_ws_bytes, s)
+    mark("rgb_train")
+    L.call("lnr_rgb_train", cs.mlp_f16, cs.n_hidden_layers, eng.enc_rgb, N, rays, eng.weights, inten, R, S,
+           1.0 / (3.0 * R), eng.rgb, eng.loss, eng.d_enc, cs.grad_mlp, eng.ws, eng.ws_bytes, s)
+    mark("grid_bwd")
+    L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(cs.desc), rays, eng.z, R, S, eng.d_enc, N, cs.grad_table,
+           eng.bwd_ws, eng.bwd_ws_bytes, L.BWD_COUNTS_READY, s)
+    mark("adam")
+    L.call("lnr_adam_step", cs.params, cs.shadow, cs.grad, cs.m, cs.v, cs.n_padded, 1, 0.0, 0.9, 0.999, 1e-8, s)
+    mark("end")
+    torch.cuda.synchronize()
+    return {ev[i][0]: float(ev[i][1].elapsed_time(ev[i + 1][1])) for i in range(len(ev) - 1)}
+
+
 def main():
     args = parse()
     if args.config == "C3":
         return bench_render(args)
+    if args.config == "CAM":
+        return bench_camera(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

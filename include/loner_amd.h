@@ -20,6 +20,8 @@
  *   lnr_ogm_update                Optimizer._step_occupancy_grid  src/mapping/optimizer.py:897-908
  *   lnr_rgb_render                colour head (SH4 + 2^19 HashGrid + FullyFusedMLP) + colour map
  *                                 src/models/nerf_tcnn.py:80-95, src/models/rendering_tcnn.py:283-289
+ *   lnr_rgb_train / lnr_build_camera_rays  colour-head training (camera phase)
+ *                                 src/mapping/optimizer.py:541-688,861-894, src/common/ray_utils.py:175-212
  *   lnr_motion_compensate / lnr_sky_rays  per-keyframe scan preprocessing
  *                                 src/common/sensors.py:169-231, examples/fdt_optimize_implicit_map_utils.py:38-77
  *   lnr_build_lidar_rays          per-step ray selection (RANDOM / MASK / sky) + KeyFrame.build_lidar_rays
@@ -263,6 +265,36 @@ typedef struct lnr_ray_window {
 int lnr_build_lidar_rays(const lnr_ray_window* window, int32_t select, const int32_t* given, uint32_t key,
                          int64_t slot0, int64_t n_slots, float* rays, float* depth, uint8_t* valid,
                          int32_t* point_index, float* far_ref, void* stream);
+
+/* Camera rays (KeyFrame.build_camera_rays, src/mapping/keyframe.py:108-127 ->
+ * CameraRayDirections.build_rays, src/common/ray_utils.py:175-212): for pixel p = j * width + i,
+ * rays[k] = [o, d, -d, i, j, r_min / scale, get_far_val(o, d)] with d = normalise(R dirs[p]),
+ * o = (t + shift) / scale; intensities[k] = image[p] (channels floats, optional).  dirs = the
+ * (height * width, 3) undistorted camera-frame directions (get_ray_directions, ray_utils.py:62-124,
+ * computed once per calibration by the host). */
+typedef struct lnr_camera_desc {
+  int32_t width, height, channels;
+  float scale;        /* WorldCube.scale_factor */
+  float shift[3];     /* WorldCube.shift */
+  float r_min;        /* ray_range[0] (metres) */
+  float pose[12];     /* camera pose in the world, 3x4 [R | t] rows */
+} lnr_camera_desc;
+int lnr_build_camera_rays(const lnr_camera_desc* cam, const float* dirs, const float* image, const int64_t* pixels,
+                          int64_t n, float* rays, float* intensities, void* stream);
+
+/* Colour-head training, camera phase (Optimizer._do_iterate_optimizer_camera + compute_loss_camera,
+ * src/mapping/optimizer.py:541-688,861-894): sigma frozen and detached (weights = the sigma pass's
+ * compositing weights, lnr_field_render); rgb as lnr_rgb_render; loss = l1(rgb, intensities) as a
+ * mean over the 3 * (global) rays: inv_count = 1 / (3 n_rays_global).  Writes rgb (R,3), loss[0]
+ * (optional; local rays only), d_enc (level-major float2, the colour-grid backward's input, as
+ * lnr_field_train's) and d_w (OVERWRITTEN: the colour MLP's weight gradient, tcnn flat layout,
+ * lnr_rgb_mlp_params floats).  Deterministic (fixed-order slab reduction). */
+int64_t lnr_rgb_mlp_params(int32_t n_hidden_layers);
+int64_t lnr_rgb_train_workspace_bytes(int32_t n_hidden_layers, int64_t n_rays);
+int lnr_rgb_train(const uint16_t* w_rgb, int32_t n_hidden_layers, const uint32_t* enc_rgb, int64_t enc_stride,
+                  const float* rays, const float* weights, const float* intensities, int64_t n_rays,
+                  int32_t n_samples, float inv_count, float* rgb, float* loss, float* d_enc, float* d_w,
+                  void* workspace, int64_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- optimiser */
 /* torch.optim.Adam (no weight decay); step is 1-based.  shadow (fp16) may be NULL. */

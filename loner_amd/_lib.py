@@ -65,6 +65,13 @@ class MotionComp(ctypes.Structure):
                 ("target_inv", ctypes.c_float * 12), ("identity", ctypes.c_int32)]
 
 
+class CameraDesc(ctypes.Structure):
+    """``lnr_camera_desc``."""
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("channels", ctypes.c_int32),
+                ("scale", ctypes.c_float), ("shift", ctypes.c_float * 3), ("r_min", ctypes.c_float),
+                ("pose", ctypes.c_float * 12)]
+
+
 class SkyParams(ctypes.Structure):
     """``lnr_sky_params``."""
     _fields_ = [("rot", ctypes.c_float * 9), ("top_rows", ctypes.c_int32), ("horizon_deg", ctypes.c_float)]
@@ -107,6 +114,11 @@ _SIGNATURES = {
     "lnr_field_render": (ctypes.c_int, [c_p, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_i32, c_f, c_p, c_u32, c_i64, c_p,
                                         c_p, c_p, c_p, c_p]),
     "lnr_rgb_render": (ctypes.c_int, [c_p, c_i32, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_p, c_p]),
+    "lnr_rgb_mlp_params": (c_i64, [c_i32]),
+    "lnr_rgb_train_workspace_bytes": (c_i64, [c_i32, c_i64]),
+    "lnr_rgb_train": (ctypes.c_int, [c_p, c_i32, c_p, c_i64, c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_p, c_p, c_p,
+                                     c_p, c_i64, c_p]),
+    "lnr_build_camera_rays": (ctypes.c_int, [ctypes.POINTER(CameraDesc), c_p, c_p, c_p, c_i64, c_p, c_p, c_p]),
     "lnr_motion_compensate": (ctypes.c_int, [ctypes.POINTER(MotionComp), c_p, c_p, c_p, c_i64, c_p]),
     "lnr_sky_rays_capacity": (c_i64, []),
     "lnr_sky_rays": (ctypes.c_int, [c_p, c_i64, ctypes.POINTER(SkyParams), c_p, c_i64, c_p, c_p]),

@@ -96,6 +96,19 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Max of a NON-NEGATIVE float over the wave on DPP (row shifts, row_bcast15/31: no LDS permutes),
+// read back from lane 63 so the result is wave-uniform.
+__device__ __forceinline__ float wave_max_nonneg(float v) {
+  int x = __float_as_int(v);  // non-negative floats order like their bit patterns; 0 is the identity
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true));  // row_shr:1
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true));  // row_shr:2
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true));  // row_shr:4
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true));  // row_shr:8 -> lane 15 of each row
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false));  // row_bcast:15 into rows 1, 3
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false));  // row_bcast:31 into rows 2, 3
+  return __int_as_float(__builtin_amdgcn_readlane(x, 63));
+}
+
 // Block-wide sum of K values for a block of NT threads (NT/64 waves).  `scratch` needs
 // K * (NT/64) floats; all threads receive the totals.  Contains two barriers.
 template <int NT, int K>

@@ -221,3 +221,62 @@ extern "C" int lnr_build_lidar_rays(const lnr_ray_window* w, int32_t select, con
                      n_slots, rays, depth, valid, point_index, far_ref);
   LNR_RETURN_LAUNCH("lnr_build_lidar_rays");
 }
+
+// ------------------------------------------------------------------ camera rays
+// KeyFrame.build_camera_rays -> CameraRayDirections.build_rays (src/mapping/keyframe.py:108-127,
+// src/common/ray_utils.py:175-212): pixel p = j * W + i of the undistorted per-pixel directions
+// table, rotated by the camera pose, normalised; origin = (t + shift) / scale; view direction = -d;
+// near = r_min / scale; far = get_far_val(o, d, no_nan=True) (NOT clipped by r_max here); the
+// intensities are the image row p.  fp32 in the reference's operation order.
+__global__ void __launch_bounds__(256) k_build_camera_rays(lnr_camera_desc cam, const float* __restrict__ dirs,
+                                                           const float* __restrict__ image,
+                                                           const int64_t* __restrict__ pixels, int64_t n,
+                                                           float* __restrict__ rays, float* __restrict__ intens) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int64_t p = pixels[k];
+  const float sc = cam.scale;
+  float o[3], d[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) o[r] = (cam.pose[4 * r + 3] + cam.shift[r]) / sc;
+  const float dx = dirs[3 * p + 0], dy = dirs[3 * p + 1], dz = dirs[3 * p + 2];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) d[r] = (dx * cam.pose[4 * r + 0] + dy * cam.pose[4 * r + 1]) + dz * cam.pose[4 * r + 2];
+  const float nrm = sqrtf((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
+#pragma unroll
+  for (int r = 0; r < 3; ++r) d[r] = d[r] / nrm;
+  float far_clip = INFINITY;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const float dd = d[r] + 1e-15f;
+    const float t0 = fmaxf((-1.0f - o[r]) / dd, 0.0f);
+    const float t1 = fmaxf((1.0f - o[r]) / dd, 0.0f);
+    far_clip = fminf(far_clip, fmaxf(t0, t1));
+  }
+  float* ry = rays + 13 * k;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    ry[r] = o[r];
+    ry[3 + r] = d[r];
+    ry[6 + r] = -d[r];
+  }
+  ry[9] = (float)(p % cam.width);
+  ry[10] = (float)(p / cam.width);
+  ry[11] = cam.r_min / sc;
+  ry[12] = far_clip;
+  if (intens)
+    for (int c = 0; c < cam.channels; ++c) intens[k * cam.channels + c] = image[p * cam.channels + c];
+}
+
+extern "C" int lnr_build_camera_rays(const lnr_camera_desc* cam, const float* dirs, const float* image,
+                                     const int64_t* pixels, int64_t n, float* rays, float* intensities,
+                                     void* stream) {
+  LNR_REQUIRE(cam != nullptr && n >= 0, "lnr_build_camera_rays: bad arguments");
+  LNR_REQUIRE(cam->width > 0 && cam->height > 0 && cam->channels > 0 && cam->scale > 0.f,
+              "lnr_build_camera_rays: bad camera description");
+  if (n == 0) return LNR_OK;
+  LNR_REQUIRE(dirs && pixels && rays && (intensities == nullptr || image), "lnr_build_camera_rays: null pointer");
+  hipLaunchKernelGGL(k_build_camera_rays, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), *cam,
+                     dirs, image, pixels, n, rays, intensities);
+  LNR_RETURN_LAUNCH("lnr_build_camera_rays");
+}

@@ -18,67 +18,9 @@
 // permuted by hid_perm (mlp.hpp).  Weights of every layer live in registers (NH hidden-to-hidden
 // layers, template).  The colour encodings are read once (64 B per sample): the kernel is bound by
 // the MFMA chain (8 + 8 * NH + 2 MFMAs per 16 samples) and that read.
-#include "mlp.hpp"
-#include "sh.hpp"
+#include "rgb.hpp"
 
 namespace lnr {
-
-constexpr int kRgbWaves = 4;
-constexpr int kRgbIn = 48, kRgbWidth = 64, kRgbOutPad = 16;
-
-template <int NH>
-struct RgbWeights {
-  half8_t a0[4];          // layer 0, enc columns: W0[16t + c][8g + j]
-  half8_t as[4];          // layer 0, SH columns (k-step zero-padded to 32): W0[16t + c][32 + 8g + j], g < 2
-  half8_t ah[NH > 0 ? NH : 1][4][2];  // hidden layer h, row tile t, k-step s: Wh[16t + c][hid_perm(s, g, j)]
-  half8_t ao[2];          // output: Wout[c][hid_perm(s, g, j)]
-};
-
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
-
-// 8 halves = 4 packed dwords: 16 contiguous bytes, or two 8-byte runs (hid_perm: 4g..4g+3 and
-// 16+4g..16+4g+3 of a 32-wide k-step).
-__device__ __forceinline__ half8_t ld_half8(const uint16_t* p) {
-  return __builtin_bit_cast(half8_t, *reinterpret_cast<const u32x4_t*>(p));
-}
-__device__ __forceinline__ half8_t ld_half8_perm(const uint16_t* row, int s, int g) {
-  const u32x2_t lo = *reinterpret_cast<const u32x2_t*>(row + 32 * s + 4 * g);
-  const u32x2_t hi = *reinterpret_cast<const u32x2_t*>(row + 32 * s + 16 + 4 * g);
-  const u32x4_t v = {lo.x, lo.y, hi.x, hi.y};
-  return __builtin_bit_cast(half8_t, v);
-}
-
-template <int NH>
-__device__ __forceinline__ void load_rgb_weights(const uint16_t* __restrict__ w, RgbWeights<NH>& rw) {
-  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-  const uint16_t* w0 = w;  // (64, 48)
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    rw.a0[t] = ld_half8(w0 + (16 * t + c) * kRgbIn + 8 * g);
-    const half8_t z = {};
-    rw.as[t] = g < 2 ? ld_half8(w0 + (16 * t + c) * kRgbIn + 32 + 8 * g) : z;
-  }
-  const uint16_t* wh = w0 + kRgbWidth * kRgbIn;
-#pragma unroll
-  for (int h = 0; h < NH; ++h) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) rw.ah[h][t][s] = ld_half8_perm(wh + (16 * t + c) * kRgbWidth, s, g);
-    wh += kRgbWidth * kRgbWidth;
-  }
-#pragma unroll
-  for (int s = 0; s < 2; ++s) rw.ao[s] = ld_half8_perm(wh + c * kRgbWidth, s, g);
-}
-
-// B operand (k-step s) from a layer's fp16-valued activations h[4t + r] = hid 16t + 4g + r.
-__device__ __forceinline__ half8_t hid_operand(const float (&h)[16], int s) {
-  half8_t b;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) b[j] = (_Float16)h[4 * (2 * s + (j >> 2)) + (j & 3)];
-  return b;
-}
 
 struct RgbArgs {
   const uint16_t* w;      // tcnn flat params of the colour network
@@ -89,9 +31,14 @@ struct RgbArgs {
   int64_t n_rays;
   int32_t S;
   float* rgb;             // (R, 3)
+  // training (lnr_rgb_train): L1 loss against the pixel intensities, mean over 3 x n_rays_global
+  const float* gt;        // (R, 3)
+  float* g;               // (R, 3) dL/drgb = sign(rgb - gt) * inv_count
+  float* ray_loss;        // (R) sum_k |rgb_k - gt_k|
+  float inv_count;
 };
 
-template <int NH>
+template <int NH, bool TRAIN>
 __global__ void __launch_bounds__(64 * kRgbWaves) k_rgb_render(RgbArgs a) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   RgbWeights<NH> rw;
@@ -153,8 +100,383 @@ __global__ void __launch_bounds__(64 * kRgbWaves) k_rgb_render(RgbArgs a) {
       for (int k = 0; k < 3; ++k) acc_c[k] += __shfl_xor(acc_c[k], off, 64);
     }
     if (lane < 3) a.rgb[3 * r + lane] = (lane == 0 ? acc_c[0] : lane == 1 ? acc_c[1] : acc_c[2]) + (1.0f - acc_w);
+    if (TRAIN && lane == 0) {  // nn.functional.l1_loss(rgb.reshape(-1, 1), gt.reshape(-1, 1)) (optimizer.py:883-884)
+      float l = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float d = acc_c[k] + (1.0f - acc_w) - a.gt[3 * r + k];
+        a.g[3 * r + k] = (d > 0.f ? a.inv_count : (d < 0.f ? -a.inv_count : 0.f));  // torch.sign
+        l += fabsf(d);
+      }
+      a.ray_loss[r] = l;
+    }
   }
 }
+
+
+// ------------------------------------------------------------------ colour-head training backward
+// Camera phase of the reference (optimizer.py:541-688, compute_loss_camera :861-894): sigma frozen
+// and detached, so dL/dlogit_i = g_ray * w_i * col_i * (1 - col_i) with g_ray = dL/drgb from
+// k_rgb_render<NH, true>.  One workgroup = 4 waves, one 16-sample tile per wave per iteration:
+//   1. each wave re-runs its tile's forward (bit-identical to the render), then the backward chain
+//      dO -> dH_NH -> ... -> dH_0 -> d_enc on MFMA with per-wave power-of-two scaling of the fp16
+//      operands (the chain's scale is tracked per layer); d_enc goes to HBM (level-major float2,
+//      as lnr_field_train's) for the colour-grid backward;
+//   2. every layer's input X_l (fp16) and scaled output gradient dY_l (fp16) are staged in LDS;
+//   3. after a barrier, matrix l's weight gradient dW_l = sum_s dY_l[:, s] X_l[:, s]^T is
+//      accumulated by ONE owner wave (16x16x16 MFMA per source wave, unscaled by that wave's
+//      factor in fp32), so the 16 weight tiles of a matrix live in one wave's registers;
+//   4. at the end each owner writes its tiles to the workgroup's slab; k_rgb_reduce_slabs sums the
+//      slabs in a fixed order (bitwise reproducible).
+// Hidden-layer operands (forward, and transposed with the hid_perm k order) are pre-arranged in LDS
+// so each is one conflict-free 16-B read per lane.
+typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
+constexpr int kRgbBwdWaves = 4;
+constexpr int kRgbXRows = 48;                       // colour-grid features (32) + SH (16)
+constexpr int kRgbCols = 16 * kRgbBwdWaves;         // samples per workgroup iteration
+constexpr int kRgbLd = kRgbCols + 8;                // halfs per staged row
+
+template <int NH>
+struct RgbBwdLds {
+  static constexpr int kOps = 8 * NH;                        // hidden operands per direction
+  static constexpr int kXRows = kRgbXRows + 64 * (NH + 1);   // X_0 = [enc; SH], X_{l+1} = H_l
+  static constexpr int kYRows = 64 * (NH + 1) + 16;          // dH_0 .. dH_NH, dO (16 rows)
+  _Float16 w[2 * (kOps > 0 ? kOps : 1) * 512];
+  _Float16 x[kXRows * kRgbLd];
+  _Float16 y[kYRows * kRgbLd];
+  float inv[kRgbBwdWaves][NH + 2];                           // 1 / scale of dY_l per source wave
+  int valid[kRgbBwdWaves];
+};
+
+template <int NH>
+constexpr int rgb_mlp_params() { return 64 * kRgbIn + NH * 64 * 64 + kRgbOutPad * 64; }
+
+template <int NH>
+__device__ __forceinline__ int rgb_layer_offset(int l) {  // tcnn flat offset of matrix l (l = NH + 1: output)
+  return l == 0 ? 0 : 64 * kRgbIn + (l - 1) * 64 * 64;
+}
+
+__device__ __forceinline__ void scale_chain(float (&v)[16], float& scale) {
+  float mx = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) mx = fmaxf(mx, fabsf(v[k]));
+  const float k2 = grad_scale(wave_max_nonneg(mx));
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] *= k2;
+  scale *= k2;
+}
+
+
+// Owner accumulation for matrix i.  KIND 0: hidden (64 x 64, acc tiles 4t + m), 1: W0 (64 x 48, acc
+// tiles 3t + m), 2: output (16 x 64, acc tiles 12 + m; its owner never also owns a hidden matrix).
+template <int KIND>
+struct RgbOwnerShape {
+  static constexpr int rt = KIND == 2 ? 1 : 4, ct = KIND == 1 ? 3 : 4;
+  static constexpr int ld = KIND == 1 ? kRgbIn : kRgbWidth;
+  __device__ static constexpr int slot(int t, int m) { return KIND == 0 ? 4 * t + m : (KIND == 1 ? 3 * t + m : 12 + m); }
+};
+
+template <int NH, int KIND>
+__device__ __forceinline__ void rgb_owner(const RgbBwdLds<NH>& sm, int i, float (&acc)[16][4]) {
+  using Sh = RgbOwnerShape<KIND>;
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int ybase = 64 * i;  // dO sits at 64 (NH + 1) = 64 i for the output
+  const int xbase = i == 0 ? 0 : kRgbXRows + 64 * (i - 1);
+  for (int sw = 0; sw < kRgbBwdWaves; ++sw) {
+    if (!sm.valid[sw]) continue;
+    const float inv = sm.inv[sw][i];
+    const int cs = 16 * sw + 4 * g;
+    half4_t ya[Sh::rt], xb[Sh::ct];
+#pragma unroll
+    for (int t = 0; t < Sh::rt; ++t) ya[t] = *reinterpret_cast<const half4_t*>(&sm.y[(ybase + 16 * t + c) * kRgbLd + cs]);
+#pragma unroll
+    for (int m = 0; m < Sh::ct; ++m) xb[m] = *reinterpret_cast<const half4_t*>(&sm.x[(xbase + 16 * m + c) * kRgbLd + cs]);
+#pragma unroll
+    for (int t = 0; t < Sh::rt; ++t)
+#pragma unroll
+      for (int m = 0; m < Sh::ct; ++m) {
+        float4_t d = {0.f, 0.f, 0.f, 0.f};
+        d = __builtin_amdgcn_mfma_f32_16x16x16f16(ya[t], xb[m], d, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[Sh::slot(t, m)][q] = fmaf(d[q], inv, acc[Sh::slot(t, m)][q]);
+      }
+  }
+}
+
+template <int NH, int KIND>
+__device__ __forceinline__ void rgb_owner_store(float* __restrict__ sb, int i, const float (&acc)[16][4]) {
+  using Sh = RgbOwnerShape<KIND>;
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  float* mat = sb + rgb_layer_offset<NH>(i);
+#pragma unroll
+  for (int t = 0; t < Sh::rt; ++t)
+#pragma unroll
+    for (int m = 0; m < Sh::ct; ++m)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) mat[(16 * t + 4 * g + q) * Sh::ld + 16 * m + c] = acc[Sh::slot(t, m)][q];
+}
+
+template <int NH>
+__global__ void __launch_bounds__(64 * kRgbBwdWaves) k_rgb_bwd_tiles(RgbArgs a, float* __restrict__ d_enc,
+                                                                     float* __restrict__ slab) {
+  __shared__ RgbBwdLds<NH> sm;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  // ---- weights: layer 0 / output in registers, hidden operands in LDS
+  const uint16_t* w0 = a.w;
+  half8_t a0[4], as[4], b0t[2][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    a0[t] = ld_half8(w0 + (16 * t + c) * kRgbIn + 8 * g);
+    const half8_t z = {};
+    as[t] = g < 2 ? ld_half8(w0 + (16 * t + c) * kRgbIn + 32 + 8 * g) : z;
+  }
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        b0t[m][s2][j] = __builtin_bit_cast(_Float16, w0[hid_perm(s2, g, j) * kRgbIn + 16 * m + c]);
+  const uint16_t* wo = a.w + rgb_layer_offset<NH>(NH + 1);  // (16, 64)
+  half8_t ao[2], aot[4];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) ao[s2] = ld_half8_perm(wo + c * kRgbWidth, s2, g);
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)  // A = Wout^T: [hid 16t + c][k = output 8g + j], outputs 0..2 only
+      aot[t][j] = (g == 0 && j < 3) ? __builtin_bit_cast(_Float16, wo[j * kRgbWidth + 16 * t + c]) : (_Float16)0.f;
+  for (int op = wid; op < 2 * RgbBwdLds<NH>::kOps; op += kRgbBwdWaves) {
+    const bool tr = op >= RgbBwdLds<NH>::kOps;
+    const int o = tr ? op - RgbBwdLds<NH>::kOps : op;
+    const int l = o >> 3, t = (o >> 1) & 3, s2 = o & 1;  // hidden matrix l + 1
+    const uint16_t* wl = a.w + rgb_layer_offset<NH>(l + 1);
+    half8_t v;
+    if (!tr) {
+      v = ld_half8_perm(wl + (16 * t + c) * kRgbWidth, s2, g);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = __builtin_bit_cast(_Float16, wl[hid_perm(s2, g, j) * kRgbWidth + 16 * t + c]);
+    }
+    *reinterpret_cast<half8_t*>(&sm.w[op * 512 + lane * 8]) = v;
+  }
+  // ---- owner jobs: matrix i (0 = W0, 1..NH hidden, NH + 1 = output) -> wave i, the 5th to wave 0
+  float acc[16][4];
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[k][q] = 0.f;
+  __syncthreads();
+
+  const int64_t n_tiles = a.n_rays * (int64_t)(a.S / 16);
+  const int64_t per_iter = (int64_t)gridDim.x * kRgbBwdWaves;
+  const int64_t n_iter = (n_tiles + per_iter - 1) / per_iter;
+  float2* denc = reinterpret_cast<float2*>(d_enc);
+  // software pipelining: the next tile's HBM inputs are in flight while this tile computes (one wave
+  // per SIMD at this LDS footprint, so latency is hidden by ILP only)
+  uint32_t nx[4];
+  float nw = 0.f, ng[3] = {0.f, 0.f, 0.f}, nd[3] = {0.f, 0.f, 0.f};
+  auto prefetch = [&](int64_t tl) {
+    if (tl >= n_tiles) return;
+    const int64_t m0 = tl * 16, rr = m0 / a.S;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) nx[q] = a.enc[(int64_t)(4 * g + q) * a.enc_stride + m0 + c];
+    nw = a.weights[m0 + c];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      ng[k] = a.g[3 * rr + k];
+      nd[k] = a.rays[13 * rr + 6 + k];
+    }
+  };
+  prefetch((int64_t)blockIdx.x * kRgbBwdWaves + wid);
+  for (int64_t it = 0; it < n_iter; ++it) {
+    const int64_t tile = it * per_iter + (int64_t)blockIdx.x * kRgbBwdWaves + wid;
+    const bool valid = tile < n_tiles;
+    if (valid) {
+      const int64_t n0 = tile * 16;
+      half8_t benc;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        benc[2 * q + 0] = __builtin_bit_cast(_Float16, (uint16_t)(nx[q] & 0xFFFFu));
+        benc[2 * q + 1] = __builtin_bit_cast(_Float16, (uint16_t)(nx[q] >> 16));
+      }
+      const float w_s = nw, g_r[3] = {ng[0], ng[1], ng[2]};
+      float sh[16];
+      sh_eval<4>((nd[0] + 1.0f) / 2.0f, (nd[1] + 1.0f) / 2.0f, (nd[2] + 1.0f) / 2.0f, sh);
+      prefetch(tile + per_iter);
+      half8_t bsh = {};
+      if (g < 2) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bsh[j] = (_Float16)sh[8 * g + j];
+      }
+      const int col = 16 * wid + c;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sm.x[(8 * g + j) * kRgbLd + col] = benc[j];
+      if (g < 2) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sm.x[(32 + 8 * g + j) * kRgbLd + col] = bsh[j];
+      }
+      // forward (as k_rgb_render), H_l staged as X_{l+1}, ReLU masks kept as bits
+      float h[16];
+      uint32_t mask[NH + 1];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float4_t ac = {0.f, 0.f, 0.f, 0.f};
+        ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[t], benc, ac, 0, 0, 0);
+        ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(as[t], bsh, ac, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) h[4 * t + q] = round_f16(fmaxf(ac[q], 0.f));
+      }
+#pragma unroll
+      for (int l = 0; l <= NH; ++l) {
+        uint32_t mk = 0;
+        _Float16* xr = sm.x + (kRgbXRows + 64 * l) * kRgbLd + col;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int hid = 16 * (k >> 2) + 4 * g + (k & 3);
+          xr[hid * kRgbLd] = (_Float16)h[k];
+          mk |= (h[k] > 0.f ? 1u : 0u) << k;
+        }
+        mask[l] = mk;
+        if (l == NH) break;
+        const half8_t b0 = hid_operand(h, 0), b1 = hid_operand(h, 1);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const half8_t w_0 = *reinterpret_cast<const half8_t*>(&sm.w[((8 * l + 2 * t) + 0) * 512 + lane * 8]);
+          const half8_t w_1 = *reinterpret_cast<const half8_t*>(&sm.w[((8 * l + 2 * t) + 1) * 512 + lane * 8]);
+          float4_t ac = {0.f, 0.f, 0.f, 0.f};
+          ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(w_0, b0, ac, 0, 0, 0);
+          ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(w_1, b1, ac, 0, 0, 0);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) h[4 * t + q] = round_f16(fmaxf(ac[q], 0.f));
+        }
+      }
+      float4_t o = {0.f, 0.f, 0.f, 0.f};
+      o = __builtin_amdgcn_mfma_f32_16x16x32_f16(ao[0], hid_operand(h, 0), o, 0, 0, 0);
+      o = __builtin_amdgcn_mfma_f32_16x16x32_f16(ao[1], hid_operand(h, 1), o, 0, 0, 0);
+      // dL/dlogit (rows 0..2 of the padded output, lanes g == 0)
+      float dl[3] = {0.f, 0.f, 0.f};
+      if (g == 0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const float hc = round_f16(o[k]);
+          const float cl = round_f16(1.0f / (1.0f + expf(-hc)));
+          dl[k] = g_r[k] * w_s * cl * (1.0f - cl);
+        }
+      }
+      float mx = fmaxf(fabsf(dl[0]), fmaxf(fabsf(dl[1]), fabsf(dl[2])));
+      float scale = grad_scale(wave_max_nonneg(mx));
+      {
+        _Float16* yr = sm.y + (64 * (NH + 1)) * kRgbLd + col;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) yr[(4 * g + q) * kRgbLd] = (_Float16)(q < 3 && g == 0 ? dl[q < 3 ? q : 0] * scale : 0.f);
+        if (lane == 0) sm.inv[wid][NH + 1] = 1.0f / scale;
+      }
+      half8_t bo = {};
+      if (g == 0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) bo[k] = (_Float16)(dl[k] * scale);
+      }
+      float dh[16];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float4_t ac = {0.f, 0.f, 0.f, 0.f};
+        ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(aot[t], bo, ac, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dh[4 * t + q] = ((mask[NH] >> (4 * t + q)) & 1u) ? ac[q] : 0.f;
+      }
+      // dH_NH .. dH_0: rescale, stage, propagate
+#pragma unroll
+      for (int l = NH; l >= 0; --l) {
+        scale_chain(dh, scale);
+        _Float16* yr = sm.y + (64 * l) * kRgbLd + col;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) yr[(16 * (k >> 2) + 4 * g + (k & 3)) * kRgbLd] = (_Float16)dh[k];
+        if (lane == 0) sm.inv[wid][l] = 1.0f / scale;
+        if (l == 0) break;
+        const half8_t b0 = hid_operand(dh, 0), b1 = hid_operand(dh, 1);
+        float nd[16];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int base = RgbBwdLds<NH>::kOps + 8 * (l - 1) + 2 * t;
+          const half8_t w_0 = *reinterpret_cast<const half8_t*>(&sm.w[(base + 0) * 512 + lane * 8]);
+          const half8_t w_1 = *reinterpret_cast<const half8_t*>(&sm.w[(base + 1) * 512 + lane * 8]);
+          float4_t ac = {0.f, 0.f, 0.f, 0.f};
+          ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(w_0, b0, ac, 0, 0, 0);
+          ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(w_1, b1, ac, 0, 0, 0);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) nd[4 * t + q] = ((mask[l - 1] >> (4 * t + q)) & 1u) ? ac[q] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) dh[k] = nd[k];
+      }
+      // d_enc = W0[:, :32]^T dH_0 (true value: / scale)
+      {
+        const half8_t b0 = hid_operand(dh, 0), b1 = hid_operand(dh, 1);
+        const float inv = 1.0f / scale;
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          float4_t ac = {0.f, 0.f, 0.f, 0.f};
+          ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0t[m][0], b0, ac, 0, 0, 0);
+          ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0t[m][1], b1, ac, 0, 0, 0);
+          const int lvl = 8 * m + 2 * g;
+          denc[(int64_t)lvl * a.enc_stride + n0 + c] = make_float2(ac[0] * inv, ac[1] * inv);
+          denc[(int64_t)(lvl + 1) * a.enc_stride + n0 + c] = make_float2(ac[2] * inv, ac[3] * inv);
+        }
+      }
+    }
+    if (lane == 0) sm.valid[wid] = valid ? 1 : 0;
+    lds_barrier();  // LDS only: the d_enc stores and the next tile's loads stay in flight
+    // owners: dW_i += dY_i X_i^T over the 4 source waves' samples
+    if (wid == 0) rgb_owner<NH, 1>(sm, 0, acc);                       // W0
+    if (wid >= 1 && wid <= NH) rgb_owner<NH, 0>(sm, wid, acc);        // hidden
+    if (wid == (NH + 1) % kRgbBwdWaves) rgb_owner<NH, 2>(sm, NH + 1, acc);  // output
+    lds_barrier();
+  }
+  float* sb = slab + (int64_t)blockIdx.x * rgb_mlp_params<NH>();
+  if (wid == 0) rgb_owner_store<NH, 1>(sb, 0, acc);
+  if (wid >= 1 && wid <= NH) rgb_owner_store<NH, 0>(sb, wid, acc);
+  if (wid == (NH + 1) % kRgbBwdWaves) rgb_owner_store<NH, 2>(sb, NH + 1, acc);
+}
+
+// d_w[i] = sum over the nb slabs, fixed order (as reduce_slabs_fixed, any parameter count)
+__global__ void __launch_bounds__(64 * kSlabWaves) k_rgb_reduce_slabs(const float* __restrict__ slab, int nb, int P,
+                                                                      float* __restrict__ dw) {
+  __shared__ float part[kSlabWaves][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  const int per = (nb + kSlabWaves - 1) / kSlabWaves;
+  const int b0 = wid * per, b1 = b0 + per < nb ? b0 + per : nb;
+  float s = 0.f;
+  if (i < P)
+    for (int b = b0; b < b1; ++b) s += slab[(int64_t)b * P + i];
+  part[wid][lane] = s;
+  __syncthreads();
+  if (wid == 0 && i < P) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < kSlabWaves; ++w) t += part[w][lane];
+    dw[i] = t;
+  }
+}
+
+// loss = inv_count * sum_r ray_loss[r], one workgroup, fixed order
+__global__ void __launch_bounds__(1024) k_rgb_loss_sum(const float* __restrict__ ray_loss, int64_t n, float inv,
+                                                       float* out) {
+  __shared__ float red[16];
+  float v = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) v += ray_loss[i];
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < 16; ++w) t += red[w];
+    out[0] = t * inv;
+  }
+}
+
+constexpr int kRgbBwdMaxBlocks = 256;
 
 }  // namespace lnr
 
@@ -170,15 +492,73 @@ extern "C" int lnr_rgb_render(const uint16_t* w_rgb, int32_t n_hidden_layers, co
   LNR_REQUIRE(enc_stride >= n_rays * (int64_t)n_samples, "lnr_rgb_render: enc_stride too small");
   if (n_rays == 0) return LNR_OK;
   LNR_REQUIRE(w_rgb && enc_rgb && rays && weights && rgb, "lnr_rgb_render: null pointer");
-  RgbArgs a{w_rgb, enc_rgb, enc_stride, rays, weights, n_rays, n_samples, rgb};
+  RgbArgs a{};
+  a.w = w_rgb; a.enc = enc_rgb; a.enc_stride = enc_stride; a.rays = rays; a.weights = weights; a.n_rays = n_rays;
+  a.S = n_samples; a.rgb = rgb;
   const int64_t nb = (n_rays + kRgbWaves - 1) / kRgbWaves;
   const dim3 grid((unsigned)(nb < 4096 ? nb : 4096)), block(64 * kRgbWaves);
   hipStream_t st = as_stream(stream);
   switch (n_hidden_layers - 1) {
-    case 0: hipLaunchKernelGGL(k_rgb_render<0>, grid, block, 0, st, a); break;
-    case 1: hipLaunchKernelGGL(k_rgb_render<1>, grid, block, 0, st, a); break;
-    case 2: hipLaunchKernelGGL(k_rgb_render<2>, grid, block, 0, st, a); break;
-    default: hipLaunchKernelGGL(k_rgb_render<3>, grid, block, 0, st, a); break;
+    case 0: hipLaunchKernelGGL((k_rgb_render<0, false>), grid, block, 0, st, a); break;
+    case 1: hipLaunchKernelGGL((k_rgb_render<1, false>), grid, block, 0, st, a); break;
+    case 2: hipLaunchKernelGGL((k_rgb_render<2, false>), grid, block, 0, st, a); break;
+    default: hipLaunchKernelGGL((k_rgb_render<3, false>), grid, block, 0, st, a); break;
   }
   LNR_RETURN_LAUNCH("lnr_rgb_render");
+}
+
+extern "C" int64_t lnr_rgb_mlp_params(int32_t n_hidden_layers) {
+  return 64 * kRgbIn + (int64_t)(n_hidden_layers - 1) * 64 * 64 + kRgbOutPad * 64;
+}
+
+extern "C" int64_t lnr_rgb_train_workspace_bytes(int32_t n_hidden_layers, int64_t n_rays) {
+  const int64_t P = lnr_rgb_mlp_params(n_hidden_layers);
+  return (int64_t)kRgbBwdMaxBlocks * P * 4 + ((3 * n_rays + 63) / 64) * 64 * 4 + ((n_rays + 63) / 64) * 64 * 4;
+}
+
+template <int NH>
+static int rgb_train_launch(RgbArgs a, float* d_enc, float* d_w, float* slab, float* loss, hipStream_t st) {
+  const int64_t nb_r = (a.n_rays + kRgbWaves - 1) / kRgbWaves;
+  hipLaunchKernelGGL((k_rgb_render<NH, true>), dim3((unsigned)(nb_r < 4096 ? nb_r : 4096)), dim3(64 * kRgbWaves), 0,
+                     st, a);
+  const int64_t tiles = a.n_rays * (int64_t)(a.S / 16);
+  const int64_t want = (tiles + kRgbBwdWaves - 1) / kRgbBwdWaves;
+  const int nb = (int)(want < kRgbBwdMaxBlocks ? want : kRgbBwdMaxBlocks);
+  hipLaunchKernelGGL(k_rgb_bwd_tiles<NH>, dim3(nb), dim3(64 * kRgbBwdWaves), 0, st, a, d_enc, slab);
+  const int P = rgb_mlp_params<NH>();
+  hipLaunchKernelGGL(k_rgb_reduce_slabs, dim3((P + 63) / 64), dim3(64 * kSlabWaves), 0, st, slab, nb, P, d_w);
+  if (loss) hipLaunchKernelGGL(k_rgb_loss_sum, dim3(1), dim3(1024), 0, st, a.ray_loss, a.n_rays, a.inv_count, loss);
+  return LNR_OK;
+}
+
+extern "C" int lnr_rgb_train(const uint16_t* w_rgb, int32_t n_hidden_layers, const uint32_t* enc_rgb,
+                             int64_t enc_stride, const float* rays, const float* weights, const float* intensities,
+                             int64_t n_rays, int32_t n_samples, float inv_count, float* rgb, float* loss,
+                             float* d_enc, float* d_w, void* workspace, int64_t workspace_bytes, void* stream) {
+  LNR_REQUIRE(n_hidden_layers >= 1 && n_hidden_layers <= 4,
+              "lnr_rgb_train: n_hidden_layers=%d not supported (1..4, 64 neurons)", n_hidden_layers);
+  LNR_REQUIRE(n_rays >= 0 && n_samples > 0 && n_samples % 16 == 0,
+              "lnr_rgb_train: n_samples=%d must be a positive multiple of 16", n_samples);
+  LNR_REQUIRE(enc_stride >= n_rays * (int64_t)n_samples, "lnr_rgb_train: enc_stride too small");
+  LNR_REQUIRE(workspace_bytes >= lnr_rgb_train_workspace_bytes(n_hidden_layers, n_rays),
+              "lnr_rgb_train: workspace too small (%lld < %lld bytes)", (long long)workspace_bytes,
+              (long long)lnr_rgb_train_workspace_bytes(n_hidden_layers, n_rays));
+  if (n_rays == 0) return LNR_OK;
+  LNR_REQUIRE(w_rgb && enc_rgb && rays && weights && intensities && rgb && d_enc && d_w && workspace,
+              "lnr_rgb_train: null pointer");
+  const int64_t P = lnr_rgb_mlp_params(n_hidden_layers);
+  float* slab = reinterpret_cast<float*>(workspace);
+  float* g = slab + (int64_t)kRgbBwdMaxBlocks * P;
+  float* ray_loss = g + ((3 * n_rays + 63) / 64) * 64;
+  RgbArgs a{};
+  a.w = w_rgb; a.enc = enc_rgb; a.enc_stride = enc_stride; a.rays = rays; a.weights = weights; a.n_rays = n_rays;
+  a.S = n_samples; a.rgb = rgb; a.gt = intensities; a.g = g; a.ray_loss = ray_loss; a.inv_count = inv_count;
+  hipStream_t st = as_stream(stream);
+  switch (n_hidden_layers - 1) {
+    case 0: rgb_train_launch<0>(a, d_enc, d_w, slab, loss, st); break;
+    case 1: rgb_train_launch<1>(a, d_enc, d_w, slab, loss, st); break;
+    case 2: rgb_train_launch<2>(a, d_enc, d_w, slab, loss, st); break;
+    default: rgb_train_launch<3>(a, d_enc, d_w, slab, loss, st); break;
+  }
+  LNR_RETURN_LAUNCH("lnr_rgb_train");
 }

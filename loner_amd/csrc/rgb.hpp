@@ -1,0 +1,67 @@
+// Colour head (tcnn FullyFusedMLP 48 -> 64 x (NH+1) -> 3, padded 16) operand layouts on gfx950 MFMA,
+// shared by the render kernel (rgb.hip) and the training kernels (rgb_train.hip).  See rgb.hip.
+#pragma once
+#include "mlp.hpp"
+#include "sh.hpp"
+
+namespace lnr {
+
+
+constexpr int kRgbWaves = 4;
+constexpr int kRgbIn = 48, kRgbWidth = 64, kRgbOutPad = 16;
+
+template <int NH>
+struct RgbWeights {
+  half8_t a0[4];          // layer 0, enc columns: W0[16t + c][8g + j]
+  half8_t as[4];          // layer 0, SH columns (k-step zero-padded to 32): W0[16t + c][32 + 8g + j], g < 2
+  half8_t ah[NH > 0 ? NH : 1][4][2];  // hidden layer h, row tile t, k-step s: Wh[16t + c][hid_perm(s, g, j)]
+  half8_t ao[2];          // output: Wout[c][hid_perm(s, g, j)]
+};
+
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+
+// 8 halves = 4 packed dwords: 16 contiguous bytes, or two 8-byte runs (hid_perm: 4g..4g+3 and
+// 16+4g..16+4g+3 of a 32-wide k-step).
+__device__ __forceinline__ half8_t ld_half8(const uint16_t* p) {
+  return __builtin_bit_cast(half8_t, *reinterpret_cast<const u32x4_t*>(p));
+}
+__device__ __forceinline__ half8_t ld_half8_perm(const uint16_t* row, int s, int g) {
+  const u32x2_t lo = *reinterpret_cast<const u32x2_t*>(row + 32 * s + 4 * g);
+  const u32x2_t hi = *reinterpret_cast<const u32x2_t*>(row + 32 * s + 16 + 4 * g);
+  const u32x4_t v = {lo.x, lo.y, hi.x, hi.y};
+  return __builtin_bit_cast(half8_t, v);
+}
+
+template <int NH>
+__device__ __forceinline__ void load_rgb_weights(const uint16_t* __restrict__ w, RgbWeights<NH>& rw) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const uint16_t* w0 = w;  // (64, 48)
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    rw.a0[t] = ld_half8(w0 + (16 * t + c) * kRgbIn + 8 * g);
+    const half8_t z = {};
+    rw.as[t] = g < 2 ? ld_half8(w0 + (16 * t + c) * kRgbIn + 32 + 8 * g) : z;
+  }
+  const uint16_t* wh = w0 + kRgbWidth * kRgbIn;
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) rw.ah[h][t][s] = ld_half8_perm(wh + (16 * t + c) * kRgbWidth, s, g);
+    wh += kRgbWidth * kRgbWidth;
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s) rw.ao[s] = ld_half8_perm(wh + c * kRgbWidth, s, g);
+}
+
+// B operand (k-step s) from a layer's fp16-valued activations h[4t + r] = hid 16t + 4g + r.
+__device__ __forceinline__ half8_t hid_operand(const float (&h)[16], int s) {
+  half8_t b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b[j] = (_Float16)h[4 * (2 * s + (j >> 2)) + (j & 3)];
+  return b;
+}
+
+}  // namespace lnr
