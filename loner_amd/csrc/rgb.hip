@@ -182,25 +182,39 @@ __device__ __forceinline__ void rgb_owner(const RgbBwdLds<NH>& sm, int i, float 
   const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int ybase = 64 * i;  // dO sits at 64 (NH + 1) = 64 i for the output
   const int xbase = i == 0 ? 0 : kRgbXRows + 64 * (i - 1);
+  // the four source tiles are brought to one power-of-two scale (the largest tile's: the others
+  // shift down exactly, or into fp16 subnormals), summed in the MFMA accumulator, then unscaled once
+  float imax = 0.f;
+#pragma unroll
+  for (int sw = 0; sw < kRgbBwdWaves; ++sw)
+    if (sm.valid[sw]) imax = fmaxf(imax, sm.inv[sw][i]);
+  float4_t tmp[Sh::rt][Sh::ct];
+#pragma unroll
+  for (int t = 0; t < Sh::rt; ++t)
+#pragma unroll
+    for (int m = 0; m < Sh::ct; ++m) tmp[t][m] = float4_t{0.f, 0.f, 0.f, 0.f};
   for (int sw = 0; sw < kRgbBwdWaves; ++sw) {
     if (!sm.valid[sw]) continue;
-    const float inv = sm.inv[sw][i];
+    const _Float16 r = (_Float16)(sm.inv[sw][i] / imax);  // 2^-k, k >= 0
+    const half4_t rv = {r, r, r, r};
     const int cs = 16 * sw + 4 * g;
     half4_t ya[Sh::rt], xb[Sh::ct];
 #pragma unroll
-    for (int t = 0; t < Sh::rt; ++t) ya[t] = *reinterpret_cast<const half4_t*>(&sm.y[(ybase + 16 * t + c) * kRgbLd + cs]);
+    for (int t = 0; t < Sh::rt; ++t)
+      ya[t] = *reinterpret_cast<const half4_t*>(&sm.y[(ybase + 16 * t + c) * kRgbLd + cs]) * rv;
 #pragma unroll
     for (int m = 0; m < Sh::ct; ++m) xb[m] = *reinterpret_cast<const half4_t*>(&sm.x[(xbase + 16 * m + c) * kRgbLd + cs]);
 #pragma unroll
     for (int t = 0; t < Sh::rt; ++t)
 #pragma unroll
-      for (int m = 0; m < Sh::ct; ++m) {
-        float4_t d = {0.f, 0.f, 0.f, 0.f};
-        d = __builtin_amdgcn_mfma_f32_16x16x16f16(ya[t], xb[m], d, 0, 0, 0);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[Sh::slot(t, m)][q] = fmaf(d[q], inv, acc[Sh::slot(t, m)][q]);
-      }
+      for (int m = 0; m < Sh::ct; ++m) tmp[t][m] = __builtin_amdgcn_mfma_f32_16x16x16f16(ya[t], xb[m], tmp[t][m], 0, 0, 0);
   }
+#pragma unroll
+  for (int t = 0; t < Sh::rt; ++t)
+#pragma unroll
+    for (int m = 0; m < Sh::ct; ++m)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[Sh::slot(t, m)][q] = fmaf(tmp[t][m][q], imax, acc[Sh::slot(t, m)][q]);
 }
 
 template <int NH, int KIND>
