@@ -41,8 +41,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="C2", choices=["C1", "C2", "C3", "C4", "CAM"],
-                    help="C1/C2/C4: optimiser step; C3: inference render (peak depth, N_samples_test=2048); "
+    ap.add_argument("--config", default="C2", choices=["C1", "C2", "C3", "C4", "C5", "CAM"],
+                    help="C1/C2/C4: optimiser step; C5: C4-shaped independent submap jobs, one per GPU "
+                         "(replicas, no collectives); C3: inference render (peak depth, N_samples_test=2048); "
                          "CAM: colour-head training iteration (camera phase)")
     ap.add_argument("--rays", default="device", choices=["device", "resident"],
                     help="device: select + build each step's rays on the GPU from the resident window; "
@@ -401,9 +402,19 @@ def main():
     from loner_amd import synthetic as syn
     kind, nkf, rpk, spk, strat, n_samples, preset = syn.CONFIGS[args.config]
     scale = syn.CUBES[kind][0]
+    replicas = args.config == "C5"  # independent jobs: own window per rank, no data-path collective
 
     # ---- workload
-    if args.rays == "device":
+    if args.rays == "device" and replicas:
+        from loner_amd.rays import RayWindow
+        scans = syn.make_window(kind, nkf, seed=1000 + rank, start=50 * rank)
+        window = RayWindow(scans, syn.world_cube(kind), syn.SENSORS[kind]["ray_range"], n_lidar=rpk, n_sky=spk,
+                           strategy=strat, device=dev)
+        del scans
+        if not window.all_valid:
+            raise RuntimeError("bench window must give a fixed batch")
+        R = window.n_slots
+    elif args.rays == "device":
         # one global keyframe window (nkf keyframes per rank), resident on every rank; rank r builds
         # the slots of its own nkf keyframes each step (a contiguous R/g slice)
         from loner_amd.rays import RayWindow
@@ -428,17 +439,19 @@ def main():
                         loss=S_.LossConfig.from_dict(LOSS_PRESETS[preset]))
     state = S_.FieldState(cfg, device=dev)
     allreduce = None
-    if dist is not None:
+    if dist is not None and not replicas:
         def allreduce(t, async_op=False):
             return dist.all_reduce(t, async_op=async_op)
-    eng = S_.StepEngine(state, R, seed=12345, allreduce=allreduce, ray_offset=rank * R)
+    eng = S_.StepEngine(state, R, seed=12345 + (rank if replicas else 0), allreduce=allreduce,
+                        ray_offset=0 if replicas else rank * R)
+    r_glob = R if replicas else R * world
 
     def run(i, prof=None):
         if args.rays == "device":
-            return eng.step_window(window, global_step=i, n_rays_global=R * world, prof=prof)
+            return eng.step_window(window, global_step=i, n_rays_global=r_glob, prof=prof)
         rays, dgt = batches[i % len(batches)]
         return eng.step(rays, dgt, global_step=i, scale=scale, far_ref=far_ref[i % len(batches)],
-                        n_rays_global=R * world, prof=prof)
+                        n_rays_global=r_glob, prof=prof)
 
     for i in range(args.warmup):
         run(i)
@@ -490,7 +503,7 @@ def main():
         "config": {"workload": f"{args.config}: {nkf} KF x ({rpk} + {spk} sky) rays x {n_samples} samples per GPU, "
                                f"L=16 T=2^18 hash grid + 64-wide sigma MLP, {preset} loss (L1_JS)",
                    "rays_per_gpu": R, "samples_per_ray": n_samples, "global_rays": R * world,
-                   "parallelism": f"dp{world}" if world > 1 else "single"},
+                   "parallelism": (f"replicas{world}" if replicas else f"dp{world}") if world > 1 else "single"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "hash-grid backward stage (k_bwd_scan_*, k_bwd_scatter, k_bwd_level_max, k_bwd_accum)",

@@ -189,4 +189,7 @@ CONFIGS = {
     "C2": ("quad", 16, 512, 0, "RANDOM", 512, "default"),
     "C3": ("canteen", 8, 512, 0, "RANDOM", 2048, "default"),
     "C4": ("forest", 16, 512, 64, "MASK", 512, "haveri"),
+    # C5 submaps: C4-like independent single-GPU jobs, one per GPU, no collectives
+    # (examples/fdt_segment_and_optimize_submaps.py:24,86-109); each rank its own trajectory segment
+    "C5": ("forest", 16, 512, 64, "MASK", 512, "haveri"),
 }
