@@ -175,7 +175,17 @@ typedef struct lnr_loss_params {
                                 when non-NULL it overrides inv_n_opaque (= 1/max(count,1)) */
   const float* dev_far_ref;  /* optional DEVICE scalar overriding far_ref (rays built on the device:
                                 lnr_build_lidar_rays writes it) */
+  uint32_t* dev_status;      /* optional DEVICE word: LNR_STATUS_* bits are OR-ed in (no host sync; the
+                                caller reads it when it chooses, e.g. once per window) */
 } lnr_loss_params;
+
+/* Status bits (replace the reference's per-step host checks):
+ *   LNR_STATUS_NAN_LOSS     loss is NaN: optimizer.py:854 asserts "NaN Loss Encountered"
+ *   LNR_STATUS_INF_LOSS     loss is +-inf
+ *   LNR_STATUS_SIGMA_CLIPPED a sigma was non-finite and clipped by nan_to_num (nerf_tcnn.py:74-78 warns) */
+#define LNR_STATUS_NAN_LOSS 1u
+#define LNR_STATUS_INF_LOSS 2u
+#define LNR_STATUS_SIGMA_CLIPPED 4u
 
 /* Per-ray partial sums written by the loss kernels: [depth_sq_err, los_sum, opacity_abs_err, eps, opaque] */
 #define LNR_RAY_STATS 5

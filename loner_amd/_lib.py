@@ -44,7 +44,11 @@ class LossParams(ctypes.Structure):
                 ("depthloss_lambda", ctypes.c_float), ("min_depth_eps", ctypes.c_float),
                 ("min_js", ctypes.c_float), ("max_js", ctypes.c_float), ("js_alpha", ctypes.c_float),
                 ("los_eps", ctypes.c_float), ("far_ref", ctypes.c_float), ("inv_n_opaque", ctypes.c_float),
-                ("inv_rs", ctypes.c_float), ("dev_n_opaque", ctypes.c_void_p), ("dev_far_ref", ctypes.c_void_p)]
+                ("inv_rs", ctypes.c_float), ("dev_n_opaque", ctypes.c_void_p), ("dev_far_ref", ctypes.c_void_p),
+                ("dev_status", ctypes.c_void_p)]
+
+
+STATUS_NAN_LOSS, STATUS_INF_LOSS, STATUS_SIGMA_CLIPPED = 1, 2, 4
 
 
 SELECT = {"RANDOM": 0, "MASK": 1, "ALL": 2, "GIVEN": 3}

@@ -392,6 +392,7 @@ __device__ __forceinline__ void mlp_forward_ray(const FieldArgs& a, const RaySha
     float h[16];
     const float sg = sigma_tile_fwd(sw, b, h);
     if (g == 0) sh.sig[tb + c] = sigma_to_f16(sg);
+    if (a.lp.dev_status && __any(!isfinite(round_f16(sg))) && lane == 0) atomicOr(a.lp.dev_status, LNR_STATUS_SIGMA_CLIPPED);
   }
   __syncthreads();
 }
@@ -720,6 +721,7 @@ __global__ void __launch_bounds__(NT) k_field_wave(FieldArgs a) {
       float h[16];
       const float sgm = sigma_tile_fwd(sw, load_enc_operand(a.enc, a.enc_stride, r * S + tb + c, true), h);
       if (g == 0) sig[tb + c] = sigma_to_f16(sgm);
+      if (a.lp.dev_status && __any(!isfinite(round_f16(sgm))) && lane == 0) atomicOr(a.lp.dev_status, LNR_STATUS_SIGMA_CLIPPED);
     }
     wave_lds_handoff();
     composite_loss_wave<C>(a, sig, r);
@@ -846,6 +848,10 @@ __global__ void __launch_bounds__(kReduceThreads) k_loss_finalize(const float* _
     const float lterm = v[1] * lp.inv_rs;
     const float oterm = v[2] * inv_nop;
     out[0] = lp.depthloss_lambda * dterm + lp.los_lambda * lterm + oterm;
+    if (lp.dev_status) {
+      const uint32_t bits = (isnan(out[0]) ? LNR_STATUS_NAN_LOSS : 0u) | (isinf(out[0]) ? LNR_STATUS_INF_LOSS : 0u);
+      if (bits) atomicOr(lp.dev_status, bits);
+    }
     out[1] = n > 0 ? v[3] / (float)n : 0.f;
     out[2] = dterm;
     out[3] = lterm;

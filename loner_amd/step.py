@@ -13,6 +13,7 @@ Parameter layout (tcnn ``NetworkWithInputEncoding``: network first, then encodin
 fp32 master + Adam moments; an fp16 shadow of the whole buffer feeds the forward kernels.
 """
 import math
+import warnings
 from dataclasses import dataclass, field
 
 import torch
@@ -171,6 +172,8 @@ class StepEngine:
         # field has trained a few steps, and the extra count pass (d_enc reads) costs more than the
         # records it saves (3.35 vs 3.18 ms/step), so it is opt-in for sparse-gradient workloads.
         self.count_in_forward = count_in_forward
+        self.status = torch.zeros(1, dtype=torch.int32, device=state.device)  # LNR_STATUS_* bits
+        self._warned_clip = False
         # level ranges of the bucketed gradient all-reduce, finest first (their records dominate the
         # accumulation, so the first ranges' exchange overlaps the later ranges' accumulation)
         nl = self.cfg.n_levels
@@ -214,7 +217,23 @@ class StepEngine:
         lp.inv_rs = 1.0 / float(n_rays_global * self.S)
         lp.dev_n_opaque = self.n_opaque.data_ptr()
         lp.dev_far_ref = None if dev_far_ref is None else dev_far_ref.data_ptr()
+        lp.dev_status = self.status.data_ptr()
         return lp
+
+    def check_status(self, clear=True):
+        """Read the device status word (one host sync; call it as often as the caller wants, e.g. once
+        per window).  Raises like the reference's per-step ``assert not torch.isnan(loss), "NaN Loss
+        Encountered"`` (optimizer.py:854) and warns once, like DecoupledNeRF (nerf_tcnn.py:74-78),
+        when a non-finite sigma was clipped.  Returns the bits."""
+        bits = int(self.status.item())
+        if clear:
+            self.status.zero_()
+        if bits & L.STATUS_SIGMA_CLIPPED and not self._warned_clip:
+            self._warned_clip = True
+            warnings.warn("Clipping infinite outputs. Will not warn about this again (but it will happen again)")
+        if bits & L.STATUS_NAN_LOSS:
+            raise RuntimeError("NaN Loss Encountered")
+        return bits
 
     def _allreduce_async(self, t):
         """``allreduce(t, async_op=True)`` when the hook supports it (torch.distributed's

@@ -77,3 +77,36 @@ def test_ragged_sample_counts_step(L, S):
         assert np.isfinite(out.cpu().numpy()[0])
         grads.append(st.grad.clone())
     assert torch.equal(grads[0], grads[1])
+
+
+def test_status_flags_replace_the_nan_assert(L):
+    """The device status word: a clean step leaves it 0; a NaN loss sets LNR_STATUS_NAN_LOSS and
+    check_status raises the reference's "NaN Loss Encountered" (optimizer.py:854); an infinite
+    sigma sets LNR_STATUS_SIGMA_CLIPPED and warns once (nerf_tcnn.py:74-78) without failing."""
+    import warnings
+    from loner_amd import step as S_
+    from loner_amd import synthetic as syn
+    win = syn.make_window("quad", 1, seed=3)
+    rays, dgt = syn.build_batch(win, "quad", 40, 0, "RANDOM", seed=2)
+    rays, dgt = rays.cuda(), dgt.cuda()
+    sc, far = syn.CUBES["quad"][0], float(rays[0, -1])
+    st = S_.FieldState(S_.StepConfig(n_samples=64), device="cuda:0", table_init=0.3)
+    eng = S_.StepEngine(st, rays.shape[0], seed=4)
+    eng.step(rays, dgt, global_step=1, scale=sc, far_ref=far)
+    assert eng.check_status() == 0
+    eng.step(rays, dgt, global_step=2, scale=float("nan"), far_ref=far)
+    with pytest.raises(RuntimeError, match="NaN Loss Encountered"):
+        eng.check_status()
+    assert eng.check_status() == 0  # cleared by the read
+    st2 = S_.FieldState(S_.StepConfig(n_samples=64), device="cuda:0", table_init=0.3)
+    with torch.no_grad():
+        st2.params[:2048].fill_(1e4)  # fp16 hidden activations overflow -> sigma inf -> clipped
+        st2.params[2048:3072].fill_(1e4)
+    st2.refresh_shadow()
+    eng2 = S_.StepEngine(st2, rays.shape[0], seed=4)
+    eng2.step(rays, dgt, global_step=1, scale=sc, far_ref=far)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        bits = eng2.check_status()
+    assert bits & L.STATUS_SIGMA_CLIPPED
+    assert any("Clipping infinite outputs" in str(x.message) for x in w)
