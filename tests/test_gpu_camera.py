@@ -164,3 +164,55 @@ def test_camera_step_learns_and_is_deterministic(L):
         eng2.step(rays[:n], inten[:n])
         eng3.step(rays[:n], inten[:n])
     assert torch.equal(cs2.params, cs3.params)
+
+
+def test_camera_two_shards_match_single_batch(L):
+    """Data-parallel camera phase: two engines on the two halves of the rays (draws keyed by global
+    ray index, loss normalised by the global ray count, one gradient all-reduce) reproduce the
+    single-engine iteration, and both replicas hold identical parameters after Adam."""
+    import threading
+    from loner_amd import camera as C
+    fr, cs_ref, eng_ref = _camera_setup()
+    R = fr.n_rays(1)
+    rays = torch.empty(R, 13, device="cuda:0")
+    inten = torch.empty(R, 3, device="cuda:0")
+    fr.build(1, rays, inten)
+    loss_ref = float(eng_ref.step(rays, inten, global_step=7).item())
+    g_ref = host(cs_ref.grad).copy()
+
+    bar = threading.Barrier(2)
+    slots = [None, None]
+
+    def make_allreduce(rank):
+        def allreduce(t):
+            torch.cuda.synchronize()
+            slots[rank] = t
+            bar.wait()
+            if rank == 0:
+                tot = slots[0] + slots[1]
+                slots[0].copy_(tot)
+                slots[1].copy_(tot)
+                torch.cuda.synchronize()
+            bar.wait()
+        return allreduce
+
+    states = [_camera_setup()[1], _camera_setup()[1]]
+    field = eng_ref.field
+    losses = [None, None]
+
+    def run(rank):
+        s0, s1 = (0, R // 2) if rank == 0 else (R // 2, R)
+        eng = C.CameraStepEngine(field, states[rank], n_rays=s1 - s0, n_samples=128, lr=0.01, seed=0,
+                                 allreduce=make_allreduce(rank), ray_offset=s0)
+        losses[rank] = float(eng.step(rays[s0:s1].contiguous(), inten[s0:s1].contiguous(), global_step=7,
+                                      n_rays_global=R).item())
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert losses[0] + losses[1] == pytest.approx(loss_ref, rel=1e-5)
+    g = host(states[0].grad)
+    assert _rel(g, g_ref) < 1e-5
+    assert torch.equal(states[0].params, states[1].params)
