@@ -186,6 +186,9 @@ typedef struct lnr_loss_params {
 #define LNR_STATUS_NAN_LOSS 1u
 #define LNR_STATUS_INF_LOSS 2u
 #define LNR_STATUS_SIGMA_CLIPPED 4u
+#define LNR_STATUS_NONFINITE_OUTPUT 8u  /* lnr_status_scan found nan/inf (rendering_tcnn.py:419-424 DEBUG scan) */
+/* ORs `bit` into the device word `status` when any of values[0..n) is nan or inf (no host sync). */
+int lnr_status_scan(const float* values, int64_t n, uint32_t bit, uint32_t* status, void* stream);
 
 /* Per-ray partial sums written by the loss kernels: [depth_sq_err, los_sum, opacity_abs_err, eps, opaque] */
 #define LNR_RAY_STATS 5

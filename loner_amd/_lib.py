@@ -48,7 +48,7 @@ class LossParams(ctypes.Structure):
                 ("dev_status", ctypes.c_void_p)]
 
 
-STATUS_NAN_LOSS, STATUS_INF_LOSS, STATUS_SIGMA_CLIPPED = 1, 2, 4
+STATUS_NAN_LOSS, STATUS_INF_LOSS, STATUS_SIGMA_CLIPPED, STATUS_NONFINITE_OUTPUT = 1, 2, 4, 8
 
 
 SELECT = {"RANDOM": 0, "MASK": 1, "ALL": 2, "GIVEN": 3}
@@ -118,6 +118,7 @@ _SIGNATURES = {
     "lnr_field_render": (ctypes.c_int, [c_p, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_i32, c_f, c_p, c_u32, c_i64, c_p,
                                         c_p, c_p, c_p, c_p]),
     "lnr_rgb_render": (ctypes.c_int, [c_p, c_i32, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_p, c_p]),
+    "lnr_status_scan": (ctypes.c_int, [c_p, c_i64, c_u32, c_p, c_p]),
     "lnr_rgb_mlp_params": (c_i64, [c_i32]),
     "lnr_rgb_train_workspace_bytes": (c_i64, [c_i32, c_i64]),
     "lnr_rgb_train": (ctypes.c_int, [c_p, c_i32, c_p, c_i64, c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_p, c_p, c_p,

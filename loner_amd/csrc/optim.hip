@@ -251,3 +251,24 @@ extern "C" int lnr_f32_to_f16(const float* src, uint16_t* dst, int64_t n, void* 
   hipLaunchKernelGGL(k_f32_to_f16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), src, dst, n);
   LNR_RETURN_LAUNCH("lnr_f32_to_f16");
 }
+
+// ------------------------------------------------------------------ status scan
+// rendering_tcnn.py:419-424 (DEBUG): every result tensor is scanned for nan/inf on the host.  Here
+// one launch ORs `bit` into the device status word when any of the n values is not finite.
+__global__ void __launch_bounds__(256) k_status_scan(const float* __restrict__ x, int64_t n, uint32_t bit,
+                                                     uint32_t* status) {
+  bool bad = false;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    bad |= !isfinite(x[i]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(status, bit);
+}
+
+extern "C" int lnr_status_scan(const float* values, int64_t n, uint32_t bit, uint32_t* status, void* stream) {
+  LNR_REQUIRE(n >= 0 && status != nullptr, "lnr_status_scan: bad arguments");
+  if (n == 0) return LNR_OK;
+  LNR_REQUIRE(values != nullptr, "lnr_status_scan: null values");
+  const int64_t want = (n + 255) / 256;
+  hipLaunchKernelGGL(k_status_scan, dim3((unsigned)(want < 1024 ? want : 1024)), dim3(256), 0, as_stream(stream), values,
+                     n, bit, status);
+  LNR_RETURN_LAUNCH("lnr_status_scan");
+}

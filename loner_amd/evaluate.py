@@ -81,6 +81,7 @@ class DepthRenderer:
         self.z = torch.empty(self.chunk, self.S, dtype=torch.float32, device=dev)
         self.enc = torch.empty(state.cfg.n_levels, self.chunk * self.S, dtype=torch.int32, device=dev)
         self.color = color
+        self.status = torch.zeros(1, dtype=torch.int32, device=dev)  # LNR_STATUS_* bits (DEBUG scan)
         if color is not None:
             if self.S % 16:
                 raise ValueError("colour rendering needs n_samples % 16 == 0")
@@ -121,7 +122,19 @@ class DepthRenderer:
                        stride, None, 0, s)
                 L.call("lnr_rgb_render", c.mlp, c.n_hidden_layers, self.enc_rgb, stride, rc, self.weights, n, self.S,
                        rgb[r0:r0 + n], s)
+        for t in (depth, opacity, variance) + ((rgb,) if rgb is not None else ()):
+            L.call("lnr_status_scan", t, t.numel(), L.STATUS_NONFINITE_OUTPUT, self.status, s)
         return depth, opacity, variance
+
+    def check_status(self, clear=True):
+        """Model.forward's DEBUG scan (rendering_tcnn.py:419-424) without a per-render sync: prints the
+        reference's message when any rendered output held nan/inf since the last check."""
+        bits = int(self.status.item())
+        if clear:
+            self.status.zero_()
+        if bits & L.STATUS_NONFINITE_OUTPUT:
+            print("! [Numerical Error] a rendered output contains nan or inf.")
+        return bits
 
 
 def scan_window(scan, pose, world_cube, ray_range, device):

@@ -110,3 +110,17 @@ def test_status_flags_replace_the_nan_assert(L):
         bits = eng2.check_status()
     assert bits & L.STATUS_SIGMA_CLIPPED
     assert any("Clipping infinite outputs" in str(x.message) for x in w)
+
+
+def test_status_scan_flags_nonfinite(L):
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    x = torch.ones(100000, device="cuda")
+    L.call("lnr_status_scan", x, x.numel(), L.STATUS_NONFINITE_OUTPUT, st, L.stream())
+    assert int(st.item()) == 0
+    x[77777] = float("inf")
+    L.call("lnr_status_scan", x, x.numel(), L.STATUS_NONFINITE_OUTPUT, st, L.stream())
+    assert int(st.item()) == L.STATUS_NONFINITE_OUTPUT
+    x[77777] = float("nan")
+    st.zero_()
+    L.call("lnr_status_scan", x, x.numel(), 1, st, L.stream())
+    assert int(st.item()) == 1
