@@ -176,26 +176,35 @@ struct RgbOwnerShape {
   __device__ static constexpr int slot(int t, int m) { return KIND == 0 ? 4 * t + m : (KIND == 1 ? 3 * t + m : 12 + m); }
 };
 
+// The owner's tiles accumulate in the MFMA accumulators themselves, at a running power-of-two scale
+// `run` (values held = true x run): a source tile whose own scale s is larger is shifted down by
+// run / s <= 1 in fp16 (exact, or into subnormals for tiles far below the running maximum); a tile
+// that needs a smaller scale first rescales the accumulators (rare: the running maximum only grows).
 template <int NH, int KIND>
-__device__ __forceinline__ void rgb_owner(const RgbBwdLds<NH>& sm, int i, float (&acc)[16][4]) {
+__device__ __forceinline__ void rgb_owner(const RgbBwdLds<NH>& sm, int i, float4_t (&acc)[16], float& run) {
   using Sh = RgbOwnerShape<KIND>;
   const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int ybase = 64 * i;  // dO sits at 64 (NH + 1) = 64 i for the output
   const int xbase = i == 0 ? 0 : kRgbXRows + 64 * (i - 1);
-  // the four source tiles are brought to one power-of-two scale (the largest tile's: the others
-  // shift down exactly, or into fp16 subnormals), summed in the MFMA accumulator, then unscaled once
-  float imax = 0.f;
+  float imax = 0.f;  // 1 / the smallest scale of this iteration's tiles
 #pragma unroll
   for (int sw = 0; sw < kRgbBwdWaves; ++sw)
     if (sm.valid[sw]) imax = fmaxf(imax, sm.inv[sw][i]);
-  float4_t tmp[Sh::rt][Sh::ct];
+  if (imax == 0.f) return;
+  const float s_new = 1.0f / imax;
+  if (s_new < run) {  // wave-uniform
+    if (run != INFINITY) {
+      const float f = s_new / run;
 #pragma unroll
-  for (int t = 0; t < Sh::rt; ++t)
+      for (int t = 0; t < Sh::rt; ++t)
 #pragma unroll
-    for (int m = 0; m < Sh::ct; ++m) tmp[t][m] = float4_t{0.f, 0.f, 0.f, 0.f};
+        for (int m = 0; m < Sh::ct; ++m) acc[Sh::slot(t, m)] *= f;
+    }
+    run = s_new;
+  }
   for (int sw = 0; sw < kRgbBwdWaves; ++sw) {
     if (!sm.valid[sw]) continue;
-    const _Float16 r = (_Float16)(sm.inv[sw][i] / imax);  // 2^-k, k >= 0
+    const _Float16 r = (_Float16)(run * sm.inv[sw][i]);  // run / s_sw = 2^-k, k >= 0
     const half4_t rv = {r, r, r, r};
     const int cs = 16 * sw + 4 * g;
     half4_t ya[Sh::rt], xb[Sh::ct];
@@ -207,27 +216,23 @@ __device__ __forceinline__ void rgb_owner(const RgbBwdLds<NH>& sm, int i, float 
 #pragma unroll
     for (int t = 0; t < Sh::rt; ++t)
 #pragma unroll
-      for (int m = 0; m < Sh::ct; ++m) tmp[t][m] = __builtin_amdgcn_mfma_f32_16x16x16f16(ya[t], xb[m], tmp[t][m], 0, 0, 0);
+      for (int m = 0; m < Sh::ct; ++m)
+        acc[Sh::slot(t, m)] = __builtin_amdgcn_mfma_f32_16x16x16f16(ya[t], xb[m], acc[Sh::slot(t, m)], 0, 0, 0);
   }
-#pragma unroll
-  for (int t = 0; t < Sh::rt; ++t)
-#pragma unroll
-    for (int m = 0; m < Sh::ct; ++m)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) acc[Sh::slot(t, m)][q] = fmaf(tmp[t][m][q], imax, acc[Sh::slot(t, m)][q]);
 }
 
 template <int NH, int KIND>
-__device__ __forceinline__ void rgb_owner_store(float* __restrict__ sb, int i, const float (&acc)[16][4]) {
+__device__ __forceinline__ void rgb_owner_store(float* __restrict__ sb, int i, const float4_t (&acc)[16], float run) {
   using Sh = RgbOwnerShape<KIND>;
   const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   float* mat = sb + rgb_layer_offset<NH>(i);
+  const float inv = run == INFINITY ? 0.f : 1.0f / run;
 #pragma unroll
   for (int t = 0; t < Sh::rt; ++t)
 #pragma unroll
     for (int m = 0; m < Sh::ct; ++m)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) mat[(16 * t + 4 * g + q) * Sh::ld + 16 * m + c] = acc[Sh::slot(t, m)][q];
+      for (int q = 0; q < 4; ++q) mat[(16 * t + 4 * g + q) * Sh::ld + 16 * m + c] = acc[Sh::slot(t, m)][q] * inv;
 }
 
 template <int NH>
@@ -275,11 +280,10 @@ __global__ void __launch_bounds__(64 * kRgbBwdWaves) k_rgb_bwd_tiles(RgbArgs a, 
     *reinterpret_cast<half8_t*>(&sm.w[op * 512 + lane * 8]) = v;
   }
   // ---- owner jobs: matrix i (0 = W0, 1..NH hidden, NH + 1 = output) -> wave i, the 5th to wave 0
-  float acc[16][4];
+  float4_t acc[16];
 #pragma unroll
-  for (int k = 0; k < 16; ++k)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[k][q] = 0.f;
+  for (int k = 0; k < 16; ++k) acc[k] = float4_t{0.f, 0.f, 0.f, 0.f};
+  float run_a = INFINITY, run_b = INFINITY;  // running scales of the (up to two) owned matrices
   __syncthreads();
 
   const int64_t n_tiles = a.n_rays * (int64_t)(a.S / 16);
@@ -442,15 +446,15 @@ __global__ void __launch_bounds__(64 * kRgbBwdWaves) k_rgb_bwd_tiles(RgbArgs a, 
     if (lane == 0) sm.valid[wid] = valid ? 1 : 0;
     lds_barrier();  // LDS only: the d_enc stores and the next tile's loads stay in flight
     // owners: dW_i += dY_i X_i^T over the 4 source waves' samples
-    if (wid == 0) rgb_owner<NH, 1>(sm, 0, acc);                       // W0
-    if (wid >= 1 && wid <= NH) rgb_owner<NH, 0>(sm, wid, acc);        // hidden
-    if (wid == (NH + 1) % kRgbBwdWaves) rgb_owner<NH, 2>(sm, NH + 1, acc);  // output
+    if (wid == 0) rgb_owner<NH, 1>(sm, 0, acc, run_a);                       // W0
+    if (wid >= 1 && wid <= NH) rgb_owner<NH, 0>(sm, wid, acc, run_a);        // hidden
+    if (wid == (NH + 1) % kRgbBwdWaves) rgb_owner<NH, 2>(sm, NH + 1, acc, run_b);  // output
     lds_barrier();
   }
   float* sb = slab + (int64_t)blockIdx.x * rgb_mlp_params<NH>();
-  if (wid == 0) rgb_owner_store<NH, 1>(sb, 0, acc);
-  if (wid >= 1 && wid <= NH) rgb_owner_store<NH, 0>(sb, wid, acc);
-  if (wid == (NH + 1) % kRgbBwdWaves) rgb_owner_store<NH, 2>(sb, NH + 1, acc);
+  if (wid == 0) rgb_owner_store<NH, 1>(sb, 0, acc, run_a);
+  if (wid >= 1 && wid <= NH) rgb_owner_store<NH, 0>(sb, wid, acc, run_a);
+  if (wid == (NH + 1) % kRgbBwdWaves) rgb_owner_store<NH, 2>(sb, NH + 1, acc, run_b);
 }
 
 // d_w[i] = sum over the nb slabs, fixed order (as reduce_slabs_fixed, any parameter count)
