@@ -49,6 +49,9 @@ def parse():
                     help="device: select + build each step's rays on the GPU from the resident window; "
                          "resident: cycle prebuilt ray batches")
     ap.add_argument("--batches", type=int, default=4, help="--rays resident: distinct batches cycled per rank")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: each rank optimises the config's full batch (global batch grows with N); "
+                         "strong: the config's batch is split over the N ranks (SURVEY.md §8(e))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rays", type=int, default=256, help="rays per CPU-baseline step (x512 samples)")
     ap.add_argument("--cpu-steps", type=int, default=36)
@@ -418,7 +421,7 @@ def main():
         # one global keyframe window (nkf keyframes per rank), resident on every rank; rank r builds
         # the slots of its own nkf keyframes each step (a contiguous R/g slice)
         from loner_amd.rays import RayWindow
-        scans = syn.make_window(kind, nkf * world, seed=1000)
+        scans = syn.make_window(kind, nkf if args.scaling == "strong" else nkf * world, seed=1000)
         window = RayWindow(scans, syn.world_cube(kind), syn.SENSORS[kind]["ray_range"], n_lidar=rpk, n_sky=spk,
                            strategy=strat, device=dev)
         del scans
@@ -426,6 +429,8 @@ def main():
             raise RuntimeError("bench window must give a fixed, evenly sharded batch")
         R = window.n_slots // world
     else:
+        if args.scaling == "strong":
+            raise SystemExit("--scaling strong needs --rays device")
         batches = []
         for b in range(args.batches):
             win = syn.make_window(kind, nkf, seed=1000 * rank + b, start=17 * b + 5 * rank)
@@ -494,14 +499,15 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.scaling == "strong" and not replicas else "weak",
         "vs_baseline": None,
         "dtype": "fp16 params/activations, fp32 accumulate+optimizer",
         "data": f"synthetic {kind} LiDAR scene (analytic ray-cast), "
                 + ("keyframe scans resident in HBM, rays selected + built on the GPU every step"
                    if args.rays == "device" else "prebuilt rays resident in HBM") + "; random-init sigma field",
-        "config": {"workload": f"{args.config}: {nkf} KF x ({rpk} + {spk} sky) rays x {n_samples} samples per GPU, "
-                               f"L=16 T=2^18 hash grid + 64-wide sigma MLP, {preset} loss (L1_JS)",
+        "config": {"workload": f"{args.config}: {nkf} KF x ({rpk} + {spk} sky) rays x {n_samples} samples "
+                               + ("in total, split over the GPUs, " if args.scaling == "strong" else "per GPU, ")
+                               + f"L=16 T=2^18 hash grid + 64-wide sigma MLP, {preset} loss (L1_JS)",
                    "rays_per_gpu": R, "samples_per_ray": n_samples, "global_rays": R * world,
                    "parallelism": (f"replicas{world}" if replicas else f"dp{world}") if world > 1 else "single"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
