@@ -91,6 +91,13 @@ int lnr_hashgrid_fwd(const lnr_grid_desc* d, const float* pos01, int64_t n, cons
 int lnr_hashgrid_fwd_rays(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
                           int32_t n_samples, const uint16_t* table, uint32_t* enc, int64_t enc_stride,
                           void* bwd_ws, int64_t bwd_ws_bytes, void* stream);
+/* Forward of samples whose compositing weight can be zero (the colour head: rgb = sum w_i c_i + ...,
+ * rendering_tcnn.py:286): samples with live[n] == 0 (exactly) get a zero encoding and issue no
+ * gathers, every other sample is encoded exactly as lnr_hashgrid_fwd_rays does.  live = the (R,S)
+ * weights of the sigma pass.  No backward histogram. */
+int lnr_hashgrid_fwd_rays_live(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
+                               int32_t n_samples, const uint16_t* table, const float* live, uint32_t* enc,
+                               int64_t enc_stride, void* stream);
 /* Backward: d_table (n_entries,2) fp32 = scatter of corner weights * d_enc, as an atomic-free
  * binned scatter with int64 fixed-point accumulation.  d_table is OVERWRITTEN (every
  * entry, zero where no sample touches it) and the result is bitwise reproducible; `workspace`

@@ -15,10 +15,14 @@ namespace lnr {
 
 template <class PosFn, bool COUNT>
 __global__ void __launch_bounds__(1024) k_hashgrid_fwd(GridArgs a, PosFn pos, int64_t n, const uint32_t* __restrict__ table,
-                                                      uint32_t* __restrict__ enc, int64_t stride, BwdWorkspace ws) {
+                                                      uint32_t* __restrict__ enc, int64_t stride, BwdWorkspace ws,
+                                                      const float* __restrict__ live) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t l = blockIdx.y;
   const bool in = i < n;
+  // live (forward only, never with COUNT): samples whose weight is exactly 0 get a zero encoding and
+  // issue no gathers
+  const bool use = in && (COUNT || live == nullptr || live[i] != 0.f);
   if (!COUNT && !in) return;
   __shared__ uint32_t hist[COUNT ? kMaxChunksPerLevel : 1];
   if (COUNT) {
@@ -30,7 +34,8 @@ __global__ void __launch_bounds__(1024) k_hashgrid_fwd(GridArgs a, PosFn pos, in
   if (lv.fine) {  // block-uniform
     FineCell c;
     fine_cell(lv, x, y, z, c);
-    if (in) {
+    if (!COUNT && in && !use) enc[(int64_t)l * stride + i] = 0u;
+    if (use) {
       const uint32_t* tl = table + lv.offset;
       uint32_t v[8];
 #ifdef LNR_FWD_X4
@@ -76,7 +81,8 @@ __global__ void __launch_bounds__(1024) k_hashgrid_fwd(GridArgs a, PosFn pos, in
   }
   Corners c;
   level_corners(lv, x, y, z, c);
-  if (in) {
+  if (!COUNT && in && !use) enc[(int64_t)l * stride + i] = 0u;
+  if (use) {
     uint32_t v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = table[c.idx[k]];
@@ -210,7 +216,8 @@ static int check_desc(const lnr_grid_desc* d, const char* who) {
 
 template <class PosFn>
 static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16_t* table, uint32_t* enc,
-                      int64_t enc_stride, void* bwd_ws, int64_t bwd_ws_bytes, hipStream_t st, const char* who) {
+                      int64_t enc_stride, void* bwd_ws, int64_t bwd_ws_bytes, hipStream_t st, const char* who,
+                      const float* live = nullptr) {
   GridArgs a = make_args(d);
   LNR_REQUIRE(n < (int64_t(1) << 31), "%s: n=%lld samples exceeds 2^31", who, (long long)n);
   dim3 grid((unsigned)((n + 255) / 256), d->n_levels);
@@ -224,10 +231,10 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
     // one workgroup per histogram row (kSB samples) so the row is written whole
     dim3 gridc((unsigned)w.n_sb, d->n_levels);
     hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, true>), gridc, dim3(kSB), 0, st, a, pos, n,
-                       reinterpret_cast<const uint32_t*>(table), enc, enc_stride, w);
+                       reinterpret_cast<const uint32_t*>(table), enc, enc_stride, w, nullptr);
   } else {
     hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, false>), grid, dim3(256), 0, st, a, pos, n,
-                       reinterpret_cast<const uint32_t*>(table), enc, enc_stride, BwdWorkspace{});
+                       reinterpret_cast<const uint32_t*>(table), enc, enc_stride, BwdWorkspace{}, live);
   }
   LNR_RETURN_LAUNCH(who);
 }
@@ -253,6 +260,18 @@ extern "C" int lnr_hashgrid_fwd_rays(const lnr_grid_desc* d, const float* rays, 
   LNR_REQUIRE(rays && z && table && enc, "lnr_hashgrid_fwd_rays: null pointer");
   return launch_fwd(d, PosFromRays{rays, z, n_samples}, n, table, enc, enc_stride, bwd_ws, bwd_ws_bytes,
                     as_stream(stream), "lnr_hashgrid_fwd_rays");
+}
+
+extern "C" int lnr_hashgrid_fwd_rays_live(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
+                                          int32_t n_samples, const uint16_t* table, const float* live, uint32_t* enc,
+                                          int64_t enc_stride, void* stream) {
+  if (int e = check_desc(d, "lnr_hashgrid_fwd_rays_live")) return e;
+  const int64_t n = n_rays * (int64_t)n_samples;
+  LNR_REQUIRE(n_rays >= 0 && n_samples > 0 && enc_stride >= n, "lnr_hashgrid_fwd_rays_live: bad sizes");
+  if (n == 0) return LNR_OK;
+  LNR_REQUIRE(rays && z && table && enc && live, "lnr_hashgrid_fwd_rays_live: null pointer");
+  return launch_fwd(d, PosFromRays{rays, z, n_samples}, n, table, enc, enc_stride, nullptr, 0, as_stream(stream),
+                    "lnr_hashgrid_fwd_rays_live", live);
 }
 
 extern "C" int lnr_hashgrid_bwd_atomic(const lnr_grid_desc* d, const float* pos01, int64_t n, const float* d_enc,

@@ -57,6 +57,10 @@ __global__ void __launch_bounds__(64 * kRgbWaves) k_rgb_render(RgbArgs a) {
     float acc_c[3] = {0.f, 0.f, 0.f}, acc_w = 0.f;
     const int64_t base = r * a.S;
     for (int tb = 0; tb < a.S; tb += 16) {
+      const float w = a.weights[base + tb + c];
+      // a tile whose 16 weights are all exactly 0 adds nothing to rgb (w * colour = 0): skipped
+      // (its encodings may be the zeros of lnr_hashgrid_fwd_rays_live)
+      if (__ballot(w != 0.f) == 0ull) continue;
       const half8_t benc = load_enc_operand(a.enc, a.enc_stride, base + tb + c, true);
       float h[16];
 #pragma unroll
@@ -83,7 +87,6 @@ __global__ void __launch_bounds__(64 * kRgbWaves) k_rgb_render(RgbArgs a) {
       o = __builtin_amdgcn_mfma_f32_16x16x32_f16(rw.ao[0], hid_operand(h, 0), o, 0, 0, 0);
       o = __builtin_amdgcn_mfma_f32_16x16x32_f16(rw.ao[1], hid_operand(h, 1), o, 0, 0, 0);
       if (g == 0) {  // rows 0..2 = the three colour channels of sample tb + c
-        const float w = a.weights[base + tb + c];
         acc_w += w;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -310,18 +313,33 @@ __global__ void __launch_bounds__(64 * kRgbBwdWaves) k_rgb_bwd_tiles(RgbArgs a, 
   for (int64_t it = 0; it < n_iter; ++it) {
     const int64_t tile = it * per_iter + (int64_t)blockIdx.x * kRgbBwdWaves + wid;
     const bool valid = tile < n_tiles;
+    bool skip = false;
+    half8_t benc;
+    float w_s = 0.f, g_r[3] = {0.f, 0.f, 0.f}, sh[16];
     if (valid) {
-      const int64_t n0 = tile * 16;
-      half8_t benc;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         benc[2 * q + 0] = __builtin_bit_cast(_Float16, (uint16_t)(nx[q] & 0xFFFFu));
         benc[2 * q + 1] = __builtin_bit_cast(_Float16, (uint16_t)(nx[q] >> 16));
       }
-      const float w_s = nw, g_r[3] = {ng[0], ng[1], ng[2]};
-      float sh[16];
+      w_s = nw;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) g_r[k] = ng[k];
       sh_eval<4>((nd[0] + 1.0f) / 2.0f, (nd[1] + 1.0f) / 2.0f, (nd[2] + 1.0f) / 2.0f, sh);
       prefetch(tile + per_iter);
+      skip = __ballot(w_s != 0.f) == 0ull;  // all 16 weights exactly 0: no gradient anywhere in the tile
+    }
+    if (valid && skip) {
+      const int64_t n0 = tile * 16;
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int lvl = 8 * m + 2 * g;
+        denc[(int64_t)lvl * a.enc_stride + n0 + c] = make_float2(0.f, 0.f);
+        denc[(int64_t)(lvl + 1) * a.enc_stride + n0 + c] = make_float2(0.f, 0.f);
+      }
+    }
+    if (valid && !skip) {
+      const int64_t n0 = tile * 16;
       half8_t bsh = {};
       if (g < 2) {
 #pragma unroll
@@ -443,7 +461,7 @@ __global__ void __launch_bounds__(64 * kRgbBwdWaves) k_rgb_bwd_tiles(RgbArgs a, 
         }
       }
     }
-    if (lane == 0) sm.valid[wid] = valid ? 1 : 0;
+    if (lane == 0) sm.valid[wid] = (valid && !skip) ? 1 : 0;
     lds_barrier();  // LDS only: the d_enc stores and the next tile's loads stay in flight
     // owners: dW_i += dY_i X_i^T over the 4 source waves' samples
     if (wid == 0) rgb_owner<NH, 1>(sm, 0, acc, run_a);                       // W0

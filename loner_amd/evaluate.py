@@ -118,8 +118,9 @@ class DepthRenderer:
                    self.weights if cw else None, s)
             if cw:
                 c = self.color
-                L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(c.desc), rc, self.z, n, self.S, c.table, self.enc_rgb,
-                       stride, None, 0, s)
+                # zero-weight samples cannot change rgb: no colour-grid gathers for them
+                L.call("lnr_hashgrid_fwd_rays_live", L.ctypes.byref(c.desc), rc, self.z, n, self.S, c.table,
+                       self.weights, self.enc_rgb, stride, s)
                 L.call("lnr_rgb_render", c.mlp, c.n_hidden_layers, self.enc_rgb, stride, rc, self.weights, n, self.S,
                        rgb[r0:r0 + n], s)
         for t in (depth, opacity, variance) + ((rgb,) if rgb is not None else ()):

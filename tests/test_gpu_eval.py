@@ -187,3 +187,36 @@ def test_training_learns_the_map(L):
     after = float(host(E.compute_l1_depth(rend, held, held["pose"], wc, rr, key=1)))
     assert np.isfinite(host(out)[0])
     assert after < 0.2 * before and after < 5.0, (before, after)
+
+
+def test_live_colour_encode_is_exact(L):
+    """lnr_hashgrid_fwd_rays_live: samples of weight exactly 0 get a zero encoding and no gathers,
+    the others the same bits as lnr_hashgrid_fwd_rays; the colour map is bit-identical either way."""
+    from loner_amd import evaluate as E
+    from loner_amd import step as S_
+    from loner_amd import synthetic as syn
+    st = _state(S_)
+    color = E.ColorHead.init(4, seed=11)
+    scan = syn.make_window("canteen", 1, seed=6)[0]
+    keep = torch.arange(0, scan["distances"].shape[0], 97)[:256]
+    scan = dict(directions=scan["directions"][:, keep].contiguous(), distances=scan["distances"][keep].contiguous(),
+                pose=scan["pose"])
+    win = E.scan_window(scan, scan["pose"], syn.world_cube("canteen"), syn.SENSORS["canteen"]["ray_range"], "cuda:0")
+    rays, _, _ = win.build_all()
+    R, S = rays.shape[0], 512
+    rend = E.DepthRenderer(st, n_samples=S, chunk=R, color=color)
+    key = L.step_key(12, 0)
+    rgb = torch.empty(R, 3, dtype=torch.float32, device="cuda")
+    rend.render(rays, key, "default", rgb=rgb)
+    w = rend.weights[:R]
+    zero = (w == 0).reshape(-1)
+    assert 0.05 < float(zero.float().mean()) < 0.95  # both kinds of sample present
+    live = rend.enc_rgb.clone()
+    s = L.stream()
+    full = torch.empty_like(live)
+    L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(color.desc), rays, rend.z, R, S, color.table, full, R * S, None, 0, s)
+    assert torch.equal(live[:, ~zero], full[:, ~zero])
+    assert int(live[:, zero].abs().sum()) == 0
+    rgb_full = torch.empty_like(rgb)
+    L.call("lnr_rgb_render", color.mlp, 4, full, R * S, rays, rend.weights, R, S, rgb_full, s)
+    assert torch.equal(rgb, rgb_full)
