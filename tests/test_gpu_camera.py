@@ -216,3 +216,22 @@ def test_camera_two_shards_match_single_batch(L):
     g = host(states[0].grad)
     assert _rel(g, g_ref) < 1e-5
     assert torch.equal(states[0].params, states[1].params)
+
+
+def test_camera_skip_zero_matches_default(L):
+    """CameraStepEngine(skip_zero=True) (zero-weight samples: no colour gathers, backward counts only
+    non-zero d_enc) gives the default path's gradient: the skipped samples contribute exactly 0."""
+    from loner_amd import camera as C
+    fr, cs_a, eng_a = _camera_setup()
+    _, cs_b, eng_ref = _camera_setup()
+    eng_b = C.CameraStepEngine(eng_ref.field, cs_b, n_rays=eng_ref.R, n_samples=128, lr=0.01, seed=0, skip_zero=True)
+    R = fr.n_rays(1)
+    rays = torch.empty(R, 13, device="cuda:0")
+    inten = torch.empty(R, 3, device="cuda:0")
+    fr.build(1, rays, inten)
+    la = float(eng_a.step(rays, inten, global_step=5).item())
+    lb = float(eng_b.step(rays, inten, global_step=5).item())
+    assert la == lb
+    assert float((eng_b.weights[:R] == 0).float().mean()) > 0.05  # the path is exercised
+    assert torch.equal(cs_a.grad[:cs_a.n_mlp], cs_b.grad[:cs_b.n_mlp])
+    assert _rel(host(cs_b.grad), host(cs_a.grad)) < 1e-6
