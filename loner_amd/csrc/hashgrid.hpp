@@ -29,6 +29,15 @@ constexpr int kMaxBuckets = 2048;
 #define LNR_SLICE_LOG2 18
 #endif
 constexpr int64_t kSliceRecords = int64_t(1) << LNR_SLICE_LOG2;
+// Slice size of the coarse (run-merging) levels' buckets, tunable on its own: they are few buckets
+// holding most of their level's records (level 0 is one 4096-entry chunk).  Measured at C2: 2^16 and
+// 2^17 cut those levels' accumulation in isolation (436 -> 231 us at level 0) but not the fused
+// all-level launch (~650 us either way), while k_bwd_finalize, which sums a split bucket's partial
+// chunks in one workgroup, grew 39 -> 71 -> 127 us; so the default equals the fine levels'.
+#ifndef LNR_SLICE_LOG2_COARSE
+#define LNR_SLICE_LOG2_COARSE LNR_SLICE_LOG2
+#endif
+constexpr int64_t kSliceRecordsCoarse = int64_t(1) << LNR_SLICE_LOG2_COARSE;
 
 struct GridArgs {
   LevelParams lv[LNR_MAX_LEVELS];
@@ -292,10 +301,12 @@ struct BwdWorkspace {
 inline int64_t bwd_n_sb(int64_t n) { return (n + kSB - 1) / kSB; }
 inline int64_t bwd_n_chunks(int64_t n) { return (bwd_n_sb(n) + kRowsPerChunk - 1) / kRowsPerChunk; }
 
-// Upper bound on the partial chunks: a split bucket holds c > kSliceRecords records in
-// ceil(c / kSliceRecords) <= 2c / kSliceRecords slices, and sum(c) <= 8 N L.
+// Upper bound on the partial chunks: a split bucket holds c > slice records in
+// ceil(c / slice) <= 2c / slice slices, and sum(c) <= 8 N per level.
+inline uint32_t merge_levels_for(const lnr_grid_desc* d);
 inline int64_t bwd_max_partials(const lnr_grid_desc* d, int64_t n) {
-  return 2 * (8 * n * (int64_t)d->n_levels) / kSliceRecords + 1;
+  const int64_t m = merge_levels_for(d);
+  return 2 * (8 * n * m) / kSliceRecordsCoarse + 2 * (8 * n * ((int64_t)d->n_levels - m)) / kSliceRecords + 2;
 }
 
 inline int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }

@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(kMaxChunksPerLevel) k_bwd_scan_rows(GridArgs a
 }
 
 // Bucket segment starts, work-item (slice) prefix and split-bucket partial prefix.
-__global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint32_t n_buckets) {
+__global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint32_t n_buckets, uint32_t coarse_end) {
   __shared__ uint64_t w_seg[16];
   __shared__ uint32_t w_sl[16], w_pp[16];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
@@ -108,7 +108,8 @@ __global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint
   for (int q = 0; q < 2; ++q) {
     const uint32_t b = 2 * t + q;
     const uint32_t c = b < n_buckets ? ws.counts[b] : 0u;
-    const uint32_t k = (uint32_t)((c + kSliceRecords - 1) / kSliceRecords);
+    const int64_t slr = b < coarse_end ? kSliceRecordsCoarse : kSliceRecords;
+    const uint32_t k = (uint32_t)((c + slr - 1) / slr);
     seg[q] = c;
     sl[q] = b < n_buckets ? (k > 0 ? k : 1) : 0u;
     pp[q] = b < n_buckets && k > 1 ? k : 0u;
@@ -427,9 +428,10 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
     const uint32_t b = lo;
     const uint32_t nsl = ws.slice_pre[b + 1] - ws.slice_pre[b];
     const uint32_t j = s - ws.slice_pre[b];
-    const uint64_t beg = ws.seg_start[b] + (uint64_t)j * kSliceRecords;
+    const uint64_t slr = b < a.bucket_base[a.merge_levels] ? kSliceRecordsCoarse : kSliceRecords;
+    const uint64_t beg = ws.seg_start[b] + (uint64_t)j * slr;
     uint64_t end = ws.seg_start[b + 1];
-    if (beg + kSliceRecords < end) end = beg + kSliceRecords;
+    if (beg + slr < end) end = beg + slr;
     uint32_t l = 0;
     while (l + 1 < a.n_levels && a.bucket_base[l + 1] <= b) ++l;
     const uint32_t chunk = b - a.bucket_base[l];
@@ -550,7 +552,7 @@ static void launch_accum(const GridArgs& a, const BwdWorkspace& w, const lnr_gri
                          uint32_t l1, float* d_table, hipStream_t st) {
   const uint32_t b0 = a.bucket_base[l0], b1 = a.bucket_base[l1];
   if (b1 <= b0) return;
-  const int64_t max_slices = (b1 - b0) + (8 * n * (int64_t)(l1 - l0)) / kSliceRecords + 1;
+  const int64_t max_slices = (b1 - b0) + (8 * n * (int64_t)(l1 - l0)) / kSliceRecordsCoarse + 1;
   const unsigned g = (unsigned)(max_slices < 4096 ? max_slices : 4096);
   hipLaunchKernelGGL(k_bwd_accum, dim3(g), dim3(kAccumThreads), 2 * kChunk * sizeof(unsigned long long), st, a, w,
                      d_table, b0, b1);
@@ -579,7 +581,7 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
   }
   hipLaunchKernelGGL(k_bwd_chunk_sums, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
   hipLaunchKernelGGL(k_bwd_scan_rows, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
-  hipLaunchKernelGGL(k_bwd_scan_buckets, dim3(1), dim3(1024), 0, st, w, a.n_buckets);
+  hipLaunchKernelGGL(k_bwd_scan_buckets, dim3(1), dim3(1024), 0, st, w, a.n_buckets, a.bucket_base[a.merge_levels]);
   {
     const float2* de = reinterpret_cast<const float2*>(d_enc);
     const uint32_t m = a.merge_levels, L = d->n_levels;
