@@ -198,7 +198,7 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
                                                                              int64_t stride, BwdWorkspace ws, uint32_t l0,
                                                                              bool skip_zero) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float2* stage_v = reinterpret_cast<float2*>(smem);                         // [kCap]
+  RecVal* stage_v = reinterpret_cast<RecVal*>(smem);                         // [kCap]
   uint64_t* gbase = reinterpret_cast<uint64_t*>(stage_v + kCap);             // [kMaxChunksPerLevel]
   uint32_t* stage_w = reinterpret_cast<uint32_t*>(gbase + kMaxChunksPerLevel);  // [kCap]
   uint32_t* rank_ctr = stage_w + kCap;                                       // [kMaxChunksPerLevel]
@@ -278,12 +278,12 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
     if (staged) {
       const uint32_t t = start[bk] + rank;
       stage_w[t] = word;
-      stage_v[t] = val;
+      stage_v[t] = pack_rec(val.x, val.y);
       sbk[t] = (uint8_t)bk;
     } else {
       const uint64_t dst = gbase[bk] + rank;
       ws.rec_w[dst] = word;
-      ws.rec_v[dst] = val;
+      ws.rec_v[dst] = pack_rec(val.x, val.y);
     }
   };
   // 2. records: rank, then place (hashgrid.hpp "Backward records")
@@ -387,7 +387,7 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
   LNR_PHASE(5 * kind + 3, t4, t3);
 }
 
-constexpr size_t kScatterLds = (size_t)kCap * 8 + kMaxChunksPerLevel * 8 + (size_t)kCap * 4 + kMaxChunksPerLevel * 4 +
+constexpr size_t kScatterLds = (size_t)kCap * sizeof(RecVal) + kMaxChunksPerLevel * 8 + (size_t)kCap * 4 + kMaxChunksPerLevel * 4 +
                                (kMaxChunksPerLevel + 1) * 4 + (kSB / 64) * 4 + kCap;
 static_assert(kScatterLds <= 65536, "scatter LDS within the default dynamic limit");
 
@@ -452,27 +452,40 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
     lds_barrier();
     LNR_STAMP(t1);
     const bool coherent = l < a.merge_levels;
-    // 2 records per lane per load (8-B words, 16-B values), 4 loads in flight: 4 K records per
+    // 2 records per lane per load (8-B words, 8-B packed values or 16-B fp32), 4 loads in flight: 4 K records per
     // workgroup trip; a lane's two records are handled as two lane-ordered streams (merging
     // equal entries of coherent levels is an optimisation only: the int64 sums are exact)
     const uint64_t beg2 = beg & ~1ull;
     for (uint64_t rb = beg2 + 2 * (threadIdx.x & ~63u); rb < end; rb += 2 * LNR_ACCUM_LOADS * kAccumThreads) {
       uint2 qw[LNR_ACCUM_LOADS];
+#ifndef LNR_REC_PACKED
       float4 qv[LNR_ACCUM_LOADS];
+#else
+      u32x2 qp[LNR_ACCUM_LOADS];  // unpacked where consumed, so the loads stay in flight together
+#endif
 #pragma unroll
       for (int u = 0; u < LNR_ACCUM_LOADS; ++u) {
         const uint64_t rr = rb + 2 * lane + (uint64_t)u * 2 * kAccumThreads;
         const uint64_t rc = rr < end ? rr : beg2;  // unconditional loads: no branch to wait at
         const u32x2 w2 = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(&ws.rec_w[rc]));
+#ifndef LNR_REC_PACKED
         const f32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(&ws.rec_v[rc]));
-        qw[u] = make_uint2(rr < beg || rr >= end ? kRecNone : w2.x, rr + 1 >= end ? kRecNone : w2.y);
         qv[u] = make_float4(v4.x, v4.y, v4.z, v4.w);
+#else
+        qp[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(&ws.rec_v[rc]));
+#endif
+        qw[u] = make_uint2(rr < beg || rr >= end ? kRecNone : w2.x, rr + 1 >= end ? kRecNone : w2.y);
       }
 #pragma unroll
       for (int u = 0; u < 2 * LNR_ACCUM_LOADS; ++u) {
         const uint32_t w = (u & 1) ? qw[u >> 1].y : qw[u >> 1].x;
+#ifndef LNR_REC_PACKED
         const float v0 = (u & 1) ? qv[u >> 1].z : qv[u >> 1].x;
         const float v1 = (u & 1) ? qv[u >> 1].w : qv[u >> 1].y;
+#else
+        const float2 vv = unpack_rec((u & 1) ? qp[u >> 1].y : qp[u >> 1].x);
+        const float v0 = vv.x, v1 = vv.y;
+#endif
         const bool ok = w != kRecNone;
         const uint32_t e0 = ok ? (w & (kChunk - 1)) : 0xFFFFFFFFu;
         if (coherent) {  // single-corner records arriving in runs of equal entries
