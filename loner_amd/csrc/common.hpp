@@ -148,6 +148,9 @@ __device__ __forceinline__ unsigned long long stamp() {
 #define LNR_STAMP(var) unsigned long long var = (threadIdx.x == 0) ? ::lnr::stamp() : 0ull
 #define LNR_PHASE(k, t1, t0) \
   if (threadIdx.x == 0 && (blockIdx.x & 63) == 0) atomicAdd(&::lnr::g_phase[k], (t1) - (t0))  // 1/64 sampled
+// sampled by an explicit key (e.g. the row, so every level of a level-fastest grid is sampled)
+#define LNR_PHASE_BY(key, k, t1, t0) \
+  if (threadIdx.x == 0 && ((key) & 63) == 0) atomicAdd(&::lnr::g_phase[k], (t1) - (t0))
 #define LNR_PHASE_EXPORT(tu)                                                                      \
   extern "C" int lnr_debug_phases_##tu(unsigned long long* out32) {                              \
     if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(::lnr::g_phase), 32 * 8) != hipSuccess) return -1; \
@@ -157,6 +160,7 @@ __device__ __forceinline__ unsigned long long stamp() {
 #else
 #define LNR_STAMP(var)
 #define LNR_PHASE(k, t1, t0)
+#define LNR_PHASE_BY(key, k, t1, t0)
 #define LNR_PHASE_EXPORT(tu)
 #endif
 

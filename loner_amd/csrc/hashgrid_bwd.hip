@@ -299,7 +299,7 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
     row_starts();
     LNR_STAMP(t1b);
     lds_barrier();
-    LNR_PHASE(5 * kind + 4, t1b, t1);
+    LNR_PHASE_BY(sb, 5 * kind + 4, t1b, t1);
     staged = start[nb] <= (uint32_t)kCap;  // block-uniform
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -381,10 +381,10 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
     }
   }
   LNR_STAMP(t4);
-  LNR_PHASE(5 * kind + 0, t1, t0);
-  LNR_PHASE(5 * kind + 1, t2, t1);
-  LNR_PHASE(5 * kind + 2, t3, t2);
-  LNR_PHASE(5 * kind + 3, t4, t3);
+  LNR_PHASE_BY(sb, 5 * kind + 0, t1, t0);
+  LNR_PHASE_BY(sb, 5 * kind + 1, t2, t1);
+  LNR_PHASE_BY(sb, 5 * kind + 2, t3, t2);
+  LNR_PHASE_BY(sb, 5 * kind + 3, t4, t3);
 }
 
 constexpr size_t kScatterLds = (size_t)kCap * sizeof(RecVal) + kMaxChunksPerLevel * 8 + (size_t)kCap * 4 + kMaxChunksPerLevel * 4 +
