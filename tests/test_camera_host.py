@@ -1,0 +1,45 @@
+"""Camera-phase host logic on CPU: the per-window pixel schedule of Optimizer._do_iterate_optimizer_camera
+(optimizer.py:581-601,626-644, FULL_CONFIG) and the pinhole direction table (get_ray_directions,
+ray_utils.py:62-124, no distortion)."""
+import numpy as np
+import torch
+
+from loner_amd import camera as C
+
+
+def _frames(masks=None, n=100, W=20, H=15, K=3):
+    imgs = [np.zeros((W * H, 3), np.float32) for _ in range(K)]
+    poses = [np.eye(4)[:3] for _ in range(K)]
+    dirs = C.pinhole_directions(W, H, np.array([[10.0, 0, 9.5], [0, 10.0, 7.0], [0, 0, 1]]))
+    return C.CameraFrames(dirs, W, H, imgs, poses, dict(scale_factor=10.0, shift=[0, 0, 0]), (0.5, 30.0),
+                          masks=masks, n_rays_per_kf=n, seed=3, device="cpu")
+
+
+def test_schedule_matches_reference_slices():
+    """num_iterations = floor(min masked pixels / n); iteration it takes
+    full_indices[kf, max(n*it - 1, 0) : min(n*(it + 1) - 1, n_iter * n)]."""
+    rng = np.random.default_rng(0)
+    masks = [rng.uniform(size=300) > p for p in (0.2, 0.5, 0.3)]
+    fr = _frames(masks)
+    counts = [int(m.sum()) for m in masks]
+    n = 100
+    n_iter = min(counts) // n
+    assert fr.n_iter == n_iter
+    for it in range(n_iter):
+        lo, hi = max(n * it - 1, 0), min(n * (it + 1) - 1, n_iter * n)
+        assert fr.iteration_slice(it) == (lo, hi)
+        assert fr.n_rays(it) == 3 * (hi - lo)
+    for k, m in enumerate(masks):  # each keyframe's schedule is a permutation of its masked pixels
+        perm = fr.perm[k].numpy()
+        assert len(perm) == n_iter * n and len(set(perm.tolist())) == len(perm)
+        assert m[perm].all()
+
+
+def test_pinhole_directions():
+    W, H = 6, 4
+    K = np.array([[5.0, 0, 2.5], [0, 4.0, 1.5], [0, 0, 1]])
+    d = C.pinhole_directions(W, H, K).numpy()
+    assert d.shape == (W * H, 3)
+    for p in (0, 7, W * H - 1):
+        x, y = p % W, p // W
+        np.testing.assert_allclose(d[p], [(x - 2.5) / 5.0, (y - 1.5) / 4.0, 1.0], rtol=1e-6)
