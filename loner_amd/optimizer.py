@@ -1,0 +1,236 @@
+"""``Optimizer``: the reference's mapping optimiser surface (src/mapping/optimizer.py:60-511) on the
+fused path, for the sigma field.
+
+    opt = Optimizer(settings, calibration, world_cube, device)   # settings = mapper.optimizer
+    loss = opt.iterate_optimizer(keyframe_window)                # one window, its iteration schedule
+
+The schedule logic follows the reference:
+* the keyframe schedule picks the iteration schedule by the running keyframe count (:141-152);
+* ``skip_pose_refinement`` drops the first iteration config when there are several (:218-219);
+* a fresh Adam (``lrate_sigma_mlp``, ExponentialLR ``lrate_gamma`` stepped every iteration) per
+  iteration config (:255-265);
+* RANDOM / MASK / FIXED ray selection with sky rays (:279-424);
+* the OGM update when ``global_step % N_iters_acc == 0``, checked before the increment (:466-469).
+
+Rays are selected and built on the device from the window held in HBM (``RayWindow``). Each
+iteration is ``StepEngine.step``: no host synchronisation until the window's final loss is read.
+
+Scope: the map, i.e. the sigma head.
+* Pose optimisation (tracking, joint refinement) is out of scope. An iteration config that asks
+  for it with a frozen sigma head (tracking only) raises ``NotImplementedError``; a joint config
+  runs the map part with the poses fixed, and warns once.
+* The colour head trains in the camera phase (``loner_amd.camera``), as ``iterate_optimizer_camera``
+  does.
+
+Keyframes are ``loner_amd`` scan dicts (``directions`` (3,P), ``distances`` (P,), optional
+``sky_directions`` (3,Q), ``pose`` (4,4)), or objects with the reference's KeyFrame accessors
+(``get_lidar_scan()`` with ``ray_directions``, ``distances`` and ``sky_rays``, and
+``get_lidar_pose().get_transformation_matrix()``).
+"""
+import warnings
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib as L
+from .rays import RayWindow
+from .step import FieldState, LossConfig, StepConfig, StepEngine
+
+
+def _g(obj, key, default=None):
+    """settings[key] for dicts, getattr for Settings-like objects."""
+    if obj is None:
+        return default
+    if isinstance(obj, dict):
+        return obj.get(key, default)
+    return getattr(obj, key, default)
+
+
+@dataclass
+class OptimizationSettings:
+    """optimizer.py:41-58."""
+    num_iterations: int = 1
+    freeze_poses: bool = False
+    latest_kf_only: bool = False
+    freeze_sigma_mlp: bool = False
+    freeze_rgb_mlp: bool = False
+
+    @staticmethod
+    def from_dict(d):
+        return OptimizationSettings(d.get("num_iterations", 1), d.get("freeze_poses", False),
+                                    d.get("latest_kf_only", False), d.get("freeze_sigma_mlp", False),
+                                    d.get("freeze_rgb_mlp", False))
+
+
+def _scan_dict(kf):
+    if isinstance(kf, dict):
+        return kf
+    scan = kf.get_lidar_scan()
+    d = dict(directions=scan.ray_directions, distances=scan.distances,
+             pose=kf.get_lidar_pose().get_transformation_matrix().detach())
+    sky = getattr(scan, "sky_rays", None)
+    if sky is not None and sky.numel() > 0:
+        d["sky_directions"] = sky
+    return d
+
+
+class Optimizer:
+    def __init__(self, settings, calibration=None, world_cube=None, device="cuda", use_gt_poses=False,
+                 lidar_only=True, enable_sky_segmentation=True, seed=0):
+        if world_cube is None:
+            raise ValueError("Optimizer needs the world cube")
+        self._settings = settings
+        self._calibration = calibration
+        self._device = torch.device(device)
+        self._use_gt_poses = use_gt_poses
+        self._lidar_only = lidar_only
+        self._enable_sky_segmentation = enable_sky_segmentation
+        self._world_cube = world_cube
+        mc = _g(settings, "model_config")
+        model = _g(mc, "model")
+        render = _g(model, "render")
+        occ = _g(model, "occ_model")
+        train = _g(mc, "train")
+        self._ray_range = tuple(float(x) for x in _g(model, "ray_range", _g(_g(mc, "data"), "ray_range", (1.0, 75.0))))
+        self._samples_strategy = _g(_g(settings, "samples_selection"), "strategy", "OGM")
+        if self._samples_strategy not in ("OGM", "UNIFORM"):
+            raise RuntimeError(f"Can't find samples_selection strategy: {self._samples_strategy}")
+        self._rays_strategy = _g(_g(settings, "rays_selection"), "strategy", "RANDOM")
+        if self._rays_strategy not in ("RANDOM", "MASK", "FIXED"):
+            raise RuntimeError(f"Can't find rays_selection strategy: {self._rays_strategy}")
+        ns = _g(settings, "num_samples")
+        self._num_lidar_samples = int(_g(ns, "lidar", 512))
+        self._num_sky_samples = int(_g(ns, "sky", 0))
+        loss = _g(mc, "loss")
+        self.cfg = StepConfig(
+            n_samples=int(_g(render, "N_samples_train", 512)), perturb=float(_g(render, "perturb", 1.0)),
+            raw_noise_std=float(_g(render, "raw_noise_std", 1.0)), lr=float(_g(train, "lrate_sigma_mlp", 0.01)),
+            occ_res=int(_g(occ, "voxel_size", 100)), occ_lr=float(_g(occ, "lr", 1e-4)),
+            n_iters_acc=int(_g(occ, "N_iters_acc", 10)), sampler=self._samples_strategy,
+            loss=LossConfig.from_dict(dict(loss)) if loss is not None else LossConfig())
+        self._lr_gamma = float(_g(train, "lrate_gamma", 1.0))
+        self.state = FieldState(self.cfg, device=self._device, seed=seed)
+        self._seed = int(seed)
+        self._engine = None
+        self._keyframe_schedule = _g(settings, "keyframe_schedule") or [
+            dict(num_keyframes=-1, iteration_schedule=[dict(num_iterations=1, freeze_poses=True,
+                                                            freeze_sigma_mlp=False, freeze_rgb_mlp=True)])]
+        self._optimization_settings = OptimizationSettings()
+        self._keyframe_count = 0
+        self._global_step = 0
+        self._warned_poses = False
+        self._fixed_gen = torch.Generator(device="cpu").manual_seed(seed)
+
+    # ------------------------------------------------------------------ schedule
+    def _iteration_schedule(self):
+        """optimizer.py:141-152."""
+        cumulative = 0
+        schedule = None
+        for item in self._keyframe_schedule:
+            kf_count = item["num_keyframes"]
+            schedule = item["iteration_schedule"]
+            cumulative += kf_count
+            if cumulative >= self._keyframe_count + 1 or kf_count == -1:
+                break
+        return schedule
+
+    def _engine_for(self, n_rays):
+        if self._engine is None or self._engine.n_rays < n_rays:
+            self._engine = StepEngine(self.state, n_rays, seed=self._seed)
+        return self._engine
+
+    def iterate_optimizer(self, keyframe_window, optimizer_settings: OptimizationSettings = None) -> float:
+        schedule = self._iteration_schedule()
+        result = self._do_iterate_optimizer(keyframe_window, schedule, optimizer_settings)
+        self._keyframe_count += 1
+        return result
+
+    def _do_iterate_optimizer(self, keyframe_window, iteration_schedule, optimizer_settings=None) -> float:
+        if len(iteration_schedule) > 1 and _g(self._settings, "skip_pose_refinement", False):
+            iteration_schedule = iteration_schedule[1:]
+        if optimizer_settings is not None:
+            iteration_schedule = [None]
+        scans = [_scan_dict(kf) for kf in keyframe_window]
+        loss = None
+        for config in iteration_schedule:
+            os_ = optimizer_settings if config is None else OptimizationSettings.from_dict(config)
+            freeze_poses = os_.freeze_poses or bool(_g(self._settings, "freeze_poses", False)) or self._use_gt_poses
+            if not freeze_poses:
+                if os_.freeze_sigma_mlp:
+                    raise NotImplementedError("pose tracking (frozen sigma head, free poses) is outside this build's "
+                                              "scope (SURVEY.md §8)")
+                if not self._warned_poses:
+                    self._warned_poses = True
+                    warnings.warn("pose optimisation is outside this build's scope: the poses stay fixed and "
+                                  "only the map is optimised")
+            if os_.freeze_sigma_mlp:
+                continue  # nothing of the map to optimise in this config
+            window_scans = scans
+            if os_.latest_kf_only and len(scans) > 1:
+                window_scans = scans[-1:]
+            self.state.reset_optimizer()  # a new torch.optim.Adam per iteration config (:255-265)
+            loss = self._run_config(window_scans, int(os_.num_iterations))
+        return float(loss[0].item()) if loss is not None else float("nan")
+
+    def _run_config(self, scans, num_iterations):
+        n_sky = self._num_sky_samples if self._enable_sky_segmentation else 0
+        fixed = self._rays_strategy == "FIXED"
+        window = RayWindow(scans, self._world_cube, self._ray_range, n_lidar=self._num_lidar_samples, n_sky=n_sky,
+                           strategy="RANDOM" if fixed else self._rays_strategy, device=self._device)
+        eng = self._engine_for(window.n_slots)
+        out = None
+        if fixed:
+            given, num_iterations = self._fixed_schedule(scans, window)
+        for it in range(num_iterations):
+            eng.lr_factor = self._lr_gamma ** it  # ExponentialLR stepped after every iteration
+            if fixed:
+                out = self._fixed_step(eng, window, given, it)
+            else:
+                out = eng.step_window(window, global_step=self._global_step, iteration_idx=it)
+            self._global_step += 1
+        eng.lr_factor = 1.0
+        return out
+
+    # ------------------------------------------------------------------ FIXED ray selection
+    def _fixed_schedule(self, scans, window):
+        """optimizer.py:279-299: every keyframe's points in a random order, padded to the longest scan
+        with a permutation of its first points; num_iterations = floor(max length / n)."""
+        n = self._num_lidar_samples
+        lengths = [int(s["distances"].numel()) for s in scans]
+        max_len = max(lengths)
+        n_iter = max_len // n
+        full = torch.zeros(len(scans), max_len, dtype=torch.int64)
+        for k, P in enumerate(lengths):
+            idx = torch.arange(P)
+            pad = max_len - P
+            full[k] = torch.cat((idx[torch.randperm(P, generator=self._fixed_gen)],
+                                 idx[torch.randperm(pad, generator=self._fixed_gen)]))
+        return full, n_iter
+
+    def _fixed_step(self, eng, window, full, it):
+        """Iteration it: keyframe k's points full[k, max(n it - 1, 0) : min(n (it + 1) - 1, n_iter n)]
+        (optimizer.py:302-317) plus its sky draws, as GIVEN indices into the window's slots."""
+        n = self._num_lidar_samples
+        n_iter = full.shape[1] // n
+        lo, hi = max(n * it - 1, 0), min(n * (it + 1) - 1, n_iter * n)
+        K = full.shape[0]
+        given = torch.zeros(window.n_slots, dtype=torch.int32)
+        keep = torch.zeros(window.n_slots, dtype=torch.bool)
+        ray_off, n_sel = window.ray_off_host, window.n_sel_host
+        for k in range(K):
+            base = int(ray_off[k])
+            m = hi - lo
+            given[base:base + m] = full[k, lo:hi].to(torch.int32)
+            keep[base:base + m] = True
+            n_sky_k = int(ray_off[k + 1]) - base - int(n_sel[k])
+            if n_sky_k > 0:
+                q = int(window.sky_count_host[k])
+                given[base + int(n_sel[k]):base + int(n_sel[k]) + n_sky_k] = torch.randint(
+                    0, q, (n_sky_k,), generator=self._fixed_gen, dtype=torch.int64).to(torch.int32)
+                keep[base + int(n_sel[k]):base + int(n_sel[k]) + n_sky_k] = True
+        dev = self._device
+        key = L.step_key(eng.seed, self._global_step)
+        rays, depth, valid, _, far_ref = window.build(key, 0, window.n_slots, given=given.to(dev))
+        sel = keep.to(dev) & valid.bool()
+        rays, depth = rays[sel].contiguous(), depth[sel].contiguous()
+        return eng.step(rays, depth, self._global_step, it, scale=window.scale, far_ref=far_ref)

@@ -168,6 +168,8 @@ class RayWindow:
         self.n_trunk = torch.tensor(n_trunk, **i32) if order else None
         self.n_sel_trunk = torch.tensor(n_sel_trunk, **i32) if order else None
         self.n_sel = torch.tensor(n_sel, **i32)
+        self.n_sel_host = list(n_sel)                                       # LiDAR slots per keyframe
+        self.sky_count_host = [sky_off[k + 1] - sky_off[k] for k in range(K)]  # sky directions per keyframe
         counts = [a + b for a, b in zip(n_sel, n_sky_k)]
         self.ray_off_host = [0]
         for c in counts:

@@ -172,6 +172,7 @@ class StepEngine:
         # field has trained a few steps, and the extra count pass (d_enc reads) costs more than the
         # records it saves (3.35 vs 3.18 ms/step), so it is opt-in for sparse-gradient workloads.
         self.count_in_forward = count_in_forward
+        self.lr_factor = 1.0  # ExponentialLR: the caller sets gamma^k (optimizer.py:262, stepped per iteration)
         self.status = torch.zeros(1, dtype=torch.int32, device=state.device)  # LNR_STATUS_* bits
         self._warned_clip = False
         # level ranges of the bucketed gradient all-reduce, finest first (their records dominate the
@@ -331,8 +332,8 @@ class StepEngine:
         # 7. Adam (+ fp16 shadow)
         st.adam_step += 1
         m(prof, "adam")
-        L.call("lnr_adam_step", st.params, st.shadow, st.grad, st.m, st.v, st.n_padded, st.adam_step, cfg.lr, 0.9,
-               0.999, 1e-8, s)
+        L.call("lnr_adam_step", st.params, st.shadow, st.grad, st.m, st.v, st.n_padded, st.adam_step,
+               cfg.lr * self.lr_factor, 0.9, 0.999, 1e-8, s)
         m(prof, "adam")
         # 8. loss scalars (device)
         L.call("lnr_loss_finalize", self.stats, R, L.ctypes.byref(lp), self.loss_out, s)
