@@ -23,6 +23,32 @@ The Adam state is torch's own layout (``state[i] = {'step', 'exp_avg', 'exp_avg_
 import torch
 
 SIGMA_KEY = "nerf_model._model_sigma.params"
+# the colour branch (nerf_tcnn.py:40-52): colour HashGrid, SH direction encoding (no parameters),
+# colour FullyFusedMLP
+COLOR_GRID_KEY = "nerf_model._pos_encoding.params"
+DIR_ENC_KEY = "nerf_model._dir_encoding.params"
+COLOR_MLP_KEY = "nerf_model._model_intensity.params"
+
+
+def color_params(color_state):
+    """{module path: flat params} of a ``loner_amd.camera.ColorState``, for ``other_params``."""
+    cs = color_state
+    return {COLOR_GRID_KEY: cs.params[cs.n_mlp:cs.n_params], DIR_ENC_KEY: cs.params[:0],
+            COLOR_MLP_KEY: cs.params[:cs.n_mlp]}
+
+
+def load_color(ck, color_state):
+    """Restore a ColorState from a checkpoint dict's colour-branch params (sizes must match)."""
+    net = ck["network_state_dict"]
+    for k in (COLOR_GRID_KEY, COLOR_MLP_KEY):
+        if k not in net:
+            raise KeyError(f"checkpoint has no {k!r}")
+    t, m = net[COLOR_GRID_KEY].reshape(-1), net[COLOR_MLP_KEY].reshape(-1)
+    cs = color_state
+    if t.numel() != cs.n_params - cs.n_mlp or m.numel() != cs.n_mlp:
+        raise RuntimeError(f"colour head size mismatch: table {t.numel()} vs {cs.n_params - cs.n_mlp}, "
+                           f"mlp {m.numel()} vs {cs.n_mlp}")
+    cs.load(t, m)
 
 
 def _adam_state_dict(m, v, step, lr):

@@ -19,8 +19,8 @@ Scope: the map, i.e. the sigma head.
 * Pose optimisation (tracking, joint refinement) is out of scope. An iteration config that asks
   for it with a frozen sigma head (tracking only) raises ``NotImplementedError``; a joint config
   runs the map part with the poses fixed, and warns once.
-* The colour head trains in the camera phase (``loner_amd.camera``), as ``iterate_optimizer_camera``
-  does.
+* The colour head trains in the camera phase: ``iterate_optimizer_camera(frames)`` over a
+  ``loner_amd.camera.CameraFrames`` window (``loner_amd.camera``).
 
 Keyframes are ``loner_amd`` scan dicts (``directions`` (3,P), ``distances`` (P,), optional
 ``sky_directions`` (3,Q), ``pose`` (4,4)), or objects with the reference's KeyFrame accessors
@@ -190,6 +190,38 @@ class Optimizer:
             self._global_step += 1
         eng.lr_factor = 1.0
         return out
+
+    # ------------------------------------------------------------------ camera phase
+    def iterate_optimizer_camera(self, frames, color=None, n_samples=None) -> float:
+        """Optimizer.iterate_optimizer_camera (optimizer.py:517-688) for one camera window
+        (``loner_amd.camera.CameraFrames``): the sigma head frozen, a new Adam over the colour head
+        at ``lrate_rgb`` with ExponentialLR ``lrate_gamma``, ``frames.n_iter`` iterations.  The colour
+        head (``loner_amd.camera.ColorState``) is created on first use and kept in ``self.color``."""
+        from .camera import CameraStepEngine, ColorState
+        train = _g(_g(self._settings, "model_config"), "train")
+        if color is not None:
+            self.color = color
+        elif getattr(self, "color", None) is None:
+            self.color = ColorState(device=self._device, seed=self._seed + 1)
+        S = int(n_samples or self.cfg.n_samples)
+        n_max = max(frames.n_rays(it) for it in range(frames.n_iter)) if frames.n_iter else 0
+        eng = getattr(self, "_camera_engine", None)
+        if eng is None or eng.R < n_max or eng.S != S or eng.color is not self.color:
+            eng = CameraStepEngine(self.state, self.color, n_rays=max(n_max, 1), n_samples=S,
+                                   perturb=self.cfg.perturb, raw_noise_std=self.cfg.raw_noise_std,
+                                   lr=float(_g(train, "lrate_rgb", 0.01)),
+                                   gamma=float(_g(train, "lrate_gamma", 1.0)), seed=self._seed)
+            self._camera_engine = eng
+        self.color.reset_optimizer()  # torch.optim.Adam over the colour parameters (:576)
+        rays = torch.empty(max(n_max, 1), 13, dtype=torch.float32, device=self._device)
+        inten = torch.empty(max(n_max, 1), 3, dtype=torch.float32, device=self._device)
+        loss = None
+        for it in range(frames.n_iter):
+            n = frames.build(it, rays, inten)
+            loss = eng.step(rays[:n], inten[:n], global_step=self._global_step)
+            self._global_step += 1
+        self._keyframe_count += 1
+        return float(loss.item()) if loss is not None else float("nan")
 
     # ------------------------------------------------------------------ FIXED ray selection
     def _fixed_schedule(self, scans, window):

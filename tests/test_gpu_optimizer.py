@@ -87,3 +87,30 @@ def test_strategies_run(L, strategy, sky):
         assert opt._global_step == max(int(s["distances"].numel()) for s in scans) // 64
     else:
         assert opt._global_step == 3
+
+
+def test_camera_phase_and_checkpoint(L, tmp_path):
+    """iterate_optimizer_camera trains the colour head with the sigma head frozen; the checkpoint
+    carries both branches under the reference's module paths and restores them."""
+    from loner_amd import camera as C
+    from loner_amd import checkpoint as ckp
+    from loner_amd.optimizer import Optimizer
+    scans, cube = _window("quad", 2)
+    opt = Optimizer(_settings(n_it=3), None, cube, "cuda:0")
+    opt.iterate_optimizer(scans)
+    sigma_before = opt.state.params.clone()
+    W, H = 32, 24
+    dirs = C.pinhole_directions(W, H, np.array([[30.0, 0, 15.5], [0, 30.0, 11.5], [0, 0, 1]]))
+    imgs = [np.full((W * H, 3), 0.3, np.float32)]
+    pose = scans[0]["pose"].numpy()[:3]
+    fr = C.CameraFrames(dirs, W, H, imgs, [pose], cube, (1.0, 75.0), n_rays_per_kf=128, device="cuda:0")
+    l0 = opt.iterate_optimizer_camera(fr)
+    assert np.isfinite(l0) and opt.color.adam_step == fr.n_iter
+    assert torch.equal(opt.state.params, sigma_before)  # the sigma head is frozen in the camera phase
+    path = tmp_path / "ck.tar"
+    ckp.save_checkpoint(str(path), opt.state, opt._global_step, other_params=ckp.color_params(opt.color))
+    ck = torch.load(str(path), map_location="cpu", weights_only=True)
+    assert set(ck["network_state_dict"]) >= {ckp.SIGMA_KEY, ckp.COLOR_GRID_KEY, ckp.COLOR_MLP_KEY, ckp.DIR_ENC_KEY}
+    cs2 = C.ColorState(device="cuda:0", seed=99)
+    ckp.load_color(ck, cs2)
+    assert torch.equal(cs2.shadow, opt.color.shadow)  # fp16 round trip of the fp16 shadow
