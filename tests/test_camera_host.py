@@ -2,7 +2,6 @@
 (optimizer.py:581-601,626-644, FULL_CONFIG) and the pinhole direction table (get_ray_directions,
 ray_utils.py:62-124, no distortion)."""
 import numpy as np
-import torch
 
 from loner_amd import camera as C
 

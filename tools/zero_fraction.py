@@ -1,6 +1,10 @@
+"""Fractions of zero-weight samples and zero colour gradients in one CAM-shaped camera iteration
+(GPU box): the inputs behind the camera phase's skip_zero measurement.
+
+    python tools/zero_fraction.py
+"""
 import sys, torch, numpy as np
 sys.path.insert(0, '.')
-import bench
 from loner_amd import camera as C, step as S_, synthetic as syn
 torch.cuda.set_device(0)
 dev = torch.device("cuda", 0)
