@@ -301,6 +301,16 @@ typedef struct lnr_camera_desc {
 } lnr_camera_desc;
 int lnr_build_camera_rays(const lnr_camera_desc* cam, const float* dirs, const float* image, const int64_t* pixels,
                           int64_t n, float* rays, float* intensities, void* stream);
+/* A whole camera window in one launch: frames = DEVICE array of n_frames {camera, image}; frame f
+ * fills slots [f n_per_frame, (f + 1) n_per_frame) from pixels[f stride + first + j] (a window's
+ * per-frame pixel schedules, optimizer.py:626-644).  intensities may be NULL. */
+typedef struct lnr_camera_frame {
+  lnr_camera_desc cam;
+  const float* image;   /* (height * width, channels) fp32, DEVICE */
+} lnr_camera_frame;
+int lnr_build_camera_rays_window(const lnr_camera_frame* frames, int32_t n_frames, const float* dirs,
+                                 const int64_t* pixels, int64_t stride, int64_t first, int64_t n_per_frame,
+                                 float* rays, float* intensities, void* stream);
 
 /* Colour-head training, camera phase (Optimizer._do_iterate_optimizer_camera + compute_loss_camera,
  * src/mapping/optimizer.py:541-688,861-894): sigma frozen and detached (weights = the sigma pass's

@@ -76,6 +76,11 @@ class CameraDesc(ctypes.Structure):
                 ("pose", ctypes.c_float * 12)]
 
 
+class CameraFrame(ctypes.Structure):
+    """``lnr_camera_frame``."""
+    _fields_ = [("cam", CameraDesc), ("image", ctypes.c_void_p)]
+
+
 class SkyParams(ctypes.Structure):
     """``lnr_sky_params``."""
     _fields_ = [("rot", ctypes.c_float * 9), ("top_rows", ctypes.c_int32), ("horizon_deg", ctypes.c_float)]
@@ -126,6 +131,7 @@ _SIGNATURES = {
     "lnr_rgb_train": (ctypes.c_int, [c_p, c_i32, c_p, c_i64, c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_p, c_p, c_p,
                                      c_p, c_i64, c_p]),
     "lnr_build_camera_rays": (ctypes.c_int, [ctypes.POINTER(CameraDesc), c_p, c_p, c_p, c_i64, c_p, c_p, c_p]),
+    "lnr_build_camera_rays_window": (ctypes.c_int, [c_p, c_i32, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
     "lnr_motion_compensate": (ctypes.c_int, [ctypes.POINTER(MotionComp), c_p, c_p, c_p, c_i64, c_p]),
     "lnr_sky_rays_capacity": (c_i64, []),
     "lnr_sky_rays": (ctypes.c_int, [c_p, c_i64, ctypes.POINTER(SkyParams), c_p, c_i64, c_p, c_p]),

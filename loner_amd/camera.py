@@ -161,6 +161,15 @@ class CameraFrames:
             for i, v in enumerate(self.poses[k].reshape(-1).tolist()):
                 cam.pose[i] = v
             self.descs.append(cam)
+        # the window on the device for lnr_build_camera_rays_window: {camera, image} per frame, and
+        # the per-frame pixel schedules as one (K, keep) array
+        arr = (L.CameraFrame * len(self.images))()
+        for k, img in enumerate(self.images):
+            arr[k].cam = self.descs[k]
+            arr[k].image = img.data_ptr()
+        self.frames_dev = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(dev)
+        self.perm2d = torch.stack(self.perm).contiguous() if keep > 0 else torch.zeros(len(self.images), 1,
+                                                                                       dtype=torch.int64, device=dev)
 
     def iteration_slice(self, it):
         """[max(n*it - 1, 0), min(n*(it + 1) - 1, n_iter*n)) (optimizer.py:633-635)."""
@@ -177,10 +186,8 @@ class CameraFrames:
         order (optimizer.py:614-655).  Returns the ray count."""
         lo, hi = self.iteration_slice(it)
         n = max(hi - lo, 0)
-        s = L.stream(self.device)
-        for k, img in enumerate(self.images):
-            L.call("lnr_build_camera_rays", L.ctypes.byref(self.descs[k]), self.dirs, img, self.perm[k][lo:hi], n,
-                   rays[k * n:(k + 1) * n], intensities[k * n:(k + 1) * n], s)
+        L.call("lnr_build_camera_rays_window", self.frames_dev, len(self.images), self.dirs, self.perm2d, self.keep, lo,
+               n, rays, intensities, L.stream(self.device))  # every keyframe in one launch
         return len(self.images) * n
 
 

@@ -228,13 +228,9 @@ extern "C" int lnr_build_lidar_rays(const lnr_ray_window* w, int32_t select, con
 // table, rotated by the camera pose, normalised; origin = (t + shift) / scale; view direction = -d;
 // near = r_min / scale; far = get_far_val(o, d, no_nan=True) (NOT clipped by r_max here); the
 // intensities are the image row p.  fp32 in the reference's operation order.
-__global__ void __launch_bounds__(256) k_build_camera_rays(lnr_camera_desc cam, const float* __restrict__ dirs,
-                                                           const float* __restrict__ image,
-                                                           const int64_t* __restrict__ pixels, int64_t n,
-                                                           float* __restrict__ rays, float* __restrict__ intens) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  const int64_t p = pixels[k];
+__device__ __forceinline__ void camera_ray(const lnr_camera_desc& cam, const float* __restrict__ dirs,
+                                           const float* __restrict__ image, int64_t p, int64_t k,
+                                           float* __restrict__ rays, float* __restrict__ intens) {
   const float sc = cam.scale;
   float o[3], d[3];
 #pragma unroll
@@ -268,6 +264,29 @@ __global__ void __launch_bounds__(256) k_build_camera_rays(lnr_camera_desc cam, 
     for (int c = 0; c < cam.channels; ++c) intens[k * cam.channels + c] = image[p * cam.channels + c];
 }
 
+__global__ void __launch_bounds__(256) k_build_camera_rays(lnr_camera_desc cam, const float* __restrict__ dirs,
+                                                           const float* __restrict__ image,
+                                                           const int64_t* __restrict__ pixels, int64_t n,
+                                                           float* __restrict__ rays, float* __restrict__ intens) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  camera_ray(cam, dirs, image, pixels[k], k, rays, intens);
+}
+
+// every frame of a camera window in one launch: frame f's slots [f n_per, (f + 1) n_per) take its
+// pixels[f stride + first + j]
+__global__ void __launch_bounds__(256) k_build_camera_rays_window(const lnr_camera_frame* __restrict__ frames,
+                                                                  int32_t n_frames, const float* __restrict__ dirs,
+                                                                  const int64_t* __restrict__ pixels, int64_t stride,
+                                                                  int64_t first, int64_t n_per,
+                                                                  float* __restrict__ rays, float* __restrict__ intens) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= (int64_t)n_frames * n_per) return;
+  const int64_t f = k / n_per, j = k - f * n_per;
+  const lnr_camera_frame fr = frames[f];
+  camera_ray(fr.cam, dirs, fr.image, pixels[f * stride + first + j], k, rays, intens);
+}
+
 extern "C" int lnr_build_camera_rays(const lnr_camera_desc* cam, const float* dirs, const float* image,
                                      const int64_t* pixels, int64_t n, float* rays, float* intensities,
                                      void* stream) {
@@ -279,4 +298,17 @@ extern "C" int lnr_build_camera_rays(const lnr_camera_desc* cam, const float* di
   hipLaunchKernelGGL(k_build_camera_rays, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), *cam,
                      dirs, image, pixels, n, rays, intensities);
   LNR_RETURN_LAUNCH("lnr_build_camera_rays");
+}
+
+extern "C" int lnr_build_camera_rays_window(const lnr_camera_frame* frames, int32_t n_frames, const float* dirs,
+                                            const int64_t* pixels, int64_t stride, int64_t first, int64_t n_per_frame,
+                                            float* rays, float* intensities, void* stream) {
+  LNR_REQUIRE(n_frames >= 0 && n_per_frame >= 0 && first >= 0 && first + n_per_frame <= stride,
+              "lnr_build_camera_rays_window: bad sizes");
+  const int64_t n = (int64_t)n_frames * n_per_frame;
+  if (n == 0) return LNR_OK;
+  LNR_REQUIRE(frames && dirs && pixels && rays, "lnr_build_camera_rays_window: null pointer");
+  hipLaunchKernelGGL(k_build_camera_rays_window, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream),
+                     frames, n_frames, dirs, pixels, stride, first, n_per_frame, rays, intensities);
+  LNR_RETURN_LAUNCH("lnr_build_camera_rays_window");
 }
