@@ -76,7 +76,11 @@ def _scan_dict(kf):
 
 class Optimizer:
     def __init__(self, settings, calibration=None, world_cube=None, device="cuda", use_gt_poses=False,
-                 lidar_only=True, enable_sky_segmentation=True, seed=0):
+                 lidar_only=True, enable_sky_segmentation=True, seed=0, allreduce=None, rank=0, world=1):
+        """``allreduce`` / ``rank`` / ``world``: data-parallel over ranks (one process per GPU):
+        rank r optimises the contiguous slice ``shard_range(window slots, r, world)`` of every
+        window's rays; the opaque count and the gradients are summed with ``allreduce(t,
+        async_op=...)`` (e.g. ``torch.distributed.all_reduce``), so every rank holds the same map."""
         if world_cube is None:
             raise ValueError("Optimizer needs the world cube")
         self._settings = settings
@@ -111,6 +115,9 @@ class Optimizer:
         self._lr_gamma = float(_g(train, "lrate_gamma", 1.0))
         self.state = FieldState(self.cfg, device=self._device, seed=seed)
         self._seed = int(seed)
+        self._allreduce, self._rank, self._world = allreduce, int(rank), int(world)
+        if self._world > 1 and allreduce is None:
+            raise ValueError("world > 1 needs an allreduce")
         self._engine = None
         self._keyframe_schedule = _g(settings, "keyframe_schedule") or [
             dict(num_keyframes=-1, iteration_schedule=[dict(num_iterations=1, freeze_poses=True,
@@ -134,10 +141,18 @@ class Optimizer:
                 break
         return schedule
 
-    def _engine_for(self, n_rays):
-        if self._engine is None or self._engine.n_rays < n_rays:
-            self._engine = StepEngine(self.state, n_rays, seed=self._seed)
-        return self._engine
+    def _engine_for(self, n_slots):
+        """The engine for a window of n_slots rays and this rank's slot range [s0, s1) of it (all of
+        them on one GPU).  The engine is reused while its capacity suffices; its ray_offset (the
+        global index of its first ray, which keys the draws) follows the window."""
+        from .shard import shard_range
+        s0, s1 = shard_range(n_slots, self._rank, self._world)
+        e = self._engine
+        if e is None or e.n_rays < s1 - s0:
+            e = StepEngine(self.state, s1 - s0, seed=self._seed, allreduce=self._allreduce, ray_offset=s0)
+            self._engine = e
+        e.ray_offset = s0
+        return e, s1 - s0
 
     def iterate_optimizer(self, keyframe_window, optimizer_settings: OptimizationSettings = None) -> float:
         schedule = self._iteration_schedule()
@@ -177,16 +192,19 @@ class Optimizer:
         fixed = self._rays_strategy == "FIXED"
         window = RayWindow(scans, self._world_cube, self._ray_range, n_lidar=self._num_lidar_samples, n_sky=n_sky,
                            strategy="RANDOM" if fixed else self._rays_strategy, device=self._device)
-        eng = self._engine_for(window.n_slots)
+        eng, n_local = self._engine_for(window.n_slots)
         out = None
         if fixed:
+            if self._world > 1:
+                raise NotImplementedError("FIXED ray selection is single-GPU here (its batch size varies)")
             given, num_iterations = self._fixed_schedule(scans, window)
         for it in range(num_iterations):
             eng.lr_factor = self._lr_gamma ** it  # ExponentialLR stepped after every iteration
             if fixed:
                 out = self._fixed_step(eng, window, given, it)
             else:
-                out = eng.step_window(window, global_step=self._global_step, iteration_idx=it)
+                out = eng.step_window(window, global_step=self._global_step, iteration_idx=it,
+                                      n_rays_global=window.n_slots, n_slots=n_local)
             self._global_step += 1
         eng.lr_factor = 1.0
         return out

@@ -361,22 +361,28 @@ class StepEngine:
         self.allreduce(g)
         L.call("lnr_sgd_step", (st.occ), g, st.occ.numel(), self.cfg.occ_lr, s)
 
-    def step_window(self, window, global_step, iteration_idx=0, n_rays_global=None, prof=None, **kw):
+    def step_window(self, window, global_step, iteration_idx=0, n_rays_global=None, prof=None, n_slots=None, **kw):
         """One optimiser step whose rays are selected and built on the device from a resident
         ``loner_amd.rays.RayWindow`` (optimizer.py:363-424 + the step above).  This rank builds the
-        window's slots [ray_offset, ray_offset + capacity).  When the window can produce invalid rays
-        (``window.all_valid`` False) they are dropped as the reference drops them, which needs the
-        batch size on the host: one synchronisation, only on such windows."""
+        window's slots [ray_offset, ray_offset + n_slots) (n_slots <= capacity, default the
+        capacity).  When the window can produce invalid rays (``window.all_valid`` False) they are
+        dropped as the reference drops them, which needs the batch size on the host: one
+        synchronisation, only on such windows."""
+        n = self.n_rays if n_slots is None else int(n_slots)
+        if not 0 <= n <= self.n_rays or self.ray_offset + n > window.n_slots:
+            raise ValueError(f"slots [{self.ray_offset}, {self.ray_offset + n}) outside the window "
+                             f"({window.n_slots}) or the engine capacity ({self.n_rays})")
         key = L.step_key(self.seed, global_step)
         m = self._mark
         m(prof, "rays")
-        window.build(key, self.ray_offset, self.n_rays, self.rays, self.depth_gt, self.ray_valid, None, self.far_ref)
+        window.build(key, self.ray_offset, n, self.rays[:n], self.depth_gt[:n], self.ray_valid[:n], None,
+                     self.far_ref)
         m(prof, "rays")
-        rays, dgt = self.rays, self.depth_gt
+        rays, dgt = self.rays[:n], self.depth_gt[:n]
         if n_rays_global is None:
             n_rays_global = window.n_slots
         if not window.all_valid:
-            keep = self.ray_valid.bool()
+            keep = self.ray_valid[:n].bool()
             rays, dgt = rays[keep].contiguous(), dgt[keep].contiguous()
             cnt = torch.tensor([float(rays.shape[0])], device=self.state.device)
             if self.allreduce is not None:

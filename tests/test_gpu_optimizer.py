@@ -114,3 +114,49 @@ def test_camera_phase_and_checkpoint(L, tmp_path):
     cs2 = C.ColorState(device="cuda:0", seed=99)
     ckp.load_color(ck, cs2)
     assert torch.equal(cs2.shadow, opt.color.shadow)  # fp16 round trip of the fp16 shadow
+
+
+def _dp_worker(rank, world, port, out):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from loner_amd.optimizer import Optimizer
+    scans, cube = _window("forest", 2)
+
+    def allreduce(t, async_op=False):
+        return dist.all_reduce(t, async_op=async_op)
+
+    opt = Optimizer(_settings("MASK", n_it=4, sky=8), None, cube, "cuda:0", seed=2, allreduce=allreduce, rank=rank,
+                    world=world)
+    opt.iterate_optimizer(scans)
+    torch.cuda.synchronize()
+    np.save(os.path.join(out, f"p{rank}.npy"), opt.state.params.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_optimizer_data_parallel_gloo(L, tmp_path):
+    """Optimizer(allreduce, rank, world): two gloo ranks on the window's two ray shards give the same
+    map on both replicas, and the single-GPU map to a tolerance (summation order, OGM atomics)."""
+    import socket
+    import torch.multiprocessing as mp
+    from loner_amd.optimizer import Optimizer
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=150)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    p0, p1 = np.load(tmp_path / "p0.npy"), np.load(tmp_path / "p1.npy")
+    assert np.array_equal(p0, p1)
+    scans, cube = _window("forest", 2)
+    opt = Optimizer(_settings("MASK", n_it=4, sky=8), None, cube, "cuda:0", seed=2)
+    opt.iterate_optimizer(scans)
+    ref = opt.state.params.cpu().numpy()
+    assert np.linalg.norm(p0 - ref) / np.linalg.norm(ref) < 1e-4
