@@ -331,8 +331,9 @@ int lnr_rgb_train(const uint16_t* w_rgb, int32_t n_hidden_layers, const uint32_t
 int lnr_adam_step(float* param, uint16_t* shadow, const float* grad, float* m, float* v, int64_t n, int32_t step,
                   float lr, float beta1, float beta2, float eps, void* stream);
 /* OGM update: occ (res^3) -= lr * grid_sample^T(logits_grad(z*scale - depth_gt*scale)).  grad_ws is
- * workspace of ws_words fp32 (lnr_ogm_workspace_words(occ_res) for full speed: replicas of the grid
- * that spread same-voxel atomics; any ws_words >= res^3 works).  It is zeroed by the call. */
+ * workspace of ws_words fp32 (lnr_ogm_workspace_words(occ_res) for full speed; at least 3 res^3):
+ * the splat accumulates in int64 fixed point in replicas of the grid that spread same-voxel
+ * atomics (bitwise reproducible), and grad_ws[0, res^3) receives the fp32 gradient. */
 int64_t lnr_ogm_workspace_words(int32_t occ_res);
 int lnr_ogm_update(const float* rays, const float* z, const float* depth_gt, int64_t n_rays, int32_t n_samples,
                    float scale, float lr, float* occ, float* grad_ws, int64_t ws_words, int32_t occ_res, void* stream);

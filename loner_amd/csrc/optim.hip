@@ -63,11 +63,16 @@ __device__ __forceinline__ float logits_grad(float x) {
   return 0.25f * fr - 2.5f * oc;
 }
 
-constexpr int32_t kOgmReplicas = 8;
+// The splat accumulates in int64 fixed point (2^28 units: a sample adds |w g| <= 2.5, so 2^31 samples
+// stay below 2^63), so the grid gradient does not depend on the atomics' order: bitwise
+// reproducible.  Workspace (floats): [0, V) the float result, then n_rep int64 replicas.
+constexpr int32_t kOgmReplicas = 3;
+constexpr float kOgmFix = 268435456.0f;  // 2^28
 
 __global__ void __launch_bounds__(256) k_ogm_grad(const float* __restrict__ rays, const float* __restrict__ z,
                                                   const float* __restrict__ dgt, int64_t n_rays, int32_t S,
-                                                  float scale, float* __restrict__ grad, int32_t R, int32_t n_rep) {
+                                                  float scale, unsigned long long* __restrict__ grad, int32_t R,
+                                                  int32_t n_rep) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   // replica of the grid this workgroup adds into: the rays of one keyframe share their first
   // voxels, so one copy would serialise hundreds of same-address atomics at the memory side
@@ -110,27 +115,31 @@ __global__ void __launch_bounds__(256) k_ogm_grad(const float* __restrict__ rays
       if (lane - o >= head_lane) p += q;
     }
     const bool tail = (lane == 63) || ((heads >> (lane + 1)) & 1ull);
-    if (tail && idx >= 0) atomicAdd(&grad[idx], p);
+    if (tail && idx >= 0) atomicAdd(&grad[idx], (unsigned long long)__float2ll_rn(p * kOgmFix));
   }
 }
 
-// replica 0 += replicas 1..n_rep-1 (fixed order)
-__global__ void k_sum_replicas(float* __restrict__ g, int64_t nv, int32_t n_rep) {
+// out = (sum of the int64 replicas) / 2^28 (exact integer sum, one rounding)
+__global__ void k_sum_replicas(const unsigned long long* __restrict__ g, int64_t nv, int32_t n_rep,
+                               float* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nv) return;
-  float s = g[i];
-  for (int k = 1; k < n_rep; ++k) s += g[(int64_t)k * nv + i];
-  g[i] = s;
+  long long s = 0;
+  for (int k = 0; k < n_rep; ++k) s += (long long)g[(int64_t)k * nv + i];
+  out[i] = (float)((double)s * (1.0 / 268435456.0));
 }
 
 static int ogm_grad_launch(const float* rays, const float* z, const float* depth_gt, int64_t n_rays, int32_t n_samples,
                            float scale, float* grad_ws, int64_t ws_words, int32_t occ_res, hipStream_t st,
                            const char* who) {
   const int64_t nv = (int64_t)occ_res * occ_res * occ_res;
-  LNR_REQUIRE(ws_words >= nv, "%s: grad_ws holds %lld words, needs >= %lld", who, (long long)ws_words, (long long)nv);
-  int64_t rep = ws_words / nv;
+  LNR_REQUIRE(ws_words >= 3 * nv, "%s: grad_ws holds %lld words, needs >= %lld (3 res^3)", who, (long long)ws_words,
+              (long long)(3 * nv));
+  const int64_t rep = (ws_words / nv - 1) / 2;  // int64 replicas after the float result
   const int32_t n_rep = (int32_t)(rep > kOgmReplicas ? kOgmReplicas : rep);
-  if (hipMemsetAsync(grad_ws, 0, (size_t)n_rep * nv * sizeof(float), st) != hipSuccess) {
+  unsigned long long* g64 = reinterpret_cast<unsigned long long*>(grad_ws + nv + (nv & 1));  // 8-B aligned
+  LNR_REQUIRE((nv + (nv & 1)) + 2 * n_rep * nv <= ws_words, "%s: grad_ws too small", who);
+  if (hipMemsetAsync(g64, 0, (size_t)n_rep * nv * sizeof(unsigned long long), st) != hipSuccess) {
     set_error("%s: hipMemsetAsync failed", who);
     return LNR_ERR_HIP;
   }
@@ -138,10 +147,9 @@ static int ogm_grad_launch(const float* rays, const float* z, const float* depth
   if (n > 0) {
     LNR_REQUIRE(rays && z && depth_gt, "%s: null pointer", who);
     hipLaunchKernelGGL(k_ogm_grad, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rays, z, depth_gt, n_rays,
-                       n_samples, scale, grad_ws, occ_res, n_rep);
+                       n_samples, scale, g64, occ_res, n_rep);
   }
-  if (n_rep > 1)
-    hipLaunchKernelGGL(k_sum_replicas, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, grad_ws, nv, n_rep);
+  hipLaunchKernelGGL(k_sum_replicas, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, g64, nv, n_rep, grad_ws);
   return LNR_OK;
 }
 
@@ -200,7 +208,8 @@ extern "C" int lnr_adam_step(float* param, uint16_t* shadow, const float* grad, 
 
 extern "C" int64_t lnr_ogm_workspace_words(int32_t occ_res) {
   if (occ_res < 1) return -1;
-  return (int64_t)kOgmReplicas * occ_res * occ_res * occ_res;
+  const int64_t nv = (int64_t)occ_res * occ_res * occ_res;
+  return nv + (nv & 1) + 2 * kOgmReplicas * nv;  // float result + int64 replicas
 }
 
 extern "C" int lnr_ogm_update(const float* rays, const float* z, const float* depth_gt, int64_t n_rays,

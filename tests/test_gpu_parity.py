@@ -300,7 +300,8 @@ def test_ogm_update_golden(L, replicas):
     rays, z, dgt = g["rays"], g["z"], g["depth_gt"]
     R, S = z.shape
     grid = cu(occ.reshape(-1).copy())
-    words = int(L.lib().lnr_ogm_workspace_words(100)) if replicas else grid.numel()
+    # minimum workspace: the fp32 result + one int64 copy of the grid (3 res^3 words)
+    words = int(L.lib().lnr_ogm_workspace_words(100)) if replicas else 3 * grid.numel()
     ws = torch.full((words,), 7.0, device="cuda")  # garbage: the call zeroes its workspace
     L.call("lnr_ogm_update", (cu(rays)), (cu(z)), (cu(dgt)), R, S, float(g["scale"]),
            float(g["occ_lr"]), (grid), (ws), words, 100, L.stream())
@@ -310,6 +311,11 @@ def test_ogm_update_golden(L, replicas):
     mask = np.ones(delta.size, bool)
     mask[idx] = False
     assert np.abs(delta[mask]).max() < 1e-7
+    # int64 fixed-point splat: a second update from the same grid is bitwise identical
+    grid2 = cu(occ.reshape(-1).copy())
+    L.call("lnr_ogm_update", (cu(rays)), (cu(z)), (cu(dgt)), R, S, float(g["scale"]),
+           float(g["occ_lr"]), (grid2), (ws), words, 100, L.stream())
+    assert np.array_equal(host(grid2), host(grid))
 
 
 # ------------------------------------------------------------------ Adam
