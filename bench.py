@@ -19,6 +19,8 @@ loss normaliser are all-reduced over RCCL once per step.
 Rank 0 prints one JSON line (contract in the task statement), including
   roofline      hash-grid backward stage (the dominant stage) against HBM peak, algorithmic bytes
                 1024 B/sample, duration from HIP events on the launch stream
+  mfma          the sigma MLP (12,672 FLOP/sample) over the field stage against the dense fp16 MFMA
+                peak, plus the PMC MFMA-busy fraction of its kernels from profiles/*_mfma_<cfg>.json
   cpu_baseline  the pure-PyTorch CPU restatement (oracle/torch_step.py) on a bounded sample, host threads
 """
 import argparse
@@ -34,6 +36,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 TB/s measured copy)
+MFMA_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA (MI355X_MICROARCH.md; sparsity figures excluded)
+MLP_FLOP_PER_SAMPLE = 12672  # sigma MLP 32->64->1(16): fwd 2*(32*64 + 64*1) = 4224, bwd 2x
 
 
 def parse():
@@ -82,6 +86,17 @@ def pmc_traffic(cfg_name):
         return None, None
     rec = json.load(open(files[-1]))
     return rec["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+
+
+def pmc_mfma(cfg_name):
+    """Per sigma-MLP kernel MFMA busy fractions from the newest committed PMC pass of this bench
+    command (profiles/<round>_mfma_<cfg>.json, tools/refresh_profiles.py); None if there is none."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_mfma_{cfg_name}.json")))
+    if not files:
+        return None, None
+    rec = json.load(open(files[-1]))
+    return {k: v["mfma_busy_frac"] for k, v in rec["kernels"].items()}, os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(cfg_name, n_rays, n_steps):
@@ -332,8 +347,8 @@ def bench_camera(args):
             "config": {"workload": f"CAM: {n_kf} KF x {per_kf} camera rays x {S} samples, colour head SH4 + L=16 "
                                    f"T=2^19 + 48->64x4->3 MLP, L1 loss, Adam",
                        "rays": R, "samples_per_ray": S, "parallelism": "single"},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": 2500.0, "unit": "TFLOP/s",
-                         "frac": achieved / 2500.0, "traffic": None,
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / MFMA_PEAK_TFLOPS, "traffic": None,
                          "kernel": "lnr_rgb_train (colour forward x2 + L1 + MLP backward, MFMA fp16)",
                          "algorithmic_flop_per_launch": flop, "ms_per_launch": bwd_ms},
             "stage_ms": stage_ms}
@@ -498,6 +513,8 @@ def main():
     bwd_ms = stage_ms["grid_bwd"]
     achieved = 1024.0 * N / (bwd_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args.config)
+    busy, busy_src = pmc_mfma(args.config)
+    mlp_tflops = MLP_FLOP_PER_SAMPLE * N / (stage_ms["field"] * 1e-3) / 1e12
     line = {
         "metric": "ray-samples/sec per optimizer step",
         "value": value,
@@ -522,6 +539,11 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "hash-grid backward stage (k_bwd_scan_*, k_bwd_scatter, k_bwd_level_max, k_bwd_accum)",
                      "algorithmic_bytes_per_launch": 1024 * N, "ms_per_launch": bwd_ms},
+        # the sigma MLP (fwd 4224 + bwd 8448 FLOP/sample) over the field stage
+        # (k_field_wave + k_mlp_bwd_tiles), against the dense fp16 MFMA peak
+        "mfma": {"achieved": mlp_tflops, "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": mlp_tflops / MFMA_PEAK_TFLOPS,
+                 "flop_per_sample": MLP_FLOP_PER_SAMPLE, "ms_per_launch": stage_ms["field"],
+                 "busy": busy, "busy_source": busy_src},
         "stage_ms": stage_ms,
         "loss": float(loss[0]),
     }

@@ -1,6 +1,6 @@
 # GPU box: the committed profile set for one config (tools/refresh_profiles.py turns it into profiles/):
 #   bench.json (plain run, with cpu_baseline), prof/ (rocprofv3 --kernel-trace --stats of the same
-#   bench command), pmc/FETCH_SIZE and pmc/WRITE_SIZE (one --pmc pass each, kernel trace only).
+#   bench command), pmc/FETCH_SIZE, pmc/WRITE_SIZE and pmc/MFMA (one --pmc pass each, kernel trace only).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 CFG=${1:-C2}
@@ -14,4 +14,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run 
   python3 $R/bench.py --config $CFG --no-cpu-baseline > $R/gpurun_out/bench_prof.json 2> $R/gpurun_out/bench_prof.err \
   || { tail -20 $R/gpurun_out/bench_prof.err; exit 1; }
 bash $R/tools/pmc_hbm.sh || exit 1
+bash $R/tools/pmc_mfma.sh || exit 1
 echo profiles done
