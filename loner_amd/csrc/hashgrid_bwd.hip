@@ -223,7 +223,10 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
   //    the sample's position inputs and d_enc, and (wave 0) the row's offsets.
   const int64_t ic = in ? i : n - 1;
   const typename PosFn::Raw raw = pos.load(ic);
-  const float2 g_raw = d_enc[(int64_t)l * stride + ic];
+  // d_enc is read once: a nontemporal load keeps it from displacing the L2 lines in which adjacent
+  // rows' bucket runs combine (scatter -1.5 % at C2)
+  const f32x2 g_nt = __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(&d_enc[(int64_t)l * stride + ic]));
+  const float2 g_raw = make_float2(g_nt.x, g_nt.y);
   uint32_t h0[2] = {0u, 0u}, h1[2] = {0u, 0u};
   uint64_t seg[2] = {0ull, 0ull};
   const bool last = sb + 1 >= ws.n_sb;
