@@ -13,6 +13,10 @@
 
 namespace lnr {
 
+// The encoding is written once, as whole lines, and read by the field kernels after this launch: a
+// nontemporal store keeps it out of the way of the table slices in L2 (step -0.01 ms at C2)
+__device__ __forceinline__ void store_enc(uint32_t* p, uint32_t v) { __builtin_nontemporal_store(v, p); }
+
 template <class PosFn, bool COUNT>
 __global__ void __launch_bounds__(1024) k_hashgrid_fwd(GridArgs a, PosFn pos, int64_t n, const uint32_t* __restrict__ table,
                                                       uint32_t* __restrict__ enc, int64_t stride, BwdWorkspace ws,
@@ -71,7 +75,7 @@ __global__ void __launch_bounds__(1024) k_hashgrid_fwd(GridArgs a, PosFn pos, in
         f0 = fmaf(w, t.x, f0);
         f1 = fmaf(w, t.y, f1);
       }
-      enc[(int64_t)l * stride + i] = (uint32_t)f2h(f0) | ((uint32_t)f2h(f1) << 16);
+      store_enc(enc + (int64_t)l * stride + i, (uint32_t)f2h(f0) | ((uint32_t)f2h(f1) << 16));
     }
     if (COUNT) {
       lds_barrier();
@@ -93,7 +97,7 @@ __global__ void __launch_bounds__(1024) k_hashgrid_fwd(GridArgs a, PosFn pos, in
       f0 = fmaf(c.w[k], t.x, f0);
       f1 = fmaf(c.w[k], t.y, f1);
     }
-    enc[(int64_t)l * stride + i] = (uint32_t)f2h(f0) | ((uint32_t)f2h(f1) << 16);
+    store_enc(enc + (int64_t)l * stride + i, (uint32_t)f2h(f0) | ((uint32_t)f2h(f1) << 16));
   }
   if (COUNT) {
     lds_barrier();
