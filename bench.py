@@ -42,7 +42,9 @@ MLP_FLOP_PER_SAMPLE = 12672  # sigma MLP 32->64->1(16): fwd 2*(32*64 + 64*1) = 4
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default: WORLD_SIZE under a launcher, else 1).  Without a launcher "
+                         "(WORLD_SIZE unset) and N > 1, bench.py starts the N rank processes itself")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="C2", choices=["C1", "C2", "C3", "C4", "C5", "CAM"],
@@ -53,9 +55,10 @@ def parse():
                     help="device: select + build each step's rays on the GPU from the resident window; "
                          "resident: cycle prebuilt ray batches")
     ap.add_argument("--batches", type=int, default=4, help="--rays resident: distinct batches cycled per rank")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+    ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
                     help="weak: each rank optimises the config's full batch (global batch grows with N); "
-                         "strong: the config's batch is split over the N ranks (SURVEY.md §8(e))")
+                         "strong: the config's batch is split over the N ranks (SURVEY.md §8(e)).  Default: "
+                         "strong for C4 at N > 1 (the headline C4 curve at R = 9216), weak otherwise")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rays", type=int, default=256, help="rays per CPU-baseline step (x512 samples)")
     ap.add_argument("--cpu-steps", type=int, default=36)
@@ -399,13 +402,63 @@ def _camera_stages(eng, fr, rays, inten, L):
     return {ev[i][0]: float(ev[i][1].elapsed_time(ev[i + 1][1])) for i in range(len(ev) - 1)}
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """``--gpus N`` without a launcher: start N rank processes of this same command (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT set as torch.distributed.run sets them), one per GPU,
+    and wait.  This process never touches the GPU (it only counts devices, which does not initialise
+    HIP).  Any rank failing ends the others and the exit status is that rank's; rank 0 prints the line."""
+    import signal
+    import subprocess
+    backend = os.environ.get("LONER_DIST_BACKEND", "nccl")
+    n_dev = torch.cuda.device_count()
+    if backend == "nccl" and n_dev < n:
+        raise SystemExit(f"bench.py --gpus {n}: only {n_dev} GPU(s) visible (one rank per GPU over RCCL; "
+                         f"LONER_DIST_BACKEND=gloo shares GPUs between ranks)")
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:  # a failed rank would leave the others blocked in a collective
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    if rc:
+        print(f"bench.py: a rank exited with status {rc}", file=sys.stderr)
+    sys.exit(rc)
+
+
 def main():
     args = parse()
-    if args.config == "C3":
-        return bench_render(args)
-    if args.config == "CAM":
-        return bench_camera(args)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        return spawn_ranks(args.gpus)
+    world = int(env_world or "1")
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.config in ("C3", "CAM"):
+        if world > 1:
+            raise SystemExit(f"bench.py --config {args.config} is a single-GPU bench (no sharded path)")
+        return bench_render(args) if args.config == "C3" else bench_camera(args)
+    if args.scaling is None:
+        args.scaling = "strong" if args.config == "C4" and world > 1 else "weak"
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # LONER_DIST_BACKEND=gloo rehearses the multi-rank path on fewer GPUs than ranks (ranks share
@@ -419,6 +472,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         else:
             dist.init_process_group(backend)
+        if dist.get_world_size() != world:
+            raise RuntimeError(f"process group has {dist.get_world_size()} ranks, WORLD_SIZE={world}")
     else:
         dist = None
         torch.cuda.set_device(0)
@@ -546,6 +601,8 @@ def main():
                  "busy": busy, "busy_source": busy_src},
         "stage_ms": stage_ms,
         "loss": float(loss[0]),
+        # the process group as torch.distributed reports it (None: a single process, no group)
+        "dist": ({"backend": dist.get_backend(), "ranks": dist.get_world_size()} if dist is not None else None),
     }
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_rays, args.cpu_steps)

@@ -1,0 +1,58 @@
+"""Backward-stage diagnostics at a bench config (GPU box): per level, the share of samples whose
+d_enc is exactly zero, max |d_enc|, and the record count of each level's buckets (from the
+backward workspace after a step).  python tools/diag_bwd.py [C2|C4]"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main(cfg_name="C2"):
+    import bench
+    from loner_amd import step as S_
+    from loner_amd import synthetic as syn
+    from loner_amd.rays import RayWindow
+    kind, nkf, rpk, spk, strat, S, preset = syn.CONFIGS[cfg_name]
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    scans = syn.make_window(kind, nkf, seed=1000)
+    window = RayWindow(scans, syn.world_cube(kind), syn.SENSORS[kind]["ray_range"], n_lidar=rpk, n_sky=spk,
+                       strategy=strat, device=dev)
+    cfg = S_.StepConfig(n_samples=S, loss=S_.LossConfig.from_dict(bench.LOSS_PRESETS[preset]))
+    st = S_.FieldState(cfg, device=dev)
+    eng = S_.StepEngine(st, window.n_slots, seed=12345)
+    for it in [0, 10, 50]:
+        while True:
+            eng.step_window(window, global_step=it)
+            break
+        torch.cuda.synchronize()
+        de = eng.d_enc[:, :eng.N].float()
+        zero = (de == 0).all(-1).float().mean(1).cpu().numpy()
+        mx = de.abs().amax((1, 2)).cpu().numpy()
+        print(f"step {it}: zero-gradient share per level {np.round(zero, 3).tolist()}")
+        print(f"  max|d_enc| per level {[f'{v:.2e}' for v in mx]}")
+        # bucket record counts: counts[] lives at the layout's 'counts' offset; recompute from seg_start
+        nb = int(sum((int(st.desc.size[l]) + 4095) // 4096 for l in range(st.desc.n_levels)))
+        print(f"  buckets {nb}")
+    # warm steps for the timing shape
+    for it in range(60, 80):
+        eng.step_window(window, global_step=it)
+    torch.cuda.synchronize()
+    de = eng.d_enc[:, :eng.N].float()
+    zero = (de == 0).all(-1).float().mean(1).cpu().numpy()
+    print(f"step 79: zero-gradient share per level {np.round(zero, 3).tolist()}")
+    # magnitude distribution relative to the level max (fp16 range check)
+    for l in [0, 5, 10, 15]:
+        a = de[l].abs().flatten()
+        a = a[a > 0]
+        m = float(a.max())
+        q = torch.quantile(a[:: max(1, a.numel() // 1000000)], torch.tensor([0.001, 0.01, 0.5], device=a.device))
+        print(f"  level {l}: max {m:.3e}, quantiles(0.1%,1%,50%)/max {[f'{float(v)/m:.2e}' for v in q]}")
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
