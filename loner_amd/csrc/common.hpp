@@ -109,6 +109,18 @@ __device__ __forceinline__ float wave_max_nonneg(float v) {
   return __int_as_float(__builtin_amdgcn_readlane(x, 63));
 }
 
+// Inclusive prefix sum of a u32 over the wave on DPP (row shifts, then row_bcast15/31), no LDS.
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+  int x = (int)v;
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);   // row_shr:1 (row edge reads 0)
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);   // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);   // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);   // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 into rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 into rows 2, 3
+  return (uint32_t)x;
+}
+
 // Block-wide sum of K values for a block of NT threads (NT/64 waves).  `scratch` needs
 // K * (NT/64) floats; all threads receive the totals.  Contains two barriers.
 template <int NT, int K>

@@ -49,10 +49,13 @@ struct GridArgs {
 
 // Levels whose cell edge spans several consecutive samples of a ray (resolution <= 256 at the
 // reference's ray lengths / sample counts) produce runs of equal corner indices.
+#ifndef LNR_MERGE_MAX_RES
+#define LNR_MERGE_MAX_RES 256
+#endif
 inline uint32_t merge_levels_for(const lnr_grid_desc* d) {
   uint32_t m = 0;
   for (uint32_t l = 0; l < d->n_levels; ++l)
-    if (d->resolution[l] <= 256) m = l + 1;
+    if (d->resolution[l] <= LNR_MERGE_MAX_RES) m = l + 1;
   return m;
 }
 
@@ -323,6 +326,7 @@ struct BwdWorkspace {
   long long* partial;    // [max_partials][2 * kChunk] int64 fixed-point partial sums of split buckets
   uint32_t* rec_w;       // [8 * N * L] record words (see "Backward records")
   RecVal* rec_v;         // [8 * N * L] record values (see "Backward records")
+  uint8_t* ovf;          // [L][n_sb] 1 where the level-looped scatter left (row, level) to k_bwd_scatter_overflow
   int64_t n_sb;
   int64_t n_chunks;
 };
@@ -341,7 +345,7 @@ inline int64_t bwd_max_partials(const lnr_grid_desc* d, int64_t n) {
 inline int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
 
 struct WsLayout {
-  int64_t hist, chunk_sum, blockmax, level_max, counts, seg_start, slice_pre, part_pre, partial, rec_w, rec_v, total;
+  int64_t hist, chunk_sum, blockmax, level_max, counts, seg_start, slice_pre, part_pre, partial, rec_w, rec_v, ovf, total;
 };
 
 inline WsLayout ws_layout(const lnr_grid_desc* d, const GridArgs& a, int64_t n) {
@@ -360,6 +364,7 @@ inline WsLayout ws_layout(const lnr_grid_desc* d, const GridArgs& a, int64_t n) 
   // +2 records: the accumulate loads records in pairs
   w.rec_w = b;     b += align256((8 * n * (int64_t)d->n_levels + 2) * 4);
   w.rec_v = b;     b += align256((8 * n * (int64_t)d->n_levels + 2) * (int64_t)sizeof(RecVal));
+  w.ovf = b;       b += align256(nsb * (int64_t)d->n_levels);
   w.total = b;
   return w;
 }
@@ -381,6 +386,7 @@ inline BwdWorkspace carve_workspace(void* base, const GridArgs& a, const lnr_gri
   w.partial = reinterpret_cast<long long*>(p + L.partial);
   w.rec_w = reinterpret_cast<uint32_t*>(p + L.rec_w);
   w.rec_v = reinterpret_cast<RecVal*>(p + L.rec_v);
+  w.ovf = reinterpret_cast<uint8_t*>(p + L.ovf);
   w.n_sb = bwd_n_sb(n);
   w.n_chunks = bwd_n_chunks(n);
   return w;

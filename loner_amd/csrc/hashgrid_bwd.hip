@@ -192,12 +192,12 @@ enum : int { kLevelsCoherent = 0, kLevelsFine = 1, kLevelsGeneric = 2, kLevelsAn
 #ifndef LNR_SCATTER_WAVES_PER_EU
 #define LNR_SCATTER_WAVES_PER_EU 1
 #endif
+// One (histogram row sb, level l) of the scatter; KIND as below, kLevelsAny meaning "any level".
 template <class PosFn, int KIND>
-__global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(GridArgs a, PosFn pos, int64_t n,
-                                                                             const float2* __restrict__ d_enc,
-                                                                             int64_t stride, BwdWorkspace ws, uint32_t l0,
-                                                                             bool skip_zero) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+__device__ __forceinline__ void scatter_row_level(const GridArgs& a, const PosFn& pos, int64_t n,
+                                                  const float2* __restrict__ d_enc, int64_t stride,
+                                                  const BwdWorkspace& ws, uint32_t l, int64_t sb, bool skip_zero,
+                                                  char* smem) {
   RecVal* stage_v = reinterpret_cast<RecVal*>(smem);                         // [kCap]
   uint64_t* gbase = reinterpret_cast<uint64_t*>(stage_v + kCap);             // [kMaxChunksPerLevel]
   uint32_t* stage_w = reinterpret_cast<uint32_t*>(gbase + kMaxChunksPerLevel);  // [kCap]
@@ -205,8 +205,6 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
   uint32_t* start = rank_ctr + kMaxChunksPerLevel;                           // [kMaxChunksPerLevel + 1]
   float* wmax = reinterpret_cast<float*>(start + kMaxChunksPerLevel + 1);    // [kSB / 64]
   uint8_t* sbk = reinterpret_cast<uint8_t*>(wmax + kSB / 64);                // [kCap] bucket of each staged record
-  const uint32_t l = KIND == kLevelsAny ? blockIdx.x % a.n_levels : l0 + blockIdx.y;
-  const int64_t sb = KIND == kLevelsAny ? (int64_t)(blockIdx.x / a.n_levels) : xcd_row(blockIdx.x, gridDim.x);
   const int kind = KIND != kLevelsAny ? KIND
                    : a.lv[l].fine           ? kLevelsFine
                    : l < a.merge_levels     ? kLevelsCoherent
@@ -388,6 +386,250 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
   LNR_PHASE_BY(sb, 5 * kind + 1, t2, t1);
   LNR_PHASE_BY(sb, 5 * kind + 2, t3, t2);
   LNR_PHASE_BY(sb, 5 * kind + 3, t4, t3);
+}
+
+template <class PosFn, int KIND>
+__global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(GridArgs a, PosFn pos, int64_t n,
+                                                                             const float2* __restrict__ d_enc,
+                                                                             int64_t stride, BwdWorkspace ws, uint32_t l0,
+                                                                             bool skip_zero) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t l = KIND == kLevelsAny ? blockIdx.x % a.n_levels : l0 + blockIdx.y;
+  const int64_t sb = KIND == kLevelsAny ? (int64_t)(blockIdx.x / a.n_levels) : xcd_row(blockIdx.x, gridDim.x);
+  scatter_row_level<PosFn, KIND>(a, pos, n, d_enc, stride, ws, l, sb, skip_zero, smem);
+}
+
+// The (row, level) items the level-looped scatter could not stage (more than kCap records: rows of
+// coherent levels whose runs did not merge, or pathological split pairs), each as above.
+template <class PosFn>
+__global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter_overflow(GridArgs a, PosFn pos, int64_t n,
+                                                                                      const float2* __restrict__ d_enc,
+                                                                                      int64_t stride, BwdWorkspace ws,
+                                                                                      bool skip_zero) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ unsigned long long masks[kSB / 64];
+  // workgroup b checks the flags of items [b kSB, (b + 1) kSB), item = level * n_sb + row
+  const int64_t items = ws.n_sb * a.n_levels;
+  const int64_t it = (int64_t)blockIdx.x * kSB + threadIdx.x;
+  const unsigned long long m = __ballot(it < items && ws.ovf[it] != 0);
+  if ((threadIdx.x & 63) == 0) masks[threadIdx.x >> 6] = m;
+  __syncthreads();
+  for (int w = 0; w < kSB / 64; ++w) {
+    for (unsigned long long mm = masks[w]; mm; mm &= mm - 1) {
+      const int64_t q = (int64_t)blockIdx.x * kSB + 64 * w + __ffsll((long long)mm) - 1;
+      scatter_row_level<PosFn, kLevelsAny>(a, pos, n, d_enc, stride, ws, (uint32_t)(q / ws.n_sb), q % ws.n_sb,
+                                           skip_zero, smem);
+      lds_barrier();
+    }
+  }
+}
+
+// Level-looped scatter: one workgroup per histogram row walks every level, so a sample's position is
+// loaded and decoded once (not once per level), the next level's d_enc and histogram row are in
+// flight while this level ranks and places, and the copy-out of level l - 1 overlaps the ranking of
+// level l (double-buffered staging, one barrier per level).  A level's bucket starts come from the
+// forward's histogram alone, so wave 0 computes them one level ahead and every record is placed the
+// moment its rank returns.  Same records, counts and blockmax as k_bwd_scatter.
+// ---------------------------------------------------------------------------------------------
+// Level-looped scatter: one workgroup per histogram row walks every level.
+//  * All global loads happen in the prologue: the sample's position, its d_enc at every level (32
+//    registers) and, wave w, the histogram rows of levels 2w and 2w + 1, turned at once into every
+//    level's bucket starts.  The level loop then issues only LDS operations and the copy-out
+//    stores, so nothing in it ever waits on global memory.
+//  * Each record is ranked (returning LDS atomic) and placed at once, 16 B {word, global slot, v0,
+//    v1} in bucket order; the copy-out of level l - 1 overlaps level l (double-buffered stage, one
+//    barrier per level).
+//  * A (row, level) with more than kRowsCap records is flagged and left to k_bwd_scatter_overflow.
+// Same records, counts and blockmax as k_bwd_scatter.
+constexpr int kRowsCap = 2176;  // 4.25 records per sample: fine rows hold 4 + the rare split pairs
+template <int NL, int NB>
+struct RowsLds {
+  uint4 stage[2][kRowsCap];   // staged records {word, global slot, v0, v1}, bucket order
+  uint2 sg[NL][NB];           // per level and bucket: {start in the stage, global slot of the run}
+  uint32_t total[NL];         // records of the row at each level
+  uint32_t ctr[2][NB];        // rank counters
+  float wmax[2][kSB / 64];
+  LevelParams lv[NL];         // the level table (kernel arguments indexed per level would be loads)
+};
+static_assert(sizeof(RecVal) == 8, "the level-looped scatter stages fp32 record values");
+
+// NL levels, the first NM coherent (run-merging) and the rest fine, at most NB buckets per level:
+// compile-time, so the level loop unrolls into straight-line code.  Record slots are 32-bit (the
+// launcher checks 8 N L < 2^32).
+template <class PosFn, int NL, int NM, int NB>
+__global__ void __launch_bounds__(kSB) __attribute__((amdgpu_waves_per_eu(4, 4)))
+k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ d_enc, int64_t stride, BwdWorkspace ws,
+                   bool skip_zero) {
+  static_assert(NL <= 2 * (kSB / 64), "wave w prepares levels 2w and 2w + 1");
+  static_assert(NB <= 128, "two buckets per lane");
+  __shared__ RowsLds<NL, NB> sm;
+  const int64_t sb = xcd_row(blockIdx.x, gridDim.x);
+  const int64_t i = sb * kSB + threadIdx.x;
+  const bool in = i < n;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const bool last = sb + 1 >= ws.n_sb;
+  const int64_t ic = in ? i : n - 1;
+  uint32_t* rec_v32 = reinterpret_cast<uint32_t*>(ws.rec_v);
+  const uint32_t spare = (uint32_t)(8 * n * (int64_t)NL);  // one of the 2 slack records past the last slot
+
+  // prologue 1: the level table and zero rank counters
+  if (threadIdx.x < NL * (sizeof(LevelParams) / 4))
+    reinterpret_cast<uint32_t*>(sm.lv)[threadIdx.x] = reinterpret_cast<const uint32_t*>(a.lv)[threadIdx.x];
+  if (threadIdx.x < 2 * NB) (&sm.ctr[0][0])[threadIdx.x] = 0u;
+  // prologue 2: every global load of the kernel
+  const typename PosFn::Raw raw = pos.load(ic);
+  f32x2 g[NL];
+#pragma unroll
+  for (int l = 0; l < NL; ++l)  // read once: nontemporal, so they do not displace the runs' L2 lines
+    g[l] = __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(&d_enc[(int64_t)l * stride + ic]));
+  uint32_t h0[2][2], h1[2][2];
+  uint64_t seg[2][2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const uint32_t l = 2 * wid + p;
+    if (l < (uint32_t)NL) {
+      const uint32_t b0 = a.bucket_base[l], nb = a.bucket_base[l + 1] - b0;
+      const uint32_t* row = ws.hist + (int64_t)b0 * ws.n_sb + sb * nb;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const uint32_t b = min(2u * lane + q, nb - 1u);
+        h0[p][q] = row[b];
+        h1[p][q] = (last ? ws.counts + b0 : row + nb)[b];  // next row's offset, or the bucket total
+        seg[p][q] = ws.seg_start[b0 + b];
+      }
+    }
+  }
+  float x = 0.f, y = 0.f, z = 0.f;
+  pos.eval(raw, x, y, z);
+  // prologue 3: wave w's levels' bucket starts (a wave prefix over the buckets, two per lane)
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const uint32_t l = 2 * wid + p;
+    if (l < (uint32_t)NL) {
+      const uint32_t nb = a.bucket_base[l + 1] - a.bucket_base[l];
+      const uint32_t c0 = 2 * lane < nb ? h1[p][0] - h0[p][0] : 0u;
+      const uint32_t c1 = 2 * lane + 1 < nb ? h1[p][1] - h0[p][1] : 0u;
+      const uint32_t inc = wave_incl_scan_u32(c0 + c1);
+      const uint32_t ex = inc - c0 - c1;
+      if (2 * lane < nb) sm.sg[l][2 * lane] = make_uint2(ex, (uint32_t)(seg[p][0] + h0[p][0]));
+      if (2 * lane + 1 < nb) sm.sg[l][2 * lane + 1] = make_uint2(ex + c0, (uint32_t)(seg[p][1] + h0[p][1]));
+      if (lane == 63) {
+        sm.total[l] = inc;
+        ws.ovf[(int64_t)l * ws.n_sb + sb] = inc > (uint32_t)kRowsCap;  // unstaged: k_bwd_scatter_overflow's item
+      }
+    }
+  }
+  lds_barrier();
+
+  // copy level l's staged row out (consecutive threads -> consecutive slots of a run); a second wave
+  // publishes the row's max |value|.  Every lane stores on every trip (lanes past the row's records
+  // into the spare slot), so the trip count is fixed
+  auto copy_out = [&](uint32_t l) {
+    const int sbuf = l & 1;
+    const uint32_t total = sm.total[l];
+    const uint32_t lim = total <= (uint32_t)kRowsCap ? total : 0u;
+#pragma unroll
+    for (int u = 0; u < (kRowsCap + kSB - 1) / kSB; ++u) {
+      const uint32_t t = threadIdx.x + u * kSB;
+      const uint4 q = sm.stage[sbuf][t < (uint32_t)kRowsCap ? t : kRowsCap - 1];
+      const uint32_t d = t < lim ? q.y : spare;
+      ws.rec_w[d] = q.x;
+      *reinterpret_cast<u32x2*>(rec_v32 + 2 * (uint64_t)d) = u32x2{q.z, q.w};
+    }
+    if (wid == 1) {
+      const float mm = wave_max_nonneg(lane < kSB / 64 ? sm.wmax[sbuf][lane] : 0.f);
+      if (lane == 0) ws.blockmax[(int64_t)l * ws.n_sb + sb] = mm;
+    }
+  };
+
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    const int sbuf = l & 1;
+    const LevelParams lv = sm.lv[l];
+    const bool staged = sm.total[l] <= (uint32_t)kRowsCap;  // block-uniform
+    uint32_t* ctr = sm.ctr[sbuf];
+    const uint2* sgl = sm.sg[l];
+    const float2 gv = in ? make_float2(g[l].x, g[l].y) : make_float2(0.f, 0.f);
+    const bool inr = staged && in;  // an unstaged row emits nothing here: k_bwd_scatter_overflow redoes it
+    const bool act = inr && (!skip_zero || gv.x != 0.f || gv.y != 0.f);
+    float m = 0.f;
+    // rank (returning LDS atomics) and place: all start reads, then all atomics, then all writes
+    auto place = [&](const bool (&valid)[4], const uint32_t (&bk)[4], const uint32_t (&word)[4],
+                     const float2 (&val)[4]) {
+      uint2 s4[4];
+      uint32_t rank[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s4[k] = valid[k] ? sgl[bk[k]] : make_uint2(0u, 0u);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) rank[k] = valid[k] ? atomicAdd(&ctr[bk[k]], 1u) : 0u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (valid[k]) {
+          m = fmaxf(m, fmaxf(fabsf(val[k].x), fabsf(val[k].y)));
+          sm.stage[sbuf][s4[k].x + rank[k]] = make_uint4(word[k], s4[k].y + rank[k], __float_as_uint(val[k].x),
+                                                         __float_as_uint(val[k].y));
+        }
+    };
+    bool v4[4];
+    uint32_t bk4[4], w4[4];
+    float2 val4[4];
+    if (l >= NM) {  // fine: one record per x-pair (hashgrid.hpp "Backward records")
+      FineCell c;
+      fine_cell(lv, x, y, z, c);
+      const bool split = c.d >= (uint32_t)kChunk;
+      const uint32_t code = ((uint32_t)__popc(c.d) << kChunkLog2) | (tx_unorm16(c.tx) << 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t e0 = c.e[j];
+        const float wyz = ((j & 1) ? c.ty : 1.0f - c.ty) * ((j & 2) ? c.tz : 1.0f - c.tz);
+        const float w0 = split ? fine_weight(c, j, 0) : wyz;
+        v4[j] = act;
+        bk4[j] = e0 >> kChunkLog2;
+        w4[j] = (e0 & (kChunk - 1)) | (split ? 0u : code);
+        val4[j] = make_float2(w0 * gv.x, w0 * gv.y);
+      }
+      place(v4, bk4, w4, val4);
+      if (__ballot(act && split)) {  // pairs spanning two chunks: the second corners on their own
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t e1 = c.e[j] ^ c.d;
+          const float w1 = fine_weight(c, j, 1);
+          v4[j] = act && split;
+          bk4[j] = e1 >> kChunkLog2;
+          w4[j] = e1 & (kChunk - 1);
+          val4[j] = make_float2(w1 * gv.x, w1 * gv.y);
+        }
+        place(v4, bk4, w4, val4);
+      }
+    } else {  // coherent: corner k summed over the run of lanes that share it, 4 corners at a time
+      Corners c;
+      level_corners(lv, x, y, z, c);
+      const uint32_t off = lv.offset;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int k = 4 * h + kk;
+          const uint32_t idx = in ? c.idx[k] : 0xFFFFFFFFu;
+          float v0 = c.w[k] * gv.x, v1 = c.w[k] * gv.y;
+          const RunInfo ri = lane_runs_dpp(idx);
+          run_sum_dpp(ri, v0, v1);
+          v4[kk] = inr && ri.tail;
+          const uint32_t e = v4[kk] ? idx - off : 0u;
+          bk4[kk] = e >> kChunkLog2;
+          w4[kk] = e & (kChunk - 1);
+          val4[kk] = make_float2(v0, v1);
+        }
+        place(v4, bk4, w4, val4);
+      }
+    }
+    m = wave_max_nonneg(m);
+    if (lane == 0) sm.wmax[sbuf][wid] = m;
+    if (threadIdx.x < NB) sm.ctr[sbuf ^ 1][threadIdx.x] = 0u;  // level l + 1's counters (last used by l - 1)
+    if (l >= 1) copy_out(l - 1);
+    lds_barrier();
+  }
+  copy_out(NL - 1);
 }
 
 constexpr size_t kScatterLds = (size_t)kCap * sizeof(RecVal) + kMaxChunksPerLevel * 8 + (size_t)kCap * 4 + kMaxChunksPerLevel * 4 +
@@ -603,7 +845,20 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
     const uint32_t m = a.merge_levels, L = d->n_levels;
     bool all_fine = true;
     for (uint32_t l = m; l < L; ++l) all_fine = all_fine && a.lv[l].fine;
-#ifndef LNR_EXP_SPLIT_SCATTER
+#if !defined(LNR_EXP_SPLIT_SCATTER) && !defined(LNR_EXP_SCATTER_PER_LEVEL)
+    uint32_t maxnb = 0;
+    for (uint32_t l = 0; l < L; ++l) maxnb = std::max(maxnb, a.bucket_base[l + 1] - a.bucket_base[l]);
+    // the reference's grids: 16 levels (base 16, scale 2), 2^18 (sigma) or 2^19 (colour) entries
+    const bool rows = L == 16 && all_fine && 8 * n * (int64_t)L + 2 < (int64_t(1) << 32);
+    if (rows && m == 5 && maxnb <= 64) {
+      hipLaunchKernelGGL((k_bwd_scatter_rows<PosFn, 16, 5, 64>), dim3((unsigned)w.n_sb), dim3(kSB), 0, st, a, pos, n,
+                         de, stride, w, skip_zero);
+      hipLaunchKernelGGL((k_bwd_scatter_overflow<PosFn>), dim3((unsigned)((w.n_sb * L + kSB - 1) / kSB)), dim3(kSB),
+                         kScatterLds, st, a, pos, n, de, stride, w, skip_zero);
+    } else
+      hipLaunchKernelGGL((k_bwd_scatter<PosFn, kLevelsAny>), dim3((unsigned)(w.n_sb * L)), dim3(kSB), kScatterLds, st,
+                         a, pos, n, de, stride, w, 0u, skip_zero);
+#elif defined(LNR_EXP_SCATTER_PER_LEVEL)
     (void)m;
     (void)all_fine;
     hipLaunchKernelGGL((k_bwd_scatter<PosFn, kLevelsAny>), dim3((unsigned)(w.n_sb * L)), dim3(kSB), kScatterLds, st, a,
