@@ -91,7 +91,8 @@ def test_hashgrid_fwd_rays_matches_positions(L):
     assert np.all(np.abs(got - ref) <= 1.01 * ulp)
 
 
-@pytest.mark.parametrize("variant", ["bucketed", "bucketed_fwd_counts", "atomic"])
+@pytest.mark.parametrize("variant", ["bucketed", "bucketed_fwd_counts", "atomic", "bucketed_scattered",
+                                     "bucketed_scattered_fwd_counts"])
 def test_hashgrid_bwd(L, variant):
     rng = np.random.default_rng(2)
     # a few "rays" of sorted samples so the coarse-level run merge is exercised
@@ -103,6 +104,11 @@ def test_hashgrid_bwd(L, variant):
     pos = (((o[:, None] + dr[:, None] * t[:, :, None]) + 1) / 2).reshape(-1, 3).astype(np.float32)
     n = R * S - 77  # ragged tail
     pos = pos[:n]
+    if "scattered" in variant:
+        # unsorted positions: no runs merge, coherent rows carry 8 records per sample, more than the
+        # level-looped scatter stages, so every coherent (row, level) takes the overflow pass
+        pos = rng.uniform(0.0, 1.0, (n, 3)).astype(np.float32)
+        variant = variant.replace("_scattered", "")
     lay = ohg.GridLayout(16, 2, 18, 16)
     d = L.grid_desc(16, 2, 18, 16)
     denc = rng.normal(0, 1, (n, 32)).astype(np.float32)
