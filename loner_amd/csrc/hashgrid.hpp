@@ -137,18 +137,39 @@ struct PosFromRays {
 struct Corners {
   uint32_t idx[8];
   float w[8];
-  float tx, ty, tz;  // cell fractions (the backward's x-pair records split by tx)
+  float tx, ty, tz;     // cell fractions (the backward's x-pair records split by tx)
+  uint32_t cx, cy, cz;  // the cell (coherent levels merge runs of lanes in one cell)
 };
 
+// POW2: the caller guarantees a power-of-two table size (size_mask != 0), so no modulo path.
+template <bool POW2 = false>
 __device__ __forceinline__ void level_corners(const LevelParams& p, float x, float y, float z, Corners& c) {
   // tcnn pos_fract: pos = fmaf(scale, x, 0.5); cell = floor(pos); frac = pos - cell
   float px = fmaf(p.scale, x, 0.5f), py = fmaf(p.scale, y, 0.5f), pz = fmaf(p.scale, z, 0.5f);
   float fx = floorf(px), fy = floorf(py), fz = floorf(pz);
   uint32_t cx = (uint32_t)(int)fx, cy = (uint32_t)(int)fy, cz = (uint32_t)(int)fz;
   float tx = px - fx, ty = py - fy, tz = pz - fz;
+  c.cx = cx;
+  c.cy = cy;
+  c.cz = cz;
   c.tx = tx;
   c.ty = ty;
   c.tz = tz;
+  // grid_index per corner from per-axis terms formed once: the hash XORs x with y*P1 and z*P2, the
+  // dense walk adds x, y*res and z*res^2 (same values as grid_index, fewer multiplies)
+  uint32_t ty0, ty1, tz0, tz1;
+  if (p.hashed) {
+    ty0 = cy * 2654435761u;
+    tz0 = cz * 805459861u;
+    ty1 = ty0 + 2654435761u;
+    tz1 = tz0 + 805459861u;
+  } else {
+    const uint32_t r2 = p.res * p.res;
+    ty0 = cy * p.res;
+    tz0 = cz * r2;
+    ty1 = ty0 + p.res;
+    tz1 = tz0 + r2;
+  }
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int bx = k & 1, by = (k >> 1) & 1, bz = (k >> 2) & 1;
@@ -156,7 +177,9 @@ __device__ __forceinline__ void level_corners(const LevelParams& p, float x, flo
     w *= by ? ty : 1.0f - ty;
     w *= bz ? tz : 1.0f - tz;
     c.w[k] = w;
-    c.idx[k] = p.offset + grid_index(p, cx + bx, cy + by, cz + bz);
+    const uint32_t xx = cx + bx, yy = by ? ty1 : ty0, zz = bz ? tz1 : tz0;
+    const uint32_t idx = p.hashed ? (xx ^ yy ^ zz) : (xx + yy + zz);
+    c.idx[k] = p.offset + ((POW2 || p.size_mask) ? (idx & p.size_mask) : (idx % p.size));
   }
 }
 
@@ -260,6 +283,79 @@ __device__ __forceinline__ void run_sum_dpp(const RunInfo& ri, float& v0, float&
   LNR_SEG_STEP(0x142, 0xA, (lane & 16) && h < (lane & ~15))      // row_bcast:15 -> rows 1, 3
   LNR_SEG_STEP(0x143, 0xC, lane >= 32 && h < 32)                 // row_bcast:31 -> rows 2, 3
 #undef LNR_SEG_STEP
+}
+
+// Runs of consecutive lanes in one cell (coherent levels: consecutive samples of a ray): every
+// corner index of such lanes is equal, so one run detection serves all 8 corners.  Lanes without a
+// sample (in = false) are runs of their own.
+__device__ __forceinline__ RunInfo cell_runs_dpp(bool in, uint32_t cx, uint32_t cy, uint32_t cz) {
+  const int lane = threadIdx.x & 63;
+  // wave_shr:1 (0x138): lane i reads lane i - 1 (lane 0 keeps "old", and is a head anyway)
+  const uint32_t px = (uint32_t)__builtin_amdgcn_update_dpp((int)~cx, (int)cx, 0x138, 0xF, 0xF, false);
+  const uint32_t py = (uint32_t)__builtin_amdgcn_update_dpp((int)~cy, (int)cy, 0x138, 0xF, 0xF, false);
+  const uint32_t pz = (uint32_t)__builtin_amdgcn_update_dpp((int)~cz, (int)cz, 0x138, 0xF, 0xF, false);
+  const int pin = __builtin_amdgcn_update_dpp(0, in ? 1 : 0, 0x138, 0xF, 0xF, false);
+  const bool head = (lane == 0) || !in || !pin || px != cx || py != cy || pz != cz;
+  RunInfo ri;
+  ri.heads = __ballot(head);
+  ri.head_lane = 63 - __clzll(ri.heads & ((2ull << lane) - 1ull));
+  ri.tail = (lane == 63) || ((ri.heads >> (lane + 1)) & 1ull);
+  return ri;
+}
+
+// Segmented inclusive sum of N values over runs sharing one RunInfo: the run's tail lane ends with
+// the run totals.  Each step's lane condition is computed once for all N values, and only the steps
+// the wave's runs need are taken: row shifts up to the longest within-row run prefix, the row
+// broadcasts only when a run crosses a 16-lane row boundary.  Fixed order: deterministic.
+template <int N>
+__device__ __forceinline__ void run_sum_dpp_n(const RunInfo& ri, float (&v)[N]) {
+  const int lane = threadIdx.x & 63;
+  const int h = ri.head_lane;
+  const int rs = lane & ~15;
+  // longest distance from a lane back to its run's first lane in the same row (0..15), wave-uniform
+  int d = lane - (h > rs ? h : rs);
+  d = max(d, __builtin_amdgcn_update_dpp(0, d, 0x111, 0xF, 0xF, true));
+  d = max(d, __builtin_amdgcn_update_dpp(0, d, 0x112, 0xF, 0xF, true));
+  d = max(d, __builtin_amdgcn_update_dpp(0, d, 0x114, 0xF, 0xF, true));
+  d = max(d, __builtin_amdgcn_update_dpp(0, d, 0x118, 0xF, 0xF, true));
+  d = max(d, __builtin_amdgcn_update_dpp(0, d, 0x142, 0xA, 0xF, false));
+  d = max(d, __builtin_amdgcn_update_dpp(0, d, 0x143, 0xC, 0xF, false));
+  const int dmax = __builtin_amdgcn_readlane(d, 63);
+  const bool cross = (ri.heads & 0x0001000100010000ull) != 0x0001000100010000ull;
+  // every row enabled and bound_ctrl: a source lane outside the shift reads 0 (no "old" operand to
+  // initialise); the lane conditions exclude the rows a broadcast does not address
+#define LNR_SEG_STEP_N(CTRL, RMASK, COND)                                                  \
+  {                                                                                        \
+    float q[N];                                                                            \
+    _Pragma("unroll") for (int k = 0; k < N; ++k) q[k] =                                   \
+        __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[k]), CTRL, 0xF, 0xF, true)); \
+    if (COND) {                                                                            \
+      _Pragma("unroll") for (int k = 0; k < N; ++k) v[k] += q[k];                          \
+    }                                                                                      \
+  }
+  if (dmax >= 1) LNR_SEG_STEP_N(0x111, 0xF, lane - 1 >= h)
+  if (dmax >= 2) LNR_SEG_STEP_N(0x112, 0xF, lane - 2 >= h)
+  if (dmax >= 4) LNR_SEG_STEP_N(0x114, 0xF, lane - 4 >= h)
+  if (dmax >= 8) LNR_SEG_STEP_N(0x118, 0xF, lane - 8 >= h)
+  if (cross) {
+    LNR_SEG_STEP_N(0x142, 0xA, (lane & 16) && h < rs)  // row_bcast:15 -> rows 1, 3
+    LNR_SEG_STEP_N(0x143, 0xC, lane >= 32 && h < 32)   // row_bcast:31 -> rows 2, 3
+  }
+#undef LNR_SEG_STEP_N
+}
+
+// Coherent-level records of one lane: corner k's (g0, g1) contributions summed over the lane's run;
+// valid at the run's tail lanes (in).  The forward's histogram, the scatters and the count kernel
+// all merge this way, so their record counts agree.
+__device__ __forceinline__ void coherent_run_values(const Corners& c, bool in, float g0, float g1, RunInfo& ri,
+                                                    float (&v)[16]) {
+  ri = cell_runs_dpp(in, c.cx, c.cy, c.cz);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    v[2 * k] = c.w[k] * g0;
+    v[2 * k + 1] = c.w[k] * g1;
+  }
+  run_sum_dpp_n<16>(ri, v);
 }
 
 // The same in int64 (exact and associative: the result does not depend on the record order).
@@ -456,11 +552,10 @@ __device__ __forceinline__ void count_block_records(const GridArgs& a, uint32_t 
                                                     bool act, uint32_t* hist, const BwdWorkspace& ws) {
   const uint32_t off = a.lv[l].offset;
   if (l < a.merge_levels) {
+    const RunInfo ri = cell_runs_dpp(in, c.cx, c.cy, c.cz);  // every lane must take part in the ballot
+    if (in && ri.tail) {  // run tails only: few lanes
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint32_t idx = in ? c.idx[k] : 0xFFFFFFFFu;
-      const RunInfo ri = lane_runs_dpp(idx);  // every lane must take part in the ballot
-      if (in && ri.tail) atomicAdd(&hist[(idx - off) >> kChunkLog2], 1u);  // run tails only: few lanes
+      for (int k = 0; k < 8; ++k) atomicAdd(&hist[(c.idx[k] - off) >> kChunkLog2], 1u);
     }
   } else if (act) {
 #pragma unroll

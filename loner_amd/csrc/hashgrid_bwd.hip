@@ -325,17 +325,16 @@ __device__ __forceinline__ void scatter_row_level(const GridArgs& a, const PosFn
     const uint32_t off = lv.offset;
     if (kind == kLevelsCoherent) {  // corner k summed over the run of lanes that share it
       staged = start[nb] <= (uint32_t)kCap;
+      RunInfo ri;
+      float v[16];
+      coherent_run_values(c, in, g.x, g.y, ri, v);
+      const bool valid = in && ri.tail;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const uint32_t idx = in ? c.idx[k] : 0xFFFFFFFFu;
-        float v0 = c.w[k] * g.x, v1 = c.w[k] * g.y;
-        const RunInfo ri = lane_runs_dpp(idx);
-        run_sum_dpp(ri, v0, v1);
-        const bool valid = in && ri.tail;
-        const uint32_t e = valid ? idx - off : 0u;
+        const uint32_t e = valid ? c.idx[k] - off : 0u;
         const uint32_t bk = e >> kChunkLog2;
         const uint32_t rank = valid ? atomicAdd(&rank_ctr[bk], 1u) : 0u;  // run tails only: few lanes
-        place(valid, bk, rank, e & (kChunk - 1), make_float2(v0, v1));
+        place(valid, bk, rank, e & (kChunk - 1), make_float2(v[2 * k], v[2 * k + 1]));
       }
     } else {  // generic non-coherent levels (configurations without power-of-two hashed tables)
       row_starts();
@@ -443,13 +442,13 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter_o
 // Same records, counts and blockmax as k_bwd_scatter.
 constexpr int kRowsCap = 2176;  // 4.25 records per sample: fine rows hold 4 + the rare split pairs
 template <int NL, int NB>
-struct RowsLds {
-  uint4 stage[2][kRowsCap];   // staged records {word, global slot, v0, v1}, bucket order
+struct RowsLds {  // the small tables first: their addresses fit the 16-bit LDS instruction offset
   uint2 sg[NL][NB];           // per level and bucket: {start in the stage, global slot of the run}
   uint32_t total[NL];         // records of the row at each level
   uint32_t ctr[2][NB];        // rank counters
   float wmax[2][kSB / 64];
   LevelParams lv[NL];         // the level table (kernel arguments indexed per level would be loads)
+  uint4 stage[2][kRowsCap];   // staged records {word, global slot, v0, v1}, bucket order
 };
 static_assert(sizeof(RecVal) == 8, "the level-looped scatter stages fp32 record values");
 
@@ -554,23 +553,23 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ 
     const bool act = inr && (!skip_zero || gv.x != 0.f || gv.y != 0.f);
     float m = 0.f;
     // rank (returning LDS atomics) and place: all start reads, then all atomics, then all writes
-    auto place = [&](const bool (&valid)[4], const uint32_t (&bk)[4], const uint32_t (&word)[4],
-                     const float2 (&val)[4]) {
-      uint2 s4[4];
-      uint32_t rank[4];
+    // (one lane-level branch for the 4 records: they share their validity)
+    auto place = [&](bool valid, const uint32_t (&bk)[4], const uint32_t (&word)[4], const float2 (&val)[4]) {
+      if (valid) {
+        uint2 s4[4];
+        uint32_t rank[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) s4[k] = valid[k] ? sgl[bk[k]] : make_uint2(0u, 0u);
+        for (int k = 0; k < 4; ++k) s4[k] = sgl[bk[k]];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) rank[k] = valid[k] ? atomicAdd(&ctr[bk[k]], 1u) : 0u;
+        for (int k = 0; k < 4; ++k) rank[k] = atomicAdd(&ctr[bk[k]], 1u);
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (valid[k]) {
+        for (int k = 0; k < 4; ++k) {
           m = fmaxf(m, fmaxf(fabsf(val[k].x), fabsf(val[k].y)));
           sm.stage[sbuf][s4[k].x + rank[k]] = make_uint4(word[k], s4[k].y + rank[k], __float_as_uint(val[k].x),
                                                          __float_as_uint(val[k].y));
         }
+      }
     };
-    bool v4[4];
     uint32_t bk4[4], w4[4];
     float2 val4[4];
     if (l >= NM) {  // fine: one record per x-pair (hashgrid.hpp "Backward records")
@@ -583,44 +582,41 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ 
         const uint32_t e0 = c.e[j];
         const float wyz = ((j & 1) ? c.ty : 1.0f - c.ty) * ((j & 2) ? c.tz : 1.0f - c.tz);
         const float w0 = split ? fine_weight(c, j, 0) : wyz;
-        v4[j] = act;
         bk4[j] = e0 >> kChunkLog2;
         w4[j] = (e0 & (kChunk - 1)) | (split ? 0u : code);
         val4[j] = make_float2(w0 * gv.x, w0 * gv.y);
       }
-      place(v4, bk4, w4, val4);
+      place(act, bk4, w4, val4);
       if (__ballot(act && split)) {  // pairs spanning two chunks: the second corners on their own
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const uint32_t e1 = c.e[j] ^ c.d;
           const float w1 = fine_weight(c, j, 1);
-          v4[j] = act && split;
           bk4[j] = e1 >> kChunkLog2;
           w4[j] = e1 & (kChunk - 1);
           val4[j] = make_float2(w1 * gv.x, w1 * gv.y);
         }
-        place(v4, bk4, w4, val4);
+        place(act && split, bk4, w4, val4);
       }
     } else {  // coherent: corner k summed over the run of lanes that share it, 4 corners at a time
       Corners c;
-      level_corners(lv, x, y, z, c);
+      level_corners<true>(lv, x, y, z, c);
       const uint32_t off = lv.offset;
+      RunInfo ri;
+      float v[16];
+      coherent_run_values(c, in, gv.x, gv.y, ri, v);
+      const bool valid = inr && ri.tail;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
           const int k = 4 * h + kk;
-          const uint32_t idx = in ? c.idx[k] : 0xFFFFFFFFu;
-          float v0 = c.w[k] * gv.x, v1 = c.w[k] * gv.y;
-          const RunInfo ri = lane_runs_dpp(idx);
-          run_sum_dpp(ri, v0, v1);
-          v4[kk] = inr && ri.tail;
-          const uint32_t e = v4[kk] ? idx - off : 0u;
+          const uint32_t e = c.idx[k] - off;
           bk4[kk] = e >> kChunkLog2;
           w4[kk] = e & (kChunk - 1);
-          val4[kk] = make_float2(v0, v1);
+          val4[kk] = make_float2(v[2 * k], v[2 * k + 1]);
         }
-        place(v4, bk4, w4, val4);
+        place(valid, bk4, w4, val4);
       }
     }
     m = wave_max_nonneg(m);
@@ -849,7 +845,9 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
     uint32_t maxnb = 0;
     for (uint32_t l = 0; l < L; ++l) maxnb = std::max(maxnb, a.bucket_base[l + 1] - a.bucket_base[l]);
     // the reference's grids: 16 levels (base 16, scale 2), 2^18 (sigma) or 2^19 (colour) entries
-    const bool rows = L == 16 && all_fine && 8 * n * (int64_t)L + 2 < (int64_t(1) << 32);
+    bool pow2 = true;
+    for (uint32_t l = 0; l < L; ++l) pow2 = pow2 && a.lv[l].size_mask != 0;
+    const bool rows = L == 16 && all_fine && pow2 && 8 * n * (int64_t)L + 2 < (int64_t(1) << 32);
     if (rows && m == 5 && maxnb <= 64) {
       hipLaunchKernelGGL((k_bwd_scatter_rows<PosFn, 16, 5, 64>), dim3((unsigned)w.n_sb), dim3(kSB), 0, st, a, pos, n,
                          de, stride, w, skip_zero);
