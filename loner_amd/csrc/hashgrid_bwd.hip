@@ -645,6 +645,27 @@ __global__ void __launch_bounds__(256) k_bwd_level_max(BwdWorkspace ws) {
 
 constexpr int kAccumThreads = 1024;
 
+// Fixed-point exponent of bucket b: |record| < 2^E (the level's max) and at most cnt records in the
+// bucket, so every value, and every partial or total sum, stays below 2^50 in magnitude: inside the
+// exact-integer range of the double-precision conversion below.  The unit is 2^(lg cnt + E - 50),
+// about 2^-32 of the level maximum at C2's bucket sizes.
+__device__ __forceinline__ int bucket_k2(const BwdWorkspace& ws, uint32_t l, uint32_t b) {
+  int E;
+  frexpf(ws.level_max[l], &E);
+  const uint64_t bcnt = ws.seg_start[b + 1] - ws.seg_start[b];
+  const int lg = 64 - __clzll((long long)(bcnt > 0 ? bcnt : 1));  // ceil-ish log2(cnt + 1)
+  const int k2 = 50 - lg - E;
+  return k2 > 120 ? 120 : (k2 < -120 ? -120 : k2);
+}
+
+// round(x) as int64 for |x| < 2^51: x + 1.5 2^52 in double places the rounded integer in the low
+// mantissa bits, and the constant's low word is 0, so only the high word needs the subtraction.
+__device__ __forceinline__ unsigned long long fixed_i64(float x) {
+  const double d = (double)x + 6755399441055744.0;
+  const unsigned long long b = (unsigned long long)__double_as_longlong(d);
+  return b - 0x4338000000000000ull;
+}
+
 #ifndef LNR_ACCUM_WAVES_PER_EU
 #define LNR_ACCUM_WAVES_PER_EU 8
 #endif
@@ -678,75 +699,44 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
     const uint32_t chunk = b - a.bucket_base[l];
     const uint32_t ent0 = chunk * kChunk;
     const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
-    // fixed-point scale: |v| < 2^E, at most `cnt` records in the whole bucket -> |sum| < 2^62
-    // (one scale per bucket, so split buckets' int64 partials add exactly)
-    int E;
-    frexpf(ws.level_max[l], &E);
-    const uint64_t bcnt = ws.seg_start[b + 1] - ws.seg_start[b];
-    const uint64_t cnt = bcnt > 0 ? bcnt : 1;
-    const int lg = 64 - __clzll((long long)cnt);  // ceil-ish log2(cnt + 1)
-    int k2 = 62 - lg - E;
-    k2 = k2 > 120 ? 120 : (k2 < -120 ? -120 : k2);
+    const int k2 = bucket_k2(ws, l, b);  // one scale per bucket: split buckets' partials add exactly
     const float scale = ldexpf(1.f, k2);
     LNR_STAMP(t0);
     for (int t = threadIdx.x; t < 2 * kChunk; t += blockDim.x) acc[t] = 0ull;
     lds_barrier();
     LNR_STAMP(t1);
-    const bool coherent = l < a.merge_levels;
-    // 2 records per lane per load (8-B words, 8-B packed values or 16-B fp32), 4 loads in flight: 4 K records per
-    // workgroup trip; a lane's two records are handled as two lane-ordered streams (merging
-    // equal entries of coherent levels is an optimisation only: the int64 sums are exact)
+    // 2 records per lane per load (8-B words, 16-B fp32 value pairs), LNR_ACCUM_LOADS loads in flight;
+    // a pair record (p > 0) adds (1 - tx) v to corner e0 and tx v to e1 = e0 ^ (2^p - 1), a single
+    // record (p = 0, tx = 0) adds v to e0.  int64 sums: the result does not depend on the order.
     const uint64_t beg2 = beg & ~1ull;
     for (uint64_t rb = beg2 + 2 * (threadIdx.x & ~63u); rb < end; rb += 2 * LNR_ACCUM_LOADS * kAccumThreads) {
       uint2 qw[LNR_ACCUM_LOADS];
-#ifndef LNR_REC_PACKED
       float4 qv[LNR_ACCUM_LOADS];
-#else
-      u32x2 qp[LNR_ACCUM_LOADS];  // unpacked where consumed, so the loads stay in flight together
-#endif
 #pragma unroll
       for (int u = 0; u < LNR_ACCUM_LOADS; ++u) {
         const uint64_t rr = rb + 2 * lane + (uint64_t)u * 2 * kAccumThreads;
         const uint64_t rc = rr < end ? rr : beg2;  // unconditional loads: no branch to wait at
         const u32x2 w2 = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(&ws.rec_w[rc]));
-#ifndef LNR_REC_PACKED
         const f32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(&ws.rec_v[rc]));
         qv[u] = make_float4(v4.x, v4.y, v4.z, v4.w);
-#else
-        qp[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(&ws.rec_v[rc]));
-#endif
         qw[u] = make_uint2(rr < beg || rr >= end ? kRecNone : w2.x, rr + 1 >= end ? kRecNone : w2.y);
       }
 #pragma unroll
       for (int u = 0; u < 2 * LNR_ACCUM_LOADS; ++u) {
         const uint32_t w = (u & 1) ? qw[u >> 1].y : qw[u >> 1].x;
-#ifndef LNR_REC_PACKED
-        const float v0 = (u & 1) ? qv[u >> 1].z : qv[u >> 1].x;
-        const float v1 = (u & 1) ? qv[u >> 1].w : qv[u >> 1].y;
-#else
-        const float2 vv = unpack_rec((u & 1) ? qp[u >> 1].y : qp[u >> 1].x);
-        const float v0 = vv.x, v1 = vv.y;
-#endif
-        const bool ok = w != kRecNone;
-        const uint32_t e0 = ok ? (w & (kChunk - 1)) : 0xFFFFFFFFu;
-        if (coherent) {  // single-corner records arriving in runs of equal entries
-          long long i0 = ok ? __float2ll_rn(v0 * scale) : 0, i1 = ok ? __float2ll_rn(v1 * scale) : 0;
-          const RunInfo ri = lane_runs(e0);
-          run_sum_i64(ri, i0, i1);
-          if (ok && ri.tail) {
-            atomicAdd(&acc[e0], (unsigned long long)i0);
-            atomicAdd(&acc[1 * kChunk + e0], (unsigned long long)i1);
-          }
-        } else if (ok) {
+        if (w != kRecNone) {
+          const float v0 = ((u & 1) ? qv[u >> 1].z : qv[u >> 1].x) * scale;
+          const float v1 = ((u & 1) ? qv[u >> 1].w : qv[u >> 1].y) * scale;
+          const uint32_t e0 = w & (kChunk - 1);
           const uint32_t p = (w >> kChunkLog2) & 15u;
           const float tx = (float)(w >> 16) * kInvU16;  // 0 for single-corner records
           const float s0 = 1.0f - tx;
-          atomicAdd(&acc[e0], (unsigned long long)__float2ll_rn(s0 * v0 * scale));
-          atomicAdd(&acc[1 * kChunk + e0], (unsigned long long)__float2ll_rn(s0 * v1 * scale));
+          atomicAdd(&acc[e0], fixed_i64(s0 * v0));
+          atomicAdd(&acc[kChunk + e0], fixed_i64(s0 * v1));
           if (p) {
             const uint32_t e1 = e0 ^ ((1u << p) - 1u);
-            atomicAdd(&acc[e1], (unsigned long long)__float2ll_rn(tx * v0 * scale));
-            atomicAdd(&acc[1 * kChunk + e1], (unsigned long long)__float2ll_rn(tx * v1 * scale));
+            atomicAdd(&acc[e1], fixed_i64(tx * v0));
+            atomicAdd(&acc[kChunk + e1], fixed_i64(tx * v1));
           }
         }
       }
@@ -784,14 +774,7 @@ __global__ void __launch_bounds__(256) k_bwd_finalize(GridArgs a, BwdWorkspace w
   while (l + 1 < a.n_levels && a.bucket_base[l + 1] <= b) ++l;
   const uint32_t ent0 = (b - a.bucket_base[l]) * kChunk;
   const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
-  // the accumulate kernel's per-bucket scale
-  int E;
-  frexpf(ws.level_max[l], &E);
-  const uint64_t bcnt = ws.seg_start[b + 1] - ws.seg_start[b];
-  const int lg = 64 - __clzll((long long)(bcnt > 0 ? bcnt : 1));
-  int k2 = 62 - lg - E;
-  k2 = k2 > 120 ? 120 : (k2 < -120 ? -120 : k2);
-  const float inv = ldexpf(1.f, -k2);
+  const float inv = ldexpf(1.f, -bucket_k2(ws, l, b));  // the accumulate kernel's per-bucket scale
   const long long* src = ws.partial + (int64_t)ws.part_pre[b] * (2 * kChunk);
   float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0);
   for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) {

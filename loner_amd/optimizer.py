@@ -195,8 +195,6 @@ class Optimizer:
         eng, n_local = self._engine_for(window.n_slots)
         out = None
         if fixed:
-            if self._world > 1:
-                raise NotImplementedError("FIXED ray selection is single-GPU here (its batch size varies)")
             given, num_iterations = self._fixed_schedule(scans, window)
         for it in range(num_iterations):
             eng.lr_factor = self._lr_gamma ** it  # ExponentialLR stepped after every iteration
@@ -282,5 +280,19 @@ class Optimizer:
         key = L.step_key(eng.seed, self._global_step)
         rays, depth, valid, _, far_ref = window.build(key, 0, window.n_slots, given=given.to(dev))
         sel = keep.to(dev) & valid.bool()
-        rays, depth = rays[sel].contiguous(), depth[sel].contiguous()
-        return eng.step(rays, depth, self._global_step, it, scale=window.scale, far_ref=far_ref)
+        rays, depth = rays[sel], depth[sel]
+        n_glob = rays.shape[0]
+        if self._world > 1:
+            # data parallel: every rank builds the same FIXED batch (one generator, one seed), so its
+            # size is known everywhere; all-reducing the kept counts checks that, and rank r steps the
+            # contiguous slice shard_range(n, r, world) with its draws keyed by global ray index
+            from .shard import shard_range
+            cnt = torch.tensor([float(n_glob)], device=dev)
+            self._allreduce(cnt)
+            if int(cnt.item()) != n_glob * self._world:
+                raise RuntimeError("FIXED ray selection diverged across ranks")
+            s0, s1 = shard_range(n_glob, self._rank, self._world)
+            rays, depth = rays[s0:s1], depth[s0:s1]
+            eng.ray_offset = s0
+        return eng.step(rays.contiguous(), depth.contiguous(), self._global_step, it, scale=window.scale,
+                        far_ref=far_ref, n_rays_global=n_glob)

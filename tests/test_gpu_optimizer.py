@@ -116,19 +116,29 @@ def test_camera_phase_and_checkpoint(L, tmp_path):
     assert torch.equal(cs2.shadow, opt.color.shadow)  # fp16 round trip of the fp16 shadow
 
 
-def _dp_worker(rank, world, port, out):
+def _dp_window(strategy):
+    """The DP test's window; FIXED runs floor(points / 64) iterations, so its scans are cut to 300
+    points (4 iterations): long runs amplify summation-order differences through Adam."""
+    scans, cube = _window("forest", 2)
+    if strategy == "FIXED":
+        scans = [dict(s, directions=s["directions"][:, :300].contiguous(), distances=s["distances"][:300].contiguous())
+                 for s in scans]
+    return scans, cube
+
+
+def _dp_worker(rank, world, port, out, strategy="MASK"):
     import os
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     from loner_amd.optimizer import Optimizer
-    scans, cube = _window("forest", 2)
+    scans, cube = _dp_window(strategy)
 
     def allreduce(t, async_op=False):
         return dist.all_reduce(t, async_op=async_op)
 
-    opt = Optimizer(_settings("MASK", n_it=4, sky=8), None, cube, "cuda:0", seed=2, allreduce=allreduce, rank=rank,
+    opt = Optimizer(_settings(strategy, n_it=4, sky=8), None, cube, "cuda:0", seed=2, allreduce=allreduce, rank=rank,
                     world=world)
     opt.iterate_optimizer(scans)
     torch.cuda.synchronize()
@@ -137,9 +147,11 @@ def _dp_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_optimizer_data_parallel_gloo(L, tmp_path):
+@pytest.mark.parametrize("strategy", ["MASK", "FIXED"])
+def test_optimizer_data_parallel_gloo(L, tmp_path, strategy):
     """Optimizer(allreduce, rank, world): two gloo ranks on the window's two ray shards give the same
-    map on both replicas, and the single-GPU map to a tolerance (summation order, OGM atomics)."""
+    map on both replicas, and the single-GPU map to a tolerance (summation order, OGM atomics).
+    FIXED: each rank takes its slice of the iteration's FIXED batch (optimizer.py:269,380)."""
     import socket
     import torch.multiprocessing as mp
     from loner_amd.optimizer import Optimizer
@@ -147,7 +159,7 @@ def test_optimizer_data_parallel_gloo(L, tmp_path):
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
-    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, str(tmp_path), strategy)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
@@ -155,8 +167,9 @@ def test_optimizer_data_parallel_gloo(L, tmp_path):
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     p0, p1 = np.load(tmp_path / "p0.npy"), np.load(tmp_path / "p1.npy")
     assert np.array_equal(p0, p1)
-    scans, cube = _window("forest", 2)
-    opt = Optimizer(_settings("MASK", n_it=4, sky=8), None, cube, "cuda:0", seed=2)
+    scans, cube = _dp_window(strategy)
+    opt = Optimizer(_settings(strategy, n_it=4, sky=8), None, cube, "cuda:0", seed=2)
     opt.iterate_optimizer(scans)
     ref = opt.state.params.cpu().numpy()
+    assert opt._global_step == 4
     assert np.linalg.norm(p0 - ref) / np.linalg.norm(ref) < 1e-4
