@@ -29,6 +29,7 @@ c_i64 = ctypes.c_int64
 c_i32 = ctypes.c_int32
 c_u32 = ctypes.c_uint32
 c_f = ctypes.c_float
+c_d = ctypes.c_double
 
 
 class GridDesc(ctypes.Structure):
@@ -139,7 +140,7 @@ _SIGNATURES = {
     "lnr_count_opaque": (ctypes.c_int, [c_p, c_i64, c_f, c_p, c_p, c_p]),
     "lnr_build_lidar_rays": (ctypes.c_int, [ctypes.POINTER(RayWindowDesc), c_i32, c_p, c_u32, c_i64, c_i64, c_p, c_p,
                                             c_p, c_p, c_p, c_p]),
-    "lnr_adam_step": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i32, c_f, c_f, c_f, c_f, c_p]),
+    "lnr_adam_step": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i32, c_d, c_d, c_d, c_d, c_p]),
     "lnr_ogm_workspace_words": (c_i64, [c_i32]),
     "lnr_ogm_update": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_f, c_f, c_p, c_p, c_i64, c_i32, c_p]),
     "lnr_ogm_grad": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_i64, c_i32, c_p]),

@@ -190,19 +190,22 @@ static unsigned grid1d(int64_t n, int64_t cap = 1 << 20) {
 using namespace lnr;
 
 extern "C" int lnr_adam_step(float* param, uint16_t* shadow, const float* grad, float* m, float* v, int64_t n,
-                             int32_t step, float lr, float beta1, float beta2, float eps, void* stream) {
+                             int32_t step, double lr, double beta1, double beta2, double eps, void* stream) {
   LNR_REQUIRE(n >= 0 && step >= 1, "lnr_adam_step: n=%lld step=%d", (long long)n, step);
   if (n == 0) return LNR_OK;
   LNR_REQUIRE(param && grad && m && v, "lnr_adam_step: null pointer");
   LNR_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) % 16 == 0 &&
                   (shadow == nullptr || (uintptr_t)shadow % 8 == 0),
               "lnr_adam_step: buffers must be 16-byte aligned");
-  const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
-  const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
-  const float step_size = (float)((double)lr / bc1);
+  // the hyper-parameters arrive as doubles (Python floats) and every derived scalar is formed in double
+  // before its single rounding to fp32, as torch.optim.Adam forms them (1 - beta2 from the float 0.999f
+  // would be 1.3e-5 off)
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  const float step_size = (float)(lr / bc1);
   const float bc2_sqrt = (float)std::sqrt(bc2);
   hipLaunchKernelGGL(k_adam, dim3(grid1d(n / 4, 8192)), dim3(256), 0, as_stream(stream), param, shadow, grad, m, v, n,
-                     (float)(1.0 - (double)beta1), beta2, (float)(1.0 - (double)beta2), step_size, bc2_sqrt, eps);
+                     (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), step_size, bc2_sqrt, (float)eps);
   LNR_RETURN_LAUNCH("lnr_adam_step");
 }
 

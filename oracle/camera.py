@@ -45,6 +45,21 @@ def build_camera_rays(dirs, image, pixels, pose3x4, scale, shift, r_min, width):
     return rays, inten
 
 
+def composite_rgb(weights, col):
+    """raw2outputs' colour map with white background (rendering_tcnn.py:283-289):
+    rgb = sum_i w_i c_i + 1 - sum_i w_i; weights (R,S), col (R,S,3) -> (R,3) fp64."""
+    w = np.asarray(weights, np.float64)
+    return (w[..., None] * np.asarray(col, np.float64)).sum(1) + (1 - w.sum(1, keepdims=True))
+
+
+def rgb_loss_grad(rgb, gt, weights, n_rays):
+    """compute_loss_camera (optimizer.py:861-894): l1_loss over 3 x n_rays colour values, and its
+    gradient with respect to each sample's colour, w_i sign(rgb - gt) / (3 n) -> (loss, (R,S,3))."""
+    diff = np.asarray(rgb, np.float64) - np.asarray(gt, np.float64)
+    g = np.sign(diff) / (3.0 * n_rays)
+    return np.abs(diff).sum() / (3.0 * n_rays), np.asarray(weights, np.float64)[..., None] * g[:, None, :]
+
+
 def rgb_forward(enc32, rays, weights, mats_f16, S):
     """enc32 (N, 32) fp16 colour-grid features, rays (R, 13), weights (R, S) -> (rgb (R,3) fp64,
     x (N,48) fp16, hidden list, col (N,3) fp64)."""
@@ -54,8 +69,7 @@ def rgb_forward(enc32, rays, weights, mats_f16, S):
     x = np.concatenate([np.asarray(enc32, np.float16), h_d], 1)
     out16, hidden = omlp.forward(x, mats_f16)
     col = (1 / (1 + np.exp(-out16[:, :3].astype(np.float32)))).astype(np.float16).astype(np.float64)
-    w = np.asarray(weights, np.float64).reshape(R, S)
-    rgb = (w[..., None] * col.reshape(R, S, 3)).sum(1) + (1 - w.sum(1, keepdims=True))
+    rgb = composite_rgb(np.asarray(weights, np.float64).reshape(R, S), col.reshape(R, S, 3))
     return rgb, x, hidden, col
 
 
@@ -64,13 +78,11 @@ def rgb_train(enc32, rays, weights, gt, mats_f16, S, n_rays_global=None):
     R = rays.shape[0]
     rgb, x, hidden, col = rgb_forward(enc32, rays, weights, mats_f16, S)
     n = R if n_rays_global is None else n_rays_global
-    diff = rgb - np.asarray(gt, np.float64)
-    g = np.sign(diff) / (3.0 * n)
-    w = np.asarray(weights, np.float64).reshape(-1)
-    dcol = w[:, None] * np.repeat(g, S, axis=0)
+    loss, dcol = rgb_loss_grad(rgb, gt, np.asarray(weights, np.float64).reshape(R, S), n)
+    dcol = dcol.reshape(-1, 3)
     dlogit = dcol * col * (1 - col)
     d_out = np.zeros((x.shape[0], mats_f16[-1].shape[0]))
     d_out[:, :3] = dlogit
     d_x, dws = omlp.backward(x, mats_f16, hidden, d_out)
-    return dict(rgb=rgb, loss=np.abs(diff).sum() / (3.0 * n), d_enc=d_x[:, :32],
+    return dict(rgb=rgb, loss=loss, d_enc=d_x[:, :32],
                 d_w=np.concatenate([dw.reshape(-1) for dw in dws]))

@@ -329,5 +329,159 @@ def main():
     print("golden vectors written to", OUT)
 
 
+# ---------------------------------------------------------------------------------------------
+# Round-2 fixtures (``python tests/golden/make_golden.py r2``): the camera phase and colour
+# compositing, the camera loss and its colour gradient, torch.optim.Adam on tcnn-style fp16 params,
+# and the checkpoint's key layout.  They go to their own files; main()'s fixtures are not touched.
+
+def _tcnn_shape_stub():
+    """A shape-only tinycudann stand-in: each module owns a flat ``params`` Parameter on the meta
+    device, sized by loner_amd.tcnn's restatement of tcnn v1.7's parameter counts (so the SIZES in
+    the key fixture are this build's formulas; the KEYS and module paths are the reference's)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    from loner_amd import tcnn as ltc
+    m = types.ModuleType("tinycudann")
+
+    class _Base(torch.nn.Module):
+        dtype = torch.half
+
+        def __init__(self, n):
+            super().__init__()
+            self.params = torch.nn.Parameter(torch.empty(n, device="meta"))
+
+    class Encoding(_Base):
+        def __init__(self, n_input_dims, encoding_config, seed=1337, dtype=torch.half):
+            cfg = dict(encoding_config)
+            n = ltc._GridSpec(n_input_dims, cfg).n_params if cfg.get("otype") == "HashGrid" else 0
+            super().__init__(n)
+            self.n_output_dims = n_input_dims if cfg.get("otype") != "HashGrid" else \
+                int(cfg["n_levels"]) * int(cfg["n_features_per_level"])
+            if cfg.get("otype") == "SphericalHarmonics":
+                self.n_output_dims = int(cfg["degree"]) ** 2
+
+    class Network(_Base):
+        def __init__(self, n_input_dims, n_output_dims, network_config, seed=1337):
+            super().__init__(ltc._MLPSpec(n_input_dims, n_output_dims, dict(network_config)).n_params)
+
+    class NetworkWithInputEncoding(_Base):
+        def __init__(self, n_input_dims, n_output_dims, encoding_config, network_config, seed=1337):
+            g = ltc._GridSpec(n_input_dims, dict(encoding_config))
+            mlp = ltc._MLPSpec(g.n_levels * g.n_features, n_output_dims, dict(network_config))
+            super().__init__(mlp.n_params + g.n_params)
+
+    m.Encoding, m.Network, m.NetworkWithInputEncoding = Encoding, Network, NetworkWithInputEncoding
+    return m
+
+
+class FixedColorModel(torch.nn.Module):
+    """Stand-in for Model in compute_loss_camera: per-sample colours are a leaf Parameter, composited
+    by the reference's own raw2outputs (white background, sigma_only=False) with fixed sigma, z and
+    noise, so autograd gives the loss gradient with respect to the colours."""
+
+    def __init__(self, ref, colors, sigma, z, far):
+        super().__init__()
+        self.ref, self.colors = ref, torch.nn.Parameter(colors)
+        self.sigma, self.z, self.far = sigma, z, far
+
+    def forward(self, rays, sampler, scale, camera=True, return_variance=True):
+        raw = torch.cat([self.colors, self.sigma[..., None]], -1)
+        rgb, depth, w, op, var = self.ref.rendering.raw2outputs(raw, self.z, rays[:, 3:6], 1.0, True, sigma_only=False,
+                                                                far=self.far, ret_var=True)
+        return {"rgb_fine": rgb, "depth_fine": depth, "weights_fine": w}
+
+
+def main_r2():
+    import yaml
+    sys.modules["tinycudann"] = _tcnn_shape_stub()
+    ref = import_reference()
+    rng = np.random.default_rng(20261016)
+    torch.set_num_threads(4)
+
+    # ---- camera rays: get_ray_directions (ray_utils.py:62-124, no distortion) and
+    #      CameraRayDirections.build_rays (:175-212)
+    W, H = 40, 24
+    K = torch.tensor([[31.5, 0.0, 19.25], [0.0, 30.0, 11.75], [0.0, 0.0, 1.0]])
+    dirs, gx, gy = ref.ray_utils.get_ray_directions(H, W, newK=K, with_indices=True)
+    crd = ref.ray_utils.CameraRayDirections.__new__(ref.ray_utils.CameraRayDirections)
+    crd.directions, crd.i_meshgrid, crd.j_meshgrid = dirs, gx, gy
+    a, b = 0.6, -0.3
+    Rz = torch.tensor([[np.cos(a), -np.sin(a), 0], [np.sin(a), np.cos(a), 0], [0, 0, 1]], dtype=torch.float32)
+    Rx = torch.tensor([[1, 0, 0], [0, np.cos(b), -np.sin(b)], [0, np.sin(b), np.cos(b)]], dtype=torch.float32)
+    T = torch.eye(4)
+    T[:3, :3] = Rz @ Rx
+    T[:3, 3] = torch.tensor([3.0, -7.5, 1.25])
+    pose = NS(get_transformation_matrix=lambda: T.clone())
+    wc = ref.pose_utils.WorldCube(torch.tensor([37.5]), torch.tensor([-2.0, 4.0, 0.5]))
+    img = torch.from_numpy(rng.uniform(0, 1, (H, W, 3)).astype(np.float32))
+    pix = torch.from_numpy(rng.choice(W * H, 300, replace=False))
+    rays_c, inten = crd.build_rays(pix, pose, NS(image=img), wc, torch.tensor([1.0, 75.0]))
+    np.savez_compressed(f"{OUT}/camera_rays.npz", K=K.numpy(), width=np.int64(W), height=np.int64(H),
+                        directions=dirs.numpy(), grid_x=gx.numpy(), grid_y=gy.numpy(), pose=T.numpy(),
+                        scale=np.float32(37.5), shift=np.float32([-2.0, 4.0, 0.5]), ray_range=np.float32([1.0, 75.0]),
+                        image=img.numpy(), pixels=pix.numpy(), rays=rays_c.numpy(), intensities=inten.numpy())
+
+    # ---- colour compositing, white background (rendering_tcnn.py:219-295 with sigma_only=False), and
+    #      compute_loss_camera (optimizer.py:861-894) with its gradient w.r.t. the per-sample colours
+    R, S = 48, 64
+    rays = rays_c[:R].clone()
+    z = torch.sort(torch.from_numpy(rng.uniform(0.02, 0.9, (R, S)).astype(np.float32)), 1).values
+    far = rays[:, -1:].clone()
+    sig = torch.from_numpy(sigma_profiles(rng, z.numpy(), (z[:, S // 3]).numpy(), far[:, 0].numpy()))
+    col = torch.from_numpy(rng.uniform(0.0, 1.0, (R, S, 3)).astype(np.float16).astype(np.float32))
+    noise = rng.normal(0, 1, (R, S)).astype(np.float32)
+    with DrawQueue([noise]):
+        rgb, depth, wts, op, var = ref.rendering.raw2outputs(torch.cat([col, sig[..., None]], -1), z, rays[:, 3:6], 1.0,
+                                                             True, sigma_only=False, far=far, ret_var=True)
+    gt = torch.from_numpy(rng.uniform(0, 1, (R, 3)).astype(np.float32))
+    o = make_optimizer(ref, LOSS_DEFAULT, 37.5, None, sig.clone(), S)
+    o._model = FixedColorModel(ref, col.clone(), sig, z, far)
+    with DrawQueue([noise]):
+        loss = o.compute_loss_camera((rays, gt), None, 0)
+    loss.backward()
+    np.savez_compressed(f"{OUT}/camera_loss.npz", rays=rays.numpy(), z=z.numpy(), sigma=sig.numpy(), colors=col.numpy(),
+                        noise=noise, rgb=rgb.numpy(), depth=depth.numpy(), weights=wts.numpy(), opacity=op.numpy(),
+                        gt=gt.numpy(), loss=np.float64(loss.item()), d_colors=o._model.colors.grad.numpy())
+
+    # ---- torch.optim.Adam on tcnn-style fp16 params (optimizer.py:257-265,460; Adam defaults), the
+    #      gradient arriving as tcnn's binding hands it over: computed with the loss scaled by 128,
+    #      stored fp16, then divided by 128 (in fp16).  The same steps on an fp32 Parameter fed the
+    #      identical fp16-rounded gradients (the fp32 master this build keeps) are stored beside it.
+    n, steps = 4096, 5
+    p0 = rng.uniform(-1e-4, 1e-4, n).astype(np.float32)
+    p0[:64] = rng.uniform(-0.3, 0.3, 64)  # MLP-like weights
+    graw = np.stack([rng.normal(0, 1, n) * 10.0 ** rng.uniform(-8, -2, n) for _ in range(steps)]).astype(np.float32)
+    graw[:, 3000:] = 0.0  # untouched table entries
+    g16 = ((torch.from_numpy(graw) * 128.0).half() / 128.0)  # fp16, as tcnn's binding returns it
+    out = {}
+    for tag, dt in (("fp16", torch.float16), ("fp32", torch.float32)):
+        prm = torch.nn.Parameter(torch.from_numpy(p0.copy()).to(dt))  # (a copy: .to(float32) would alias p0)
+        opt = torch.optim.Adam([prm], lr=0.01)
+        hist = []
+        for k in range(steps):
+            prm.grad = g16[k].to(dt)
+            opt.step()
+            hist.append(prm.detach().float().numpy().copy())
+        out[f"params_{tag}"] = np.stack(hist)
+        out[f"exp_avg_sq_{tag}"] = opt.state[prm]["exp_avg_sq"].float().numpy()
+    np.savez_compressed(f"{OUT}/adam_fp16.npz", p0=p0, grad_raw=graw, grad_f16=g16.float().numpy(), lr=np.float32(0.01),
+                        **out)
+
+    # ---- checkpoint key layout: the reference's Model / OccupancyGridModel state_dict keys
+    nerf_cfg = yaml.safe_load(open(os.path.join(REF, "cfg", "nerf_config", "default_nerf_hash.yaml")))
+    model = ref.model_tcnn.Model(NS(model_type="nerf_decoupled", nerf_config=nerf_cfg, num_colors=3))
+    occ = ref.model_tcnn.OccupancyGridModel(NS(voxel_size=100))
+    import json
+    keys = dict(network_state_dict={k: list(v.shape) for k, v in model.state_dict().items()},
+                occ_model_state_dict={k: list(v.shape) for k, v in occ.state_dict().items()},
+                sigma_parameters=[n for n, _ in model.nerf_model._model_sigma.named_parameters()],
+                note="keys and module paths from the reference's Model; sizes from the shape-only tcnn stand-in "
+                     "(loner_amd.tcnn's restatement of tcnn v1.7's parameter counts)")
+    json.dump(keys, open(f"{OUT}/ckpt_keys.json", "w"), indent=1, sort_keys=True)
+    print("round-2 golden vectors written to", OUT)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "r2":
+        main_r2()
+    else:
+        main()
