@@ -86,11 +86,16 @@ def test_depth_renderer_vs_oracle(L, strategy):
     d = host(depth)
     if strategy == "default":
         np.testing.assert_allclose(d, ro["depth"], rtol=2e-4, atol=1e-6)
-    else:  # peak depth is a sample position: equal, or one sample over where T crosses 0.5 within rounding
-        assert np.mean(d != ro["depth"]) <= 0.02
+    else:  # peak depth is a sample position: <= 0.1 % of rays may take the adjacent sample (T crossing 0.5
+        # within rounding); tests/test_gpu_depth_parity.py holds the >= 2,000-ray version of this bar
+        diff = np.flatnonzero(d != ro["depth"])
+        assert len(diff) <= 1e-3 * len(d), len(diff)
+        for r in diff:
+            i, j = np.flatnonzero(z[r] == d[r]), np.flatnonzero(z[r] == ro["depth"][r])
+            assert len(i) and len(j) and abs(int(i[0]) - int(j[0])) <= 1
     np.testing.assert_allclose(host(opacity), ro["opacity"], rtol=1e-4, atol=1e-5)
     l1 = np.abs(d - ro["depth"]).mean() * win.scale
-    assert l1 < (1e-3 if strategy == "default" else 0.05), l1  # metres
+    assert l1 < 1e-3, l1  # metres
 
 
 def test_compute_l1_depth(L):
