@@ -60,8 +60,8 @@ def parse():
                          "strong: the config's batch is split over the N ranks (SURVEY.md §8(e)).  Default: "
                          "strong for C4 at N > 1 (the headline C4 curve at R = 9216), weak otherwise")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rays", type=int, default=256, help="rays per CPU-baseline step (x512 samples)")
-    ap.add_argument("--cpu-steps", type=int, default=36)
+    ap.add_argument("--cpu-rays", type=int, default=512, help="rays per reduced-config CPU-baseline step (x512 samples)")
+    ap.add_argument("--cpu-steps", type=int, default=24)
     return ap.parse_args()
 
 
@@ -102,17 +102,33 @@ def pmc_mfma(cfg_name):
     return {k: v["mfma_busy_frac"] for k, v in rec["kernels"].items()}, os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(cfg_name, n_rays, n_steps):
-    """The pure-PyTorch CPU restatement of the step (oracle/torch_step.py) on a bounded sample of the
-    same workload, on the host threads this job may use (rank 0, N=1 only)."""
+def host_cpu_share():
+    """(threads, why): the host threads this job may use.  The GPU pool sets OMP_NUM_THREADS to the job's
+    CPU share (16 per GPU) while os.cpu_count() reports every core of the shared host, so the share
+    caps the count; without it, the affinity mask."""
+    n_aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if omp > 0:
+        n = min(omp, n_aff)
+        return n, (f"the job's CPU share: OMP_NUM_THREADS={omp} (os.cpu_count()={os.cpu_count()} counts the whole "
+                   f"shared host, affinity {n_aff})")
+    return n_aff, f"the affinity mask ({n_aff} of os.cpu_count()={os.cpu_count()})"
+
+
+def _cpu_model():
+    try:
+        return next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except (OSError, StopIteration):
+        return "host CPU"
+
+
+def _time_torch_steps(kind, strat, preset, n_rays, S, n_steps):
+    """ray-samples/s and seconds of n_steps pure-PyTorch CPU steps (oracle/torch_step.py) of n_rays x S."""
     from oracle import torch_step as ts
     from loner_amd import synthetic as syn
-    kind, nkf, rpk, spk, strat, S, preset = syn.CONFIGS[cfg_name]
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
-    prev = torch.get_num_threads()
-    torch.set_num_threads(threads)
-    win = syn.make_window(kind, 2, seed=99)
-    rays, dgt = syn.build_batch(win, kind, n_rays // 2, 0, strat, seed=7)
+    nkf = 1 if n_rays <= 512 else 2
+    win = syn.make_window(kind, nkf, seed=99)
+    rays, dgt = syn.build_batch(win, kind, n_rays // nkf, 0, strat, seed=7)
     field = ts.TorchField()
     scale = syn.CUBES[kind][0]
     ts.train_step(field, rays, dgt, scale, LOSS_PRESETS[preset], 1, S=S)  # warm-up (discarded)
@@ -120,41 +136,56 @@ def cpu_baseline(cfg_name, n_rays, n_steps):
     for it in range(n_steps):
         ts.train_step(field, rays, dgt, scale, LOSS_PRESETS[preset], 2 + it, S=S)
     dt = time.perf_counter() - t0
+    return rays.shape[0] * S * n_steps / dt, dt, rays.shape[0]
+
+
+def cpu_baseline(cfg_name, n_rays, n_steps):
+    """The pure-PyTorch CPU restatement of the step (oracle/torch_step.py: forward + autograd backward +
+    Adam) on BASELINE.md's two CPU shapes, on the host threads this job may use (rank 0, N=1 only;
+    SURVEY.md §8(d)): C1 (1 keyframe x 512 rays x 64 samples) and a reduced C2 (512 rays x 512 samples)
+    of this config's scene.  ``value`` is the reduced-C2 rate (the C1 rate on the C1 line)."""
+    from loner_amd import synthetic as syn
+    kind, nkf, rpk, spk, strat, S, preset = syn.CONFIGS[cfg_name]
+    threads, why = host_cpu_share()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    c1_rate, c1_dt, _ = _time_torch_steps("quad", "RANDOM", "default", 512, 64, 20)
+    rate, dt, r = _time_torch_steps(kind, strat, preset, n_rays, 512, n_steps)
     torch.set_num_threads(prev)
-    cpu = ""
-    try:
-        cpu = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
-    except (OSError, StopIteration):
-        pass
-    return {"value": rays.shape[0] * S * n_steps / dt, "unit": "ray-samples/s", "cores": threads, "kind": "port",
-            "sample": f"{n_steps} optimiser steps of {rays.shape[0]} rays x {S} samples ({cfg_name} scene), pure-PyTorch "
-                      f"CPU restatement (oracle/torch_step.py: forward + autograd backward + Adam), {threads} threads "
-                      f"on {cpu or 'host CPU'}, {dt:.1f} s"}
+    cpu = _cpu_model()
+    c1 = {"value": c1_rate, "unit": "ray-samples/s", "cores": threads,
+          "sample": f"C1: 20 steps of 1 keyframe x 512 rays x 64 samples (quad), {c1_dt:.1f} s"}
+    main = {"value": rate, "unit": "ray-samples/s", "cores": threads, "kind": "port", "cores_why": why,
+            "cpu_model": cpu,
+            "sample": f"reduced {cfg_name}: {n_steps} optimiser steps of {r} rays x 512 samples ({cfg_name} scene), "
+                      f"pure-PyTorch CPU restatement (oracle/torch_step.py: forward + autograd backward + Adam), "
+                      f"{threads} threads on {cpu}, {dt:.1f} s", "c1": c1}
+    if cfg_name == "C1":
+        main.update(value=c1_rate, sample=c1["sample"] + f", {threads} threads on {cpu}")
+    return main
+
 
 def cpu_baseline_render(kind, n_rays, S):
-    """Oracle forward render (OGM sampler, sigma field, peak compositing) on a bounded sample."""
-    from oracle import hashgrid as ohg
-    from oracle import mlp as omlp
-    from oracle import render as orender
-    from oracle import rng as orng
-    from oracle import step as ostep
+    """The same pure-PyTorch restatement's forward render (oracle/torch_step.render_step: OGM sampler,
+    sigma field, peak compositing) on a bounded sample of the C3 workload, same threads as above."""
+    from oracle import torch_step as ts
     from loner_amd import synthetic as syn
+    threads, why = host_cpu_share()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
     win = syn.make_window(kind, 1, seed=99)
     rays, _ = syn.build_batch(win, kind, n_rays, 0, "RANDOM", seed=7)
-    rays = rays.numpy()
-    field = ostep.OracleField()
-    w0, w1, table = field.split16()
+    field = ts.TorchField()
+    ts.render_step(field, rays[:8], S)  # warm-up (discarded)
     t0 = time.perf_counter()
-    a, b = orng.ray_sample_grid(np.arange(n_rays), S // 2)
-    z = orender.ogm_samples(rays, S, field.occ, None, orng.uniform(1, orng.STREAM_PDF, a, b))
-    xyz = (rays[:, None, 0:3] + rays[:, None, 3:6] * z[:, :, None]).astype(np.float32)
-    pos = ((xyz + np.float32(1)) / np.float32(2)).astype(np.float32).reshape(-1, 3)
-    out16, _ = omlp.forward(ohg.encode(pos, table, field.layout), [w0, w1])
-    orender.raw2outputs_adjusted(out16[:, 0].astype(np.float32).reshape(n_rays, S), z, rays[:, 3:6])
+    ts.render_step(field, rays, S)
     dt = time.perf_counter() - t0
-    return {"value": n_rays * S / dt, "unit": "ray-samples/s", "cores": 1, "kind": "port",
-            "sample": f"one render of {n_rays} rays x {S} samples (C3 scene), sigma head + peak depth only, "
-                      f"numpy oracle, {dt:.1f} s"}
+    torch.set_num_threads(prev)
+    cpu = _cpu_model()
+    return {"value": n_rays * S / dt, "unit": "ray-samples/s", "cores": threads, "kind": "port", "cores_why": why,
+            "cpu_model": cpu,
+            "sample": f"one render of {n_rays} rays x {S} samples (C3 scene), sigma head + peak depth, pure-PyTorch "
+                      f"CPU restatement (oracle/torch_step.render_step), {threads} threads on {cpu}, {dt:.1f} s"}
 
 
 def bench_render(args):
@@ -246,7 +277,7 @@ def bench_render(args):
                          "algorithmic_bytes_per_launch": 512 * N, "ms_per_launch": enc_ms},
             "stage_ms": stage_ms}
     if not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline_render(kind, 512, S)
+        line["cpu_baseline"] = cpu_baseline_render(kind, 4096, S)
     print(json.dumps(line), flush=True)
 
 

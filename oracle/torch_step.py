@@ -71,8 +71,8 @@ class TorchField:
         return (h @ self.w1.t())[:, :1]
 
 
-def sample_ogm(field, rays, S):
-    """OccGridRaySampler.get_samples (ray_sampling.py:53-92) in torch, training mode (jitter)."""
+def sample_ogm(field, rays, S, perturb=1.0):
+    """OccGridRaySampler.get_samples (ray_sampling.py:53-92) in torch; perturb 1 = training (jitter)."""
     with torch.no_grad():
         R, H = rays.shape[0], S // 2
         near, far = rays[:, -2:-1], rays[:, -1:]
@@ -80,7 +80,7 @@ def sample_ogm(field, rays, S):
         z = near * (1 - t) + far * t
         mid = 0.5 * (z[:, 1:] + z[:, :-1])
         upper, lower = torch.cat([mid, z[:, -1:]], -1), torch.cat([z[:, :1], mid], -1)
-        z = lower + (upper - lower) * torch.rand(R, H)
+        z = lower + (upper - lower) * torch.rand(R, H) if perturb else z
         pts = rays[:, None, 0:3] + rays[:, None, 3:6] * z[..., None]
         logits = torch.nn.functional.grid_sample(field.occ, pts.reshape(1, 1, R, H, 3), align_corners=False)
         p = torch.sigmoid(logits.reshape(R, H))
@@ -145,3 +145,19 @@ def train_step(field, rays, depth_gt, scale, cfg, global_step, S=512):
     loss.backward()
     field.opt.step()
     return float(loss.detach())
+
+
+def render_step(field, rays, S=2048):
+    """Model.forward(testing=True) for the sigma head in torch, no autograd (the C3 CPU baseline):
+    OGM samples without jitter (random importance draws), the sigma field, peak ("adjusted")
+    compositing (rendering_tcnn.py:70-214: depth at the first sample with T <= 0.5).  Returns the depths."""
+    with torch.no_grad():
+        R = rays.shape[0]
+        z = sample_ogm(field, rays, S, perturb=0.0)
+        xyz = rays[:, None, 0:3] + rays[:, None, 3:6] * z[..., None]
+        sig = field.sigma(((xyz + 1) / 2).reshape(-1, 3)).reshape(R, S)
+        d = torch.cat([z[:, 1:] - z[:, :-1], torch.full((R, 1), 1e10)], -1) * rays[:, 3:6].norm(dim=-1, keepdim=True)
+        alpha = 1 - torch.exp(-d * torch.relu(sig))
+        T = torch.cumprod(torch.cat([torch.ones(R, 1), 1 - alpha + 1e-10], -1), -1)
+        hit = (T[:, 1:] <= 0.5) & (T[:, :-1] > 0.5)
+        return torch.where(hit.any(-1), z.gather(1, hit.float().argmax(-1, keepdim=True))[:, 0], torch.zeros(R))
