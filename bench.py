@@ -517,11 +517,13 @@ def main():
     replicas = args.config == "C5"  # independent jobs: own window per rank, no data-path collective
 
     # ---- workload
+    submap = None
     if args.rays == "device" and replicas:
+        # rank r optimises submap r (mod the part count) of the segmented trajectory, in its own cube
         from loner_amd.rays import RayWindow
-        scans = syn.make_window(kind, nkf, seed=1000 + rank, start=50 * rank)
-        window = RayWindow(scans, syn.world_cube(kind), syn.SENSORS[kind]["ray_range"], n_lidar=rpk, n_sky=spk,
-                           strategy=strat, device=dev)
+        scans, cube, submap = syn.submap_window(rank, nkf, seed=1000 + rank)
+        window = RayWindow(scans, cube, syn.SENSORS[kind]["ray_range"], n_lidar=rpk, n_sky=spk, strategy=strat,
+                           device=dev)
         del scans
         if not window.all_valid:
             raise RuntimeError("bench window must give a fixed batch")
@@ -620,7 +622,8 @@ def main():
                                + ("in total, split over the GPUs, " if args.scaling == "strong" else "per GPU, ")
                                + f"L=16 T=2^18 hash grid + 64-wide sigma MLP, {preset} loss (L1_JS)",
                    "rays_per_gpu": R, "samples_per_ray": n_samples, "global_rays": R * world,
-                   "parallelism": (f"replicas{world}" if replicas else f"dp{world}") if world > 1 else "single"},
+                   "parallelism": (f"replicas{world}" if replicas else f"dp{world}") if world > 1 else "single",
+                   **({"submap_rank0": submap} if submap is not None else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "hash-grid backward stage (k_bwd_scan_*, k_bwd_scatter, k_bwd_level_max, k_bwd_accum)",

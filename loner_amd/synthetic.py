@@ -129,15 +129,16 @@ def keyframe_poses(kind, n_kf, rng, start=0):
     return [_yaw_pose(7 + 12 * np.cos(a), 5 + 8 * np.sin(a), 0.5, a) for a in ang]
 
 
-def make_window(kind, n_kf=16, seed=0, dropout=0.05, start=0):
+def make_window(kind, n_kf=16, seed=0, dropout=0.05, start=0, poses=None):
     """A keyframe window: list of dicts with sensor-frame directions (3,P), distances (P,),
-    sky directions (3,Q) and the lidar pose (4,4), all torch float32 on the CPU."""
+    sky directions (3,Q) and the lidar pose (4,4), all torch float32 on the CPU.  ``poses``: explicit
+    keyframe poses (4,4) instead of the config's trajectory."""
     rng = np.random.default_rng(seed)
     sc = SENSORS[kind]
     scene = make_scene(kind, np.random.default_rng(1234))
     dirs = sensor_directions(sc["n_beams"], sc["fov"], sc["n_az"])
     window = []
-    for pose in keyframe_poses(kind, n_kf, rng, start):
+    for pose in (keyframe_poses(kind, n_kf, rng, start) if poses is None else poses):
         dw = (pose[:3, :3] @ dirs).T
         t = scene.cast(pose[:3, 3], dw, sc["ray_range"][1])
         hit = np.isfinite(t) & (t >= sc["ray_range"][0]) & (t < sc["ray_range"][1]) & (rng.uniform(size=t.shape) > dropout)
@@ -147,6 +148,25 @@ def make_window(kind, n_kf=16, seed=0, dropout=0.05, start=0):
                            sky_directions=torch.from_numpy(dirs[:, sky].astype(np.float32)),
                            pose=torch.from_numpy(pose.astype(np.float32))))
     return window
+
+
+def submap_window(part_id, n_kf=16, seed=0):
+    """C5: the haveri trajectory split into <= 50 m submaps with +-30-pose padding as
+    examples/fdt_segment_and_optimize_submaps.py does (loner_amd.submaps), submap part_id mod the part
+    count: n_kf keyframes evenly spread over its padded pose range and its own world cube
+    (compute_world_cube of those poses).  Returns (scans, WorldCube, info dict)."""
+    from . import submaps as SM
+    tum = np.load(os.path.join(ROOT, "tests", "golden", "haveri_keyframe_trajectory.npz"))["tum"]
+    parts = SM.split_trajectory(tum[:, 1:4])
+    ranges = SM.padded_ranges(parts, len(tum))
+    k = part_id % len(parts)
+    lo, hi = ranges[k]
+    idx = np.round(np.linspace(lo, hi, n_kf)).astype(int)
+    poses = [_quat_pose(tum[i, 1:4], tum[i, 4:8]) for i in idx]
+    scale, shift = SM.world_cube_from_poses(tum[lo:hi + 1, 1:4], SENSORS["forest"]["ray_range"])
+    wc = R.WorldCube(torch.tensor([scale], dtype=torch.float32), torch.from_numpy(shift))
+    info = dict(part=k, n_parts=len(parts), core=list(parts[k]), padded=[lo, hi], cube_scale=scale)
+    return make_window("forest", n_kf, seed=seed, poses=poses), wc, info
 
 
 def world_cube(kind):
