@@ -91,6 +91,18 @@ def pmc_traffic(cfg_name):
     return rec["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
 
 
+def pmc_step_traffic(cfg_name):
+    """HBM bytes per whole optimiser step (every kernel of the step; OGM kernels at their 1-in-10
+    cadence), from profiles/<round>_traffic_<cfg>_step.json (tools/refresh_profiles.py, rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes over this bench command); None if there is none."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_traffic_{cfg_name}_step.json")))
+    if not files:
+        return None, None
+    rec = json.load(open(files[-1]))
+    return rec["hbm_bytes_per_step"], os.path.relpath(files[-1], ROOT)
+
+
 def pmc_mfma(cfg_name):
     """Per sigma-MLP kernel MFMA busy fractions from the newest committed PMC pass of this bench
     command (profiles/<round>_mfma_<cfg>.json, tools/refresh_profiles.py); None if there is none."""
@@ -601,6 +613,10 @@ def main():
     bwd_ms = stage_ms["grid_bwd"]
     achieved = 1024.0 * N / (bwd_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args.config)
+    traffic_step, traffic_step_src = pmc_step_traffic(args.config)
+    # the whole step against the HBM bound: 1536 B per ray-sample (hash-grid gathers and
+    # scatter-adds) + 32 B per parameter (Adam) + 52 B per ray
+    step_bytes = 1536.0 * N + 32.0 * state.n_params + 52.0 * R
     busy, busy_src = pmc_mfma(args.config)
     mlp_tflops = MLP_FLOP_PER_SAMPLE * N / (stage_ms["field"] * 1e-3) / 1e12
     line = {
@@ -627,7 +643,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "hash-grid backward stage (k_bwd_scan_*, k_bwd_scatter, k_bwd_level_max, k_bwd_accum)",
-                     "algorithmic_bytes_per_launch": 1024 * N, "ms_per_launch": bwd_ms},
+                     "algorithmic_bytes_per_launch": 1024 * N, "ms_per_launch": bwd_ms,
+                     "step_algorithmic_bytes": step_bytes,
+                     "step_frac": step_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "traffic_step": traffic_step, "traffic_step_source": traffic_step_src},
         # the sigma MLP (fwd 4224 + bwd 8448 FLOP/sample) over the field stage
         # (k_field_wave + k_mlp_bwd_tiles), against the dense fp16 MFMA peak
         "mfma": {"achieved": mlp_tflops, "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": mlp_tflops / MFMA_PEAK_TFLOPS,

@@ -15,4 +15,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run 
   || { tail -20 $R/gpurun_out/bench_prof.err; exit 1; }
 bash $R/tools/pmc_hbm.sh || exit 1
 bash $R/tools/pmc_mfma.sh || exit 1
+bash $R/tools/pmc_step.sh $CFG || exit 1
 echo profiles done

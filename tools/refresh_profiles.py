@@ -21,8 +21,8 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BWD_KERNELS = ("k_bwd_scan_rows", "k_bwd_scan_buckets", "k_bwd_scatter", "k_bwd_level_max", "k_bwd_accum",
-               "k_bwd_finalize")
+BWD_KERNELS = ("k_bwd_chunk_sums", "k_bwd_scan_rows", "k_bwd_scan_buckets", "k_bwd_scatter_rows",
+               "k_bwd_scatter_overflow", "k_bwd_scatter", "k_bwd_level_max", "k_bwd_accum", "k_bwd_finalize")
 
 
 def per_dispatch(path):
@@ -31,11 +31,10 @@ def per_dispatch(path):
     disp = collections.defaultdict(set)
     for row in csv.DictReader(open(path)):
         name = row["Kernel_Name"]
-        key = next((k for k in BWD_KERNELS if k in name), None)
+        base = name.split("(")[0].split("<")[0].replace("void ", "").replace("lnr::", "").strip()
+        key = base if base in BWD_KERNELS else None
         if key is None:
             continue
-        if key == "k_bwd_scatter":  # one launch per level kind
-            key = "k_bwd_scatter<" + name.split("(")[0].rstrip(">").split(",")[-1].strip() + ">"
         tot[key] += float(row["Counter_Value"])
         disp[key].add(row["Dispatch_Id"])
     return {k: tot[k] / len(disp[k]) for k in tot}
@@ -67,6 +66,29 @@ def mfma_busy(path):
     return out
 
 
+OGM_KERNELS = ("k_ogm_grad", "k_sum_replicas", "k_sgd")
+
+
+def step_traffic(fetch_csv, write_csv):
+    """Per kernel name: HBM bytes per optimiser step from a --pmc pass over bench.py.  The step count is
+    k_adam's dispatch count (one Adam per step); kernels dispatched at least once per step are counted
+    whole, the OGM kernels (every 10th step) too, set-up kernels (fewer dispatches) are left out."""
+    vals = collections.defaultdict(float)
+    disp = collections.defaultdict(set)
+    for path, mult in ((fetch_csv, 2.0), (write_csv, 1.0)):  # FETCH_SIZE doubled on gfx950
+        for row in csv.DictReader(open(path)):
+            name = row["Kernel_Name"].split("(")[0].replace("void ", "")
+            vals[name] += mult * float(row["Counter_Value"]) * 1024
+            disp[name].add(row["Dispatch_Id"])
+    n_steps = max((len(d) for k, d in disp.items() if "k_adam" in k), default=0)
+    out = {}
+    for k, v in vals.items():
+        calls = len(disp[k]) // 1
+        if calls >= n_steps or any(o in k for o in OGM_KERNELS):
+            out[k] = {"bytes_per_step": v / n_steps, "dispatches": calls}
+    return n_steps, out
+
+
 def main(tag, cfg):
     out = os.path.join(ROOT, "gpurun_out")
     prof = os.path.join(ROOT, "profiles")
@@ -89,6 +111,21 @@ def main(tag, cfg):
                "kernels": kern}
         json.dump(rec, open(os.path.join(prof, f"{tag}_traffic_{cfg}.json"), "w"), indent=1)
         print(f"traffic {total / 1e9:.3f} GB per launch vs algorithmic {rec['algorithmic_bytes_per_launch'] / 1e9:.3f} GB")
+    f = glob.glob(os.path.join(out, "pmc_step", "FETCH_SIZE", "*counter_collection.csv"))
+    w = glob.glob(os.path.join(out, "pmc_step", "WRITE_SIZE", "*counter_collection.csv"))
+    if f and w:
+        n_steps, kern = step_traffic(f[0], w[0])
+        bench = json.load(open(os.path.join(out, "bench.json")))
+        total = sum(v["bytes_per_step"] for v in kern.values())
+        alg = bench["roofline"].get("step_algorithmic_bytes")
+        rec = {"what": "HBM bytes per optimiser step, every kernel of the step (rocprofv3 --pmc FETCH_SIZE and "
+                       "WRITE_SIZE passes over the bench command)", "config": cfg, "steps_profiled": n_steps,
+               "hbm_bytes_per_step": total, "step_algorithmic_bytes": alg,
+               "ratio_to_algorithmic": total / alg if alg else None,
+               "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving)",
+               "kernels": dict(sorted(kern.items(), key=lambda kv: -kv[1]["bytes_per_step"]))}
+        json.dump(rec, open(os.path.join(prof, f"{tag}_traffic_{cfg}_step.json"), "w"), indent=1)
+        print(f"step traffic {total / 1e9:.3f} GB per step vs algorithmic {(alg or 0) / 1e9:.3f} GB")
     m = glob.glob(os.path.join(out, "pmc", "MFMA", "*counter_collection.csv"))
     if m:
         kern = mfma_busy(m[0])
