@@ -99,12 +99,19 @@ int lnr_hashgrid_fwd_rays_live(const lnr_grid_desc* d, const float* rays, const 
                                int32_t n_samples, const uint16_t* table, const float* live, uint32_t* enc,
                                int64_t enc_stride, void* stream);
 /* Backward: d_table (n_entries,2) fp32 = scatter of corner weights * d_enc, as an atomic-free
- * binned scatter with int64 fixed-point accumulation.  d_table is OVERWRITTEN (every
- * entry, zero where no sample touches it) and the result is bitwise reproducible; `workspace`
- * holds at least lnr_hashgrid_bwd_workspace_bytes(d, N) bytes. */
+ * binned scatter of 8-byte records (fp16 values at a per-level power-of-two scale from max |d_enc|)
+ * with int64 fixed-point accumulation.  d_table is OVERWRITTEN (every entry, zero where
+ * no sample touches it) and the result is bitwise reproducible; `workspace` holds at least
+ * lnr_hashgrid_bwd_workspace_bytes(d, N) bytes. */
 #define LNR_BWD_COUNTS_READY 1
 #define LNR_BWD_NO_ACCUM 2      /* stop after the scatter: lnr_hashgrid_bwd_accum then finishes level ranges */
+#define LNR_BWD_LEVEL_MAX_READY 4 /* the caller stored max |d_enc| per level at lnr_hashgrid_bwd_level_max():
+                                     no pass over d_enc for it (a data-parallel caller stores the max over
+                                     ranks, so every rank's records round alike) */
 int64_t lnr_hashgrid_bwd_workspace_bytes(const lnr_grid_desc* d, int64_t n);
+/* Device address of the n_levels per-level max |d_enc| floats inside `workspace` (the same for
+ * every n: the workspace's first bytes). */
+float* lnr_hashgrid_bwd_level_max(const lnr_grid_desc* d, int64_t n, void* workspace);
 int lnr_hashgrid_bwd(const lnr_grid_desc* d, const float* pos01, int64_t n, const float* d_enc,
                      int64_t enc_stride, float* d_table, void* workspace, int64_t workspace_bytes, int32_t flags,
                      void* stream);
@@ -223,11 +230,14 @@ int lnr_composite_bwd(const float* rays, const float* z, const float* sigma, int
 int64_t lnr_field_train_workspace_words(int64_t n_rays, int32_t n_samples);
 /* Fused: sigma MLP forward from enc, compositing, loss, compositing backward, MLP backward.
  * Writes d_enc (level-major float2), accumulates d_w (3072 fp32), per-ray stats; optional outputs NULL.
+ * d_enc_level_max (optional, 16 floats): OVERWRITTEN with max |d_enc| per level, the hash-grid
+ * backward's record scales (pass lnr_hashgrid_bwd_level_max(...) and LNR_BWD_LEVEL_MAX_READY).
  * workspace: lnr_field_train_workspace_words(n_rays, n_samples) fp32 words. */
 int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, const float* rays, const float* z,
                     const float* depth_gt, int64_t n_rays, int32_t n_samples, float noise_std, const float* noise,
                     uint32_t key, int64_t ray_offset, const lnr_loss_params* lp, float* d_enc, float* d_w,
-                    float* workspace, float* ray_stats, float* depth, float* opacity, float* weights, void* stream);
+                    float* workspace, float* ray_stats, float* depth, float* opacity, float* weights,
+                    float* d_enc_level_max, void* stream);
 /* Forward-only fused render from enc (inference path, C3 shape): sigma MLP + compositing. */
 int lnr_field_render(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, const float* rays, const float* z,
                      int64_t n_rays, int32_t n_samples, int32_t strategy, float noise_std, const float* noise,

@@ -23,6 +23,7 @@ LOSS_KINDS = {"L1_JS": 0, "L2_JS": 1, "L1_LOS": 2, "L2_LOS": 3}
 RENDER_STRATEGIES = {"default": 0, "adjusted": 1}
 BWD_COUNTS_READY = 1
 BWD_NO_ACCUM = 2
+BWD_LEVEL_MAX_READY = 4
 
 c_p = ctypes.c_void_p
 c_i64 = ctypes.c_int64
@@ -95,6 +96,7 @@ _SIGNATURES = {
     "lnr_hashgrid_fwd_rays": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_p, c_i64, c_p,
                                              c_i64, c_p]),
     "lnr_hashgrid_bwd_workspace_bytes": (c_i64, [ctypes.POINTER(GridDesc), c_i64]),
+    "lnr_hashgrid_bwd_level_max": (c_p, [ctypes.POINTER(GridDesc), c_i64, c_p]),
     "lnr_hashgrid_bwd": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_i32,
                                         c_p]),
     "lnr_hashgrid_bwd_rays": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_p,
@@ -120,7 +122,7 @@ _SIGNATURES = {
     "lnr_composite_loss_bwd": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_u32, c_i64,
                                               ctypes.POINTER(LossParams), c_p, c_p, c_p, c_p, c_p, c_p]),
     "lnr_field_train": (ctypes.c_int, [c_p, c_p, c_i64, c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_u32, c_i64,
-                                       ctypes.POINTER(LossParams), c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+                                       ctypes.POINTER(LossParams), c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "lnr_field_render": (ctypes.c_int, [c_p, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_i32, c_f, c_p, c_u32, c_i64, c_p,
                                         c_p, c_p, c_p, c_p]),
     "lnr_rgb_render": (ctypes.c_int, [c_p, c_i32, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_p, c_p]),

@@ -42,6 +42,7 @@ struct FieldArgs {
   float* d_sigma;     // kSigmaGiven + train
   float* d_enc;       // kSigmaMLP + train
   float* dw_slab;     // kSigmaMLP + train: [gridDim.x][3072]
+  float* denc_max;    // optional: [16] max |d_enc| per level (float bits, atomicMax; zeroed by the ray phase)
   float* ray_stats;   // train: [R][LNR_RAY_STATS]
   // kLossExternal: upstream gradients of the render outputs (any may be NULL = zero)
   const float* g_weights;   // (R,S)
@@ -514,6 +515,7 @@ __global__ void __launch_bounds__(NT) k_field(FieldArgs a) {
 // 4 rays independently and meet once, at the end, to reduce their dW slabs.  Same arithmetic as
 // composite_ray<C, true, false> (the block version), reassociated only in the cross-lane sums.
 constexpr int kWavesPerBlock = NT / 64;
+constexpr int kSigmaLevels = 16;  // the sigma MLP's 32 inputs: 16 levels x 2 features
 
 __device__ __forceinline__ double wave_excl_prod(double p) {
   const int lane = threadIdx.x & 63;
@@ -709,6 +711,7 @@ __device__ void composite_loss_wave(const FieldArgs& a, float* sig, int64_t r) {
 // writes dL/dsigma (R, S) fp32 for phase 2.
 template <int C>
 __global__ void __launch_bounds__(NT) k_field_wave(FieldArgs a) {
+  if (a.denc_max && blockIdx.x == 0 && threadIdx.x < kSigmaLevels) a.denc_max[threadIdx.x] = 0.f;  // before k_mlp_bwd_tiles
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   constexpr int S = 64 * C;  // == a.S (checked at launch)
@@ -751,6 +754,7 @@ __global__ void __launch_bounds__(NT) k_mlp_bwd_tiles(FieldArgs a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) acc.v[t][m][q] = 0.f;
   float2* denc = reinterpret_cast<float2*>(a.d_enc);
+  float lmax[4] = {0.f, 0.f, 0.f, 0.f};  // max |d_enc| of this lane's levels 2g, 2g + 1, 8 + 2g, 9 + 2g
   const int64_t N = a.n_rays * (int64_t)a.S;  // a multiple of 64
   // software-pipelined: the next tile pair's enc / dsigma loads are in flight while this one computes
   // (2 waves per SIMD at this register count: latency is hidden by ILP, not by occupancy)
@@ -799,20 +803,61 @@ __global__ void __launch_bounds__(NT) k_mlp_bwd_tiles(FieldArgs a) {
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
       const int lvl = 8 * m + 2 * g;
-      denc[(int64_t)lvl * a.enc_stride + n0 + c] = make_float2(d[m][0] * ds0, d[m][1] * ds0);
-      denc[(int64_t)(lvl + 1) * a.enc_stride + n0 + c] = make_float2(d[m][2] * ds0, d[m][3] * ds0);
+      const float2 q0 = make_float2(d[m][0] * ds0, d[m][1] * ds0), q1 = make_float2(d[m][2] * ds0, d[m][3] * ds0);
+      denc[(int64_t)lvl * a.enc_stride + n0 + c] = q0;
+      denc[(int64_t)(lvl + 1) * a.enc_stride + n0 + c] = q1;
+      lmax[2 * m] = fmaxf(lmax[2 * m], fmaxf(fabsf(q0.x), fabsf(q0.y)));
+      lmax[2 * m + 1] = fmaxf(lmax[2 * m + 1], fmaxf(fabsf(q1.x), fabsf(q1.y)));
     }
     sigma_tile_bwd_denc(sw, h1, d);
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
       const int lvl = 8 * m + 2 * g;
-      denc[(int64_t)lvl * a.enc_stride + n0 + 16 + c] = make_float2(d[m][0] * ds1, d[m][1] * ds1);
-      denc[(int64_t)(lvl + 1) * a.enc_stride + n0 + 16 + c] = make_float2(d[m][2] * ds1, d[m][3] * ds1);
+      const float2 q0 = make_float2(d[m][0] * ds1, d[m][1] * ds1), q1 = make_float2(d[m][2] * ds1, d[m][3] * ds1);
+      denc[(int64_t)lvl * a.enc_stride + n0 + 16 + c] = q0;
+      denc[(int64_t)(lvl + 1) * a.enc_stride + n0 + 16 + c] = q1;
+      lmax[2 * m] = fmaxf(lmax[2 * m], fmaxf(fabsf(q0.x), fabsf(q0.y)));
+      lmax[2 * m + 1] = fmaxf(lmax[2 * m + 1], fmaxf(fabsf(q1.x), fabsf(q1.y)));
     }
     dw0_pair(lds, sw, h0, h1, e0, e1, ds0, ds1, scale, acc);
   }
   __syncthreads();
   write_dw_slab<NT>(reinterpret_cast<float*>(smem), acc, dw1, a.dw_slab + (int64_t)blockIdx.x * LNR_SIGMA_MLP_PARAMS);
+  if (a.denc_max) {  // the level maxima (hash-grid backward record scales): 16-lane row max, then the block's
+    __shared__ float bm[kWavesPerBlock][kSigmaLevels];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v = lmax[q];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+      if (c == 0) bm[wid][(q >> 1) * 8 + 2 * g + (q & 1)] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < kSigmaLevels) {
+      float v = 0.f;
+      for (int w = 0; w < kWavesPerBlock; ++w) v = fmaxf(v, bm[w][threadIdx.x]);
+      if (v > 0.f) atomicMax(reinterpret_cast<uint32_t*>(a.denc_max) + threadIdx.x, __float_as_uint(v));
+    }
+  }
+}
+
+// max |d_enc| per level for the per-ray field path (grid (256, 16), zeroed before)
+__global__ void __launch_bounds__(256) k_denc_max(const float2* __restrict__ d_enc, int64_t stride, int64_t n,
+                                                  float* __restrict__ out) {
+  __shared__ float red[4];
+  const float2* src = d_enc + (int64_t)blockIdx.y * stride;
+  float m = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float2 q = src[i];
+    m = fmaxf(m, fmaxf(fabsf(q.x), fabsf(q.y)));
+  }
+  m = wave_max_nonneg(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (m > 0.f) atomicMax(reinterpret_cast<uint32_t*>(out) + blockIdx.y, __float_as_uint(m));
+  }
 }
 
 static size_t wave_smem_bytes(int S) { return (size_t)kWavesPerBlock * S * 4; }
@@ -979,7 +1024,8 @@ extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t e
                                const float* z, const float* depth_gt, int64_t n_rays, int32_t n_samples,
                                float noise_std, const float* noise, uint32_t key, int64_t ray_offset,
                                const lnr_loss_params* lp, float* d_enc, float* d_w, float* workspace,
-                               float* ray_stats, float* depth, float* opacity, float* weights, void* stream) {
+                               float* ray_stats, float* depth, float* opacity, float* weights,
+                               float* d_enc_level_max, void* stream) {
   if (int e = check_rays(rays, z, n_rays, n_samples, "lnr_field_train")) return e;
   if (int e = check_lp(lp, "lnr_field_train")) return e;
   LNR_REQUIRE(n_samples % 64 == 0, "lnr_field_train: n_samples=%d must be a multiple of 64", n_samples);
@@ -990,7 +1036,7 @@ extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t e
   a.w = w; a.enc = enc; a.enc_stride = enc_stride; a.rays = rays; a.z = z; a.depth_gt = depth_gt;
   a.n_rays = n_rays; a.S = n_samples; a.noise_std = noise_std; a.noise = noise; a.key = key;
   a.ray_offset = ray_offset; a.lp = *lp; a.d_enc = d_enc; a.dw_slab = workspace; a.ray_stats = ray_stats;
-  a.depth = depth; a.opacity = opacity; a.weights = weights;
+  a.depth = depth; a.opacity = opacity; a.weights = weights; a.denc_max = d_enc_level_max;
   hipStream_t st = as_stream(stream);
   int nb;
   const int C = n_samples / 64;
@@ -1016,6 +1062,12 @@ extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t e
     nb = field_blocks(n_rays);
     int e = launch_field<true, false, kSigmaMLP>(a, nb, st, "lnr_field_train");
     if (e) return e;
+    if (d_enc_level_max) {
+      LNR_REQUIRE(hipMemsetAsync(d_enc_level_max, 0, kSigmaLevels * sizeof(float), st) == hipSuccess,
+                  "lnr_field_train: memset failed");
+      hipLaunchKernelGGL(k_denc_max, dim3(256, kSigmaLevels), dim3(256), 0, st, reinterpret_cast<const float2*>(d_enc),
+                         enc_stride, n_rays * (int64_t)n_samples, d_enc_level_max);
+    }
   }
   hipLaunchKernelGGL(k_reduce_slabs, dim3((LNR_SIGMA_MLP_PARAMS + 63) / 64), dim3(64 * kSlabWaves), 0, st, workspace, nb, d_w);
   LNR_RETURN_LAUNCH("lnr_field_train(reduce)");

@@ -21,23 +21,11 @@ constexpr int kChunkLog2 = 12;
 constexpr int kChunk = 1 << kChunkLog2;
 constexpr int kMaxChunksPerLevel = 128;
 constexpr int kMaxBuckets = 2048;
-// Records per accumulation work item.  Buckets with more records are split into slices whose int64
-// fixed-point partial chunks (one scale per bucket) k_bwd_finalize sums exactly: which records
-// land in which slice depends on LDS-atomic order, the integer sum does not;
-// 2^18 gives ~3 rounds of work items over the 512 resident 64 KB-LDS workgroups at C2/C4 sizes.
-#ifndef LNR_SLICE_LOG2
-#define LNR_SLICE_LOG2 18
-#endif
-constexpr int64_t kSliceRecords = int64_t(1) << LNR_SLICE_LOG2;
-// Slice size of the coarse (run-merging) levels' buckets, tunable on its own: they are few buckets
-// holding most of their level's records (level 0 is one 4096-entry chunk).  Measured at C2: 2^16 and
-// 2^17 cut those levels' accumulation in isolation (436 -> 231 us at level 0) but not the fused
-// all-level launch (~650 us either way), while k_bwd_finalize, which sums a split bucket's partial
-// chunks in one workgroup, grew 39 -> 71 -> 127 us; so the default equals the fine levels'.
-#ifndef LNR_SLICE_LOG2_COARSE
-#define LNR_SLICE_LOG2_COARSE LNR_SLICE_LOG2
-#endif
-constexpr int64_t kSliceRecordsCoarse = int64_t(1) << LNR_SLICE_LOG2_COARSE;
+// The accumulation splits the records of a bucket range evenly over kAccumGroups workgroups (two
+// 64 KB-LDS workgroups per CU of the 256): each walks its own record range bucket by bucket, so
+// every CU does the same work whatever the bucket sizes.  A bucket cut by a range boundary leaves an
+// int64 partial chunk per piece (at most two per workgroup) that k_bwd_finalize adds exactly.
+constexpr int kAccumGroups = 512;
 
 struct GridArgs {
   LevelParams lv[LNR_MAX_LEVELS];
@@ -50,7 +38,7 @@ struct GridArgs {
 // Levels whose cell edge spans several consecutive samples of a ray (resolution <= 256 at the
 // reference's ray lengths / sample counts) produce runs of equal corner indices.
 #ifndef LNR_MERGE_MAX_RES
-#define LNR_MERGE_MAX_RES 256
+#define LNR_MERGE_MAX_RES 512
 #endif
 inline uint32_t merge_levels_for(const lnr_grid_desc* d) {
   uint32_t m = 0;
@@ -381,47 +369,49 @@ __device__ __forceinline__ void run_sum_i64(const RunInfo& ri, long long& v0, lo
 constexpr int kSB = LNR_KSB;        // samples per histogram row / count / scatter workgroup
 constexpr int kRowsPerChunk = 256;  // histogram rows per scan chunk
 
-// Record values: two fp32 (12-B records with the word).  -DLNR_REC_PACKED: the two values share one
-// exponent with 12-bit signed mantissas (4 B: bits 0-11 m0, 12-23 m1, 24-31 E + 127;
-// v = m 2^(E - 11), 2^(E-1) <= max|v| < 2^E): fp16-level precision, 8-B records, a third less
-// record traffic.  Measured at C2 it is SLOWER (3.23 -> 3.32 ms/step: the scatter and the
-// accumulation are not bound by the record bytes alone, and packing costs VALU), so it is off.
-#ifndef LNR_REC_PACKED
-typedef float2 RecVal;
-__device__ __forceinline__ RecVal pack_rec(float v0, float v1) { return make_float2(v0, v1); }
-__device__ __forceinline__ float2 unpack_rec(RecVal r) { return r; }
-#else
-typedef uint32_t RecVal;
-__device__ __forceinline__ RecVal pack_rec(float v0, float v1) {
-  const float a = fmaxf(fabsf(v0), fabsf(v1));
-  if (!(a > 0.f) || !(a < INFINITY)) return 0u;  // zeros; non-finite gradients are flagged upstream
-  int E;
-  frexpf(a, &E);  // a = f 2^E, f in [0.5, 1)
-  E = E < -126 ? -126 : E;
-  const float s = ldexpf(1.f, 11 - E);
-  const int m0 = min(max(__float2int_rn(v0 * s), -2047), 2047);
-  const int m1 = min(max(__float2int_rn(v1 * s), -2047), 2047);
-  return ((uint32_t)m0 & 0xFFFu) | (((uint32_t)m1 & 0xFFFu) << 12) | ((uint32_t)(E + 127) << 24);
-}
-__device__ __forceinline__ float2 unpack_rec(RecVal r) {
-  const float s = ldexpf(1.f, (int)(r >> 24) - 127 - 11);
-  const int m0 = ((int)(r << 20)) >> 20, m1 = ((int)(r << 8)) >> 20;
-  return make_float2((float)m0 * s, (float)m1 * s);
-}
+// Record values, at a per-level power-of-two scale 2^k_l from the level's max |d_enc| (ws.level_max,
+// known before the scatter): every fine or generic record is w * g with w <= 1, and a coherent
+// record sums at most one wave's run of 64 lanes, so |v| 2^k_l < 2^15.
+//   default (LNR_REC_F16=1): two fp16 of v 2^k_l (8-B records {word, half2}); each record rounds to
+//                  11 bits (relative 2^-12), where tcnn's own fp16 gradient rounds every partial sum
+//   LNR_REC_F16=0: two fp32, unscaled (12-B records: a word array and a float2 array)
+// The accumulation adds v 2^(k_l + kFixedExp) as int32 into int64 sums, exact and order-free.
+#ifndef LNR_REC_F16
+#define LNR_REC_F16 1
 #endif
+constexpr bool kRecF16 = LNR_REC_F16 != 0;
+__device__ __forceinline__ int rec_exp_for(float level_max, bool coherent) {
+  int E;
+  frexpf(level_max, &E);  // level_max < 2^E (E = 0 for 0)
+  const int k = 15 - E - (coherent ? 6 : 0);
+  return k > 100 ? 100 : (k < -60 ? -60 : k);
+}
+__device__ __forceinline__ uint32_t rec_half2(float v0, float v1, float s) {
+  const _Float16 a = (_Float16)(v0 * s), b = (_Float16)(v1 * s);
+  return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+}
+// the two value words of a record: fp16 pair (+ 0) or the two fp32 bit patterns
+__device__ __forceinline__ uint2 rec_vals(float v0, float v1, float s) {
+  if (kRecF16) return make_uint2(rec_half2(v0, v1, s), 0u);
+  return make_uint2(__float_as_uint(v0), __float_as_uint(v1));
+}
+__device__ __forceinline__ float rec_v0(uint32_t a, uint32_t) {
+  return kRecF16 ? (float)__builtin_bit_cast(_Float16, (uint16_t)(a & 0xFFFFu)) : __uint_as_float(a);
+}
+__device__ __forceinline__ float rec_v1(uint32_t a, uint32_t b) {
+  return kRecF16 ? (float)__builtin_bit_cast(_Float16, (uint16_t)(a >> 16)) : __uint_as_float(b);
+}
 
 struct BwdWorkspace {
   uint32_t* hist;        // per level l: [n_sb][nb_l] record counts -> exclusive offsets within bucket
   uint32_t* chunk_sum;   // [L][n_chunks][kMaxChunksPerLevel] per-chunk column sums (k_bwd_chunk_sums)
-  float* blockmax;       // [L][n_sb] max |record value| per row
-  float* level_max;      // [LNR_MAX_LEVELS]
+  float* level_max;      // [LNR_MAX_LEVELS] max |d_enc| per level (as uint bits: k_denc_level_max's atomicMax)
   uint32_t* counts;      // [kMaxBuckets]
   uint64_t* seg_start;   // [kMaxBuckets + 1]
-  uint32_t* slice_pre;   // [kMaxBuckets + 1] work-item prefix over buckets
-  uint32_t* part_pre;    // [kMaxBuckets + 1] partial-chunk prefix (multi-slice buckets only)
-  long long* partial;    // [max_partials][2 * kChunk] int64 fixed-point partial sums of split buckets
-  uint32_t* rec_w;       // [8 * N * L] record words (see "Backward records")
-  RecVal* rec_v;         // [8 * N * L] record values (see "Backward records")
+  long long* partial;    // [2 kAccumGroups][2 * kChunk] int64 fixed-point partial sums of cut buckets
+  uint32_t* rec;         // [8 * N * L] records: LNR_REC_F16 {word, half2} pairs; else the words, then
+                         // (rec_v) the float2 values (see "Backward records")
+  float2* rec_v;
   uint8_t* ovf;          // [L][n_sb] 1 where the level-looped scatter left (row, level) to k_bwd_scatter_overflow
   int64_t n_sb;
   int64_t n_chunks;
@@ -430,36 +420,24 @@ struct BwdWorkspace {
 inline int64_t bwd_n_sb(int64_t n) { return (n + kSB - 1) / kSB; }
 inline int64_t bwd_n_chunks(int64_t n) { return (bwd_n_sb(n) + kRowsPerChunk - 1) / kRowsPerChunk; }
 
-// Upper bound on the partial chunks: a split bucket holds c > slice records in
-// ceil(c / slice) <= 2c / slice slices, and sum(c) <= 8 N per level.
-inline uint32_t merge_levels_for(const lnr_grid_desc* d);
-inline int64_t bwd_max_partials(const lnr_grid_desc* d, int64_t n) {
-  const int64_t m = merge_levels_for(d);
-  return 2 * (8 * n * m) / kSliceRecordsCoarse + 2 * (8 * n * ((int64_t)d->n_levels - m)) / kSliceRecords + 2;
-}
-
 inline int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
 
 struct WsLayout {
-  int64_t hist, chunk_sum, blockmax, level_max, counts, seg_start, slice_pre, part_pre, partial, rec_w, rec_v, ovf, total;
+  int64_t hist, chunk_sum, level_max, counts, seg_start, partial, rec, ovf, total;
 };
 
 inline WsLayout ws_layout(const lnr_grid_desc* d, const GridArgs& a, int64_t n) {
   const int64_t nsb = bwd_n_sb(n), nch = bwd_n_chunks(n);
   WsLayout w{};
   int64_t b = 0;
+  w.level_max = b; b += align256(LNR_MAX_LEVELS * 4);  // first: its address does not depend on n
   w.hist = b;      b += align256((int64_t)a.n_buckets * nsb * 4);
   w.chunk_sum = b; b += align256((int64_t)d->n_levels * nch * kMaxChunksPerLevel * 4);
-  w.blockmax = b;  b += align256((int64_t)d->n_levels * nsb * 4);
-  w.level_max = b; b += align256(LNR_MAX_LEVELS * 4);
   w.counts = b;    b += align256(kMaxBuckets * 4);
   w.seg_start = b; b += align256((kMaxBuckets + 1) * 8);
-  w.slice_pre = b; b += align256((kMaxBuckets + 1) * 4);
-  w.part_pre = b;  b += align256((kMaxBuckets + 1) * 4);
-  w.partial = b;   b += align256(bwd_max_partials(d, n) * 2 * kChunk * 8);
+  w.partial = b;   b += align256((int64_t)2 * kAccumGroups * 2 * kChunk * 8);
   // +2 records: the accumulate loads records in pairs
-  w.rec_w = b;     b += align256((8 * n * (int64_t)d->n_levels + 2) * 4);
-  w.rec_v = b;     b += align256((8 * n * (int64_t)d->n_levels + 2) * (int64_t)sizeof(RecVal));
+  w.rec = b;       b += align256((8 * n * (int64_t)d->n_levels + 2) * (kRecF16 ? 8 : 12));
   w.ovf = b;       b += align256(nsb * (int64_t)d->n_levels);
   w.total = b;
   return w;
@@ -473,15 +451,12 @@ inline BwdWorkspace carve_workspace(void* base, const GridArgs& a, const lnr_gri
   BwdWorkspace w{};
   w.hist = reinterpret_cast<uint32_t*>(p + L.hist);
   w.chunk_sum = reinterpret_cast<uint32_t*>(p + L.chunk_sum);
-  w.blockmax = reinterpret_cast<float*>(p + L.blockmax);
   w.level_max = reinterpret_cast<float*>(p + L.level_max);
   w.counts = reinterpret_cast<uint32_t*>(p + L.counts);
   w.seg_start = reinterpret_cast<uint64_t*>(p + L.seg_start);
-  w.slice_pre = reinterpret_cast<uint32_t*>(p + L.slice_pre);
-  w.part_pre = reinterpret_cast<uint32_t*>(p + L.part_pre);
   w.partial = reinterpret_cast<long long*>(p + L.partial);
-  w.rec_w = reinterpret_cast<uint32_t*>(p + L.rec_w);
-  w.rec_v = reinterpret_cast<RecVal*>(p + L.rec_v);
+  w.rec = reinterpret_cast<uint32_t*>(p + L.rec);
+  w.rec_v = reinterpret_cast<float2*>(w.rec + (8 * n * (int64_t)d->n_levels + 2));  // after the words (fp32 records)
   w.ovf = reinterpret_cast<uint8_t*>(p + L.ovf);
   w.n_sb = bwd_n_sb(n);
   w.n_chunks = bwd_n_chunks(n);
@@ -494,8 +469,8 @@ __device__ __forceinline__ uint32_t* hist_row(const GridArgs& a, const BwdWorksp
   return ws.hist + (int64_t)a.bucket_base[l] * ws.n_sb + sb * nb;
 }
 
-// Backward records.  12 bytes, stored SoA: a word w = entry within its 4096-entry chunk (bits 0-11)
-// | pair code p (bits 12-15) | tx as unorm16 (bits 16-31), and a float2 of values.
+// Backward records.  A word w = entry within its 4096-entry chunk (bits 0-11) | pair code p (bits
+// 12-15) | tx as unorm16 (bits 16-31), and two values (see "Record values").
 //   p = 0  one corner; the values are its (g0, g1) contribution (coherent levels: summed over the
 //          run of lanes that share the corner).
 //   p > 0  the two x-adjacent corners e0 and e1 = e0 ^ (2^p - 1) of one y/z edge, in one chunk; the

@@ -96,68 +96,29 @@ __global__ void __launch_bounds__(kMaxChunksPerLevel) k_bwd_scan_rows(GridArgs a
   }
 }
 
-// Bucket segment starts, work-item (slice) prefix and split-bucket partial prefix.
-__global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint32_t n_buckets, uint32_t coarse_end) {
+// Bucket segment starts: exclusive prefix of the bucket totals (records are laid out bucket-major).
+__global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint32_t n_buckets) {
   __shared__ uint64_t w_seg[16];
-  __shared__ uint32_t w_sl[16], w_pp[16];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  // two buckets per thread (n_buckets <= kMaxBuckets = 2048)
-  uint64_t seg[2];
-  uint32_t sl[2], pp[2];
+  uint64_t seg[2];  // two buckets per thread (n_buckets <= kMaxBuckets = 2048)
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const uint32_t b = 2 * t + q;
-    const uint32_t c = b < n_buckets ? ws.counts[b] : 0u;
-    const int64_t slr = b < coarse_end ? kSliceRecordsCoarse : kSliceRecords;
-    const uint32_t k = (uint32_t)((c + slr - 1) / slr);
-    seg[q] = c;
-    sl[q] = b < n_buckets ? (k > 0 ? k : 1) : 0u;
-    pp[q] = b < n_buckets && k > 1 ? k : 0u;
-  }
+  for (int q = 0; q < 2; ++q) seg[q] = 2 * t + q < (int)n_buckets ? ws.counts[2 * t + q] : 0u;
   uint64_t iseg = seg[0] + seg[1];
-  uint32_t isl = sl[0] + sl[1], ipp = pp[0] + pp[1];
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint64_t a0 = __shfl_up(iseg, o, 64);
-    const uint32_t a1 = __shfl_up(isl, o, 64), a2 = __shfl_up(ipp, o, 64);
-    if (lane >= o) {
-      iseg += a0;
-      isl += a1;
-      ipp += a2;
-    }
+    if (lane >= o) iseg += a0;
   }
-  if (lane == 63) {
-    w_seg[wid] = iseg;
-    w_sl[wid] = isl;
-    w_pp[wid] = ipp;
-  }
+  if (lane == 63) w_seg[wid] = iseg;
   lds_barrier();
   uint64_t bseg = 0;
-  uint32_t bsl = 0, bpp = 0;
-  for (int w = 0; w < wid; ++w) {
-    bseg += w_seg[w];
-    bsl += w_sl[w];
-    bpp += w_pp[w];
-  }
-  // exclusive values at this thread's first bucket
-  uint64_t e_seg = bseg + iseg - seg[0] - seg[1];
-  uint32_t e_sl = bsl + isl - sl[0] - sl[1], e_pp = bpp + ipp - pp[0] - pp[1];
-  if (t == 1023) {  // totals (n_buckets may equal 2 * blockDim)
-    ws.seg_start[n_buckets] = bseg + iseg;
-    ws.slice_pre[n_buckets] = bsl + isl;
-    ws.part_pre[n_buckets] = bpp + ipp;
-  }
+  for (int w = 0; w < wid; ++w) bseg += w_seg[w];
+  uint64_t e_seg = bseg + iseg - seg[0] - seg[1];  // exclusive value at this thread's first bucket
+  if (t == 1023) ws.seg_start[n_buckets] = bseg + iseg;  // total (n_buckets may equal 2 * blockDim)
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    const uint32_t b = 2 * t + q;
-    if (b < n_buckets) {
-      ws.seg_start[b] = e_seg;
-      ws.slice_pre[b] = e_sl;
-      ws.part_pre[b] = e_pp;
-    }
+    if (2 * t + q < (int)n_buckets) ws.seg_start[2 * t + q] = e_seg;
     e_seg += seg[q];
-    e_sl += sl[q];
-    e_pp += pp[q];
   }
 }
 
@@ -182,6 +143,7 @@ __device__ __forceinline__ int64_t xcd_row(uint32_t bx, uint32_t n) {
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // KIND: the levels one launch covers, so each gets only its own code and registers.
 // kLevelsAny: one launch over every level, grid.x = rows x levels with the level fastest, so each CU
@@ -192,19 +154,28 @@ enum : int { kLevelsCoherent = 0, kLevelsFine = 1, kLevelsGeneric = 2, kLevelsAn
 #ifndef LNR_SCATTER_WAVES_PER_EU
 #define LNR_SCATTER_WAVES_PER_EU 1
 #endif
+// Record slot dst <- {word, value words} (Record values in hashgrid.hpp)
+__device__ __forceinline__ void rec_store(const BwdWorkspace& ws, uint64_t dst, uint32_t word, uint32_t va, uint32_t vb) {
+  if (kRecF16) {
+    *reinterpret_cast<u32x2*>(ws.rec + 2 * dst) = u32x2{word, va};
+  } else {
+    ws.rec[dst] = word;
+    *reinterpret_cast<u32x2*>(&ws.rec_v[dst]) = u32x2{va, vb};
+  }
+}
+
 // One (histogram row sb, level l) of the scatter; KIND as below, kLevelsAny meaning "any level".
 template <class PosFn, int KIND>
 __device__ __forceinline__ void scatter_row_level(const GridArgs& a, const PosFn& pos, int64_t n,
                                                   const float2* __restrict__ d_enc, int64_t stride,
                                                   const BwdWorkspace& ws, uint32_t l, int64_t sb, bool skip_zero,
                                                   char* smem) {
-  RecVal* stage_v = reinterpret_cast<RecVal*>(smem);                         // [kCap]
+  uint2* stage_v = reinterpret_cast<uint2*>(smem);                           // [kCap] value words
   uint64_t* gbase = reinterpret_cast<uint64_t*>(stage_v + kCap);             // [kMaxChunksPerLevel]
   uint32_t* stage_w = reinterpret_cast<uint32_t*>(gbase + kMaxChunksPerLevel);  // [kCap]
   uint32_t* rank_ctr = stage_w + kCap;                                       // [kMaxChunksPerLevel]
   uint32_t* start = rank_ctr + kMaxChunksPerLevel;                           // [kMaxChunksPerLevel + 1]
-  float* wmax = reinterpret_cast<float*>(start + kMaxChunksPerLevel + 1);    // [kSB / 64]
-  uint8_t* sbk = reinterpret_cast<uint8_t*>(wmax + kSB / 64);                // [kCap] bucket of each staged record
+  uint8_t* sbk = reinterpret_cast<uint8_t*>(start + kMaxChunksPerLevel + 1);  // [kCap] bucket of each staged record
   const int kind = KIND != kLevelsAny ? KIND
                    : a.lv[l].fine           ? kLevelsFine
                    : l < a.merge_levels     ? kLevelsCoherent
@@ -215,6 +186,7 @@ __device__ __forceinline__ void scatter_row_level(const GridArgs& a, const PosFn
   const uint32_t b0 = a.bucket_base[l];
   const uint32_t nb = a.bucket_base[l + 1] - b0;
   const LevelParams& lv = a.lv[l];
+  const float rs = ldexpf(1.f, rec_exp_for(ws.level_max[l], l < a.merge_levels));  // record scale
   static_assert(kMaxChunksPerLevel <= 128, "two buckets per lane of wave 0");
   LNR_STAMP(t0);
   // 1. Global loads, all unconditional (clamped indices) so nothing waits for them before it must:
@@ -271,20 +243,17 @@ __device__ __forceinline__ void scatter_row_level(const GridArgs& a, const PosFn
   // fine / generic levels: samples with a zero gradient emit nothing when the histogram was
   // counted after the MLP backward (k_bwd_count, same predicate); coherent levels keep every lane
   const bool act = in && (!skip_zero || g.x != 0.f || g.y != 0.f);
-  float m = 0.f;
   bool staged = true;
   auto place = [&](bool valid, uint32_t bk, uint32_t rank, uint32_t word, float2 val) {
     if (!valid) return;
-    m = fmaxf(m, fmaxf(fabsf(val.x), fabsf(val.y)));
+    const uint2 h = rec_vals(val.x, val.y, rs);
     if (staged) {
       const uint32_t t = start[bk] + rank;
       stage_w[t] = word;
-      stage_v[t] = pack_rec(val.x, val.y);
+      stage_v[t] = h;
       sbk[t] = (uint8_t)bk;
     } else {
-      const uint64_t dst = gbase[bk] + rank;
-      ws.rec_w[dst] = word;
-      ws.rec_v[dst] = pack_rec(val.x, val.y);
+      rec_store(ws, gbase[bk] + rank, word, h.x, h.y);
     }
   };
   // 2. records: rank, then place (hashgrid.hpp "Backward records")
@@ -356,28 +325,16 @@ __device__ __forceinline__ void scatter_row_level(const GridArgs& a, const PosFn
       }
     }
   }
-  m = wave_max(m);
-  if (lane == 0) wmax[wid] = m;
   LNR_STAMP(t2);
   lds_barrier();
   LNR_STAMP(t3);
-  if (wid == 0) {
-    float mm = lane < kSB / 64 ? wmax[lane] : 0.f;
-    mm = wave_max(mm);
-    if (lane == 0) ws.blockmax[(int64_t)l * ws.n_sb + sb] = mm;
-  }
   // 3. copy the staged row out in bucket order (consecutive lanes -> consecutive slots of a run)
   if (staged) {
     const uint32_t total = start[nb];
     for (uint32_t t = threadIdx.x; t < total; t += kSB) {
       const uint32_t bk = sbk[t];
       const uint64_t dst = gbase[bk] + (t - start[bk]);
-#ifndef LNR_EXP_SKIP_STORE
-      ws.rec_w[dst] = stage_w[t];
-      ws.rec_v[dst] = stage_v[t];
-#else
-      if (stage_w[t] == 0x12345678u) ws.rec_w[dst] = 0;
-#endif
+      rec_store(ws, dst, stage_w[t], stage_v[t].x, stage_v[t].y);
     }
   }
   LNR_STAMP(t4);
@@ -446,11 +403,9 @@ struct RowsLds {  // the small tables first: their addresses fit the 16-bit LDS 
   uint2 sg[NL][NB];           // per level and bucket: {start in the stage, global slot of the run}
   uint32_t total[NL];         // records of the row at each level
   uint32_t ctr[2][NB];        // rank counters
-  float wmax[2][kSB / 64];
   LevelParams lv[NL];         // the level table (kernel arguments indexed per level would be loads)
-  uint4 stage[2][kRowsCap];   // staged records {word, global slot, v0, v1}, bucket order
+  uint4 stage[2][kRowsCap];   // staged records {word, global slot, value words}, bucket order
 };
-static_assert(sizeof(RecVal) == 8, "the level-looped scatter stages fp32 record values");
 
 // NL levels, the first NM coherent (run-merging) and the rest fine, at most NB buckets per level:
 // compile-time, so the level loop unrolls into straight-line code.  Record slots are 32-bit (the
@@ -468,7 +423,6 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const bool last = sb + 1 >= ws.n_sb;
   const int64_t ic = in ? i : n - 1;
-  uint32_t* rec_v32 = reinterpret_cast<uint32_t*>(ws.rec_v);
   const uint32_t spare = (uint32_t)(8 * n * (int64_t)NL);  // one of the 2 slack records past the last slot
 
   // prologue 1: the level table and zero rank counters
@@ -498,6 +452,9 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ 
       }
     }
   }
+  float rsc[NL];  // per-level record scales (uniform: scalar loads)
+#pragma unroll
+  for (int l = 0; l < NL; ++l) rsc[l] = ldexpf(1.f, rec_exp_for(ws.level_max[l], l < NM));
   float x = 0.f, y = 0.f, z = 0.f;
   pos.eval(raw, x, y, z);
   // prologue 3: wave w's levels' bucket starts (a wave prefix over the buckets, two per lane)
@@ -520,9 +477,8 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ 
   }
   lds_barrier();
 
-  // copy level l's staged row out (consecutive threads -> consecutive slots of a run); a second wave
-  // publishes the row's max |value|.  Every lane stores on every trip (lanes past the row's records
-  // into the spare slot), so the trip count is fixed
+  // copy level l's staged row out (consecutive threads -> consecutive slots of a run).  Every lane
+  // stores on every trip (lanes past the row's records into the spare slot), so the trip count is fixed
   auto copy_out = [&](uint32_t l) {
     const int sbuf = l & 1;
     const uint32_t total = sm.total[l];
@@ -532,12 +488,7 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ 
       const uint32_t t = threadIdx.x + u * kSB;
       const uint4 q = sm.stage[sbuf][t < (uint32_t)kRowsCap ? t : kRowsCap - 1];
       const uint32_t d = t < lim ? q.y : spare;
-      ws.rec_w[d] = q.x;
-      *reinterpret_cast<u32x2*>(rec_v32 + 2 * (uint64_t)d) = u32x2{q.z, q.w};
-    }
-    if (wid == 1) {
-      const float mm = wave_max_nonneg(lane < kSB / 64 ? sm.wmax[sbuf][lane] : 0.f);
-      if (lane == 0) ws.blockmax[(int64_t)l * ws.n_sb + sb] = mm;
+      rec_store(ws, d, q.x, q.z, q.w);
     }
   };
 
@@ -551,7 +502,7 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ 
     const float2 gv = in ? make_float2(g[l].x, g[l].y) : make_float2(0.f, 0.f);
     const bool inr = staged && in;  // an unstaged row emits nothing here: k_bwd_scatter_overflow redoes it
     const bool act = inr && (!skip_zero || gv.x != 0.f || gv.y != 0.f);
-    float m = 0.f;
+    const float rs = rsc[l];
     // rank (returning LDS atomics) and place: all start reads, then all atomics, then all writes
     // (one lane-level branch for the 4 records: they share their validity)
     auto place = [&](bool valid, const uint32_t (&bk)[4], const uint32_t (&word)[4], const float2 (&val)[4]) {
@@ -563,10 +514,10 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ 
 #pragma unroll
         for (int k = 0; k < 4; ++k) rank[k] = atomicAdd(&ctr[bk[k]], 1u);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          m = fmaxf(m, fmaxf(fabsf(val[k].x), fabsf(val[k].y)));
-          sm.stage[sbuf][s4[k].x + rank[k]] = make_uint4(word[k], s4[k].y + rank[k], __float_as_uint(val[k].x),
-                                                         __float_as_uint(val[k].y));
+        for (int k = 0; k < 4; ++k)
+        {
+          const uint2 h = rec_vals(val[k].x, val[k].y, rs);
+          sm.stage[sbuf][s4[k].x + rank[k]] = make_uint4(word[k], s4[k].y + rank[k], h.x, h.y);
         }
       }
     };
@@ -619,8 +570,6 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ 
         place(valid, bk4, w4, val4);
       }
     }
-    m = wave_max_nonneg(m);
-    if (lane == 0) sm.wmax[sbuf][wid] = m;
     if (threadIdx.x < NB) sm.ctr[sbuf ^ 1][threadIdx.x] = 0u;  // level l + 1's counters (last used by l - 1)
     if (l >= 1) copy_out(l - 1);
     lds_barrier();
@@ -628,109 +577,188 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ 
   copy_out(NL - 1);
 }
 
-constexpr size_t kScatterLds = (size_t)kCap * sizeof(RecVal) + kMaxChunksPerLevel * 8 + (size_t)kCap * 4 + kMaxChunksPerLevel * 4 +
-                               (kMaxChunksPerLevel + 1) * 4 + (kSB / 64) * 4 + kCap;
+constexpr size_t kScatterLds = (size_t)kCap * 8 + kMaxChunksPerLevel * 8 + (size_t)kCap * 4 + kMaxChunksPerLevel * 4 +
+                               (kMaxChunksPerLevel + 1) * 4 + kCap;
 static_assert(kScatterLds <= 65536, "scatter LDS within the default dynamic limit");
 
-__global__ void __launch_bounds__(256) k_bwd_level_max(BwdWorkspace ws) {
+// Max |d_enc| per level (the record scales): grid (kMaxBlocks, L), grid-stride float2 loads, one
+// atomicMax per workgroup on the float's bits (non-negative floats order as their bit patterns).
+// ws.level_max is zeroed before.
+constexpr int kMaxBlocks = 256;
+__global__ void __launch_bounds__(256) k_denc_level_max(const float2* __restrict__ d_enc, int64_t stride, int64_t n,
+                                                        BwdWorkspace ws) {
   __shared__ float red[4];
-  const float* col = ws.blockmax + (int64_t)blockIdx.x * ws.n_sb;
+  const uint32_t l = blockIdx.y;
+  const float2* src = d_enc + (int64_t)l * stride;
   float m = 0.f;
-  for (int64_t j = threadIdx.x; j < ws.n_sb; j += 256) m = fmaxf(m, col[j]);
-  m = wave_max(m);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)kMaxBlocks * 256) {
+    const float2 g = src[i];
+    m = fmaxf(m, fmaxf(fabsf(g.x), fabsf(g.y)));
+  }
+  m = wave_max_nonneg(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   lds_barrier();
-  if (threadIdx.x == 0) ws.level_max[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (m > 0.f) atomicMax(reinterpret_cast<uint32_t*>(ws.level_max) + l, __float_as_uint(m));
+  }
 }
 
-constexpr int kAccumThreads = 1024;
+#ifndef LNR_ACCUM_THREADS
+#define LNR_ACCUM_THREADS 1024
+#endif
+constexpr int kAccumThreads = LNR_ACCUM_THREADS;
 
-// Fixed-point exponent of bucket b: |record| < 2^E (the level's max) and at most cnt records in the
-// bucket, so every value, and every partial or total sum, stays below 2^50 in magnitude: inside the
-// exact-integer range of the double-precision conversion below.  The unit is 2^(lg cnt + E - 50),
-// about 2^-32 of the level maximum at C2's bucket sizes.
-__device__ __forceinline__ int bucket_k2(const BwdWorkspace& ws, uint32_t l, uint32_t b) {
-  int E;
-  frexpf(ws.level_max[l], &E);
+// Fixed-point exponent of bucket b, in the records' scaled units: |record| < 2^15 and at most cnt
+// records in the bucket.  Each converted value stays below 2^51 (the exact range of the double
+// conversion below: k2 <= 36) and every partial or total sum below 2^62 (k2 <= 47 - lg cnt), so the
+// int64 sums never overflow.  The unit is 2^(lg cnt - 47) of the scaled units, about 2^-44 of the
+// level's largest possible record at C2's bucket sizes.  (Precision here matters beyond the
+// gradients' own: Adam's eps = 1e-8 turns a one-unit difference of a near-zero gradient entry into
+// a visible step, so two runs must round alike far below the gradients' scale.)
+__device__ __forceinline__ int bucket_k2(const BwdWorkspace& ws, uint32_t b) {
   const uint64_t bcnt = ws.seg_start[b + 1] - ws.seg_start[b];
   const int lg = 64 - __clzll((long long)(bcnt > 0 ? bcnt : 1));  // ceil-ish log2(cnt + 1)
-  const int k2 = 50 - lg - E;
-  return k2 > 120 ? 120 : (k2 < -120 ? -120 : k2);
+  return 47 - lg < 36 ? 47 - lg : 36;
 }
-
+// 2^-(k2 + k_l): fixed-point units back to gradient units (double: the exponent may pass fp32's range)
+__device__ __forceinline__ double unit_back(const GridArgs& a, const BwdWorkspace& ws, uint32_t l, int k2) {
+  return ldexp(1.0, -(k2 + rec_exp_for(ws.level_max[l], l < a.merge_levels)));
+}
 // round(x) as int64 for |x| < 2^51: x + 1.5 2^52 in double places the rounded integer in the low
 // mantissa bits, and the constant's low word is 0, so only the high word needs the subtraction.
 __device__ __forceinline__ unsigned long long fixed_i64(float x) {
   const double d = (double)x + 6755399441055744.0;
-  const unsigned long long b = (unsigned long long)__double_as_longlong(d);
-  return b - 0x4338000000000000ull;
+  const unsigned long long bits = (unsigned long long)__double_as_longlong(d);
+  return bits - 0x4338000000000000ull;
 }
 
 #ifndef LNR_ACCUM_WAVES_PER_EU
 #define LNR_ACCUM_WAVES_PER_EU 8
 #endif
 #ifndef LNR_ACCUM_LOADS
-#define LNR_ACCUM_LOADS 2
+#define LNR_ACCUM_LOADS 8
 #endif
+// Workgroup i's record range [range_at(i), range_at(i + 1)) of the R records from r0: an even split.
+__device__ __forceinline__ uint64_t range_at(uint64_t r0, uint64_t R, uint32_t i) {
+  return r0 + (R * i) / kAccumGroups;
+}
+// The workgroup whose range holds record p (r0 <= p < r0 + R): the last i with range_at(i) <= p.
+__device__ __forceinline__ uint32_t group_of(uint64_t r0, uint64_t R, uint64_t p) {
+  uint32_t i = (uint32_t)(((p - r0) * kAccumGroups) / R);
+  while (i + 1 < (uint32_t)kAccumGroups && range_at(r0, R, i + 1) <= p) ++i;
+  while (i > 0 && range_at(r0, R, i) > p) --i;
+  return i;
+}
+__device__ __forceinline__ uint32_t level_of_bucket(const GridArgs& a, uint32_t b) {
+  uint32_t l = 0;
+  while (l + 1 < a.n_levels && a.bucket_base[l + 1] <= b) ++l;
+  return l;
+}
+
+#ifdef LNR_EXP_WG_TIMES
+// diagnostic (experiment builds): per accumulate workgroup {start, end, records, first level}
+static __device__ unsigned long long g_wg[kAccumGroups][4];
+extern "C" int lnr_debug_accum_wg(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg), sizeof(g_wg)) == hipSuccess ? 0 : -1;
+}
+#endif
+
+// One workgroup per kAccumGroups-th of the records of buckets [b_begin, b_end).  Per bucket piece:
+// int64 fixed-point sums in a 64 KB LDS chunk with ds_add_u64, then the fp32 gradient (a whole
+// bucket) or the piece's int64 partial chunk (a bucket the range boundaries cut; partial slot 2i for
+// a piece cut at its start, 2i + 1 for one cut only at its end).
 __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_accum(GridArgs a, BwdWorkspace ws, float* __restrict__ d_table,
                                                                                         uint32_t b_begin, uint32_t b_end) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [2][kChunk] int64 fixed point
   // (one array per feature: 8-B atomics on random entries spread over twice the bank pairs)
-  const uint32_t nbk = a.n_buckets;
-  const uint32_t s_end = ws.slice_pre[b_end];  // work items of buckets [b_begin, b_end)
   const int lane = threadIdx.x & 63;
-  for (uint32_t s = ws.slice_pre[b_begin] + blockIdx.x; s < s_end; s += gridDim.x) {
-    uint32_t lo = 0, hi = nbk;  // bucket b with slice_pre[b] <= s < slice_pre[b+1]
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (ws.slice_pre[mid] <= s) lo = mid;
-      else hi = mid;
-    }
-    const uint32_t b = lo;
-    const uint32_t nsl = ws.slice_pre[b + 1] - ws.slice_pre[b];
-    const uint32_t j = s - ws.slice_pre[b];
-    const uint64_t slr = b < a.bucket_base[a.merge_levels] ? kSliceRecordsCoarse : kSliceRecords;
-    const uint64_t beg = ws.seg_start[b] + (uint64_t)j * slr;
-    uint64_t end = ws.seg_start[b + 1];
-    if (beg + slr < end) end = beg + slr;
-    uint32_t l = 0;
-    while (l + 1 < a.n_levels && a.bucket_base[l + 1] <= b) ++l;
-    const uint32_t chunk = b - a.bucket_base[l];
-    const uint32_t ent0 = chunk * kChunk;
+  const int mix = (int)((((uint32_t)lane * 0x9E3779B1u) >> 16) ^ (uint32_t)(lane >> 2)) & (2 * LNR_ACCUM_LOADS - 1);
+  const uint64_t r0 = ws.seg_start[b_begin], R = ws.seg_start[b_end] - r0;
+#ifdef LNR_ACCUM_PAIR_REVERSE
+  const uint32_t gi = blockIdx.x < kAccumGroups / 2 ? blockIdx.x : (3 * kAccumGroups / 2 - 1) - blockIdx.x;
+#else
+  const uint32_t gi = blockIdx.x;
+#endif
+  const uint64_t rbeg = range_at(r0, R, gi), rend = range_at(r0, R, gi + 1);
+  if (rbeg >= rend) return;
+#ifdef LNR_EXP_WG_TIMES
+  unsigned long long wg_t0 = 0;
+  if (threadIdx.x == 0) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(wg_t0)::"memory");
+#endif
+  uint32_t lo = b_begin, hi = b_end;  // the bucket holding record rbeg: seg_start[lo] <= rbeg < seg_start[lo + 1]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (ws.seg_start[mid] <= rbeg) lo = mid;
+    else hi = mid;
+  }
+  for (uint32_t b = lo; b < b_end; ++b) {
+    const uint64_t s0 = ws.seg_start[b], s1 = ws.seg_start[b + 1];
+    if (s0 >= rend) break;
+    const uint64_t beg = s0 > rbeg ? s0 : rbeg, end = s1 < rend ? s1 : rend;
+    if (beg >= end) continue;  // empty bucket: k_bwd_finalize writes its zeros
+    const uint32_t l = level_of_bucket(a, b);
+    const uint32_t ent0 = (b - a.bucket_base[l]) * kChunk;
     const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
-    const int k2 = bucket_k2(ws, l, b);  // one scale per bucket: split buckets' partials add exactly
-    const float scale = ldexpf(1.f, k2);
     LNR_STAMP(t0);
     for (int t = threadIdx.x; t < 2 * kChunk; t += blockDim.x) acc[t] = 0ull;
     lds_barrier();
     LNR_STAMP(t1);
-    // 2 records per lane per load (8-B words, 16-B fp32 value pairs), LNR_ACCUM_LOADS loads in flight;
-    // a pair record (p > 0) adds (1 - tx) v to corner e0 and tx v to e1 = e0 ^ (2^p - 1), a single
+    // 2 records per lane per 16-B load, LNR_ACCUM_LOADS loads in flight (2 LNR_ACCUM_LOADS slots).
+    // Atomic instruction u takes slot (u + mix) of each lane, mix a per-lane hash: adjacent records of
+    // a bucket (one ray's consecutive samples: equal or neighbouring corners, whose equal addresses
+    // serialise within one LDS instruction) then rarely meet in one instruction.
+    // A pair record (p > 0) adds (1 - tx) v to corner e0 and tx v to e1 = e0 ^ (2^p - 1), a single
     // record (p = 0, tx = 0) adds v to e0.  int64 sums: the result does not depend on the order.
     const uint64_t beg2 = beg & ~1ull;
+    // one scale per bucket (the pieces' partials add exactly); fp16 records carry 2^k_l already,
+    // fp32 records get it here
+    const int k2 = bucket_k2(ws, b);
+    const float fs = ldexpf(1.f, k2 + (kRecF16 ? 0 : rec_exp_for(ws.level_max[l], l < a.merge_levels)));
+    const float ftx = fs * kInvU16;
     for (uint64_t rb = beg2 + 2 * (threadIdx.x & ~63u); rb < end; rb += 2 * LNR_ACCUM_LOADS * kAccumThreads) {
-      uint2 qw[LNR_ACCUM_LOADS];
-      float4 qv[LNR_ACCUM_LOADS];
+      uint2 qw[LNR_ACCUM_LOADS], qh[LNR_ACCUM_LOADS], qg[LNR_ACCUM_LOADS];  // words, value words a, b
 #pragma unroll
-      for (int u = 0; u < LNR_ACCUM_LOADS; ++u) {
-        const uint64_t rr = rb + 2 * lane + (uint64_t)u * 2 * kAccumThreads;
+      for (int k = 0; k < LNR_ACCUM_LOADS; ++k) {
+        const uint64_t rr = rb + 2 * lane + (uint64_t)k * 2 * kAccumThreads;
         const uint64_t rc = rr < end ? rr : beg2;  // unconditional loads: no branch to wait at
-        const u32x2 w2 = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(&ws.rec_w[rc]));
-        const f32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(&ws.rec_v[rc]));
-        qv[u] = make_float4(v4.x, v4.y, v4.z, v4.w);
-        qw[u] = make_uint2(rr < beg || rr >= end ? kRecNone : w2.x, rr + 1 >= end ? kRecNone : w2.y);
+        uint32_t w0, w1;
+        if (kRecF16) {
+          const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(ws.rec + 2 * rc));
+          w0 = q.x;
+          w1 = q.z;
+          qh[k] = make_uint2(q.y, q.w);
+          qg[k] = make_uint2(0u, 0u);
+        } else {
+          const u32x2 q = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(ws.rec + rc));
+          const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(&ws.rec_v[rc]));
+          w0 = q.x;
+          w1 = q.y;
+          qh[k] = make_uint2(v.x, v.z);  // value 0 of records rc, rc + 1
+          qg[k] = make_uint2(v.y, v.w);  // value 1
+        }
+        qw[k] = make_uint2(rr < beg || rr >= end ? kRecNone : w0, rr + 1 >= end ? kRecNone : w1);
       }
 #pragma unroll
       for (int u = 0; u < 2 * LNR_ACCUM_LOADS; ++u) {
-        const uint32_t w = (u & 1) ? qw[u >> 1].y : qw[u >> 1].x;
+        const int sl = (u + mix) & (2 * LNR_ACCUM_LOADS - 1);
+        uint2 qa = qw[0], qb = qh[0], qc = qg[0];
+#pragma unroll
+        for (int k = 1; k < LNR_ACCUM_LOADS; ++k)
+          if ((sl >> 1) == k) {
+            qa = qw[k];
+            qb = qh[k];
+            qc = qg[k];
+          }
+        const uint32_t w = (sl & 1) ? qa.y : qa.x;
         if (w != kRecNone) {
-          const float v0 = ((u & 1) ? qv[u >> 1].z : qv[u >> 1].x) * scale;
-          const float v1 = ((u & 1) ? qv[u >> 1].w : qv[u >> 1].y) * scale;
+          const uint32_t ha = (sl & 1) ? qb.y : qb.x, hb = (sl & 1) ? qc.y : qc.x;
+          const float v0 = rec_v0(ha, hb), v1 = rec_v1(ha, hb);
           const uint32_t e0 = w & (kChunk - 1);
           const uint32_t p = (w >> kChunkLog2) & 15u;
-          const float tx = (float)(w >> 16) * kInvU16;  // 0 for single-corner records
-          const float s0 = 1.0f - tx;
+          const float tx = (float)(w >> 16) * ftx;  // 0 for single-corner records; pre-scaled
+          const float s0 = fs - tx;
           atomicAdd(&acc[e0], fixed_i64(s0 * v0));
           atomicAdd(&acc[kChunk + e0], fixed_i64(s0 * v1));
           if (p) {
@@ -744,13 +772,13 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
     LNR_STAMP(t2);
     lds_barrier();
     LNR_STAMP(t3);
-    if (nsl == 1) {  // the final values
-      const float inv = ldexpf(1.f, -k2);
+    if (beg == s0 && end == s1) {  // the whole bucket: the final values
+      const double inv = unit_back(a, ws, l, k2);
       float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0);
       for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x)
-        dst[t] = (float)(long long)acc[(t & 1) * kChunk + (t >> 1)] * inv;
-    } else {  // this slice's int64 partial chunk
-      long long* dst = ws.partial + (int64_t)(ws.part_pre[b] + j) * (2 * kChunk);
+        dst[t] = (float)((double)(long long)acc[(t & 1) * kChunk + (t >> 1)] * inv);
+    } else {  // this piece's int64 partial chunk
+      long long* dst = ws.partial + (int64_t)(2 * gi + (beg > s0 ? 0 : 1)) * (2 * kChunk);
       for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) dst[t] = (long long)acc[(t & 1) * kChunk + (t >> 1)];
     }
     lds_barrier();
@@ -762,25 +790,46 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
     LNR_PHASE(20, 1ull, 0ull);
     LNR_PHASE(21, end - beg, 0ull);
   }
+#ifdef LNR_EXP_WG_TIMES
+  if (threadIdx.x == 0) {
+    unsigned long long t1;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+    g_wg[gi][0] = wg_t0;
+    g_wg[gi][1] = t1;
+    g_wg[gi][2] = rend - rbeg;
+    g_wg[gi][3] = level_of_bucket(a, lo);
+  }
+#endif
 }
 
-// Split buckets: d_table = sum of the slices' partial chunks, in slice order (deterministic).
+// Buckets the accumulation did not finish: cut buckets = the sum of their pieces' partial chunks in
+// workgroup order (deterministic), empty buckets = 0.  One workgroup per bucket of [b_begin, b_end).
 __global__ void __launch_bounds__(256) k_bwd_finalize(GridArgs a, BwdWorkspace ws, float* __restrict__ d_table,
-                                                      uint32_t b_begin) {
+                                                      uint32_t b_begin, uint32_t b_end) {
   const uint32_t b = b_begin + blockIdx.x;
-  const uint32_t nsl = ws.part_pre[b + 1] - ws.part_pre[b];
-  if (nsl == 0) return;
-  uint32_t l = 0;
-  while (l + 1 < a.n_levels && a.bucket_base[l + 1] <= b) ++l;
+  const uint64_t r0 = ws.seg_start[b_begin], R = ws.seg_start[b_end] - r0;
+  const uint64_t s0 = ws.seg_start[b], s1 = ws.seg_start[b + 1];
+  uint32_t g0 = 0, g1 = 0;
+  if (s1 > s0) {
+    g0 = group_of(r0, R, s0);
+    g1 = group_of(r0, R, s1 - 1);
+    if (g0 == g1) return;  // one workgroup held the whole bucket
+  }
+  const uint32_t l = level_of_bucket(a, b);
   const uint32_t ent0 = (b - a.bucket_base[l]) * kChunk;
   const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
-  const float inv = ldexpf(1.f, -bucket_k2(ws, l, b));  // the accumulate kernel's per-bucket scale
-  const long long* src = ws.partial + (int64_t)ws.part_pre[b] * (2 * kChunk);
+  const double inv = unit_back(a, ws, l, bucket_k2(ws, b));  // the accumulate kernel's per-bucket unit
   float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0);
   for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) {
     long long v = 0;
-    for (uint32_t k = 0; k < nsl; ++k) v += src[(int64_t)k * (2 * kChunk) + t];
-    dst[t] = (float)v * inv;
+    if (s1 > s0) {
+      for (uint32_t g = g0; g <= g1; ++g) {
+        const uint64_t gb = range_at(r0, R, g);
+        if (gb >= range_at(r0, R, g + 1)) continue;  // an empty range holds no piece
+        v += ws.partial[(int64_t)(2 * g + (gb > s0 ? 0 : 1)) * (2 * kChunk) + t];
+      }
+    }
+    dst[t] = (float)((double)v * inv);
   }
 }
 
@@ -789,11 +838,10 @@ static void launch_accum(const GridArgs& a, const BwdWorkspace& w, const lnr_gri
                          uint32_t l1, float* d_table, hipStream_t st) {
   const uint32_t b0 = a.bucket_base[l0], b1 = a.bucket_base[l1];
   if (b1 <= b0) return;
-  const int64_t max_slices = (b1 - b0) + (8 * n * (int64_t)(l1 - l0)) / kSliceRecordsCoarse + 1;
-  const unsigned g = (unsigned)(max_slices < 4096 ? max_slices : 4096);
-  hipLaunchKernelGGL(k_bwd_accum, dim3(g), dim3(kAccumThreads), 2 * kChunk * sizeof(unsigned long long), st, a, w,
-                     d_table, b0, b1);
-  hipLaunchKernelGGL(k_bwd_finalize, dim3(b1 - b0), dim3(256), 0, st, a, w, d_table, b0);
+  (void)n;
+  hipLaunchKernelGGL(k_bwd_accum, dim3(kAccumGroups), dim3(kAccumThreads), 2 * kChunk * sizeof(unsigned long long), st,
+                     a, w, d_table, b0, b1);
+  hipLaunchKernelGGL(k_bwd_finalize, dim3(b1 - b0), dim3(256), 0, st, a, w, d_table, b0, b1);
 }
 
 template <class PosFn>
@@ -816,9 +864,15 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
     hipLaunchKernelGGL(k_bwd_count<PosFn>, grid, dim3(kSB), 0, st, a, pos, n, reinterpret_cast<const float2*>(d_enc),
                        stride, w);
   }
+  if (!(flags & LNR_BWD_LEVEL_MAX_READY)) {
+    LNR_REQUIRE(hipMemsetAsync(w.level_max, 0, LNR_MAX_LEVELS * sizeof(float), st) == hipSuccess, "%s: memset failed",
+                who);
+    hipLaunchKernelGGL(k_denc_level_max, dim3(kMaxBlocks, d->n_levels), dim3(256), 0, st,
+                       reinterpret_cast<const float2*>(d_enc), stride, n, w);
+  }
   hipLaunchKernelGGL(k_bwd_chunk_sums, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
   hipLaunchKernelGGL(k_bwd_scan_rows, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
-  hipLaunchKernelGGL(k_bwd_scan_buckets, dim3(1), dim3(1024), 0, st, w, a.n_buckets, a.bucket_base[a.merge_levels]);
+  hipLaunchKernelGGL(k_bwd_scan_buckets, dim3(1), dim3(1024), 0, st, w, a.n_buckets);
   {
     const float2* de = reinterpret_cast<const float2*>(d_enc);
     const uint32_t m = a.merge_levels, L = d->n_levels;
@@ -831,9 +885,10 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
     bool pow2 = true;
     for (uint32_t l = 0; l < L; ++l) pow2 = pow2 && a.lv[l].size_mask != 0;
     const bool rows = L == 16 && all_fine && pow2 && 8 * n * (int64_t)L + 2 < (int64_t(1) << 32);
-    if (rows && m == 5 && maxnb <= 64) {
-      hipLaunchKernelGGL((k_bwd_scatter_rows<PosFn, 16, 5, 64>), dim3((unsigned)w.n_sb), dim3(kSB), 0, st, a, pos, n,
-                         de, stride, w, skip_zero);
+    if (rows && m >= 5 && m <= 7 && maxnb <= 64) {
+      auto kern = m == 5 ? k_bwd_scatter_rows<PosFn, 16, 5, 64>
+                         : (m == 6 ? k_bwd_scatter_rows<PosFn, 16, 6, 64> : k_bwd_scatter_rows<PosFn, 16, 7, 64>);
+      hipLaunchKernelGGL(kern, dim3((unsigned)w.n_sb), dim3(kSB), 0, st, a, pos, n, de, stride, w, skip_zero);
       hipLaunchKernelGGL((k_bwd_scatter_overflow<PosFn>), dim3((unsigned)((w.n_sb * L + kSB - 1) / kSB)), dim3(kSB),
                          kScatterLds, st, a, pos, n, de, stride, w, skip_zero);
     } else
@@ -858,7 +913,6 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
     }
 #endif
   }
-  hipLaunchKernelGGL(k_bwd_level_max, dim3(d->n_levels), dim3(256), 0, st, w);
   if (flags & LNR_BWD_NO_ACCUM) LNR_RETURN_LAUNCH(who);  // accumulate later, by level range
   launch_accum(a, w, d, n, 0, d->n_levels, d_table, st);
   LNR_RETURN_LAUNCH(who);
@@ -877,6 +931,11 @@ using namespace lnr;
 extern "C" int64_t lnr_hashgrid_bwd_workspace_bytes(const lnr_grid_desc* d, int64_t n) {
   if (d == nullptr || n < 0) return -1;
   return bwd_workspace_bytes(d, n);
+}
+
+extern "C" float* lnr_hashgrid_bwd_level_max(const lnr_grid_desc* d, int64_t n, void* workspace) {
+  if (d == nullptr || n < 0 || workspace == nullptr || check_desc_bwd(d, "lnr_hashgrid_bwd_level_max")) return nullptr;
+  return carve_workspace(workspace, make_args(d), d, n).level_max;
 }
 
 extern "C" int lnr_hashgrid_bwd(const lnr_grid_desc* d, const float* pos01, int64_t n, const float* d_enc,

@@ -190,6 +190,9 @@ class StepEngine:
         self.ws = torch.empty(L.lib().lnr_field_train_workspace_words(n_rays, self.S), dtype=torch.float32, device=dev)
         self.bwd_ws_bytes = int(L.lib().lnr_hashgrid_bwd_workspace_bytes(L.ctypes.byref(state.desc), self.N))
         self.bwd_ws = torch.empty(self.bwd_ws_bytes, dtype=torch.uint8, device=dev)
+        # the backward's per-level max |d_enc| (record scales), written by the field kernel's MLP backward
+        self.level_max_ptr = L.ctypes.c_void_p(L.lib().lnr_hashgrid_bwd_level_max(L.ctypes.byref(state.desc), self.N,
+                                                                                   L.ptr(self.bwd_ws)))
         self.stats = torch.zeros(n_rays, L.RAY_STATS, dtype=torch.float32, device=dev)
         self.depth = torch.empty(n_rays, dtype=torch.float32, device=dev)
         self.opacity = torch.empty(n_rays, dtype=torch.float32, device=dev)
@@ -301,11 +304,11 @@ class StepEngine:
         m(prof, "field")
         L.call("lnr_field_train", st.mlp_f16, self.enc, N, rays, self.z, depth_gt, R, S, cfg.raw_noise_std, noise, key,
                self.ray_offset, L.ctypes.byref(lp), self.d_enc, st.grad_mlp, self.ws, self.stats, self.depth,
-               self.opacity, None, s)
+               self.opacity, None, self.level_max_ptr, s)
         m(prof, "field")
         # 5. hash-grid backward
         m(prof, "grid_bwd")
-        flags = L.BWD_COUNTS_READY if self.count_in_forward else 0
+        flags = (L.BWD_COUNTS_READY if self.count_in_forward else 0) | L.BWD_LEVEL_MAX_READY
         if self.allreduce is None:
             L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(st.desc), rays, self.z, R, S, self.d_enc, N, st.grad_table,
                    self.bwd_ws, self.bwd_ws_bytes, flags, s)

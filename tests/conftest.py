@@ -9,6 +9,14 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
+# Hash-grid table gradient vs the fp64 oracle, relative L2.  The backward's records carry their two
+# values as fp16 at a per-level power-of-two scale (csrc/hashgrid.hpp "Record values"): each
+# corner contribution rounds once to 11 significant bits (relative 2^-12) and the int64 sums add
+# no further error.  Measured 2.1e-4 where every entry has one or two contributions (the worst case:
+# no averaging).  tcnn's own gradient for fp16 parameters is an fp16 tensor accumulated by fp16
+# atomics, so it rounds at least this much (every partial sum, not only every contribution).
+TABLE_GRAD_RTOL = 4e-4
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
