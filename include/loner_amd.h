@@ -118,7 +118,12 @@ int lnr_hashgrid_bwd(const lnr_grid_desc* d, const float* pos01, int64_t n, cons
 int lnr_hashgrid_bwd_rays(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
                           int32_t n_samples, const float* d_enc, int64_t enc_stride, float* d_table,
                           void* workspace, int64_t workspace_bytes, int32_t flags, void* stream);
-/* With flags & LNR_BWD_NO_ACCUM the two calls above stop after the scatter; this finishes the
+/* The same, from lnr_field_train's compact encoding gradient: d_enc = d_sigma[n] * J[l][n] with J
+ * level-major fp16 pairs (one uint32 per level and sample, level stride jac_stride). */
+int lnr_hashgrid_bwd_rays_jac(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
+                              int32_t n_samples, const uint32_t* d_jac, const float* d_sigma, int64_t jac_stride,
+                              float* d_table, void* workspace, int64_t workspace_bytes, int32_t flags, void* stream);
+/* With flags & LNR_BWD_NO_ACCUM the three calls above stop after the scatter; this finishes the
  * levels [level_begin, level_end) (n = samples of that call, same workspace): their slice of
  * d_table is final on return, so a data-parallel caller can all-reduce it while the next range
  * accumulates. */
@@ -232,12 +237,16 @@ int64_t lnr_field_train_workspace_words(int64_t n_rays, int32_t n_samples);
  * Writes d_enc (level-major float2), accumulates d_w (3072 fp32), per-ray stats; optional outputs NULL.
  * d_enc_level_max (optional, 16 floats): OVERWRITTEN with max |d_enc| per level, the hash-grid
  * backward's record scales (pass lnr_hashgrid_bwd_level_max(...) and LNR_BWD_LEVEL_MAX_READY).
+ * d_enc_jac (optional; n_samples 64, 128, 256 or 512): written INSTEAD of d_enc (which may be NULL):
+ * J = d sigma / d enc as level-major fp16 pairs, one uint32 per (level, sample), so that
+ * d_enc = d_sigma * J with d_sigma the (n_rays, n_samples) fp32 dL/dsigma this call leaves at
+ * workspace + lnr_dw_workspace_words(n_rays); lnr_hashgrid_bwd_rays_jac takes both (half the bytes).
  * workspace: lnr_field_train_workspace_words(n_rays, n_samples) fp32 words. */
 int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, const float* rays, const float* z,
                     const float* depth_gt, int64_t n_rays, int32_t n_samples, float noise_std, const float* noise,
                     uint32_t key, int64_t ray_offset, const lnr_loss_params* lp, float* d_enc, float* d_w,
                     float* workspace, float* ray_stats, float* depth, float* opacity, float* weights,
-                    float* d_enc_level_max, void* stream);
+                    float* d_enc_level_max, uint32_t* d_enc_jac, void* stream);
 /* Forward-only fused render from enc (inference path, C3 shape): sigma MLP + compositing. */
 int lnr_field_render(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, const float* rays, const float* z,
                      int64_t n_rays, int32_t n_samples, int32_t strategy, float noise_std, const float* noise,

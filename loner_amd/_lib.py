@@ -101,6 +101,8 @@ _SIGNATURES = {
                                         c_p]),
     "lnr_hashgrid_bwd_rays": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_p,
                                              c_i64, c_i32, c_p]),
+    "lnr_hashgrid_bwd_rays_jac": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_p, c_i64,
+                                                 c_p, c_p, c_i64, c_i32, c_p]),
     "lnr_hashgrid_bwd_accum": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_i64, c_p, c_i64, c_u32, c_u32, c_p, c_p]),
     "lnr_hashgrid_bwd_atomic": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_i64, c_p, c_i64, c_p, c_p]),
     "lnr_hashgrid_bwd_rays_atomic": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_i64, c_p,
@@ -122,7 +124,8 @@ _SIGNATURES = {
     "lnr_composite_loss_bwd": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_u32, c_i64,
                                               ctypes.POINTER(LossParams), c_p, c_p, c_p, c_p, c_p, c_p]),
     "lnr_field_train": (ctypes.c_int, [c_p, c_p, c_i64, c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_u32, c_i64,
-                                       ctypes.POINTER(LossParams), c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+                                       ctypes.POINTER(LossParams), c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
+                                       c_p]),
     "lnr_field_render": (ctypes.c_int, [c_p, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_i32, c_f, c_p, c_u32, c_i64, c_p,
                                         c_p, c_p, c_p, c_p]),
     "lnr_rgb_render": (ctypes.c_int, [c_p, c_i32, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_p, c_p]),

@@ -43,6 +43,7 @@ struct FieldArgs {
   float* d_enc;       // kSigmaMLP + train
   float* dw_slab;     // kSigmaMLP + train: [gridDim.x][3072]
   float* denc_max;    // optional: [16] max |d_enc| per level (float bits, atomicMax; zeroed by the ray phase)
+  uint32_t* d_jac;    // optional, replaces d_enc: d sigma / d enc as level-major fp16 pairs (d_enc = d_sigma J)
   float* ray_stats;   // train: [R][LNR_RAY_STATS]
   // kLossExternal: upstream gradients of the render outputs (any may be NULL = zero)
   const float* g_weights;   // (R,S)
@@ -735,8 +736,14 @@ __global__ void __launch_bounds__(NT) k_field_wave(FieldArgs a) {
   }
 }
 
+// fp16 pair (round to nearest) in one word, low half first
+__device__ __forceinline__ uint32_t pack_h2(float x, float y) {
+  return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)x) | ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)y) << 16);
+}
+
 // Phase 2, tile-parallel: sigma MLP backward over 32-sample tile pairs (no per-ray structure):
 // d_enc (level-major float2) and the per-block dW slab.
+template <bool JAC>  // JAC: write d sigma / d enc (fp16 pairs) instead of d_enc
 __global__ void __launch_bounds__(NT) k_mlp_bwd_tiles(FieldArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
@@ -804,8 +811,13 @@ __global__ void __launch_bounds__(NT) k_mlp_bwd_tiles(FieldArgs a) {
     for (int m = 0; m < 2; ++m) {
       const int lvl = 8 * m + 2 * g;
       const float2 q0 = make_float2(d[m][0] * ds0, d[m][1] * ds0), q1 = make_float2(d[m][2] * ds0, d[m][3] * ds0);
-      denc[(int64_t)lvl * a.enc_stride + n0 + c] = q0;
-      denc[(int64_t)(lvl + 1) * a.enc_stride + n0 + c] = q1;
+      if (JAC) {
+        a.d_jac[(int64_t)lvl * a.enc_stride + n0 + c] = pack_h2(d[m][0], d[m][1]);
+        a.d_jac[(int64_t)(lvl + 1) * a.enc_stride + n0 + c] = pack_h2(d[m][2], d[m][3]);
+      } else {
+        denc[(int64_t)lvl * a.enc_stride + n0 + c] = q0;
+        denc[(int64_t)(lvl + 1) * a.enc_stride + n0 + c] = q1;
+      }
       lmax[2 * m] = fmaxf(lmax[2 * m], fmaxf(fabsf(q0.x), fabsf(q0.y)));
       lmax[2 * m + 1] = fmaxf(lmax[2 * m + 1], fmaxf(fabsf(q1.x), fabsf(q1.y)));
     }
@@ -814,8 +826,13 @@ __global__ void __launch_bounds__(NT) k_mlp_bwd_tiles(FieldArgs a) {
     for (int m = 0; m < 2; ++m) {
       const int lvl = 8 * m + 2 * g;
       const float2 q0 = make_float2(d[m][0] * ds1, d[m][1] * ds1), q1 = make_float2(d[m][2] * ds1, d[m][3] * ds1);
-      denc[(int64_t)lvl * a.enc_stride + n0 + 16 + c] = q0;
-      denc[(int64_t)(lvl + 1) * a.enc_stride + n0 + 16 + c] = q1;
+      if (JAC) {
+        a.d_jac[(int64_t)lvl * a.enc_stride + n0 + 16 + c] = pack_h2(d[m][0], d[m][1]);
+        a.d_jac[(int64_t)(lvl + 1) * a.enc_stride + n0 + 16 + c] = pack_h2(d[m][2], d[m][3]);
+      } else {
+        denc[(int64_t)lvl * a.enc_stride + n0 + 16 + c] = q0;
+        denc[(int64_t)(lvl + 1) * a.enc_stride + n0 + 16 + c] = q1;
+      }
       lmax[2 * m] = fmaxf(lmax[2 * m], fmaxf(fabsf(q0.x), fabsf(q0.y)));
       lmax[2 * m + 1] = fmaxf(lmax[2 * m + 1], fmaxf(fabsf(q1.x), fabsf(q1.y)));
     }
@@ -1025,18 +1042,21 @@ extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t e
                                float noise_std, const float* noise, uint32_t key, int64_t ray_offset,
                                const lnr_loss_params* lp, float* d_enc, float* d_w, float* workspace,
                                float* ray_stats, float* depth, float* opacity, float* weights,
-                               float* d_enc_level_max, void* stream) {
+                               float* d_enc_level_max, uint32_t* d_enc_jac, void* stream) {
   if (int e = check_rays(rays, z, n_rays, n_samples, "lnr_field_train")) return e;
   if (int e = check_lp(lp, "lnr_field_train")) return e;
   LNR_REQUIRE(n_samples % 64 == 0, "lnr_field_train: n_samples=%d must be a multiple of 64", n_samples);
   LNR_REQUIRE(enc_stride >= n_rays * (int64_t)n_samples, "lnr_field_train: enc_stride too small");
   if (n_rays == 0) return LNR_OK;
-  LNR_REQUIRE(w && enc && depth_gt && d_enc && d_w && workspace && ray_stats, "lnr_field_train: null pointer");
+  LNR_REQUIRE(w && enc && depth_gt && (d_enc || d_enc_jac) && d_w && workspace && ray_stats,
+              "lnr_field_train: null pointer");
+  LNR_REQUIRE(!d_enc_jac || n_samples == 64 || n_samples == 128 || n_samples == 256 || n_samples == 512,
+              "lnr_field_train: d_enc_jac needs n_samples in {64, 128, 256, 512} (got %d)", n_samples);
   FieldArgs a{};
   a.w = w; a.enc = enc; a.enc_stride = enc_stride; a.rays = rays; a.z = z; a.depth_gt = depth_gt;
   a.n_rays = n_rays; a.S = n_samples; a.noise_std = noise_std; a.noise = noise; a.key = key;
   a.ray_offset = ray_offset; a.lp = *lp; a.d_enc = d_enc; a.dw_slab = workspace; a.ray_stats = ray_stats;
-  a.depth = depth; a.opacity = opacity; a.weights = weights; a.denc_max = d_enc_level_max;
+  a.depth = depth; a.opacity = opacity; a.weights = weights; a.denc_max = d_enc_level_max; a.d_jac = d_enc_jac;
   hipStream_t st = as_stream(stream);
   int nb;
   const int C = n_samples / 64;
@@ -1057,7 +1077,10 @@ extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t e
     const int64_t wantb = (pairs + kWavesPerBlock - 1) / kWavesPerBlock;
     const int64_t slabs = lnr_dw_workspace_words(n_rays) / LNR_SIGMA_MLP_PARAMS;  // one dW slab per block
     nb = (int)(wantb < slabs ? wantb : slabs);
-    hipLaunchKernelGGL(k_mlp_bwd_tiles, dim3(nb), dim3(NT), bwd_tiles_smem_bytes(), st, a);
+    if (d_enc_jac)
+      hipLaunchKernelGGL(k_mlp_bwd_tiles<true>, dim3(nb), dim3(NT), bwd_tiles_smem_bytes(), st, a);
+    else
+      hipLaunchKernelGGL(k_mlp_bwd_tiles<false>, dim3(nb), dim3(NT), bwd_tiles_smem_bytes(), st, a);
   } else {
     nb = field_blocks(n_rays);
     int e = launch_field<true, false, kSigmaMLP>(a, nb, st, "lnr_field_train");

@@ -122,6 +122,34 @@ struct PosFromRays {
   __device__ __forceinline__ void operator()(int64_t n, float& x, float& y, float& z) const { eval(load(n), x, y, z); }
 };
 
+// Encoding gradient sources of the backward.  GradF32: d_enc itself, level-major float2.  GradJac:
+// d_enc = d_sigma * J with J = d sigma / d enc, the sigma MLP's input Jacobian, level-major fp16
+// pairs (lnr_field_train's compact output: 4 B per sample and level instead of 8, and d_sigma 4 B
+// per sample).  load_nt: read once (nontemporal).
+typedef float gf32x2 __attribute__((ext_vector_type(2)));
+struct GradF32 {
+  const float2* g;
+  int64_t stride;
+  __device__ __forceinline__ float2 load(uint32_t l, int64_t i) const { return g[(int64_t)l * stride + i]; }
+  __device__ __forceinline__ float2 load_nt(uint32_t l, int64_t i) const {
+    const gf32x2 v = __builtin_nontemporal_load(reinterpret_cast<const gf32x2*>(&g[(int64_t)l * stride + i]));
+    return make_float2(v.x, v.y);
+  }
+};
+struct GradJac {
+  const uint32_t* jac;
+  const float* dsig;
+  int64_t stride;
+  __device__ __forceinline__ static float2 apply(uint32_t h, float s) {
+    return make_float2((float)__builtin_bit_cast(_Float16, (uint16_t)(h & 0xFFFFu)) * s,
+                       (float)__builtin_bit_cast(_Float16, (uint16_t)(h >> 16)) * s);
+  }
+  __device__ __forceinline__ float2 load(uint32_t l, int64_t i) const { return apply(jac[(int64_t)l * stride + i], dsig[i]); }
+  __device__ __forceinline__ float2 load_nt(uint32_t l, int64_t i) const {
+    return apply(__builtin_nontemporal_load(&jac[(int64_t)l * stride + i]), dsig[i]);
+  }
+};
+
 struct Corners {
   uint32_t idx[8];
   float w[8];

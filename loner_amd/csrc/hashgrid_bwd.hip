@@ -20,9 +20,8 @@ namespace lnr {
 // Histogram after the MLP backward: samples whose d_enc is zero at a non-coherent level (ReLU'd
 // sigma: relu(sigma + noise) = 0 gives dL/dsigma = 0 exactly, typically half the samples) emit no
 // records there; the scatter skips them the same way (skip_zero).
-template <class PosFn>
-__global__ void __launch_bounds__(kSB) k_bwd_count(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ d_enc,
-                                                   int64_t stride, BwdWorkspace ws) {
+template <class PosFn, class GradFn>
+__global__ void __launch_bounds__(kSB) k_bwd_count(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace ws) {
   __shared__ uint32_t hist[kMaxChunksPerLevel];
   const uint32_t l = blockIdx.y;
   const int64_t i = (int64_t)blockIdx.x * kSB + threadIdx.x;
@@ -32,7 +31,7 @@ __global__ void __launch_bounds__(kSB) k_bwd_count(GridArgs a, PosFn pos, int64_
   bool act = false;
   if (in) {
     pos(i, x, y, z);
-    const float2 g = d_enc[(int64_t)l * stride + i];
+    const float2 g = grad.load(l, i);
     act = g.x != 0.f || g.y != 0.f;
   }
   lds_barrier();
@@ -165,9 +164,8 @@ __device__ __forceinline__ void rec_store(const BwdWorkspace& ws, uint64_t dst, 
 }
 
 // One (histogram row sb, level l) of the scatter; KIND as below, kLevelsAny meaning "any level".
-template <class PosFn, int KIND>
-__device__ __forceinline__ void scatter_row_level(const GridArgs& a, const PosFn& pos, int64_t n,
-                                                  const float2* __restrict__ d_enc, int64_t stride,
+template <class PosFn, class GradFn, int KIND>
+__device__ __forceinline__ void scatter_row_level(const GridArgs& a, const PosFn& pos, int64_t n, const GradFn& grad,
                                                   const BwdWorkspace& ws, uint32_t l, int64_t sb, bool skip_zero,
                                                   char* smem) {
   uint2* stage_v = reinterpret_cast<uint2*>(smem);                           // [kCap] value words
@@ -195,8 +193,7 @@ __device__ __forceinline__ void scatter_row_level(const GridArgs& a, const PosFn
   const typename PosFn::Raw raw = pos.load(ic);
   // d_enc is read once: a nontemporal load keeps it from displacing the L2 lines in which adjacent
   // rows' bucket runs combine (scatter -1.5 % at C2)
-  const f32x2 g_nt = __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(&d_enc[(int64_t)l * stride + ic]));
-  const float2 g_raw = make_float2(g_nt.x, g_nt.y);
+  const float2 g_raw = grad.load_nt(l, ic);
   uint32_t h0[2] = {0u, 0u}, h1[2] = {0u, 0u};
   uint64_t seg[2] = {0ull, 0ull};
   const bool last = sb + 1 >= ws.n_sb;
@@ -344,23 +341,21 @@ __device__ __forceinline__ void scatter_row_level(const GridArgs& a, const PosFn
   LNR_PHASE_BY(sb, 5 * kind + 3, t4, t3);
 }
 
-template <class PosFn, int KIND>
+template <class PosFn, class GradFn, int KIND>
 __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(GridArgs a, PosFn pos, int64_t n,
-                                                                             const float2* __restrict__ d_enc,
-                                                                             int64_t stride, BwdWorkspace ws, uint32_t l0,
+                                                                             GradFn grad, BwdWorkspace ws, uint32_t l0,
                                                                              bool skip_zero) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const uint32_t l = KIND == kLevelsAny ? blockIdx.x % a.n_levels : l0 + blockIdx.y;
   const int64_t sb = KIND == kLevelsAny ? (int64_t)(blockIdx.x / a.n_levels) : xcd_row(blockIdx.x, gridDim.x);
-  scatter_row_level<PosFn, KIND>(a, pos, n, d_enc, stride, ws, l, sb, skip_zero, smem);
+  scatter_row_level<PosFn, GradFn, KIND>(a, pos, n, grad, ws, l, sb, skip_zero, smem);
 }
 
 // The (row, level) items the level-looped scatter could not stage (more than kCap records: rows of
 // coherent levels whose runs did not merge, or pathological split pairs), each as above.
-template <class PosFn>
+template <class PosFn, class GradFn>
 __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter_overflow(GridArgs a, PosFn pos, int64_t n,
-                                                                                      const float2* __restrict__ d_enc,
-                                                                                      int64_t stride, BwdWorkspace ws,
+                                                                                      GradFn grad, BwdWorkspace ws,
                                                                                       bool skip_zero) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ unsigned long long masks[kSB / 64];
@@ -373,8 +368,8 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter_o
   for (int w = 0; w < kSB / 64; ++w) {
     for (unsigned long long mm = masks[w]; mm; mm &= mm - 1) {
       const int64_t q = (int64_t)blockIdx.x * kSB + 64 * w + __ffsll((long long)mm) - 1;
-      scatter_row_level<PosFn, kLevelsAny>(a, pos, n, d_enc, stride, ws, (uint32_t)(q / ws.n_sb), q % ws.n_sb,
-                                           skip_zero, smem);
+      scatter_row_level<PosFn, GradFn, kLevelsAny>(a, pos, n, grad, ws, (uint32_t)(q / ws.n_sb), q % ws.n_sb,
+                                                   skip_zero, smem);
       lds_barrier();
     }
   }
@@ -410,10 +405,9 @@ struct RowsLds {  // the small tables first: their addresses fit the 16-bit LDS 
 // NL levels, the first NM coherent (run-merging) and the rest fine, at most NB buckets per level:
 // compile-time, so the level loop unrolls into straight-line code.  Record slots are 32-bit (the
 // launcher checks 8 N L < 2^32).
-template <class PosFn, int NL, int NM, int NB>
+template <class PosFn, class GradFn, int NL, int NM, int NB>
 __global__ void __launch_bounds__(kSB) __attribute__((amdgpu_waves_per_eu(4, 4)))
-k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ d_enc, int64_t stride, BwdWorkspace ws,
-                   bool skip_zero) {
+k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace ws, bool skip_zero) {
   static_assert(NL <= 2 * (kSB / 64), "wave w prepares levels 2w and 2w + 1");
   static_assert(NB <= 128, "two buckets per lane");
   __shared__ RowsLds<NL, NB> sm;
@@ -431,10 +425,10 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, const float2* __restrict__ 
   if (threadIdx.x < 2 * NB) (&sm.ctr[0][0])[threadIdx.x] = 0u;
   // prologue 2: every global load of the kernel
   const typename PosFn::Raw raw = pos.load(ic);
-  f32x2 g[NL];
+  float2 g[NL];
 #pragma unroll
-  for (int l = 0; l < NL; ++l)  // read once: nontemporal, so they do not displace the runs' L2 lines
-    g[l] = __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(&d_enc[(int64_t)l * stride + ic]));
+  for (int l = 0; l < NL; ++l) g[l] = grad.load_nt(l, ic);  // read once: nontemporal, so they do not
+                                                            // displace the runs' L2 lines
   uint32_t h0[2][2], h1[2][2];
   uint64_t seg[2][2];
 #pragma unroll
@@ -585,14 +579,13 @@ static_assert(kScatterLds <= 65536, "scatter LDS within the default dynamic limi
 // atomicMax per workgroup on the float's bits (non-negative floats order as their bit patterns).
 // ws.level_max is zeroed before.
 constexpr int kMaxBlocks = 256;
-__global__ void __launch_bounds__(256) k_denc_level_max(const float2* __restrict__ d_enc, int64_t stride, int64_t n,
-                                                        BwdWorkspace ws) {
+template <class GradFn>
+__global__ void __launch_bounds__(256) k_denc_level_max(GradFn grad, int64_t n, BwdWorkspace ws) {
   __shared__ float red[4];
   const uint32_t l = blockIdx.y;
-  const float2* src = d_enc + (int64_t)l * stride;
   float m = 0.f;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)kMaxBlocks * 256) {
-    const float2 g = src[i];
+    const float2 g = grad.load(l, i);
     m = fmaxf(m, fmaxf(fabsf(g.x), fabsf(g.y)));
   }
   m = wave_max_nonneg(m);
@@ -844,10 +837,9 @@ static void launch_accum(const GridArgs& a, const BwdWorkspace& w, const lnr_gri
   hipLaunchKernelGGL(k_bwd_finalize, dim3(b1 - b0), dim3(256), 0, st, a, w, d_table, b0, b1);
 }
 
-template <class PosFn>
-static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, const float* d_enc, int64_t stride,
-                               float* d_table, void* workspace, int64_t ws_bytes, int32_t flags, hipStream_t st,
-                               const char* who) {
+template <class PosFn, class GradFn>
+static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, GradFn grad, float* d_table,
+                               void* workspace, int64_t ws_bytes, int32_t flags, hipStream_t st, const char* who) {
   GridArgs a = make_args(d);
   LNR_REQUIRE(a.n_buckets <= (uint32_t)kMaxBuckets, "%s: too many table chunks (%u)", who, a.n_buckets);
   for (uint32_t l = 0; l < d->n_levels; ++l)
@@ -858,60 +850,39 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, con
               (long long)bwd_workspace_bytes(d, n));
   LNR_REQUIRE(n < (int64_t(1) << 31), "%s: n=%lld samples exceeds 2^31", who, (long long)n);
   BwdWorkspace w = carve_workspace(workspace, a, d, n);
-  dim3 grid((unsigned)w.n_sb, d->n_levels);
   const bool skip_zero = !(flags & LNR_BWD_COUNTS_READY);
-  if (!(flags & LNR_BWD_COUNTS_READY)) {
-    hipLaunchKernelGGL(k_bwd_count<PosFn>, grid, dim3(kSB), 0, st, a, pos, n, reinterpret_cast<const float2*>(d_enc),
-                       stride, w);
-  }
+  if (!(flags & LNR_BWD_COUNTS_READY))
+    hipLaunchKernelGGL((k_bwd_count<PosFn, GradFn>), dim3((unsigned)w.n_sb, d->n_levels), dim3(kSB), 0, st, a, pos, n,
+                       grad, w);
   if (!(flags & LNR_BWD_LEVEL_MAX_READY)) {
     LNR_REQUIRE(hipMemsetAsync(w.level_max, 0, LNR_MAX_LEVELS * sizeof(float), st) == hipSuccess, "%s: memset failed",
                 who);
-    hipLaunchKernelGGL(k_denc_level_max, dim3(kMaxBlocks, d->n_levels), dim3(256), 0, st,
-                       reinterpret_cast<const float2*>(d_enc), stride, n, w);
+    hipLaunchKernelGGL(k_denc_level_max<GradFn>, dim3(kMaxBlocks, d->n_levels), dim3(256), 0, st, grad, n, w);
   }
   hipLaunchKernelGGL(k_bwd_chunk_sums, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
   hipLaunchKernelGGL(k_bwd_scan_rows, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
   hipLaunchKernelGGL(k_bwd_scan_buckets, dim3(1), dim3(1024), 0, st, w, a.n_buckets);
-  {
-    const float2* de = reinterpret_cast<const float2*>(d_enc);
-    const uint32_t m = a.merge_levels, L = d->n_levels;
-    bool all_fine = true;
-    for (uint32_t l = m; l < L; ++l) all_fine = all_fine && a.lv[l].fine;
-#if !defined(LNR_EXP_SPLIT_SCATTER) && !defined(LNR_EXP_SCATTER_PER_LEVEL)
-    uint32_t maxnb = 0;
-    for (uint32_t l = 0; l < L; ++l) maxnb = std::max(maxnb, a.bucket_base[l + 1] - a.bucket_base[l]);
-    // the reference's grids: 16 levels (base 16, scale 2), 2^18 (sigma) or 2^19 (colour) entries
-    bool pow2 = true;
-    for (uint32_t l = 0; l < L; ++l) pow2 = pow2 && a.lv[l].size_mask != 0;
-    const bool rows = L == 16 && all_fine && pow2 && 8 * n * (int64_t)L + 2 < (int64_t(1) << 32);
-    if (rows && m >= 5 && m <= 7 && maxnb <= 64) {
-      auto kern = m == 5 ? k_bwd_scatter_rows<PosFn, 16, 5, 64>
-                         : (m == 6 ? k_bwd_scatter_rows<PosFn, 16, 6, 64> : k_bwd_scatter_rows<PosFn, 16, 7, 64>);
-      hipLaunchKernelGGL(kern, dim3((unsigned)w.n_sb), dim3(kSB), 0, st, a, pos, n, de, stride, w, skip_zero);
-      hipLaunchKernelGGL((k_bwd_scatter_overflow<PosFn>), dim3((unsigned)((w.n_sb * L + kSB - 1) / kSB)), dim3(kSB),
-                         kScatterLds, st, a, pos, n, de, stride, w, skip_zero);
-    } else
-      hipLaunchKernelGGL((k_bwd_scatter<PosFn, kLevelsAny>), dim3((unsigned)(w.n_sb * L)), dim3(kSB), kScatterLds, st,
-                         a, pos, n, de, stride, w, 0u, skip_zero);
-#elif defined(LNR_EXP_SCATTER_PER_LEVEL)
-    (void)m;
-    (void)all_fine;
-    hipLaunchKernelGGL((k_bwd_scatter<PosFn, kLevelsAny>), dim3((unsigned)(w.n_sb * L)), dim3(kSB), kScatterLds, st, a,
-                       pos, n, de, stride, w, 0u, skip_zero);
-#else
-    if (m > 0)
-      hipLaunchKernelGGL((k_bwd_scatter<PosFn, kLevelsCoherent>), dim3((unsigned)w.n_sb, m), dim3(kSB), kScatterLds, st,
-                         a, pos, n, de, stride, w, 0u, skip_zero);
-    if (L > m) {
-      if (all_fine)
-        hipLaunchKernelGGL((k_bwd_scatter<PosFn, kLevelsFine>), dim3((unsigned)w.n_sb, L - m), dim3(kSB), kScatterLds,
-                           st, a, pos, n, de, stride, w, m, skip_zero);
-      else
-        hipLaunchKernelGGL((k_bwd_scatter<PosFn, kLevelsGeneric>), dim3((unsigned)w.n_sb, L - m), dim3(kSB),
-                           kScatterLds, st, a, pos, n, de, stride, w, m, skip_zero);
-    }
-#endif
+  const uint32_t m = a.merge_levels, L = d->n_levels;
+  bool all_fine = true, pow2 = true;
+  uint32_t maxnb = 0;
+  for (uint32_t l = 0; l < L; ++l) {
+    if (l >= m) all_fine = all_fine && a.lv[l].fine;
+    pow2 = pow2 && a.lv[l].size_mask != 0;
+    maxnb = std::max(maxnb, a.bucket_base[l + 1] - a.bucket_base[l]);
+  }
+  // the reference's sigma grid (16 levels, base 16, scale 2, 2^18 entries): the level-looped scatter
+  // plus the pass over the rows it could not stage; other grids (the colour grid's 2^19 levels have
+  // 128 chunks): one workgroup per (row, level)
+  const bool rows = L == 16 && all_fine && pow2 && 8 * n * (int64_t)L + 2 < (int64_t(1) << 32);
+  if (rows && m >= 5 && m <= 7 && maxnb <= 64) {
+    auto kern = m == 5 ? k_bwd_scatter_rows<PosFn, GradFn, 16, 5, 64>
+                       : (m == 6 ? k_bwd_scatter_rows<PosFn, GradFn, 16, 6, 64> : k_bwd_scatter_rows<PosFn, GradFn, 16, 7, 64>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)w.n_sb), dim3(kSB), 0, st, a, pos, n, grad, w, skip_zero);
+    hipLaunchKernelGGL((k_bwd_scatter_overflow<PosFn, GradFn>), dim3((unsigned)((w.n_sb * L + kSB - 1) / kSB)),
+                       dim3(kSB), kScatterLds, st, a, pos, n, grad, w, skip_zero);
+  } else {
+    hipLaunchKernelGGL((k_bwd_scatter<PosFn, GradFn, kLevelsAny>), dim3((unsigned)(w.n_sb * L)), dim3(kSB), kScatterLds,
+                       st, a, pos, n, grad, w, 0u, skip_zero);
   }
   if (flags & LNR_BWD_NO_ACCUM) LNR_RETURN_LAUNCH(who);  // accumulate later, by level range
   launch_accum(a, w, d, n, 0, d->n_levels, d_table, st);
@@ -945,7 +916,8 @@ extern "C" int lnr_hashgrid_bwd(const lnr_grid_desc* d, const float* pos01, int6
   LNR_REQUIRE(n >= 0 && enc_stride >= n, "lnr_hashgrid_bwd: bad sizes");
   if (n == 0) return LNR_OK;
   LNR_REQUIRE(pos01 && d_enc && d_table, "lnr_hashgrid_bwd: null pointer");
-  return launch_bwd_bucketed(d, PosFromArray{pos01}, n, d_enc, enc_stride, d_table, workspace, workspace_bytes, flags,
+  return launch_bwd_bucketed(d, PosFromArray{pos01}, n, GradF32{reinterpret_cast<const float2*>(d_enc), enc_stride},
+                             d_table, workspace, workspace_bytes, flags,
                              as_stream(stream), "lnr_hashgrid_bwd");
 }
 
@@ -969,8 +941,22 @@ extern "C" int lnr_hashgrid_bwd_rays(const lnr_grid_desc* d, const float* rays, 
   LNR_REQUIRE(n_rays >= 0 && n_samples > 0 && enc_stride >= n, "lnr_hashgrid_bwd_rays: bad sizes");
   if (n == 0) return LNR_OK;
   LNR_REQUIRE(rays && z && d_enc && d_table, "lnr_hashgrid_bwd_rays: null pointer");
-  return launch_bwd_bucketed(d, PosFromRays{rays, z, n_samples}, n, d_enc, enc_stride, d_table, workspace,
+  return launch_bwd_bucketed(d, PosFromRays{rays, z, n_samples}, n,
+                             GradF32{reinterpret_cast<const float2*>(d_enc), enc_stride}, d_table, workspace,
                              workspace_bytes, flags, as_stream(stream), "lnr_hashgrid_bwd_rays");
+}
+
+extern "C" int lnr_hashgrid_bwd_rays_jac(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
+                                         int32_t n_samples, const uint32_t* d_jac, const float* d_sigma,
+                                         int64_t jac_stride, float* d_table, void* workspace, int64_t workspace_bytes,
+                                         int32_t flags, void* stream) {
+  if (int e = check_desc_bwd(d, "lnr_hashgrid_bwd_rays_jac")) return e;
+  const int64_t n = n_rays * (int64_t)n_samples;
+  LNR_REQUIRE(n_rays >= 0 && n_samples > 0 && jac_stride >= n, "lnr_hashgrid_bwd_rays_jac: bad sizes");
+  if (n == 0) return LNR_OK;
+  LNR_REQUIRE(rays && z && d_jac && d_sigma && d_table, "lnr_hashgrid_bwd_rays_jac: null pointer");
+  return launch_bwd_bucketed(d, PosFromRays{rays, z, n_samples}, n, GradJac{d_jac, d_sigma, jac_stride}, d_table,
+                             workspace, workspace_bytes, flags, as_stream(stream), "lnr_hashgrid_bwd_rays_jac");
 }
 
 LNR_PHASE_EXPORT(hashgrid_bwd)

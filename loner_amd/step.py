@@ -186,8 +186,16 @@ class StepEngine:
         dev = state.device
         self.z = torch.empty(n_rays, self.S, dtype=torch.float32, device=dev)
         self.enc = torch.empty(self.cfg.n_levels, self.N, dtype=torch.int32, device=dev)
-        self.d_enc = torch.empty(self.cfg.n_levels, self.N, 2, dtype=torch.float32, device=dev)
         self.ws = torch.empty(L.lib().lnr_field_train_workspace_words(n_rays, self.S), dtype=torch.float32, device=dev)
+        # the encoding gradient: compact (d sigma / d enc as fp16 pairs + dL/dsigma, 4 + 4/L B per sample and
+        # level) where the field kernel's per-ray path supports it, else d_enc itself (float2)
+        self.compact_denc = self.S in (64, 128, 256, 512)
+        if self.compact_denc:
+            self.d_jac = torch.empty(self.cfg.n_levels, self.N, dtype=torch.int32, device=dev)
+            self.d_enc = None
+        else:
+            self.d_enc = torch.empty(self.cfg.n_levels, self.N, 2, dtype=torch.float32, device=dev)
+        self._r_last = n_rays  # the last step's ray count (d_sigma's place in the workspace follows it)
         self.bwd_ws_bytes = int(L.lib().lnr_hashgrid_bwd_workspace_bytes(L.ctypes.byref(state.desc), self.N))
         self.bwd_ws = torch.empty(self.bwd_ws_bytes, dtype=torch.uint8, device=dev)
         # the backward's per-level max |d_enc| (record scales), written by the field kernel's MLP backward
@@ -304,21 +312,20 @@ class StepEngine:
         m(prof, "field")
         L.call("lnr_field_train", st.mlp_f16, self.enc, N, rays, self.z, depth_gt, R, S, cfg.raw_noise_std, noise, key,
                self.ray_offset, L.ctypes.byref(lp), self.d_enc, st.grad_mlp, self.ws, self.stats, self.depth,
-               self.opacity, None, self.level_max_ptr, s)
+               self.opacity, None, self.level_max_ptr, self.d_jac if self.compact_denc else None, s)
         m(prof, "field")
+        self._r_last = R
         # 5. hash-grid backward
         m(prof, "grid_bwd")
         flags = (L.BWD_COUNTS_READY if self.count_in_forward else 0) | L.BWD_LEVEL_MAX_READY
         if self.allreduce is None:
-            L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(st.desc), rays, self.z, R, S, self.d_enc, N, st.grad_table,
-                   self.bwd_ws, self.bwd_ws_bytes, flags, s)
+            self._grid_bwd(rays, R, S, N, flags, s)
             m(prof, "grid_bwd")
         else:
             # 6. data-parallel gradient exchange, bucketed by level range: each range's slice of the
             # gradient is all-reduced (async) while the next range accumulates; the MLP gradient
             # travels with the last range
-            L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(st.desc), rays, self.z, R, S, self.d_enc, N, st.grad_table,
-                   self.bwd_ws, self.bwd_ws_bytes, flags | L.BWD_NO_ACCUM, s)
+            self._grid_bwd(rays, R, S, N, flags | L.BWD_NO_ACCUM, s)
             pending = []
             for l0, l1 in self.ar_groups:
                 L.call("lnr_hashgrid_bwd_accum", L.ctypes.byref(st.desc), R * S, self.bwd_ws, self.bwd_ws_bytes, l0,
@@ -348,6 +355,31 @@ class StepEngine:
             self.ogm_update(rays, depth_gt, scale)
             m(prof, "ogm")
         return self.loss_out
+
+    def d_sigma(self, n_rays=None):
+        """dL/dsigma (n_rays * S) of the last step: lnr_field_train leaves it in its workspace after the dW
+        slabs, whose count follows the call's ray count."""
+        r = self._r_last if n_rays is None else n_rays
+        off = int(L.lib().lnr_dw_workspace_words(r))
+        return self.ws[off:off + r * self.S]
+
+    def denc_f32(self):
+        """The last step's encoding gradient as (L, N, 2) fp32 (tests and tools; the step itself keeps
+        the compact form: d_sigma * J, computed exactly so in the backward)."""
+        if not self.compact_denc:
+            return self.d_enc
+        nl, n = self.cfg.n_levels, self._r_last * self.S
+        return (self.d_jac.view(torch.float16).view(nl, self.N, 2)[:, :n].float()
+                * self.d_sigma().view(1, n, 1))
+
+    def _grid_bwd(self, rays, R, S, N, flags, s):
+        st = self.state
+        if self.compact_denc:
+            L.call("lnr_hashgrid_bwd_rays_jac", L.ctypes.byref(st.desc), rays, self.z, R, S, self.d_jac,
+                   self.d_sigma(R), N, st.grad_table, self.bwd_ws, self.bwd_ws_bytes, flags, s)
+        else:
+            L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(st.desc), rays, self.z, R, S, self.d_enc, N, st.grad_table,
+                   self.bwd_ws, self.bwd_ws_bytes, flags, s)
 
     def ogm_update(self, rays, depth_gt, scale):
         """Optimizer._step_occupancy_grid (optimizer.py:897-908).  Data-parallel: the grid gradient

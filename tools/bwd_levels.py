@@ -40,8 +40,7 @@ def main(cfg_name="C2", *extra):
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
-        L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(st.desc), rays, eng.z, R, S, eng.d_enc, N, st.grad_table,
-               eng.bwd_ws, eng.bwd_ws_bytes, L.BWD_COUNTS_READY | L.BWD_NO_ACCUM, s)
+        eng._grid_bwd(rays, R, S, N, L.BWD_COUNTS_READY | L.BWD_LEVEL_MAX_READY | L.BWD_NO_ACCUM, s)
         e1.record()
         evs = [e1]
         for (l0, l1) in ranges:

@@ -30,7 +30,7 @@ def main(cfg_name="C2"):
             eng.step_window(window, global_step=it)
             break
         torch.cuda.synchronize()
-        de = eng.d_enc[:, :eng.N].float()
+        de = eng.denc_f32().float()
         zero = (de == 0).all(-1).float().mean(1).cpu().numpy()
         mx = de.abs().amax((1, 2)).cpu().numpy()
         print(f"step {it}: zero-gradient share per level {np.round(zero, 3).tolist()}")
@@ -42,7 +42,7 @@ def main(cfg_name="C2"):
     for it in range(60, 80):
         eng.step_window(window, global_step=it)
     torch.cuda.synchronize()
-    de = eng.d_enc[:, :eng.N].float()
+    de = eng.denc_f32().float()
     zero = (de == 0).all(-1).float().mean(1).cpu().numpy()
     print(f"step 79: zero-gradient share per level {np.round(zero, 3).tolist()}")
     # magnitude distribution relative to the level max (fp16 range check)

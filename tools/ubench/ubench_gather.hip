@@ -1,9 +1,10 @@
 // Gather throughput from an L2-resident 1 MB table: cost model of the hash-grid forward's loads.
-// Each thread: K gathers at random (hashed) positions; variants differ in width / pairing.
+// Each thread: K gathers at random (hashed) positions; variants differ in width / pairing and in the
+// cache-policy bits of the load (does an L1-bypassing gather move less than a 128-B line from L2?).
 #include <hip/hip_runtime.h>
 #include <cstdio>
 __device__ __forceinline__ uint32_t mix(uint32_t x) { x ^= x >> 16; x *= 0x7feb352d; x ^= x >> 15; x *= 0x846ca68b; x ^= x >> 16; return x; }
-template <int MODE>
+template <int MODE, int AUX = 0>
 __global__ void __launch_bounds__(256) kg(const uint32_t* __restrict__ t, uint32_t mask, int K, uint32_t* out) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   uint32_t acc = 0;
@@ -21,6 +22,11 @@ __global__ void __launch_bounds__(256) kg(const uint32_t* __restrict__ t, uint32
       acc += t[e];
     } else if (MODE == 4) {  // 2 dword gathers, partner in a different line
       acc += t[e] + t[(e + 4096u) & mask];
+    } else if (MODE == 5) {  // 1 dword, nontemporal
+      acc += __builtin_nontemporal_load(t + e);
+    } else {  // 1 dword buffer load with cache-policy bits MODE - 6 (gfx950: 1 sc0, 2 nt, 8? sc1)
+      __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)t, 0, (int)((mask + 1) * 4), 0x00020000);
+      acc += __builtin_amdgcn_raw_buffer_load_b32(r, (int)(e * 4), 0, AUX);
     }
   }
   if (acc == 0x12345678u) out[0] = acc;
@@ -31,8 +37,9 @@ int main() {
   hipMalloc(&t, n * 4); hipMalloc(&out, 4); hipMemset(t, 1, n * 4);
   const int blocks = 65536, K = 8;
   hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
-  const char* names[] = {"2x dword (pair)", "1x dwordx2", "1x dwordx4", "1x dword", "2x dword (far)"};
-  for (int m = 0; m < 5; ++m) {
+  const char* names[] = {"2x dword (pair)", "1x dwordx2", "1x dwordx4", "1x dword", "2x dword (far)", "1x dword nt",
+                         "buf aux0", "buf aux1 sc0", "buf aux2 nt", "buf aux3", "buf aux16", "buf aux17"};
+  for (int m = 0; m < 12; ++m) {
     for (int rep = 0; rep < 3; ++rep) {
       hipEventRecord(a);
       switch (m) {
@@ -41,6 +48,13 @@ int main() {
         case 2: kg<2><<<blocks, 256>>>(t, n - 1, K, out); break;
         case 3: kg<3><<<blocks, 256>>>(t, n - 1, K, out); break;
         case 4: kg<4><<<blocks, 256>>>(t, n - 1, K, out); break;
+        case 5: kg<5><<<blocks, 256>>>(t, n - 1, K, out); break;
+        case 6: kg<6, 0><<<blocks, 256>>>(t, n - 1, K, out); break;
+        case 7: kg<6, 1><<<blocks, 256>>>(t, n - 1, K, out); break;
+        case 8: kg<6, 2><<<blocks, 256>>>(t, n - 1, K, out); break;
+        case 9: kg<6, 3><<<blocks, 256>>>(t, n - 1, K, out); break;
+        case 10: kg<6, 16><<<blocks, 256>>>(t, n - 1, K, out); break;
+        case 11: kg<6, 17><<<blocks, 256>>>(t, n - 1, K, out); break;
       }
       hipEventRecord(b); hipEventSynchronize(b);
       float ms; hipEventElapsedTime(&ms, a, b);
