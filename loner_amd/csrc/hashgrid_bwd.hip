@@ -797,12 +797,16 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
 
 // Buckets the accumulation did not finish: cut buckets = the sum of their pieces' partial chunks in
 // workgroup order (deterministic), empty buckets = 0.  One workgroup per bucket of [b_begin, b_end).
-__global__ void __launch_bounds__(256) k_bwd_finalize(GridArgs a, BwdWorkspace ws, float* __restrict__ d_table,
-                                                      uint32_t b_begin, uint32_t b_end) {
+constexpr int kFinalizeThreads = 1024;  // 8 consecutive values per thread: 2 kChunk in one pass
+__global__ void __launch_bounds__(kFinalizeThreads) k_bwd_finalize(GridArgs a, BwdWorkspace ws, float* __restrict__ d_table,
+                                                                   uint32_t b_begin, uint32_t b_end) {
+  static_assert(2 * kChunk == 8 * kFinalizeThreads, "one pass");
+  typedef long long i64x2 __attribute__((ext_vector_type(2)));
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
   const uint32_t b = b_begin + blockIdx.x;
   const uint64_t r0 = ws.seg_start[b_begin], R = ws.seg_start[b_end] - r0;
   const uint64_t s0 = ws.seg_start[b], s1 = ws.seg_start[b + 1];
-  uint32_t g0 = 0, g1 = 0;
+  uint32_t g0 = 1, g1 = 0;  // pieces g0..g1 (none for an empty bucket)
   if (s1 > s0) {
     g0 = group_of(r0, R, s0);
     g1 = group_of(r0, R, s1 - 1);
@@ -812,17 +816,32 @@ __global__ void __launch_bounds__(256) k_bwd_finalize(GridArgs a, BwdWorkspace w
   const uint32_t ent0 = (b - a.bucket_base[l]) * kChunk;
   const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
   const double inv = unit_back(a, ws, l, bucket_k2(ws, b));  // the accumulate kernel's per-bucket unit
-  float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0);
-  for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) {
-    long long v = 0;
-    if (s1 > s0) {
-      for (uint32_t g = g0; g <= g1; ++g) {
-        const uint64_t gb = range_at(r0, R, g);
-        if (gb >= range_at(r0, R, g + 1)) continue;  // an empty range holds no piece
-        v += ws.partial[(int64_t)(2 * g + (gb > s0 ? 0 : 1)) * (2 * kChunk) + t];
-      }
+  const uint32_t t0 = 8 * threadIdx.x;
+  if (t0 >= 2 * nent) return;
+  long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (uint32_t g = g0; g <= g1; ++g) {  // pieces in workgroup order: deterministic (and exact anyway)
+    const uint64_t gb = range_at(r0, R, g);
+    if (gb >= range_at(r0, R, g + 1)) continue;  // an empty range holds no piece
+    const i64x2* src = reinterpret_cast<const i64x2*>(ws.partial + (int64_t)(2 * g + (gb > s0 ? 0 : 1)) * (2 * kChunk) + t0);
+    i64x2 q[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = src[k];  // 4 loads in flight
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[2 * k] += q[k].x;
+      v[2 * k + 1] += q[k].y;
     }
-    dst[t] = (float)((double)v * inv);
+  }
+  float o[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o[k] = (float)((double)v[k] * inv);
+  float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0) + t0;
+  if (t0 + 8 <= 2 * nent && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0)) {
+    reinterpret_cast<f32x4v*>(dst)[0] = f32x4v{o[0], o[1], o[2], o[3]};
+    reinterpret_cast<f32x4v*>(dst)[1] = f32x4v{o[4], o[5], o[6], o[7]};
+  } else {
+    for (int k = 0; k < 8; ++k)
+      if (t0 + k < 2 * nent) dst[k] = o[k];
   }
 }
 
@@ -834,7 +853,7 @@ static void launch_accum(const GridArgs& a, const BwdWorkspace& w, const lnr_gri
   (void)n;
   hipLaunchKernelGGL(k_bwd_accum, dim3(kAccumGroups), dim3(kAccumThreads), 2 * kChunk * sizeof(unsigned long long), st,
                      a, w, d_table, b0, b1);
-  hipLaunchKernelGGL(k_bwd_finalize, dim3(b1 - b0), dim3(256), 0, st, a, w, d_table, b0, b1);
+  hipLaunchKernelGGL(k_bwd_finalize, dim3(b1 - b0), dim3(kFinalizeThreads), 0, st, a, w, d_table, b0, b1);
 }
 
 template <class PosFn, class GradFn>

@@ -1,13 +1,14 @@
-# GPU box: FETCH_SIZE and WRITE_SIZE passes (one --pmc pass each, kernel trace only) over the C2
-# kernel driver tools/exp_kernels.py -> gpurun_out/pmc/FETCH_SIZE, gpurun_out/pmc/WRITE_SIZE.
+# GPU box: FETCH_SIZE and WRITE_SIZE passes (one --pmc pass each, kernel trace only) over the bench
+# command (the backward as the bench runs it: on-device rays, OGM-trained sampling) ->
+# gpurun_out/pmc/FETCH_SIZE, gpurun_out/pmc/WRITE_SIZE (tools/refresh_profiles.py: per-launch bytes).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
+CFG=${1:-C2}
 cd /tmp && export TMPDIR=/tmp
-export EXP_STEPS=${EXP_STEPS:-5}
 for c in FETCH_SIZE WRITE_SIZE; do
   rm -rf $R/gpurun_out/pmc/$c; mkdir -p $R/gpurun_out/pmc/$c
   timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $R/gpurun_out/pmc/$c -o run -- \
-    python3 $R/tools/exp_kernels.py > $R/gpurun_out/pmc/$c/out.txt 2>&1
+    python3 $R/bench.py --config $CFG --no-cpu-baseline --steps 20 > $R/gpurun_out/pmc/$c/out.txt 2>&1
   rc=$?; echo "pmc $c rc=$rc"
   [ $rc -eq 0 ] || { tail -5 $R/gpurun_out/pmc/$c/out.txt; exit 1; }
 done
