@@ -153,22 +153,12 @@ enum : int { kLevelsCoherent = 0, kLevelsFine = 1, kLevelsGeneric = 2, kLevelsAn
 #ifndef LNR_SCATTER_WAVES_PER_EU
 #define LNR_SCATTER_WAVES_PER_EU 1
 #endif
-// Record slot dst <- {word, value words} (Record values in hashgrid.hpp)
-__device__ __forceinline__ void rec_store(const BwdWorkspace& ws, uint64_t dst, uint32_t word, uint32_t va, uint32_t vb) {
-  if (kRecF16) {
-    *reinterpret_cast<u32x2*>(ws.rec + 2 * dst) = u32x2{word, va};
-  } else {
-    ws.rec[dst] = word;
-    *reinterpret_cast<u32x2*>(&ws.rec_v[dst]) = u32x2{va, vb};
-  }
-}
-
 // One (histogram row sb, level l) of the scatter; KIND as below, kLevelsAny meaning "any level".
 template <class PosFn, class GradFn, int KIND>
 __device__ __forceinline__ void scatter_row_level(const GridArgs& a, const PosFn& pos, int64_t n, const GradFn& grad,
                                                   const BwdWorkspace& ws, uint32_t l, int64_t sb, bool skip_zero,
                                                   char* smem) {
-  uint2* stage_v = reinterpret_cast<uint2*>(smem);                           // [kCap] value words
+  uint32_t* stage_v = reinterpret_cast<uint32_t*>(smem);                     // [kCap] fp16 value pairs
   uint64_t* gbase = reinterpret_cast<uint64_t*>(stage_v + kCap);             // [kMaxChunksPerLevel]
   uint32_t* stage_w = reinterpret_cast<uint32_t*>(gbase + kMaxChunksPerLevel);  // [kCap]
   uint32_t* rank_ctr = stage_w + kCap;                                       // [kMaxChunksPerLevel]
@@ -243,14 +233,14 @@ __device__ __forceinline__ void scatter_row_level(const GridArgs& a, const PosFn
   bool staged = true;
   auto place = [&](bool valid, uint32_t bk, uint32_t rank, uint32_t word, float2 val) {
     if (!valid) return;
-    const uint2 h = rec_vals(val.x, val.y, rs);
+    const uint32_t h = rec_half2(val.x, val.y, rs);
     if (staged) {
       const uint32_t t = start[bk] + rank;
       stage_w[t] = word;
       stage_v[t] = h;
       sbk[t] = (uint8_t)bk;
     } else {
-      rec_store(ws, gbase[bk] + rank, word, h.x, h.y);
+      ws.rec[gbase[bk] + rank] = make_uint2(word, h);
     }
   };
   // 2. records: rank, then place (hashgrid.hpp "Backward records")
@@ -331,7 +321,7 @@ __device__ __forceinline__ void scatter_row_level(const GridArgs& a, const PosFn
     for (uint32_t t = threadIdx.x; t < total; t += kSB) {
       const uint32_t bk = sbk[t];
       const uint64_t dst = gbase[bk] + (t - start[bk]);
-      rec_store(ws, dst, stage_w[t], stage_v[t].x, stage_v[t].y);
+      ws.rec[dst] = make_uint2(stage_w[t], stage_v[t]);
     }
   }
   LNR_STAMP(t4);
@@ -399,7 +389,7 @@ struct RowsLds {  // the small tables first: their addresses fit the 16-bit LDS 
   uint32_t total[NL];         // records of the row at each level
   uint32_t ctr[2][NB];        // rank counters
   LevelParams lv[NL];         // the level table (kernel arguments indexed per level would be loads)
-  uint4 stage[2][kRowsCap];   // staged records {word, global slot, value words}, bucket order
+  uint4 stage[2][kRowsCap];   // staged records {word, global slot, fp16 value pair, -}, bucket order
 };
 
 // NL levels, the first NM coherent (run-merging) and the rest fine, at most NB buckets per level:
@@ -482,7 +472,7 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
       const uint32_t t = threadIdx.x + u * kSB;
       const uint4 q = sm.stage[sbuf][t < (uint32_t)kRowsCap ? t : kRowsCap - 1];
       const uint32_t d = t < lim ? q.y : spare;
-      rec_store(ws, d, q.x, q.z, q.w);
+      ws.rec[d] = make_uint2(q.x, q.z);
     }
   };
 
@@ -509,10 +499,7 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
         for (int k = 0; k < 4; ++k) rank[k] = atomicAdd(&ctr[bk[k]], 1u);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-        {
-          const uint2 h = rec_vals(val[k].x, val[k].y, rs);
-          sm.stage[sbuf][s4[k].x + rank[k]] = make_uint4(word[k], s4[k].y + rank[k], h.x, h.y);
-        }
+          sm.stage[sbuf][s4[k].x + rank[k]] = make_uint4(word[k], s4[k].y + rank[k], rec_half2(val[k].x, val[k].y, rs), 0u);
       }
     };
     uint32_t bk4[4], w4[4];
@@ -571,7 +558,7 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
   copy_out(NL - 1);
 }
 
-constexpr size_t kScatterLds = (size_t)kCap * 8 + kMaxChunksPerLevel * 8 + (size_t)kCap * 4 + kMaxChunksPerLevel * 4 +
+constexpr size_t kScatterLds = (size_t)kCap * 4 + kMaxChunksPerLevel * 8 + (size_t)kCap * 4 + kMaxChunksPerLevel * 4 +
                                (kMaxChunksPerLevel + 1) * 4 + kCap;
 static_assert(kScatterLds <= 65536, "scatter LDS within the default dynamic limit");
 
@@ -629,9 +616,15 @@ __device__ __forceinline__ unsigned long long fixed_i64(float x) {
 #ifndef LNR_ACCUM_WAVES_PER_EU
 #define LNR_ACCUM_WAVES_PER_EU 8
 #endif
-#ifndef LNR_ACCUM_LOADS
-#define LNR_ACCUM_LOADS 8
+#ifndef LNR_ACCUM_DEPTH
+#define LNR_ACCUM_DEPTH 2
 #endif
+constexpr int kAccumDepth = LNR_ACCUM_DEPTH;     // tiles loaded ahead
+constexpr int kTile = 2 * kAccumThreads;         // records per tile: 2 per thread
+static_assert(kTile == 2048, "the stage's swizzle and the strided reads assume 64-lane waves x 16 x 2");
+// the stage position of tile record q: bits 1-4 XOR bits 5-8 (record pairs stay adjacent: the stores
+// are 16 B), so a wave's reads of records 32 apart spread over the banks
+__device__ __forceinline__ uint32_t stage_pos(uint32_t q) { return q ^ (((q >> 5) & 15u) << 1); }
 // Workgroup i's record range [range_at(i), range_at(i + 1)) of the R records from r0: an even split.
 __device__ __forceinline__ uint64_t range_at(uint64_t r0, uint64_t R, uint32_t i) {
   return r0 + (R * i) / kAccumGroups;
@@ -663,11 +656,10 @@ extern "C" int lnr_debug_accum_wg(unsigned long long* out) {
 // a piece cut at its start, 2i + 1 for one cut only at its end).
 __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_accum(GridArgs a, BwdWorkspace ws, float* __restrict__ d_table,
                                                                                         uint32_t b_begin, uint32_t b_end) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [2][kChunk] int64 fixed point
-  // (one array per feature: 8-B atomics on random entries spread over twice the bank pairs)
+  __shared__ unsigned long long acc[2 * kChunk];  // int64 fixed point, one array per feature (8-B atomics
+                                                  // on random entries spread over twice the bank pairs)
+  __shared__ __attribute__((aligned(16))) uint2 stage[kTile];  // the tile's records, swizzled
   const int lane = threadIdx.x & 63;
-  const int mix = (int)((((uint32_t)lane * 0x9E3779B1u) >> 16) ^ (uint32_t)(lane >> 2)) & (2 * LNR_ACCUM_LOADS - 1);
   const uint64_t r0 = ws.seg_start[b_begin], R = ws.seg_start[b_end] - r0;
 #ifdef LNR_ACCUM_PAIR_REVERSE
   const uint32_t gi = blockIdx.x < kAccumGroups / 2 ? blockIdx.x : (3 * kAccumGroups / 2 - 1) - blockIdx.x;
@@ -698,56 +690,54 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
     for (int t = threadIdx.x; t < 2 * kChunk; t += blockDim.x) acc[t] = 0ull;
     lds_barrier();
     LNR_STAMP(t1);
-    // 2 records per lane per 16-B load, LNR_ACCUM_LOADS loads in flight (2 LNR_ACCUM_LOADS slots).
-    // Atomic instruction u takes slot (u + mix) of each lane, mix a per-lane hash: adjacent records of
-    // a bucket (one ray's consecutive samples: equal or neighbouring corners, whose equal addresses
-    // serialise within one LDS instruction) then rarely meet in one instruction.
+    // Tiles of kTile records pass through LDS: each thread loads 2 consecutive records (one 16-B load,
+    // coalesced) and stores them to the tile stage; then lane L of wave w takes records 32 L + 2 w and
+    // + 1 of the tile, so one atomic instruction holds records 32 apart.  Adjacent records of a bucket
+    // are one ray's consecutive samples (equal or neighbouring corners), and equal addresses
+    // serialise within one LDS instruction; this way they meet in one only by a hash collision.
+    // The stage is XOR-swizzled (stage_pos) so those strided reads spread over the banks.
+    // Loads run kAccumDepth tiles ahead (registers).
     // A pair record (p > 0) adds (1 - tx) v to corner e0 and tx v to e1 = e0 ^ (2^p - 1), a single
     // record (p = 0, tx = 0) adds v to e0.  int64 sums: the result does not depend on the order.
     const uint64_t beg2 = beg & ~1ull;
-    // one scale per bucket (the pieces' partials add exactly); fp16 records carry 2^k_l already,
-    // fp32 records get it here
+    // one scale per bucket (the pieces' partials add exactly); the records carry 2^k_l already
     const int k2 = bucket_k2(ws, b);
-    const float fs = ldexpf(1.f, k2 + (kRecF16 ? 0 : rec_exp_for(ws.level_max[l], l < a.merge_levels)));
+    const float fs = ldexpf(1.f, k2);
     const float ftx = fs * kInvU16;
-    for (uint64_t rb = beg2 + 2 * (threadIdx.x & ~63u); rb < end; rb += 2 * LNR_ACCUM_LOADS * kAccumThreads) {
-      uint2 qw[LNR_ACCUM_LOADS], qh[LNR_ACCUM_LOADS], qg[LNR_ACCUM_LOADS];  // words, value words a, b
+    const uint64_t n_tiles = (end - beg2 + kTile - 1) / kTile;
+    u32x4 buf[kAccumDepth];  // this thread's 2 records of the tiles ahead: {w0, v0, w1, v1}
+    auto load_tile = [&](uint64_t tile) {
+      const uint64_t rr = beg2 + tile * kTile + 2 * threadIdx.x;
+      const uint64_t rc = rr < end ? rr : beg2;  // unconditional loads
+      return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(&ws.rec[rc]));
+    };
 #pragma unroll
-      for (int k = 0; k < LNR_ACCUM_LOADS; ++k) {
-        const uint64_t rr = rb + 2 * lane + (uint64_t)k * 2 * kAccumThreads;
-        const uint64_t rc = rr < end ? rr : beg2;  // unconditional loads: no branch to wait at
-        uint32_t w0, w1;
-        if (kRecF16) {
-          const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(ws.rec + 2 * rc));
-          w0 = q.x;
-          w1 = q.z;
-          qh[k] = make_uint2(q.y, q.w);
-          qg[k] = make_uint2(0u, 0u);
-        } else {
-          const u32x2 q = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(ws.rec + rc));
-          const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(&ws.rec_v[rc]));
-          w0 = q.x;
-          w1 = q.y;
-          qh[k] = make_uint2(v.x, v.z);  // value 0 of records rc, rc + 1
-          qg[k] = make_uint2(v.y, v.w);  // value 1
-        }
-        qw[k] = make_uint2(rr < beg || rr >= end ? kRecNone : w0, rr + 1 >= end ? kRecNone : w1);
+    for (int d = 0; d < kAccumDepth; ++d) buf[d] = load_tile((uint64_t)d < n_tiles ? d : 0);
+    const uint32_t q0 = 32u * lane + 2u * (threadIdx.x >> 6);  // this lane's records in a tile
+    for (uint64_t tile = 0; tile < n_tiles; ++tile) {
+      const int slot = (int)(tile % kAccumDepth);
+      u32x4 cur = buf[0];
+#pragma unroll
+      for (int d = 1; d < kAccumDepth; ++d)
+        if (slot == d) cur = buf[d];
+      lds_barrier();  // the previous tile's stage reads are done
+      *reinterpret_cast<u32x4*>(&stage[stage_pos(2 * threadIdx.x)]) = cur;
+      {
+        const uint64_t nt = tile + kAccumDepth;
+        const u32x4 q = load_tile(nt < n_tiles ? nt : 0);
+#pragma unroll
+        for (int d = 0; d < kAccumDepth; ++d)
+          if (slot == d) buf[d] = q;
       }
+      lds_barrier();
+      const uint64_t base = beg2 + tile * kTile;
 #pragma unroll
-      for (int u = 0; u < 2 * LNR_ACCUM_LOADS; ++u) {
-        const int sl = (u + mix) & (2 * LNR_ACCUM_LOADS - 1);
-        uint2 qa = qw[0], qb = qh[0], qc = qg[0];
-#pragma unroll
-        for (int k = 1; k < LNR_ACCUM_LOADS; ++k)
-          if ((sl >> 1) == k) {
-            qa = qw[k];
-            qb = qh[k];
-            qc = qg[k];
-          }
-        const uint32_t w = (sl & 1) ? qa.y : qa.x;
-        if (w != kRecNone) {
-          const uint32_t ha = (sl & 1) ? qb.y : qb.x, hb = (sl & 1) ? qc.y : qc.x;
-          const float v0 = rec_v0(ha, hb), v1 = rec_v1(ha, hb);
+      for (int r = 0; r < 2; ++r) {
+        const uint2 rec = stage[stage_pos(q0 + r)];
+        const uint64_t rr = base + q0 + r;
+        if (rr >= beg && rr < end) {
+          const uint32_t w = rec.x;
+          const float v0 = rec_v0(rec.y), v1 = rec_v1(rec.y);
           const uint32_t e0 = w & (kChunk - 1);
           const uint32_t p = (w >> kChunkLog2) & 15u;
           const float tx = (float)(w >> 16) * ftx;  // 0 for single-corner records; pre-scaled
@@ -851,7 +841,7 @@ static void launch_accum(const GridArgs& a, const BwdWorkspace& w, const lnr_gri
   const uint32_t b0 = a.bucket_base[l0], b1 = a.bucket_base[l1];
   if (b1 <= b0) return;
   (void)n;
-  hipLaunchKernelGGL(k_bwd_accum, dim3(kAccumGroups), dim3(kAccumThreads), 2 * kChunk * sizeof(unsigned long long), st,
+  hipLaunchKernelGGL(k_bwd_accum, dim3(kAccumGroups), dim3(kAccumThreads), 0, st,
                      a, w, d_table, b0, b1);
   hipLaunchKernelGGL(k_bwd_finalize, dim3(b1 - b0), dim3(kFinalizeThreads), 0, st, a, w, d_table, b0, b1);
 }
