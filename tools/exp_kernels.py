@@ -64,8 +64,7 @@ def main():
     for i in range(steps):  # forward without histogram, then count + full backward
         L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(st.desc), rays, eng.z, R, n_samples, st.table_f16, eng.enc, N,
                None, 0, s)
-        L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(st.desc), rays, eng.z, R, n_samples, eng.d_enc, N, st.grad_table,
-               eng.bwd_ws, eng.bwd_ws_bytes, 0, s)
+        eng._grid_bwd(rays, R, n_samples, N, 0, s)
     torch.cuda.synchronize()
     print(f"{cfg_name}: {ms:.3f} ms/step (no OGM), {R * n_samples / ms * 1e3:.3e} ray-samples/s", flush=True)
 

@@ -14,6 +14,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run 
   python3 $R/bench.py --config $CFG --no-cpu-baseline > $R/gpurun_out/bench_prof.json 2> $R/gpurun_out/bench_prof.err \
   || { tail -20 $R/gpurun_out/bench_prof.err; exit 1; }
 bash $R/tools/pmc_hbm.sh $CFG || exit 1
-bash $R/tools/pmc_mfma.sh || exit 1
+bash $R/tools/pmc_mfma.sh $CFG || exit 1
 bash $R/tools/pmc_step.sh $CFG || exit 1
 echo profiles done

@@ -1,11 +1,11 @@
-# GPU box: one --pmc pass (kernel trace only) of MFMA busy cycles and GPU-active cycles over the C2
-# kernel driver tools/exp_kernels.py -> gpurun_out/pmc/MFMA (tools/refresh_profiles.py reads it).
+# GPU box: one --pmc pass (kernel trace only) of MFMA busy cycles and GPU-active cycles over the bench
+# command -> gpurun_out/pmc/MFMA (tools/refresh_profiles.py reads it).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
-export EXP_STEPS=${EXP_STEPS:-5}
+CFG=${1:-C2}
 rm -rf $R/gpurun_out/pmc/MFMA; mkdir -p $R/gpurun_out/pmc/MFMA
 timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv \
-  -d $R/gpurun_out/pmc/MFMA -o run -- python3 $R/tools/exp_kernels.py > $R/gpurun_out/pmc/MFMA/out.txt 2>&1
+  -d $R/gpurun_out/pmc/MFMA -o run -- python3 $R/bench.py --config $CFG --no-cpu-baseline --steps 20 > $R/gpurun_out/pmc/MFMA/out.txt 2>&1
 rc=$?; echo "pmc MFMA rc=$rc"
 [ $rc -eq 0 ] || { tail -5 $R/gpurun_out/pmc/MFMA/out.txt; exit 1; }
