@@ -222,7 +222,7 @@ template <class PosFn>
 static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16_t* table, uint32_t* enc,
                       int64_t enc_stride, void* bwd_ws, int64_t bwd_ws_bytes, hipStream_t st, const char* who,
                       const float* live = nullptr) {
-  GridArgs a = make_args(d);
+  GridArgs a = make_args(d, pos.samples_per_ray());
   LNR_REQUIRE(n < (int64_t(1) << 31), "%s: n=%lld samples exceeds 2^31", who, (long long)n);
   dim3 grid((unsigned)((n + 255) / 256), d->n_levels);
   if (bwd_ws) {

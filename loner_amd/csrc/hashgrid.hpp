@@ -35,19 +35,22 @@ struct GridArgs {
   uint32_t merge_levels;  // levels [0, merge_levels) merge equal corner indices across lanes
 };
 
-// Levels whose cell edge spans several consecutive samples of a ray (resolution <= 256 at the
-// reference's ray lengths / sample counts) produce runs of equal corner indices.
+// Levels whose cell edge spans several consecutive samples of a ray produce runs of equal corner
+// indices.  At the reference's 512 samples per ray (after the OGM has concentrated them) that holds
+// up to resolution 512; the sample density along a ray scales with the samples
+// per ray, so the bound does too (C1's 64 samples: resolution <= 64).  Positions not from rays: 512.
 #ifndef LNR_MERGE_MAX_RES
 #define LNR_MERGE_MAX_RES 512
 #endif
-inline uint32_t merge_levels_for(const lnr_grid_desc* d) {
+inline uint32_t merge_levels_for(const lnr_grid_desc* d, int32_t samples_per_ray = 0) {
+  const int64_t max_res = samples_per_ray > 0 ? (int64_t)LNR_MERGE_MAX_RES * samples_per_ray / 512 : LNR_MERGE_MAX_RES;
   uint32_t m = 0;
   for (uint32_t l = 0; l < d->n_levels; ++l)
-    if (d->resolution[l] <= LNR_MERGE_MAX_RES) m = l + 1;
+    if ((int64_t)d->resolution[l] <= max_res) m = l + 1;
   return m;
 }
 
-inline GridArgs make_args(const lnr_grid_desc* d) {
+inline GridArgs make_args(const lnr_grid_desc* d, int32_t samples_per_ray = 0) {
   GridArgs a{};
   a.n_levels = d->n_levels;
   for (uint32_t l = 0; l < d->n_levels; ++l) {
@@ -69,7 +72,7 @@ inline GridArgs make_args(const lnr_grid_desc* d) {
   }
   a.bucket_base[d->n_levels] = b;
   a.n_buckets = b;
-  a.merge_levels = merge_levels_for(d);
+  a.merge_levels = merge_levels_for(d, samples_per_ray);
   for (uint32_t l = 0; l < d->n_levels; ++l)
     a.lv[l].fine = (a.lv[l].hashed && a.lv[l].size_mask && l >= a.merge_levels) ? 1u : 0u;
   return a;
@@ -91,6 +94,7 @@ __device__ __forceinline__ uint32_t grid_index(const LevelParams& p, uint32_t x,
 // loads before a barrier call them on either side of it.
 struct PosFromArray {
   const float* pos;
+  int32_t samples_per_ray() const { return 0; }  // not from rays
   struct Raw {
     float x, y, z;
   };
@@ -106,6 +110,7 @@ struct PosFromRays {
   const float* rays;
   const float* zs;
   int32_t n_samples;
+  int32_t samples_per_ray() const { return n_samples; }
   struct Raw {
     float ox, oy, oz, dx, dy, dz, t;
   };
@@ -400,15 +405,18 @@ constexpr int kRowsPerChunk = 256;  // histogram rows per scan chunk
 // Record values: two fp16 of v 2^k_l (8-B records {word, half2}), at a per-level power-of-two scale
 // 2^k_l from the level's max |d_enc| (ws.level_max, known before the scatter): every fine or generic
 // record is w * g with w <= 1, and a coherent record sums at most one wave's run of 64 lanes, so
-// |v| 2^k_l < 2^15 and no record overflows.  Each record rounds to 11 significant bits (relative
+// |v| 2^k_l < 2^15 (2^k_l = 2^9 / 2^E, level max < 2^E) and no record overflows.  Each record rounds to 11 significant bits (relative
 // 2^-12), where tcnn's own fp16 gradient rounds every partial sum; the accumulation adds the
 // records exactly (int64 fixed point), so that rounding is the only one.  (fp32 values, 12-B
 // records, were measured: the scatter 0.85 against 0.69 ms and the accumulation 0.56 against 0.45
 // ms at C2.)
-__device__ __forceinline__ int rec_exp_for(float level_max, bool coherent) {
+// Every level keeps the coherent levels' 2^6 headroom, so a level's scale does not depend on which
+// levels merge runs (that follows the samples per ray); fine-level records then sit below 2^9, still
+// normal fp16 down to 2^-23 of the level's largest.
+__device__ __forceinline__ int rec_exp_for(float level_max) {
   int E;
   frexpf(level_max, &E);  // level_max < 2^E (E = 0 for 0)
-  const int k = 15 - E - (coherent ? 6 : 0);
+  const int k = 9 - E;
   return k > 100 ? 100 : (k < -60 ? -60 : k);
 }
 __device__ __forceinline__ uint32_t rec_half2(float v0, float v1, float s) {

@@ -174,7 +174,7 @@ __device__ __forceinline__ void scatter_row_level(const GridArgs& a, const PosFn
   const uint32_t b0 = a.bucket_base[l];
   const uint32_t nb = a.bucket_base[l + 1] - b0;
   const LevelParams& lv = a.lv[l];
-  const float rs = ldexpf(1.f, rec_exp_for(ws.level_max[l], l < a.merge_levels));  // record scale
+  const float rs = ldexpf(1.f, rec_exp_for(ws.level_max[l]));  // record scale
   static_assert(kMaxChunksPerLevel <= 128, "two buckets per lane of wave 0");
   LNR_STAMP(t0);
   // 1. Global loads, all unconditional (clamped indices) so nothing waits for them before it must:
@@ -349,19 +349,23 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter_o
                                                                                       bool skip_zero) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ unsigned long long masks[kSB / 64];
-  // workgroup b checks the flags of items [b kSB, (b + 1) kSB), item = level * n_sb + row
-  const int64_t items = ws.n_sb * a.n_levels;
-  const int64_t it = (int64_t)blockIdx.x * kSB + threadIdx.x;
-  const unsigned long long m = __ballot(it < items && ws.ovf[it] != 0);
-  if ((threadIdx.x & 63) == 0) masks[threadIdx.x >> 6] = m;
-  __syncthreads();
-  for (int w = 0; w < kSB / 64; ++w) {
-    for (unsigned long long mm = masks[w]; mm; mm &= mm - 1) {
-      const int64_t q = (int64_t)blockIdx.x * kSB + 64 * w + __ffsll((long long)mm) - 1;
-      scatter_row_level<PosFn, GradFn, kLevelsAny>(a, pos, n, grad, ws, (uint32_t)(q / ws.n_sb), q % ws.n_sb,
-                                                   skip_zero, smem);
-      lds_barrier();
+  // workgroup b checks items b, b + G, b + 2G, ... (G = gridDim.x, item = level * n_sb + row), kSB at
+  // a time: flagged items are runs of rows of one level, and the stride deals them over the grid
+  const int64_t items = ws.n_sb * a.n_levels, G = gridDim.x;
+  for (int64_t base = blockIdx.x; base < items; base += G * kSB) {
+    const int64_t it = base + G * threadIdx.x;
+    const unsigned long long m = __ballot(it < items && ws.ovf[it] != 0);
+    if ((threadIdx.x & 63) == 0) masks[threadIdx.x >> 6] = m;
+    __syncthreads();
+    for (int w = 0; w < kSB / 64; ++w) {
+      for (unsigned long long mm = masks[w]; mm; mm &= mm - 1) {
+        const int64_t q = base + G * (64 * w + __ffsll((long long)mm) - 1);
+        scatter_row_level<PosFn, GradFn, kLevelsAny>(a, pos, n, grad, ws, (uint32_t)(q / ws.n_sb), q % ws.n_sb,
+                                                     skip_zero, smem);
+        lds_barrier();
+      }
     }
+    __syncthreads();  // masks are rewritten
   }
 }
 
@@ -438,7 +442,7 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
   }
   float rsc[NL];  // per-level record scales (uniform: scalar loads)
 #pragma unroll
-  for (int l = 0; l < NL; ++l) rsc[l] = ldexpf(1.f, rec_exp_for(ws.level_max[l], l < NM));
+  for (int l = 0; l < NL; ++l) rsc[l] = ldexpf(1.f, rec_exp_for(ws.level_max[l]));
   float x = 0.f, y = 0.f, z = 0.f;
   pos.eval(raw, x, y, z);
   // prologue 3: wave w's levels' bucket starts (a wave prefix over the buckets, two per lane)
@@ -603,7 +607,7 @@ __device__ __forceinline__ int bucket_k2(const BwdWorkspace& ws, uint32_t b) {
 }
 // 2^-(k2 + k_l): fixed-point units back to gradient units (double: the exponent may pass fp32's range)
 __device__ __forceinline__ double unit_back(const GridArgs& a, const BwdWorkspace& ws, uint32_t l, int k2) {
-  return ldexp(1.0, -(k2 + rec_exp_for(ws.level_max[l], l < a.merge_levels)));
+  return ldexp(1.0, -(k2 + rec_exp_for(ws.level_max[l])));
 }
 // round(x) as int64 for |x| < 2^51: x + 1.5 2^52 in double places the rounded integer in the low
 // mantissa bits, and the constant's low word is 0, so only the high word needs the subtraction.
@@ -849,7 +853,7 @@ static void launch_accum(const GridArgs& a, const BwdWorkspace& w, const lnr_gri
 template <class PosFn, class GradFn>
 static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, GradFn grad, float* d_table,
                                void* workspace, int64_t ws_bytes, int32_t flags, hipStream_t st, const char* who) {
-  GridArgs a = make_args(d);
+  GridArgs a = make_args(d, pos.samples_per_ray());
   LNR_REQUIRE(a.n_buckets <= (uint32_t)kMaxBuckets, "%s: too many table chunks (%u)", who, a.n_buckets);
   for (uint32_t l = 0; l < d->n_levels; ++l)
     LNR_REQUIRE(a.bucket_base[l + 1] - a.bucket_base[l] <= (uint32_t)kMaxChunksPerLevel,
@@ -883,11 +887,15 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, Gra
   // plus the pass over the rows it could not stage; other grids (the colour grid's 2^19 levels have
   // 128 chunks): one workgroup per (row, level)
   const bool rows = L == 16 && all_fine && pow2 && 8 * n * (int64_t)L + 2 < (int64_t(1) << 32);
-  if (rows && m >= 5 && m <= 7 && maxnb <= 64) {
-    auto kern = m == 5 ? k_bwd_scatter_rows<PosFn, GradFn, 16, 5, 64>
-                       : (m == 6 ? k_bwd_scatter_rows<PosFn, GradFn, 16, 6, 64> : k_bwd_scatter_rows<PosFn, GradFn, 16, 7, 64>);
+  if (rows && m >= 3 && m <= 7 && maxnb <= 64) {
+    auto kern = m == 3   ? k_bwd_scatter_rows<PosFn, GradFn, 16, 3, 64>
+                : m == 4 ? k_bwd_scatter_rows<PosFn, GradFn, 16, 4, 64>
+                : m == 5 ? k_bwd_scatter_rows<PosFn, GradFn, 16, 5, 64>
+                : m == 6 ? k_bwd_scatter_rows<PosFn, GradFn, 16, 6, 64>
+                         : k_bwd_scatter_rows<PosFn, GradFn, 16, 7, 64>;
     hipLaunchKernelGGL(kern, dim3((unsigned)w.n_sb), dim3(kSB), 0, st, a, pos, n, grad, w, skip_zero);
-    hipLaunchKernelGGL((k_bwd_scatter_overflow<PosFn, GradFn>), dim3((unsigned)((w.n_sb * L + kSB - 1) / kSB)),
+    const int64_t items = w.n_sb * L;
+    hipLaunchKernelGGL((k_bwd_scatter_overflow<PosFn, GradFn>), dim3((unsigned)(items < 2048 ? items : 2048)),
                        dim3(kSB), kScatterLds, st, a, pos, n, grad, w, skip_zero);
   } else {
     hipLaunchKernelGGL((k_bwd_scatter<PosFn, GradFn, kLevelsAny>), dim3((unsigned)(w.n_sb * L)), dim3(kSB), kScatterLds,
