@@ -337,13 +337,15 @@ int lnr_build_camera_rays_window(const lnr_camera_frame* frames, int32_t n_frame
  * mean over the 3 * (global) rays: inv_count = 1 / (3 n_rays_global).  Writes rgb (R,3), loss[0]
  * (optional; local rays only), d_enc (level-major float2, the colour-grid backward's input, as
  * lnr_field_train's) and d_w (OVERWRITTEN: the colour MLP's weight gradient, tcnn flat layout,
- * lnr_rgb_mlp_params floats).  Deterministic (fixed-order slab reduction). */
+ * lnr_rgb_mlp_params floats).  Deterministic (fixed-order slab reduction).  d_enc_level_max
+ * (optional, 16 floats): OVERWRITTEN with max |d_enc| per level, as lnr_field_train's (pass
+ * lnr_hashgrid_bwd_level_max(...) and LNR_BWD_LEVEL_MAX_READY to the colour grid's backward). */
 int64_t lnr_rgb_mlp_params(int32_t n_hidden_layers);
 int64_t lnr_rgb_train_workspace_bytes(int32_t n_hidden_layers, int64_t n_rays);
 int lnr_rgb_train(const uint16_t* w_rgb, int32_t n_hidden_layers, const uint32_t* enc_rgb, int64_t enc_stride,
                   const float* rays, const float* weights, const float* intensities, int64_t n_rays,
                   int32_t n_samples, float inv_count, float* rgb, float* loss, float* d_enc, float* d_w,
-                  void* workspace, int64_t workspace_bytes, void* stream);
+                  void* workspace, int64_t workspace_bytes, float* d_enc_level_max, void* stream);
 
 /* ---------------------------------------------------------------- optimiser */
 /* torch.optim.Adam (no weight decay); step is 1-based.  shadow (fp16) may be NULL. */

@@ -135,7 +135,7 @@ _SIGNATURES = {
     "lnr_rgb_mlp_params": (c_i64, [c_i32]),
     "lnr_rgb_train_workspace_bytes": (c_i64, [c_i32, c_i64]),
     "lnr_rgb_train": (ctypes.c_int, [c_p, c_i32, c_p, c_i64, c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_p, c_p, c_p,
-                                     c_p, c_i64, c_p]),
+                                     c_p, c_i64, c_p, c_p]),
     "lnr_build_camera_rays": (ctypes.c_int, [ctypes.POINTER(CameraDesc), c_p, c_p, c_p, c_i64, c_p, c_p, c_p]),
     "lnr_build_camera_rays_window": (ctypes.c_int, [c_p, c_i32, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
     "lnr_motion_compensate": (ctypes.c_int, [ctypes.POINTER(MotionComp), c_p, c_p, c_p, c_i64, c_p]),

@@ -219,6 +219,9 @@ class CameraStepEngine:
         self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
         self.bwd_ws_bytes = int(L.lib().lnr_hashgrid_bwd_workspace_bytes(L.ctypes.byref(color.desc), N))
         self.bwd_ws = torch.empty(self.bwd_ws_bytes, dtype=torch.uint8, device=dev)
+        # the colour backward's per-level max |d_enc| (record scales), written by lnr_rgb_train
+        self.level_max_ptr = L.ctypes.c_void_p(L.lib().lnr_hashgrid_bwd_level_max(L.ctypes.byref(color.desc), N,
+                                                                                   L.ptr(self.bwd_ws)))
         self.ws_bytes = int(L.lib().lnr_rgb_train_workspace_bytes(color.n_hidden_layers, self.R))
         self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=dev)
 
@@ -256,9 +259,10 @@ class CameraStepEngine:
                    N, self.bwd_ws, self.bwd_ws_bytes, s)
         n_glob = R if n_rays_global is None else int(n_rays_global)
         L.call("lnr_rgb_train", cs.mlp_f16, cs.n_hidden_layers, self.enc_rgb, N, rays, self.weights, intensities, R,
-               S, 1.0 / (3.0 * n_glob), self.rgb, self.loss, self.d_enc, cs.grad_mlp, self.ws, self.ws_bytes, s)
+               S, 1.0 / (3.0 * n_glob), self.rgb, self.loss, self.d_enc, cs.grad_mlp, self.ws, self.ws_bytes,
+               self.level_max_ptr, s)
         L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(cs.desc), rays, self.z, R, S, self.d_enc, N, cs.grad_table,
-               self.bwd_ws, self.bwd_ws_bytes, 0 if self.skip_zero else L.BWD_COUNTS_READY, s)
+               self.bwd_ws, self.bwd_ws_bytes, (0 if self.skip_zero else L.BWD_COUNTS_READY) | L.BWD_LEVEL_MAX_READY, s)
         if self.allreduce is not None:
             self.allreduce(cs.grad)
         cs.adam_step += 1

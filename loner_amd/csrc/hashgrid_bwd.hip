@@ -887,6 +887,7 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, Gra
   // plus the pass over the rows it could not stage; other grids (the colour grid's 2^19 levels have
   // 128 chunks): one workgroup per (row, level)
   const bool rows = L == 16 && all_fine && pow2 && 8 * n * (int64_t)L + 2 < (int64_t(1) << 32);
+  bool looped = true;
   if (rows && m >= 3 && m <= 7 && maxnb <= 64) {
     auto kern = m == 3   ? k_bwd_scatter_rows<PosFn, GradFn, 16, 3, 64>
                 : m == 4 ? k_bwd_scatter_rows<PosFn, GradFn, 16, 4, 64>
@@ -894,12 +895,15 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, Gra
                 : m == 6 ? k_bwd_scatter_rows<PosFn, GradFn, 16, 6, 64>
                          : k_bwd_scatter_rows<PosFn, GradFn, 16, 7, 64>;
     hipLaunchKernelGGL(kern, dim3((unsigned)w.n_sb), dim3(kSB), 0, st, a, pos, n, grad, w, skip_zero);
+  } else {
+    looped = false;
+    hipLaunchKernelGGL((k_bwd_scatter<PosFn, GradFn, kLevelsAny>), dim3((unsigned)(w.n_sb * L)), dim3(kSB), kScatterLds,
+                       st, a, pos, n, grad, w, 0u, skip_zero);
+  }
+  if (looped) {  // the (row, level) items the level-looped scatter could not stage
     const int64_t items = w.n_sb * L;
     hipLaunchKernelGGL((k_bwd_scatter_overflow<PosFn, GradFn>), dim3((unsigned)(items < 2048 ? items : 2048)),
                        dim3(kSB), kScatterLds, st, a, pos, n, grad, w, skip_zero);
-  } else {
-    hipLaunchKernelGGL((k_bwd_scatter<PosFn, GradFn, kLevelsAny>), dim3((unsigned)(w.n_sb * L)), dim3(kSB), kScatterLds,
-                       st, a, pos, n, grad, w, 0u, skip_zero);
   }
   if (flags & LNR_BWD_NO_ACCUM) LNR_RETURN_LAUNCH(who);  // accumulate later, by level range
   launch_accum(a, w, d, n, 0, d->n_levels, d_table, st);

@@ -36,11 +36,13 @@ struct RgbArgs {
   float* g;               // (R, 3) dL/drgb = sign(rgb - gt) * inv_count
   float* ray_loss;        // (R) sum_k |rgb_k - gt_k|
   float inv_count;
+  float* denc_max;        // optional [16]: max |d_enc| per level (float bits, atomicMax; zeroed by the render)
 };
 
 template <int NH, bool TRAIN>
 __global__ void __launch_bounds__(64 * kRgbWaves) k_rgb_render(RgbArgs a) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  if (TRAIN && a.denc_max && blockIdx.x == 0 && threadIdx.x < 16) a.denc_max[threadIdx.x] = 0.f;  // before k_rgb_bwd_tiles
   RgbWeights<NH> rw;
   load_rgb_weights<NH>(a.w, rw);
   for (int64_t r = (int64_t)blockIdx.x * kRgbWaves + wid; r < a.n_rays; r += (int64_t)gridDim.x * kRgbWaves) {
@@ -293,6 +295,7 @@ __global__ void __launch_bounds__(64 * kRgbBwdWaves) k_rgb_bwd_tiles(RgbArgs a, 
   const int64_t per_iter = (int64_t)gridDim.x * kRgbBwdWaves;
   const int64_t n_iter = (n_tiles + per_iter - 1) / per_iter;
   float2* denc = reinterpret_cast<float2*>(d_enc);
+  float lmax[4] = {0.f, 0.f, 0.f, 0.f};  // max |d_enc| of this lane's levels 2g, 2g + 1, 8 + 2g, 9 + 2g
   // software pipelining: the next tile's HBM inputs are in flight while this tile computes (one wave
   // per SIMD at this LDS footprint, so latency is hidden by ILP only)
   uint32_t nx[4];
@@ -456,8 +459,11 @@ __global__ void __launch_bounds__(64 * kRgbBwdWaves) k_rgb_bwd_tiles(RgbArgs a, 
           ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0t[m][0], b0, ac, 0, 0, 0);
           ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0t[m][1], b1, ac, 0, 0, 0);
           const int lvl = 8 * m + 2 * g;
-          denc[(int64_t)lvl * a.enc_stride + n0 + c] = make_float2(ac[0] * inv, ac[1] * inv);
-          denc[(int64_t)(lvl + 1) * a.enc_stride + n0 + c] = make_float2(ac[2] * inv, ac[3] * inv);
+          const float2 q0 = make_float2(ac[0] * inv, ac[1] * inv), q1 = make_float2(ac[2] * inv, ac[3] * inv);
+          denc[(int64_t)lvl * a.enc_stride + n0 + c] = q0;
+          denc[(int64_t)(lvl + 1) * a.enc_stride + n0 + c] = q1;
+          lmax[2 * m] = fmaxf(lmax[2 * m], fmaxf(fabsf(q0.x), fabsf(q0.y)));
+          lmax[2 * m + 1] = fmaxf(lmax[2 * m + 1], fmaxf(fabsf(q1.x), fabsf(q1.y)));
         }
       }
     }
@@ -473,6 +479,16 @@ __global__ void __launch_bounds__(64 * kRgbBwdWaves) k_rgb_bwd_tiles(RgbArgs a, 
   if (wid == 0) rgb_owner_store<NH, 1>(sb, 0, acc, run_a);
   if (wid >= 1 && wid <= NH) rgb_owner_store<NH, 0>(sb, wid, acc, run_a);
   if (wid == (NH + 1) % kRgbBwdWaves) rgb_owner_store<NH, 2>(sb, NH + 1, acc, run_b);
+  if (a.denc_max) {  // the colour grid backward's record scales: 16-lane row max, one atomicMax per wave and level
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v = lmax[q];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+      if (c == 0 && v > 0.f)
+        atomicMax(reinterpret_cast<uint32_t*>(a.denc_max) + (q >> 1) * 8 + 2 * g + (q & 1), __float_as_uint(v));
+    }
+  }
 }
 
 // d_w[i] = sum over the nb slabs, fixed order (as reduce_slabs_fixed, any parameter count)
@@ -570,7 +586,8 @@ static int rgb_train_launch(RgbArgs a, float* d_enc, float* d_w, float* slab, fl
 extern "C" int lnr_rgb_train(const uint16_t* w_rgb, int32_t n_hidden_layers, const uint32_t* enc_rgb,
                              int64_t enc_stride, const float* rays, const float* weights, const float* intensities,
                              int64_t n_rays, int32_t n_samples, float inv_count, float* rgb, float* loss,
-                             float* d_enc, float* d_w, void* workspace, int64_t workspace_bytes, void* stream) {
+                             float* d_enc, float* d_w, void* workspace, int64_t workspace_bytes,
+                             float* d_enc_level_max, void* stream) {
   LNR_REQUIRE(n_hidden_layers >= 1 && n_hidden_layers <= 4,
               "lnr_rgb_train: n_hidden_layers=%d not supported (1..4, 64 neurons)", n_hidden_layers);
   LNR_REQUIRE(n_rays >= 0 && n_samples > 0 && n_samples % 16 == 0,
@@ -589,6 +606,7 @@ extern "C" int lnr_rgb_train(const uint16_t* w_rgb, int32_t n_hidden_layers, con
   RgbArgs a{};
   a.w = w_rgb; a.enc = enc_rgb; a.enc_stride = enc_stride; a.rays = rays; a.weights = weights; a.n_rays = n_rays;
   a.S = n_samples; a.rgb = rgb; a.gt = intensities; a.g = g; a.ray_loss = ray_loss; a.inv_count = inv_count;
+  a.denc_max = d_enc_level_max;
   hipStream_t st = as_stream(stream);
   switch (n_hidden_layers - 1) {
     case 0: rgb_train_launch<0>(a, d_enc, d_w, slab, loss, st); break;

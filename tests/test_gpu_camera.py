@@ -68,8 +68,11 @@ def test_rgb_train_vs_oracle(L, n_hidden):
     d_w = torch.full((P,), float("nan"), device=dev)
     nb = int(L.lib().lnr_rgb_train_workspace_bytes(n_hidden, R))
     ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+    lmax = torch.full((16,), 7.0, dtype=torch.float32, device=dev)  # overwritten
     L.call("lnr_rgb_train", cs.mlp_f16, n_hidden, t_enc, N, t_rays, t_w, t_gt, R, S, 1.0 / (3 * R), rgb, loss,
-           d_enc, d_w, ws, nb, L.stream(torch.device(dev)))
+           d_enc, d_w, ws, nb, lmax, L.stream(torch.device(dev)))
+    # the colour grid backward's record scales: max |d_enc| per level, exactly
+    np.testing.assert_array_equal(host(lmax), np.abs(host(d_enc)).max(axis=(1, 2)))
     got_rgb = host(rgb)
     assert np.abs(got_rgb - ref["rgb"]).max() < 5e-3
     assert abs(float(host(loss)[0]) - ref["loss"]) < 1e-3 * ref["loss"] + 1e-6
@@ -88,7 +91,7 @@ def test_rgb_train_vs_oracle(L, n_hidden):
     # deterministic: a second call gives the same bits
     d_w2 = torch.empty_like(d_w)
     L.call("lnr_rgb_train", cs.mlp_f16, n_hidden, t_enc, N, t_rays, t_w, t_gt, R, S, 1.0 / (3 * R), rgb, loss,
-           d_enc, d_w2, ws, nb, L.stream(torch.device(dev)))
+           d_enc, d_w2, ws, nb, None, L.stream(torch.device(dev)))
     assert torch.equal(d_w, d_w2)
 
 
