@@ -475,7 +475,7 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
     for (int u = 0; u < (kRowsCap + kSB - 1) / kSB; ++u) {
       const uint32_t t = threadIdx.x + u * kSB;
       const uint4 q = sm.stage[sbuf][t < (uint32_t)kRowsCap ? t : kRowsCap - 1];
-      const uint32_t d = t < lim ? q.y : spare;
+      const uint32_t d = t < lim && q.y < spare ? q.y : spare;  // (the bound: never a store outside the records)
       ws.rec[d] = make_uint2(q.x, q.z);
     }
   };
@@ -749,7 +749,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
           atomicAdd(&acc[e0], fixed_i64(s0 * v0));
           atomicAdd(&acc[kChunk + e0], fixed_i64(s0 * v1));
           if (p) {
-            const uint32_t e1 = e0 ^ ((1u << p) - 1u);
+            const uint32_t e1 = (e0 ^ ((1u << p) - 1u)) & (kChunk - 1);  // p <= 12 for every valid record
             atomicAdd(&acc[e1], fixed_i64(tx * v0));
             atomicAdd(&acc[kChunk + e1], fixed_i64(tx * v1));
           }
