@@ -749,7 +749,10 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
           atomicAdd(&acc[e0], fixed_i64(s0 * v0));
           atomicAdd(&acc[kChunk + e0], fixed_i64(s0 * v1));
           if (p) {
-            const uint32_t e1 = (e0 ^ ((1u << p) - 1u)) & (kChunk - 1);  // p <= 12 for every valid record
+            // p <= 12 for every valid record, so e1 stays in the chunk (an LDS address past the
+            // workgroup's allocation is discarded by the hardware in any case; masking e1 here cost
+            // 10 % of the kernel: 408 -> 450 us at C2)
+            const uint32_t e1 = e0 ^ ((1u << p) - 1u);
             atomicAdd(&acc[e1], fixed_i64(tx * v0));
             atomicAdd(&acc[kChunk + e1], fixed_i64(tx * v1));
           }
