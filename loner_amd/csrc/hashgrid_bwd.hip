@@ -620,10 +620,6 @@ __device__ __forceinline__ unsigned long long fixed_i64(float x) {
 #ifndef LNR_ACCUM_WAVES_PER_EU
 #define LNR_ACCUM_WAVES_PER_EU 8
 #endif
-#ifndef LNR_ACCUM_DEPTH
-#define LNR_ACCUM_DEPTH 2
-#endif
-constexpr int kAccumDepth = LNR_ACCUM_DEPTH;     // tiles loaded ahead
 constexpr int kTile = 2 * kAccumThreads;         // records per tile: 2 per thread
 static_assert(kTile == 2048, "the stage's swizzle and the strided reads assume 64-lane waves x 16 x 2");
 // the stage position of tile record q: bits 1-4 XOR bits 5-8 (record pairs stay adjacent: the stores
@@ -700,7 +696,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
     // are one ray's consecutive samples (equal or neighbouring corners), and equal addresses
     // serialise within one LDS instruction; this way they meet in one only by a hash collision.
     // The stage is XOR-swizzled (stage_pos) so those strided reads spread over the banks.
-    // Loads run kAccumDepth tiles ahead (registers).
+    // Loads run two tiles ahead (registers).
     // A pair record (p > 0) adds (1 - tx) v to corner e0 and tx v to e1 = e0 ^ (2^p - 1), a single
     // record (p = 0, tx = 0) adds v to e0.  int64 sums: the result does not depend on the order.
     const uint64_t beg2 = beg & ~1ull;
@@ -709,30 +705,15 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
     const float fs = ldexpf(1.f, k2);
     const float ftx = fs * kInvU16;
     const uint64_t n_tiles = (end - beg2 + kTile - 1) / kTile;
-    u32x4 buf[kAccumDepth];  // this thread's 2 records of the tiles ahead: {w0, v0, w1, v1}
-    auto load_tile = [&](uint64_t tile) {
-      const uint64_t rr = beg2 + tile * kTile + 2 * threadIdx.x;
+    auto load_tile = [&](uint64_t tile) {  // this thread's 2 records of a tile: {w0, v0, w1, v1}
+      const uint64_t rr = beg2 + (tile < n_tiles ? tile : 0) * kTile + 2 * threadIdx.x;
       const uint64_t rc = rr < end ? rr : beg2;  // unconditional loads
       return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(&ws.rec[rc]));
     };
-#pragma unroll
-    for (int d = 0; d < kAccumDepth; ++d) buf[d] = load_tile((uint64_t)d < n_tiles ? d : 0);
     const uint32_t q0 = 32u * lane + 2u * (threadIdx.x >> 6);  // this lane's records in a tile
-    for (uint64_t tile = 0; tile < n_tiles; ++tile) {
-      const int slot = (int)(tile % kAccumDepth);
-      u32x4 cur = buf[0];
-#pragma unroll
-      for (int d = 1; d < kAccumDepth; ++d)
-        if (slot == d) cur = buf[d];
+    auto run_tile = [&](uint64_t tile, const u32x4& cur) {
       lds_barrier();  // the previous tile's stage reads are done
       *reinterpret_cast<u32x4*>(&stage[stage_pos(2 * threadIdx.x)]) = cur;
-      {
-        const uint64_t nt = tile + kAccumDepth;
-        const u32x4 q = load_tile(nt < n_tiles ? nt : 0);
-#pragma unroll
-        for (int d = 0; d < kAccumDepth; ++d)
-          if (slot == d) buf[d] = q;
-      }
       lds_barrier();
       const uint64_t base = beg2 + tile * kTile;
 #pragma unroll
@@ -757,6 +738,19 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
             atomicAdd(&acc[kChunk + e1], fixed_i64(tx * v1));
           }
         }
+      }
+    };
+    // two tiles per trip, each in a register set of its own, its next load issued as soon as it is
+    // staged: the loads of the following two tiles are in flight while these two accumulate
+    u32x4 bufa = load_tile(0), bufb = load_tile(1);
+    for (uint64_t tile = 0; tile < n_tiles; tile += 2) {
+      const u32x4 ca = bufa;
+      bufa = load_tile(tile + 2);
+      run_tile(tile, ca);
+      if (tile + 1 < n_tiles) {  // block-uniform
+        const u32x4 cb = bufb;
+        bufb = load_tile(tile + 3);
+        run_tile(tile + 1, cb);
       }
     }
     LNR_STAMP(t2);
