@@ -620,6 +620,10 @@ __device__ __forceinline__ unsigned long long fixed_i64(float x) {
 #ifndef LNR_ACCUM_WAVES_PER_EU
 #define LNR_ACCUM_WAVES_PER_EU 8
 #endif
+#ifndef LNR_ACCUM_TRIP
+#define LNR_ACCUM_TRIP 2
+#endif
+constexpr int kAccumTrip = LNR_ACCUM_TRIP;        // tiles per trip of the accumulate loop (loads ahead)
 constexpr int kTile = 2 * kAccumThreads;         // records per tile: 2 per thread
 static_assert(kTile == 2048, "the stage's swizzle and the strided reads assume 64-lane waves x 16 x 2");
 // the stage position of tile record q: bits 1-4 XOR bits 5-8 (record pairs stay adjacent: the stores
@@ -696,7 +700,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
     // are one ray's consecutive samples (equal or neighbouring corners), and equal addresses
     // serialise within one LDS instruction; this way they meet in one only by a hash collision.
     // The stage is XOR-swizzled (stage_pos) so those strided reads spread over the banks.
-    // Loads run two tiles ahead (registers).
+    // Loads run kAccumTrip tiles ahead (registers).
     // A pair record (p > 0) adds (1 - tx) v to corner e0 and tx v to e1 = e0 ^ (2^p - 1), a single
     // record (p = 0, tx = 0) adds v to e0.  int64 sums: the result does not depend on the order.
     const uint64_t beg2 = beg & ~1ull;
@@ -740,17 +744,20 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
         }
       }
     };
-    // two tiles per trip, each in a register set of its own, its next load issued as soon as it is
-    // staged: the loads of the following two tiles are in flight while these two accumulate
-    u32x4 bufa = load_tile(0), bufb = load_tile(1);
-    for (uint64_t tile = 0; tile < n_tiles; tile += 2) {
-      const u32x4 ca = bufa;
-      bufa = load_tile(tile + 2);
-      run_tile(tile, ca);
-      if (tile + 1 < n_tiles) {  // block-uniform
-        const u32x4 cb = bufb;
-        bufb = load_tile(tile + 3);
-        run_tile(tile + 1, cb);
+    // kAccumTrip tiles per trip, each in a register set of its own (the unrolled loop indexes them
+    // statically), its next load issued as soon as it is staged: the loads of the following
+    // kAccumTrip tiles are in flight while these accumulate
+    u32x4 buf[kAccumTrip];
+#pragma unroll
+    for (int d = 0; d < kAccumTrip; ++d) buf[d] = load_tile(d);
+    for (uint64_t tile = 0; tile < n_tiles; tile += kAccumTrip) {
+#pragma unroll
+      for (int d = 0; d < kAccumTrip; ++d) {
+        if (tile + d < n_tiles) {  // block-uniform
+          const u32x4 c = buf[d];
+          buf[d] = load_tile(tile + d + kAccumTrip);
+          run_tile(tile + d, c);
+        }
       }
     }
     LNR_STAMP(t2);

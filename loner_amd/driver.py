@@ -1,0 +1,172 @@
+"""The north-star driver's LiDAR phase (examples/fdt_optimize_implicit_map.py) as host logic over the
+reference-shaped surface: which scans train and which evaluate, the shuffled keyframe windows, the
+optimiser schedule edits, and the repetition / checkpoint / stop rule.  Scan I/O (rosbag), pose
+interpolation and the metric CSV files stay with the caller: ``run_lidar_phase`` takes the training
+keyframes and two evaluation callables and returns what happened per repetition.
+
+    DriverSettings        the module constants of fdt_optimize_implicit_map.py:62-74
+    split_indices         test / train / eval scan indices (:427-431, :496)
+    configure_optimizer   the driver's schedule edits (:529-541, LiDAR phase)
+    repetition_windows    one repetition's shuffled keyframe windows (:574-613)
+    StopRule              the repetition loop's checkpoint and stop decisions (:650-727)
+    run_lidar_phase       the whole loop (:568-727)
+
+The random draws use a ``numpy.random.RandomState`` seeded like the reference's ``np.random.seed(8)``:
+the legacy global generator and a RandomState with the same seed produce the same ``choice`` stream,
+and the reference draws from it in this order: test indices, eval indices, then one shuffle per
+repetition (nothing on the path in between touches numpy's generator).
+"""
+import copy
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+
+@dataclass
+class DriverSettings:
+    """fdt_optimize_implicit_map.py:62-76 (LiDAR phase; SKIP/START/END None -> 1/0/-1 at :97-104)."""
+    chunk_size: int = 2 ** 8
+    max_window_length: int = 16
+    n_eval: int = 6
+    shuffle: bool = True
+    strategy: str = "MASK"
+    repetitions_max: int = 8
+    skip_step: int = 1
+    start_step: int = 0
+    end_step: int = 120
+    l1_threshold: float = 1.05
+    num_iterations: int = 2 ** 5
+    seed: int = 8
+
+
+def split_indices(n_scans, cfg: DriverSettings, rng):
+    """(test, train, eval) index lists over the scans ``[start_step:end_step]``.
+
+    :429  test_indices  = choice(len(poses[START:END]), N_EVAL, replace=False)
+    :430  train_indices = the rest, in order
+    :496  eval_indices  = choice(len(train_poses), N_EVAL, replace=False), positions into train
+    """
+    n = len(range(n_scans)[cfg.start_step:cfg.end_step])
+    test = rng.choice(n, cfg.n_eval, replace=False)
+    tset = set(int(t) for t in test)
+    train = [i for i in range(n) if i not in tset]
+    ev = rng.choice(len(train), cfg.n_eval, replace=False)
+    return [int(t) for t in test], train, [int(e) for e in ev]
+
+
+def configure_optimizer(opt, cfg: DriverSettings):
+    """The LiDAR phase's optimiser edits (:529-541, :574): every window runs ``num_iterations``
+    steps with poses and the colour MLP frozen, and rays are drawn with ``cfg.strategy``."""
+    opt._optimization_settings.num_iterations = cfg.num_iterations
+    opt._keyframe_count = 1
+    empty = copy.deepcopy(opt._keyframe_schedule[0])
+    empty["num_keyframes"] = -1
+    empty["iteration_schedule"][0].update(num_iterations=cfg.num_iterations, freeze_poses=True,
+                                          freeze_sigma_mlp=False, freeze_rgb_mlp=True)
+    opt._keyframe_schedule = [empty]
+    if cfg.strategy not in ("RANDOM", "MASK", "FIXED"):
+        raise RuntimeError(f"Can't find rays_selection strategy: {cfg.strategy}")
+    rs = opt._settings.get("rays_selection") if hasattr(opt._settings, "get") else None
+    if rs is not None:
+        rs["strategy"] = cfg.strategy
+    opt._rays_strategy = cfg.strategy  # read once at construction here; the reference re-reads the settings
+
+
+def repetition_windows(n_train, cfg: DriverSettings, rng):
+    """One repetition's windows (:577-613): the keyframes ``[::skip_step]`` in a shuffled order
+    (``choice(n, n, replace=False)``), cut into windows of ``max_window_length`` and a last,
+    shorter one.  Returns lists of positions into the ``[::skip_step]`` keyframe list."""
+    n = len(range(n_train)[::cfg.skip_step])
+    order = rng.choice(n, n, replace=False) if cfg.shuffle else np.arange(n)
+    order = [int(i) for i in order]
+    return [order[k:k + cfg.max_window_length] for k in range(0, n, cfg.max_window_length)]
+
+
+class StopRule:
+    """The repetition loop's decisions after each repetition (:650-727), on the mean eval L1.
+
+    First repetition (no checkpoint yet): save ``final.tar``; stop if the mean is below the
+    threshold.  The previous mean is NOT recorded then (l1s_mean_prev stays inf), so the second
+    repetition never stops for being worse.  Later repetitions save ``final_<global_step>.tar`` when
+    the maximum is reached, stop (and save) below the threshold, stop WITHOUT saving when the mean
+    got worse than the previous one, and otherwise record the mean and save.
+    """
+
+    def __init__(self, cfg: DriverSettings):
+        self.cfg = cfg
+        self.r = 0
+        self.prev = math.inf
+        self.have_ckpt = False
+
+    @property
+    def done(self):
+        return self.r >= self.cfg.repetitions_max
+
+    def after_repetition(self, eval_mean, global_step):
+        """Returns (checkpoint names to save, in order; stop reason or None)."""
+        cfg = self.cfg
+        self.r += 1
+        saves, reason = [], None
+        if not self.have_ckpt:
+            saves.append("final.tar")
+            self.have_ckpt = True
+            if self.r == cfg.repetitions_max:
+                reason = "max_repetitions"
+            if eval_mean < cfg.l1_threshold:
+                self.r = cfg.repetitions_max
+                reason = "threshold"
+        else:
+            name = f"final_{global_step}.tar"
+            if self.r == cfg.repetitions_max:
+                saves.append(name)
+                reason = "max_repetitions"
+            if eval_mean < cfg.l1_threshold:
+                self.r = cfg.repetitions_max
+                saves.append(name)
+                reason = "threshold"
+            elif self.prev < eval_mean:
+                self.r = cfg.repetitions_max
+                reason = "worse_than_previous"
+            else:
+                self.prev = eval_mean
+                saves.append(name)
+        return saves, reason
+
+
+def _stats(l1s):
+    a = np.asarray(l1s, dtype=np.float64)
+    return dict(min=float(a.min()), max=float(a.max()), mean=float(a.mean()), rmse=float(np.sqrt(np.mean(a * a))))
+
+
+def run_lidar_phase(opt, keyframes, eval_test, eval_eval, cfg: DriverSettings = None, rng=None, save=None):
+    """The LiDAR iteration loop (:568-727).
+
+    opt        an ``Optimizer`` (loner_amd.optimizer), already configured (``configure_optimizer``)
+    keyframes  the training keyframes (scan dicts), in train-index order
+    eval_test, eval_eval
+               callables returning one L1 per held-out / training evaluation scan (metres)
+    rng        the generator the caller split the scans with (``split_indices``); the shuffles
+               continue its stream, as the reference's global generator does
+    save       ``save(name, global_step)``, called for every checkpoint the reference writes
+    Returns one record per repetition: global step, test and eval L1 statistics, saved
+    checkpoint names and the stop reason.
+    """
+    cfg = cfg or DriverSettings()
+    rng = rng if rng is not None else np.random.RandomState(cfg.seed)
+    kfs = keyframes[::cfg.skip_step]
+    rule = StopRule(cfg)
+    history = []
+    while not rule.done:
+        losses = []
+        for win in repetition_windows(len(keyframes), cfg, rng):
+            losses.append(opt.iterate_optimizer([kfs[i] for i in win]))
+        test, ev = _stats(eval_test()), _stats(eval_eval())
+        saves, reason = rule.after_repetition(ev["mean"], opt._global_step)
+        for name in saves:
+            if save is not None:
+                save(name, opt._global_step)
+        history.append(dict(repetition=len(history) + 1,
+                            global_step=int(opt._global_step), windows=len(losses), loss=losses,
+                            l1_test=test, l1_eval=ev, saved=saves, stop=reason))
+    return history
