@@ -140,6 +140,11 @@ struct GradF32 {
     const gf32x2 v = __builtin_nontemporal_load(reinterpret_cast<const gf32x2*>(&g[(int64_t)l * stride + i]));
     return make_float2(v.x, v.y);
   }
+  // the split form (GradJac holds half the registers this way): per-level raw value + per-sample scale
+  typedef float2 Raw;
+  __device__ __forceinline__ Raw load_raw_nt(uint32_t l, int64_t i) const { return load_nt(l, i); }
+  __device__ __forceinline__ float scale(int64_t) const { return 0.f; }
+  __device__ __forceinline__ static float2 finish(const Raw& r, float) { return r; }
 };
 struct GradJac {
   const uint32_t* jac;
@@ -153,6 +158,12 @@ struct GradJac {
   __device__ __forceinline__ float2 load_nt(uint32_t l, int64_t i) const {
     return apply(__builtin_nontemporal_load(&jac[(int64_t)l * stride + i]), dsig[i]);
   }
+  typedef uint32_t Raw;
+  __device__ __forceinline__ Raw load_raw_nt(uint32_t l, int64_t i) const {
+    return __builtin_nontemporal_load(&jac[(int64_t)l * stride + i]);
+  }
+  __device__ __forceinline__ float scale(int64_t i) const { return dsig[i]; }
+  __device__ __forceinline__ static float2 finish(const Raw& r, float s) { return apply(r, s); }
 };
 
 struct Corners {

@@ -377,30 +377,40 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter_o
 // moment its rank returns.  Same records, counts and blockmax as k_bwd_scatter.
 // ---------------------------------------------------------------------------------------------
 // Level-looped scatter: one workgroup per histogram row walks every level.
-//  * All global loads happen in the prologue: the sample's position, its d_enc at every level (32
-//    registers) and, wave w, the histogram rows of levels 2w and 2w + 1, turned at once into every
-//    level's bucket starts.  The level loop then issues only LDS operations and the copy-out
-//    stores, so nothing in it ever waits on global memory.
+//  * All global loads happen in the prologue: the sample's position, its encoding gradient at every
+//    level (GradJac: 16 registers of fp16 pairs) and, wave w, the histogram rows of levels 2w and
+//    2w + 1, turned at once into every level's bucket starts.  The level loop then issues only LDS
+//    operations and the copy-out stores, so nothing in it ever waits on global memory.
 //  * Each record is ranked (returning LDS atomic) and placed at once, 16 B {word, global slot, v0,
-//    v1} in bucket order; the copy-out of level l - 1 overlaps level l (double-buffered stage, one
-//    barrier per level).
+//    v1} in bucket order; then the level's stage is copied out (kRowsStages).
 //  * A (row, level) with more than kRowsCap records is flagged and left to k_bwd_scatter_overflow.
 // Same records, counts and blockmax as k_bwd_scatter.
 constexpr int kRowsCap = 2176;  // 4.25 records per sample: fine rows hold 4 + the rare split pairs
+#ifndef LNR_SCATTER_STAGES
+#define LNR_SCATTER_STAGES 1
+#endif
+#ifndef LNR_SCATTER_ROWS_WPE
+#define LNR_SCATTER_ROWS_WPE 6
+#endif
+// 1 (default): one stage, copy-out after each level's placement: 44 KB of LDS and 80 VGPRs (the
+// Jacobian held as fp16 pairs), so 3 workgroups (6 waves per SIMD) share a CU; 2: double-buffered
+// stage, the copy-out of level l - 1 overlapping level l, 2 workgroups per CU (C2: 670 against 627 us)
+constexpr int kRowsStages = LNR_SCATTER_STAGES;
+static_assert(kRowsStages == 1 || kRowsStages == 2, "one or two stages");
 template <int NL, int NB>
 struct RowsLds {  // the small tables first: their addresses fit the 16-bit LDS instruction offset
   uint2 sg[NL][NB];           // per level and bucket: {start in the stage, global slot of the run}
   uint32_t total[NL];         // records of the row at each level
   uint32_t ctr[2][NB];        // rank counters
   LevelParams lv[NL];         // the level table (kernel arguments indexed per level would be loads)
-  uint4 stage[2][kRowsCap];   // staged records {word, global slot, fp16 value pair, -}, bucket order
+  uint4 stage[kRowsStages][kRowsCap];  // staged records {word, global slot, fp16 value pair, -}, bucket order
 };
 
 // NL levels, the first NM coherent (run-merging) and the rest fine, at most NB buckets per level:
 // compile-time, so the level loop unrolls into straight-line code.  Record slots are 32-bit (the
 // launcher checks 8 N L < 2^32).
 template <class PosFn, class GradFn, int NL, int NM, int NB>
-__global__ void __launch_bounds__(kSB) __attribute__((amdgpu_waves_per_eu(4, 4)))
+__global__ void __launch_bounds__(kSB) __attribute__((amdgpu_waves_per_eu(LNR_SCATTER_ROWS_WPE, LNR_SCATTER_ROWS_WPE)))
 k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace ws, bool skip_zero) {
   static_assert(NL <= 2 * (kSB / 64), "wave w prepares levels 2w and 2w + 1");
   static_assert(NB <= 128, "two buckets per lane");
@@ -419,10 +429,11 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
   if (threadIdx.x < 2 * NB) (&sm.ctr[0][0])[threadIdx.x] = 0u;
   // prologue 2: every global load of the kernel
   const typename PosFn::Raw raw = pos.load(ic);
-  float2 g[NL];
+  typename GradFn::Raw g[NL];  // (GradJac: the fp16 pair, scaled by d sigma at use: half the registers)
 #pragma unroll
-  for (int l = 0; l < NL; ++l) g[l] = grad.load_nt(l, ic);  // read once: nontemporal, so they do not
-                                                            // displace the runs' L2 lines
+  for (int l = 0; l < NL; ++l) g[l] = grad.load_raw_nt(l, ic);  // read once: nontemporal, so they do not
+                                                                // displace the runs' L2 lines
+  const float gsc = grad.scale(ic);
   uint32_t h0[2][2], h1[2][2];
   uint64_t seg[2][2];
 #pragma unroll
@@ -468,7 +479,7 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
   // copy level l's staged row out (consecutive threads -> consecutive slots of a run).  Every lane
   // stores on every trip (lanes past the row's records into the spare slot), so the trip count is fixed
   auto copy_out = [&](uint32_t l) {
-    const int sbuf = l & 1;
+    const int sbuf = kRowsStages == 2 ? (l & 1) : 0;
     const uint32_t total = sm.total[l];
     const uint32_t lim = total <= (uint32_t)kRowsCap ? total : 0u;
 #pragma unroll
@@ -482,12 +493,14 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
 
 #pragma unroll
   for (int l = 0; l < NL; ++l) {
-    const int sbuf = l & 1;
+    const int sbuf = l & 1;  // rank counters (and, with two stages, the stage)
+    const int stg = kRowsStages == 2 ? sbuf : 0;
     const LevelParams lv = sm.lv[l];
     const bool staged = sm.total[l] <= (uint32_t)kRowsCap;  // block-uniform
     uint32_t* ctr = sm.ctr[sbuf];
     const uint2* sgl = sm.sg[l];
-    const float2 gv = in ? make_float2(g[l].x, g[l].y) : make_float2(0.f, 0.f);
+    const float2 gl = GradFn::finish(g[l], gsc);
+    const float2 gv = in ? gl : make_float2(0.f, 0.f);
     const bool inr = staged && in;  // an unstaged row emits nothing here: k_bwd_scatter_overflow redoes it
     const bool act = inr && (!skip_zero || gv.x != 0.f || gv.y != 0.f);
     const float rs = rsc[l];
@@ -503,7 +516,7 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
         for (int k = 0; k < 4; ++k) rank[k] = atomicAdd(&ctr[bk[k]], 1u);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-          sm.stage[sbuf][s4[k].x + rank[k]] = make_uint4(word[k], s4[k].y + rank[k], rec_half2(val[k].x, val[k].y, rs), 0u);
+          sm.stage[stg][s4[k].x + rank[k]] = make_uint4(word[k], s4[k].y + rank[k], rec_half2(val[k].x, val[k].y, rs), 0u);
       }
     };
     uint32_t bk4[4], w4[4];
@@ -556,10 +569,16 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
       }
     }
     if (threadIdx.x < NB) sm.ctr[sbuf ^ 1][threadIdx.x] = 0u;  // level l + 1's counters (last used by l - 1)
-    if (l >= 1) copy_out(l - 1);
-    lds_barrier();
+    if (kRowsStages == 2) {
+      if (l >= 1) copy_out(l - 1);
+      lds_barrier();
+    } else {
+      lds_barrier();  // level l placed
+      copy_out(l);
+      if (l + 1 < NL) lds_barrier();  // the stage is free for level l + 1
+    }
   }
-  copy_out(NL - 1);
+  if (kRowsStages == 2) copy_out(NL - 1);
 }
 
 constexpr size_t kScatterLds = (size_t)kCap * 4 + kMaxChunksPerLevel * 8 + (size_t)kCap * 4 + kMaxChunksPerLevel * 4 +
