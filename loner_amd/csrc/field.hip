@@ -516,6 +516,9 @@ __global__ void __launch_bounds__(NT) k_field(FieldArgs a) {
 // 4 rays independently and meet once, at the end, to reduce their dW slabs.  Same arithmetic as
 // composite_ray<C, true, false> (the block version), reassociated only in the cross-lane sums.
 constexpr int kWavesPerBlock = NT / 64;
+#ifndef LNR_FIELD_SPLIT
+#define LNR_FIELD_SPLIT 1  // lnr_field_train: MLP forward and compositing as two kernels (k_sigma_fwd_tiles, k_composite_wave)
+#endif
 constexpr int kSigmaLevels = 16;  // the sigma MLP's 32 inputs: 16 levels x 2 features
 
 __device__ __forceinline__ double wave_excl_prod(double p) {
@@ -732,6 +735,52 @@ __global__ void __launch_bounds__(NT) k_field_wave(FieldArgs a) {
     wave_lds_handoff();
 #pragma unroll
     for (int k = 0; k < C; ++k) a.d_sigma[r * S + 64 * k + lane] = sig[64 * k + lane];  // coalesced
+    wave_lds_handoff();  // sig is rewritten by the next ray
+  }
+}
+
+// The same phase split in two, so neither kernel carries the other's registers (k_field_wave<8>: 211
+// registers, 2 waves per SIMD, its encoding loads exposed between rays).
+// Phase 1a, tile-parallel: sigma MLP forward over 64-sample units (4 tiles per wave trip, every load
+// first), sigma (fp16-rounded, as tcnn returns it) into a.d_sigma.
+constexpr int kSigmaFwdUnit = 64;
+__global__ void __launch_bounds__(NT) k_sigma_fwd_tiles(FieldArgs a) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+  SigmaWeights sw;
+  load_sigma_weights(a.w, sw);
+  const int64_t n_units = a.n_rays * (int64_t)a.S / kSigmaFwdUnit;
+  for (int64_t u = (int64_t)blockIdx.x * kWavesPerBlock + wid; u < n_units; u += (int64_t)gridDim.x * kWavesPerBlock) {
+    const int64_t n0 = u * kSigmaFwdUnit;
+    half8_t b[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) b[t] = load_enc_operand(a.enc, a.enc_stride, n0 + 16 * t + c, true);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float h[16];
+      const float sgm = sigma_tile_fwd(sw, b[t], h);
+      if (g == 0) a.d_sigma[n0 + 16 * t + c] = sigma_to_f16(sgm);
+      if (a.lp.dev_status && __any(!isfinite(round_f16(sgm))) && lane == 0) atomicOr(a.lp.dev_status, LNR_STATUS_SIGMA_CLIPPED);
+    }
+  }
+}
+
+// Phase 1b, one wave per ray: compositing -> loss -> compositing backward on the sigma of phase 1a,
+// dL/dsigma written over it (a.d_sigma, (R, S) fp32).
+template <int C>
+__global__ void __launch_bounds__(NT) k_composite_wave(FieldArgs a) {
+  if (a.denc_max && blockIdx.x == 0 && threadIdx.x < kSigmaLevels) a.denc_max[threadIdx.x] = 0.f;  // before k_mlp_bwd_tiles
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  constexpr int S = 64 * C;  // == a.S (checked at launch)
+  float* sig = reinterpret_cast<float*>(smem) + wid * S;
+  for (int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + wid; r < a.n_rays; r += (int64_t)gridDim.x * kWavesPerBlock) {
+#pragma unroll
+    for (int k = 0; k < C; ++k) sig[64 * k + lane] = a.d_sigma[r * S + 64 * k + lane];  // coalesced
+    wave_lds_handoff();
+    composite_loss_wave<C>(a, sig, r);
+    wave_lds_handoff();
+#pragma unroll
+    for (int k = 0; k < C; ++k) a.d_sigma[r * S + 64 * k + lane] = sig[64 * k + lane];
     wave_lds_handoff();  // sig is rewritten by the next ray
   }
 }
@@ -1068,12 +1117,26 @@ extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t e
     const int64_t want = (n_rays + kWavesPerBlock - 1) / kWavesPerBlock;
     const int nr = (int)(want < 2048 ? want : 2048);
     const size_t sm = wave_smem_bytes(n_samples);
+#if LNR_FIELD_SPLIT
+    {
+      const int64_t units = n_rays * (int64_t)n_samples / kSigmaFwdUnit;
+      const int64_t wantu = (units + kWavesPerBlock - 1) / kWavesPerBlock;
+      hipLaunchKernelGGL(k_sigma_fwd_tiles, dim3((int)(wantu < 8192 ? wantu : 8192)), dim3(NT), 0, st, a);
+    }
+    switch (C) {
+      case 1: hipLaunchKernelGGL(k_composite_wave<1>, dim3(nr), dim3(NT), sm, st, a); break;
+      case 2: hipLaunchKernelGGL(k_composite_wave<2>, dim3(nr), dim3(NT), sm, st, a); break;
+      case 4: hipLaunchKernelGGL(k_composite_wave<4>, dim3(nr), dim3(NT), sm, st, a); break;
+      default: hipLaunchKernelGGL(k_composite_wave<8>, dim3(nr), dim3(NT), sm, st, a); break;
+    }
+#else
     switch (C) {
       case 1: hipLaunchKernelGGL(k_field_wave<1>, dim3(nr), dim3(NT), sm, st, a); break;
       case 2: hipLaunchKernelGGL(k_field_wave<2>, dim3(nr), dim3(NT), sm, st, a); break;
       case 4: hipLaunchKernelGGL(k_field_wave<4>, dim3(nr), dim3(NT), sm, st, a); break;
       default: hipLaunchKernelGGL(k_field_wave<8>, dim3(nr), dim3(NT), sm, st, a); break;
     }
+#endif
     const int64_t pairs = (n_rays * (int64_t)n_samples) / 32;
     const int64_t wantb = (pairs + kWavesPerBlock - 1) / kWavesPerBlock;
     const int64_t slabs = lnr_dw_workspace_words(n_rays) / LNR_SIGMA_MLP_PARAMS;  // one dW slab per block
