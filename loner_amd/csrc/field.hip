@@ -1176,6 +1176,21 @@ extern "C" int lnr_field_render(const uint16_t* w, const uint32_t* enc, int64_t 
   a.noise_std = noise_std; a.noise = noise; a.key = key; a.ray_offset = ray_offset;
   a.depth = depth; a.opacity = opacity; a.variance = variance; a.weights = weights;
   const int nb = field_blocks(n_rays);
+#if LNR_FIELD_SPLIT
+  if (weights) {
+    // the sigma MLP tile-parallel first (k_sigma_fwd_tiles), its sigma staged in the weights buffer,
+    // which the compositing reads into LDS one ray at a time before it writes that ray's weights
+    hipStream_t st = as_stream(stream);
+    a.d_sigma = weights;
+    const int64_t units = n_rays * (int64_t)n_samples / kSigmaFwdUnit;
+    const int64_t wantu = (units + kWavesPerBlock - 1) / kWavesPerBlock;
+    hipLaunchKernelGGL(k_sigma_fwd_tiles, dim3((int)(wantu < 8192 ? wantu : 8192)), dim3(NT), 0, st, a);
+    a.d_sigma = nullptr;
+    a.sigma_in = weights;
+    if (strategy == LNR_RENDER_ADJUSTED) return launch_field<false, true, kSigmaGiven>(a, nb, st, "lnr_field_render");
+    return launch_field<false, false, kSigmaGiven>(a, nb, st, "lnr_field_render");
+  }
+#endif
   if (strategy == LNR_RENDER_ADJUSTED)
     return launch_field<false, true, kSigmaMLP>(a, nb, as_stream(stream), "lnr_field_render");
   return launch_field<false, false, kSigmaMLP>(a, nb, as_stream(stream), "lnr_field_render");

@@ -176,9 +176,11 @@ class StepEngine:
         self.status = torch.zeros(1, dtype=torch.int32, device=state.device)  # LNR_STATUS_* bits
         self._warned_clip = False
         # level ranges of the bucketed gradient all-reduce, finest first (their records dominate the
-        # accumulation, so the first ranges' exchange overlaps the later ranges' accumulation)
+        # accumulation, so the first ranges' exchange overlaps the later ranges' accumulation); the
+        # last range (levels 0-2 + the MLP: 2.4 MB at L=16, T=2^18) is the only exchange nothing
+        # overlaps, so it is kept small
         nl = self.cfg.n_levels
-        cuts = sorted({nl, max(nl - 5, 1), max(nl - 10, 1), 0}, reverse=True)
+        cuts = sorted({nl, max(nl - 5, 1), max(nl - 10, 1), min(3, nl), 0}, reverse=True)
         self.ar_groups = [(cuts[i + 1], cuts[i]) for i in range(len(cuts) - 1)]
         # callable(tensor[, async_op]) summing in place across ranks (torch.distributed.all_reduce
         # semantics), or None
