@@ -386,35 +386,45 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter_o
 //  * A (row, level) with more than kRowsCap records is flagged and left to k_bwd_scatter_overflow.
 // Same records, counts and blockmax as k_bwd_scatter.
 constexpr int kRowsCap = 2176;  // 4.25 records per sample: fine rows hold 4 + the rare split pairs
+// Stages: 1, one stage with the copy-out after each level's placement: 44 KB of LDS and 80 VGPRs
+// (GradJac: the Jacobian held as fp16 pairs), so 3 workgroups (6 waves per SIMD) share a CU; 2, a
+// double-buffered stage with the copy-out of level l - 1 overlapping level l, 79 KB, 2 workgroups
+// per CU (C2: 670 against 627 us).  GradF32's float2 gradients need 16 more registers: they keep
+// the double-buffered stage at 4 waves per SIMD (one stage would spill), except with 128 chunks
+// per level (the colour grid), whose tables leave room for one stage only.
 #ifndef LNR_SCATTER_STAGES
-#define LNR_SCATTER_STAGES 1
+#define LNR_SCATTER_STAGES 0  // 0: per gradient source as above; 1 or 2: forced (experiments)
 #endif
-#ifndef LNR_SCATTER_ROWS_WPE
-#define LNR_SCATTER_ROWS_WPE 6
+template <class GradFn, int NB>
+constexpr int rows_stages() {
+  return LNR_SCATTER_STAGES ? LNR_SCATTER_STAGES : (sizeof(typename GradFn::Raw) <= 4 || NB > 64 ? 1 : 2);
+}
+template <class GradFn, int NB>
+constexpr int rows_waves() { return rows_stages<GradFn, NB>() == 1 ? 6 : 4; }
+#ifndef LNR_ROWS_NB128
+#define LNR_ROWS_NB128 1  // the level-looped scatter for grids with up to 128 chunks per level too
 #endif
-// 1 (default): one stage, copy-out after each level's placement: 44 KB of LDS and 80 VGPRs (the
-// Jacobian held as fp16 pairs), so 3 workgroups (6 waves per SIMD) share a CU; 2: double-buffered
-// stage, the copy-out of level l - 1 overlapping level l, 2 workgroups per CU (C2: 670 against 627 us)
-constexpr int kRowsStages = LNR_SCATTER_STAGES;
-static_assert(kRowsStages == 1 || kRowsStages == 2, "one or two stages");
-template <int NL, int NB>
+template <int NL, int NB, int STG>
 struct RowsLds {  // the small tables first: their addresses fit the 16-bit LDS instruction offset
   uint2 sg[NL][NB];           // per level and bucket: {start in the stage, global slot of the run}
   uint32_t total[NL];         // records of the row at each level
   uint32_t ctr[2][NB];        // rank counters
   LevelParams lv[NL];         // the level table (kernel arguments indexed per level would be loads)
-  uint4 stage[kRowsStages][kRowsCap];  // staged records {word, global slot, fp16 value pair, -}, bucket order
+  uint4 stage[STG][kRowsCap];  // staged records {word, global slot, fp16 value pair, -}, bucket order
 };
 
 // NL levels, the first NM coherent (run-merging) and the rest fine, at most NB buckets per level:
 // compile-time, so the level loop unrolls into straight-line code.  Record slots are 32-bit (the
 // launcher checks 8 N L < 2^32).
 template <class PosFn, class GradFn, int NL, int NM, int NB>
-__global__ void __launch_bounds__(kSB) __attribute__((amdgpu_waves_per_eu(LNR_SCATTER_ROWS_WPE, LNR_SCATTER_ROWS_WPE)))
+__global__ void __launch_bounds__(kSB)
+__attribute__((amdgpu_waves_per_eu(rows_waves<GradFn, NB>(), rows_waves<GradFn, NB>())))
 k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace ws, bool skip_zero) {
   static_assert(NL <= 2 * (kSB / 64), "wave w prepares levels 2w and 2w + 1");
   static_assert(NB <= 128, "two buckets per lane");
-  __shared__ RowsLds<NL, NB> sm;
+  constexpr int kRowsStages = rows_stages<GradFn, NB>();
+  static_assert(kRowsStages == 1 || kRowsStages == 2, "one or two stages");
+  __shared__ RowsLds<NL, NB, kRowsStages> sm;
   const int64_t sb = xcd_row(blockIdx.x, gridDim.x);
   const int64_t i = sb * kSB + threadIdx.x;
   const bool in = i < n;
@@ -918,6 +928,13 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, Gra
                 : m == 6 ? k_bwd_scatter_rows<PosFn, GradFn, 16, 6, 64>
                          : k_bwd_scatter_rows<PosFn, GradFn, 16, 7, 64>;
     hipLaunchKernelGGL(kern, dim3((unsigned)w.n_sb), dim3(kSB), 0, st, a, pos, n, grad, w, skip_zero);
+#if LNR_ROWS_NB128
+  } else if (rows && m >= 5 && m <= 7 && maxnb <= 128) {  // the colour grid (2^19 entries: 128 chunks per level)
+    auto kern = m == 5   ? k_bwd_scatter_rows<PosFn, GradFn, 16, 5, 128>
+                : m == 6 ? k_bwd_scatter_rows<PosFn, GradFn, 16, 6, 128>
+                         : k_bwd_scatter_rows<PosFn, GradFn, 16, 7, 128>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)w.n_sb), dim3(kSB), 0, st, a, pos, n, grad, w, skip_zero);
+#endif
   } else {
     looped = false;
     hipLaunchKernelGGL((k_bwd_scatter<PosFn, GradFn, kLevelsAny>), dim3((unsigned)(w.n_sb * L)), dim3(kSB), kScatterLds,
