@@ -649,7 +649,7 @@ def main():
                      "step_frac": step_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "traffic_step": traffic_step, "traffic_step_source": traffic_step_src},
         # the sigma MLP (fwd 4224 + bwd 8448 FLOP/sample) over the field stage
-        # (k_field_wave + k_mlp_bwd_tiles), against the dense fp16 MFMA peak
+        # (k_sigma_fwd_tiles + k_composite_wave + k_mlp_bwd_tiles), against the dense fp16 MFMA peak
         "mfma": {"achieved": mlp_tflops, "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": mlp_tflops / MFMA_PEAK_TFLOPS,
                  "flop_per_sample": MLP_FLOP_PER_SAMPLE, "ms_per_launch": stage_ms["field"],
                  "busy": busy, "busy_source": busy_src},

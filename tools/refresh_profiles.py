@@ -40,7 +40,7 @@ def per_dispatch(path):
     return {k: tot[k] / len(disp[k]) for k in tot}
 
 
-MLP_KERNELS = ("k_field_wave", "k_mlp_bwd_tiles")
+MLP_KERNELS = ("k_sigma_fwd_tiles", "k_field_wave", "k_mlp_bwd_tiles")
 N_SIMD = 256 * 4  # 256 CUs x 4 SIMDs
 
 
