@@ -73,13 +73,19 @@ __global__ void __launch_bounds__(kMaxChunksPerLevel) k_bwd_scan_rows(GridArgs a
   const uint32_t nb = a.bucket_base[l + 1] - a.bucket_base[l];
   if (c >= nb) return;
   const uint32_t* cs = ws.chunk_sum + (int64_t)l * ws.n_chunks * kMaxChunksPerLevel + c;
-  uint32_t base = 0;
-  for (uint32_t k = 0; k < ch; ++k) base += cs[(int64_t)k * kMaxChunksPerLevel];
-  if (ch == 0) {
-    uint32_t tot = 0;
-    for (int64_t k = 0; k < ws.n_chunks; ++k) tot += cs[k * kMaxChunksPerLevel];
-    ws.counts[a.bucket_base[l] + c] = tot;
+  uint32_t base = 0, tot = 0;  // the preceding chunks' sum; all chunks' (the bucket total, chunk 0)
+  const int64_t kend = ch == 0 ? ws.n_chunks : ch;
+  for (int64_t k = 0; k < kend; k += 16) {  // 16 loads in flight (L2 hits)
+    uint32_t v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = k + u < kend ? cs[(k + u) * kMaxChunksPerLevel] : 0u;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (k + u < (int64_t)ch) base += v[u];
+      tot += v[u];
+    }
   }
+  if (ch == 0) ws.counts[a.bucket_base[l] + c] = tot;
   uint32_t* col = ws.hist + (int64_t)a.bucket_base[l] * ws.n_sb + c;
   const int64_t r0 = (int64_t)ch * kRowsPerChunk;
   const int64_t r1 = r0 + kRowsPerChunk < ws.n_sb ? r0 + kRowsPerChunk : ws.n_sb;
