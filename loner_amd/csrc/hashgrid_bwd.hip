@@ -498,6 +498,7 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
     const int sbuf = kRowsStages == 2 ? (l & 1) : 0;
     const uint32_t total = sm.total[l];
     const uint32_t lim = total <= (uint32_t)kRowsCap ? total : 0u;
+#if LNR_COPY_ALL_TRIPS
 #pragma unroll
     for (int u = 0; u < (kRowsCap + kSB - 1) / kSB; ++u) {
       const uint32_t t = threadIdx.x + u * kSB;
@@ -505,6 +506,21 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
       const uint32_t d = t < lim && q.y < spare ? q.y : spare;  // (the bound: never a store outside the records)
       ws.rec[d] = make_uint2(q.x, q.z);
     }
+#else
+    // only the trips the row's records need (block-uniform: a merged coherent row holds far fewer
+    // than kRowsCap), and only the lanes holding a record store
+#pragma unroll
+    for (int u = 0; u < (kRowsCap + kSB - 1) / kSB; ++u) {
+      if ((uint32_t)(u * kSB) < lim) {
+        const uint32_t t = threadIdx.x + u * kSB;
+        if (t < lim) {
+          const uint4 q = sm.stage[sbuf][t];
+          const uint32_t d = q.y < spare ? q.y : spare;  // (the bound: never a store outside the records)
+          ws.rec[d] = make_uint2(q.x, q.z);
+        }
+      }
+    }
+#endif
   };
 
 #pragma unroll
