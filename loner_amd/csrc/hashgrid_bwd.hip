@@ -492,8 +492,7 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
   }
   lds_barrier();
 
-  // copy level l's staged row out (consecutive threads -> consecutive slots of a run).  Every lane
-  // stores on every trip (lanes past the row's records into the spare slot), so the trip count is fixed
+  // copy level l's staged row out (consecutive threads -> consecutive slots of a run)
   auto copy_out = [&](uint32_t l) {
     const int sbuf = kRowsStages == 2 ? (l & 1) : 0;
     const uint32_t total = sm.total[l];
