@@ -407,6 +407,9 @@ constexpr int rows_stages() {
 }
 template <class GradFn, int NB>
 constexpr int rows_waves() { return rows_stages<GradFn, NB>() == 1 ? 6 : 4; }
+#ifndef LNR_PRESCALE
+#define LNR_PRESCALE 1
+#endif
 #ifndef LNR_ROWS_NB128
 #define LNR_ROWS_NB128 1  // the level-looped scatter for grids with up to 128 chunks per level too
 #endif
@@ -531,10 +534,16 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
     uint32_t* ctr = sm.ctr[sbuf];
     const uint2* sgl = sm.sg[l];
     const float2 gl = GradFn::finish(g[l], gsc);
+#if LNR_PRESCALE
+    // the level's record scale applied to the gradient once, not to every record value: a power of
+    // two, so w (g 2^k) rounds exactly as (w g) 2^k
+    const float2 gv = in ? make_float2(gl.x * rsc[l], gl.y * rsc[l]) : make_float2(0.f, 0.f);
+#else
     const float2 gv = in ? gl : make_float2(0.f, 0.f);
+#endif
     const bool inr = staged && in;  // an unstaged row emits nothing here: k_bwd_scatter_overflow redoes it
     const bool act = inr && (!skip_zero || gv.x != 0.f || gv.y != 0.f);
-    const float rs = rsc[l];
+    const float rs = LNR_PRESCALE ? 1.0f : rsc[l];
     // rank (returning LDS atomics) and place: all start reads, then all atomics, then all writes
     // (one lane-level branch for the 4 records: they share their validity)
     auto place = [&](bool valid, const uint32_t (&bk)[4], const uint32_t (&word)[4], const float2 (&val)[4]) {
