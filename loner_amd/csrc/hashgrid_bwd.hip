@@ -407,6 +407,9 @@ constexpr int rows_stages() {
 }
 template <class GradFn, int NB>
 constexpr int rows_waves() { return rows_stages<GradFn, NB>() == 1 ? 6 : 4; }
+#ifndef LNR_STAGE_SPLIT_WRITE
+#define LNR_STAGE_SPLIT_WRITE 1
+#endif
 #ifndef LNR_PRESCALE
 #define LNR_PRESCALE 1
 #endif
@@ -556,7 +559,16 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
         for (int k = 0; k < 4; ++k) rank[k] = atomicAdd(&ctr[bk[k]], 1u);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
+#if LNR_STAGE_SPLIT_WRITE
+        {  // three 32-bit fields (ds_write2_b32 + ds_write_b32: no register moves to build a b128 quad)
+          uint32_t* q = reinterpret_cast<uint32_t*>(&sm.stage[stg][s4[k].x + rank[k]]);
+          q[0] = word[k];
+          q[1] = s4[k].y + rank[k];
+          q[2] = rec_half2(val[k].x, val[k].y, rs);
+        }
+#else
           sm.stage[stg][s4[k].x + rank[k]] = make_uint4(word[k], s4[k].y + rank[k], rec_half2(val[k].x, val[k].y, rs), 0u);
+#endif
       }
     };
     uint32_t bk4[4], w4[4];
