@@ -247,7 +247,10 @@ int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, 
                     uint32_t key, int64_t ray_offset, const lnr_loss_params* lp, float* d_enc, float* d_w,
                     float* workspace, float* ray_stats, float* depth, float* opacity, float* weights,
                     float* d_enc_level_max, uint32_t* d_enc_jac, void* stream);
-/* Forward-only fused render from enc (inference path, C3 shape): sigma MLP + compositing. */
+/* Forward-only render from enc (inference path, C3 shape): sigma MLP + compositing.  With weights
+ * (R,S) given, the sigma MLP runs tile-parallel first and stages sigma in weights, which the
+ * compositing then overwrites with the weights (weights must not alias the other buffers); without,
+ * one fused kernel per ray.  Same results either way. */
 int lnr_field_render(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, const float* rays, const float* z,
                      int64_t n_rays, int32_t n_samples, int32_t strategy, float noise_std, const float* noise,
                      uint32_t key, int64_t ray_offset, float* depth, float* opacity, float* variance,
