@@ -516,6 +516,10 @@ __global__ void __launch_bounds__(NT) k_field(FieldArgs a) {
 // 4 rays independently and meet once, at the end, to reduce their dW slabs.  Same arithmetic as
 // composite_ray<C, true, false> (the block version), reassociated only in the cross-lane sums.
 constexpr int kWavesPerBlock = NT / 64;
+#ifndef LNR_MLP_BWD_BLOCKS
+#define LNR_MLP_BWD_BLOCKS 512  // workgroups of k_mlp_bwd_tiles (and dW slabs), at most: one resident round (C2: 178.8 + 7.7 us slab reduce at 1024, 175.5 + 4.9 at 512)
+#endif
+constexpr int kMlpBwdBlocks = LNR_MLP_BWD_BLOCKS;
 #ifndef LNR_FIELD_SPLIT
 #define LNR_FIELD_SPLIT 1  // lnr_field_train: MLP forward and compositing as two kernels (k_sigma_fwd_tiles, k_composite_wave)
 #endif
@@ -1141,6 +1145,7 @@ extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t e
     const int64_t wantb = (pairs + kWavesPerBlock - 1) / kWavesPerBlock;
     const int64_t slabs = lnr_dw_workspace_words(n_rays) / LNR_SIGMA_MLP_PARAMS;  // one dW slab per block
     nb = (int)(wantb < slabs ? wantb : slabs);
+    if (nb > kMlpBwdBlocks) nb = kMlpBwdBlocks;
     if (d_enc_jac)
       hipLaunchKernelGGL(k_mlp_bwd_tiles<true>, dim3(nb), dim3(NT), bwd_tiles_smem_bytes(), st, a);
     else
