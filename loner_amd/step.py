@@ -13,6 +13,7 @@ Parameter layout (tcnn ``NetworkWithInputEncoding``: network first, then encodin
 fp32 master + Adam moments; an fp16 shadow of the whole buffer feeds the forward kernels.
 """
 import math
+import os
 import warnings
 from dataclasses import dataclass, field
 
@@ -175,12 +176,20 @@ class StepEngine:
         self.lr_factor = 1.0  # ExponentialLR: the caller sets gamma^k (optimizer.py:262, stepped per iteration)
         self.status = torch.zeros(1, dtype=torch.int32, device=state.device)  # LNR_STATUS_* bits
         self._warned_clip = False
-        # level ranges of the bucketed gradient all-reduce, finest first (their records dominate the
-        # accumulation, so the first ranges' exchange overlaps the later ranges' accumulation); the
-        # last range (levels 0-2 + the MLP: 2.4 MB at L=16, T=2^18) is the only exchange nothing
-        # overlaps, so it is kept small
+        # level ranges of the bucketed gradient all-reduce, finest first: the first range's exchange
+        # overlaps the later range's accumulation.  Every range is its own accumulate + finalize
+        # launch pair, and at world size 1 over RCCL (no peer traffic; tools/dp_overhead.py) the step
+        # costs 2.18-2.25 ms with one range, 2.23-2.30 with two (levels 8-15, then 0-7 + the MLP)
+        # and 2.41-2.44 with four, against 2.12 without the hook; two ranges hide about half of the
+        # 29.7 MB exchange for a fraction of the four ranges' cost.  LONER_AR_BUCKETS = 1, 2 or 4.
         nl = self.cfg.n_levels
-        cuts = sorted({nl, max(nl - 5, 1), max(nl - 10, 1), min(3, nl), 0}, reverse=True)
+        nbk = int(os.environ.get("LONER_AR_BUCKETS", "2"))
+        if nbk <= 1:
+            cuts = [nl, 0]
+        elif nbk == 2:
+            cuts = sorted({nl, max(nl - 8, 1), 0}, reverse=True)
+        else:
+            cuts = sorted({nl, max(nl - 5, 1), max(nl - 10, 1), min(3, nl), 0}, reverse=True)
         self.ar_groups = [(cuts[i + 1], cuts[i]) for i in range(len(cuts) - 1)]
         # callable(tensor[, async_op]) summing in place across ranks (torch.distributed.all_reduce
         # semantics), or None
