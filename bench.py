@@ -59,6 +59,9 @@ def parse():
                     help="weak: each rank optimises the config's full batch (global batch grows with N); "
                          "strong: the config's batch is split over the N ranks (SURVEY.md §8(e)).  Default: "
                          "strong for C4 at N > 1 (the headline C4 curve at R = 9216), weak otherwise")
+    ap.add_argument("--shard-of", type=int, default=None, metavar="N",
+                    help="one GPU runs rank 0's shard of the config's batch split N ways (the per-rank step of an "
+                         "N-GPU strong-scaling run, without the collective): the shard floor (C4, N in 2/4/8)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rays", type=int, default=512, help="rays per reduced-config CPU-baseline step (x512 samples)")
     ap.add_argument("--cpu-steps", type=int, default=24)
@@ -177,6 +180,62 @@ def cpu_baseline(cfg_name, n_rays, n_steps):
     return main
 
 
+def rendered_depth_vs_oracle(state, window, n_rays, S, key_seed=21):
+    """BASELINE.json's second metric, "rendered-depth L1 vs reference" (SURVEY.md §8(d)): the benched field,
+    as trained by the timed steps, renders a strided n_rays subset of the bench batch through
+    loner_amd.evaluate.DepthRenderer (HIP), and the CPU oracle (oracle/: the reference's sampler,
+    compositing and tcnn-v1.7 restatement) renders the same rays on the GPU's samples.  Checker leg only
+    (rank 0, N=1, after timing), as tests/test_gpu_depth_parity.py does.  Depths in metres.
+      default   mean / max |depth - oracle| and the fraction of rays within 1 cm (bar: mean <= 1e-3 m,
+                >= 99.9 % within 1 cm)
+      adjusted  the fraction of rays whose peak depth differs, and the largest difference in sample
+                positions (bar: <= 0.1 % of rays, by at most one sample spacing)"""
+    from loner_amd import _lib as L
+    from loner_amd import evaluate as E
+    from oracle import hashgrid as ohg
+    from oracle import mlp as omlp
+    from oracle import render as orender
+    from oracle import rng as orng
+    t0 = time.perf_counter()
+    R = window.n_slots
+    rays = torch.empty(R, 13, dtype=torch.float32, device=state.device)
+    dgt = torch.empty(R, dtype=torch.float32, device=state.device)
+    key = L.step_key(key_seed, 0)
+    window.build(key, 0, R, rays, dgt)
+    stride = max(1, R // n_rays)
+    rays = rays[::stride][:n_rays].contiguous()
+    n = rays.shape[0]
+    p16 = state.params[:state.n_params].cpu().numpy().astype(np.float16)
+    nm = state.n_mlp
+    w0, w1, table = p16[:2048].reshape(64, 32), p16[2048:nm].reshape(16, 64), p16[nm:].reshape(-1, 2)
+    rn = rays.cpu().numpy()
+    scale = float(window.scale)
+    out = {"rays": n, "samples_per_ray": S, "subset": f"every {stride}th ray of the bench batch (step key {key_seed})"}
+    for strategy in ("default", "adjusted"):
+        rend = E.DepthRenderer(state, n_samples=S, chunk=n)
+        depth, _, _ = rend.render(rays, key, strategy)
+        d = depth.cpu().numpy()
+        z = rend.z[:n].cpu().numpy()
+        xyz = (rn[:, None, 0:3] + rn[:, None, 3:6] * z[:, :, None]).astype(np.float32)
+        pos = ((xyz + np.float32(1)) / np.float32(2)).astype(np.float32).reshape(-1, 3)
+        out16, _ = omlp.forward(ohg.encode(pos, table, ohg.GridLayout(16, 2, 18, 16)), [w0, w1])
+        sig = out16[:, 0].astype(np.float32).reshape(n, S)
+        if strategy == "adjusted":
+            ref = orender.raw2outputs_adjusted(sig, z, rn[:, 3:6])["depth"]
+            diff = np.flatnonzero(d != ref)
+            steps = [abs(int(np.argmax(z[r] == d[r])) - int(np.argmax(z[r] == ref[r]))) for r in diff]
+            out["adjusted"] = {"frac_rays_differ": float(len(diff) / n), "max_sample_steps": max(steps, default=0)}
+        else:
+            a, b = orng.ray_sample_grid(np.arange(n), S)
+            ref = orender.raw2outputs(sig, z, rn[:, 3:6], orng.normal(key, orng.STREAM_NOISE, a, b), rn[:, -1:])["depth"]
+            err = np.abs(d - ref).astype(np.float64) * scale
+            out["depth_l1_vs_oracle_m"] = float(err.mean())
+            out["default"] = {"mean_m": float(err.mean()), "max_m": float(err.max()),
+                              "frac_within_1cm": float((err <= 1e-2).mean())}
+    out["seconds"] = time.perf_counter() - t0
+    return out
+
+
 def cpu_baseline_render(kind, n_rays, S):
     """The same pure-PyTorch restatement's forward render (oracle/torch_step.render_step: OGM sampler,
     sigma field, peak compositing) on a bounded sample of the C3 workload, same threads as above."""
@@ -290,6 +349,7 @@ def bench_render(args):
             "stage_ms": stage_ms}
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_render(kind, 4096, S)
+        line["cpu_baseline"]["rendered_depth_vs_oracle"] = rendered_depth_vs_oracle(state, window, 256, S)
     print(json.dumps(line), flush=True)
 
 
@@ -540,6 +600,18 @@ def main():
         if not window.all_valid:
             raise RuntimeError("bench window must give a fixed batch")
         R = window.n_slots
+    elif args.rays == "device" and args.shard_of:
+        # rank 0's slice of the config's batch split --shard-of ways: the strong-scaling per-rank step
+        from loner_amd.rays import RayWindow
+        if world != 1:
+            raise SystemExit("--shard-of runs one rank's shard on one GPU (world size 1)")
+        scans = syn.make_window(kind, nkf, seed=1000)
+        window = RayWindow(scans, syn.world_cube(kind), syn.SENSORS[kind]["ray_range"], n_lidar=rpk, n_sky=spk,
+                           strategy=strat, device=dev)
+        del scans
+        if not window.all_valid or window.n_slots % args.shard_of:
+            raise RuntimeError("bench window must give a fixed, evenly sharded batch")
+        R = window.n_slots // args.shard_of
     elif args.rays == "device":
         # one global keyframe window (nkf keyframes per rank), resident on every rank; rank r builds
         # the slots of its own nkf keyframes each step (a contiguous R/g slice)
@@ -573,6 +645,8 @@ def main():
     eng = S_.StepEngine(state, R, seed=12345 + (rank if replicas else 0), allreduce=allreduce,
                         ray_offset=0 if replicas else rank * R)
     r_glob = R if replicas else R * world
+    if args.shard_of:
+        r_glob = R * args.shard_of
 
     def run(i, prof=None):
         if args.rays == "device":
@@ -638,7 +712,9 @@ def main():
                                + ("in total, split over the GPUs, " if args.scaling == "strong" else "per GPU, ")
                                + f"L=16 T=2^18 hash grid + 64-wide sigma MLP, {preset} loss (L1_JS)",
                    "rays_per_gpu": R, "samples_per_ray": n_samples, "global_rays": R * world,
-                   "parallelism": (f"replicas{world}" if replicas else f"dp{world}") if world > 1 else "single",
+                   "parallelism": (f"replicas{world}" if replicas else f"dp{world}") if world > 1 else
+                   (f"shard 0 of {args.shard_of} (one rank's strong-scaling step, no collective)" if args.shard_of
+                    else "single"),
                    **({"submap_rank0": submap} if submap is not None else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
@@ -660,6 +736,8 @@ def main():
     }
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_rays, args.cpu_steps)
+        if args.rays == "device":
+            line["cpu_baseline"]["rendered_depth_vs_oracle"] = rendered_depth_vs_oracle(state, window, 512, n_samples)
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -106,8 +106,10 @@ int lnr_hashgrid_fwd_rays_live(const lnr_grid_desc* d, const float* rays, const 
 #define LNR_BWD_COUNTS_READY 1
 #define LNR_BWD_NO_ACCUM 2      /* stop after the scatter: lnr_hashgrid_bwd_accum then finishes level ranges */
 #define LNR_BWD_LEVEL_MAX_READY 4 /* the caller stored max |d_enc| per level at lnr_hashgrid_bwd_level_max():
-                                     no pass over d_enc for it (a data-parallel caller stores the max over
-                                     ranks, so every rank's records round alike) */
+                                     no pass over d_enc for it.  The maxima may be rank-local under data
+                                     parallelism: they only pick each level's power-of-two record scale,
+                                     fp16 rounding is scale-invariant, and the fixed-point unit sits far
+                                     below what reaches Adam */
 int64_t lnr_hashgrid_bwd_workspace_bytes(const lnr_grid_desc* d, int64_t n);
 /* Device address of the n_levels per-level max |d_enc| floats inside `workspace` (the same for
  * every n: the workspace's first bytes). */

@@ -805,9 +805,14 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
           atomicAdd(&acc[e0], fixed_i64(s0 * v0));
           atomicAdd(&acc[kChunk + e0], fixed_i64(s0 * v1));
           if (p) {
-            // p <= 12 for every valid record, so e1 stays in the chunk (an LDS address past the
-            // workgroup's allocation is discarded by the hardware in any case; masking e1 here cost
-            // 10 % of the kernel: 408 -> 450 us at C2)
+            // Invariant: the scatter writes p <= 12 (kChunkLog2) for every record, so e1 stays inside
+            // this chunk.  A corrupted record with p in 13..15 would put e1 up to 32767, which still
+            // lands inside this workgroup's LDS (the second feature array or the tile stage) and
+            // would corrupt sums silently; the mask is not applied in the product build because it
+            // cost 10 % of the kernel (408 -> 450 us at C2).  -DLNR_BWD_CHECK traps instead.
+#ifdef LNR_BWD_CHECK
+            if (p > kChunkLog2) __builtin_trap();
+#endif
             const uint32_t e1 = e0 ^ ((1u << p) - 1u);
             atomicAdd(&acc[e1], fixed_i64(tx * v0));
             atomicAdd(&acc[kChunk + e1], fixed_i64(tx * v1));

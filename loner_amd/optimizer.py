@@ -284,12 +284,16 @@ class Optimizer:
         n_glob = rays.shape[0]
         if self._world > 1:
             # data parallel: every rank builds the same FIXED batch (one generator, one seed), so its
-            # size is known everywhere; all-reducing the kept counts checks that, and rank r steps the
-            # contiguous slice shard_range(n, r, world) with its draws keyed by global ray index
+            # size is known everywhere; all-reducing [n, n^2] checks that, and rank r steps the
+            # contiguous slice shard_range(n, r, world) with its draws keyed by global ray index.
+            # world * sum(n^2) == sum(n)^2 holds iff every rank's n is equal (Cauchy-Schwarz), and every
+            # rank evaluates it on the same sums, so all ranks reach the same verdict (none is left
+            # waiting in a later collective)
             from .shard import shard_range
-            cnt = torch.tensor([float(n_glob)], device=dev)
+            cnt = torch.tensor([float(n_glob), float(n_glob) ** 2], dtype=torch.float64, device=dev)
             self._allreduce(cnt)
-            if int(cnt.item()) != n_glob * self._world:
+            s1_, s2_ = (float(v) for v in cnt.cpu())
+            if s2_ * self._world != s1_ * s1_:
                 raise RuntimeError("FIXED ray selection diverged across ranks")
             s0, s1 = shard_range(n_glob, self._rank, self._world)
             rays, depth = rays[s0:s1], depth[s0:s1]

@@ -154,7 +154,7 @@ def submap_window(part_id, n_kf=16, seed=0):
     """C5: the haveri trajectory split into <= 50 m submaps with +-30-pose padding as
     examples/fdt_segment_and_optimize_submaps.py does (loner_amd.submaps), submap part_id mod the part
     count: n_kf keyframes evenly spread over its padded pose range and its own world cube
-    (compute_world_cube of those poses).  Returns (scans, WorldCube, info dict)."""
+    (compute_world_cube of all the padded range's poses, pose_utils.py:285-314).  Returns (scans, WorldCube, info dict)."""
     from . import submaps as SM
     tum = np.load(os.path.join(ROOT, "tests", "golden", "haveri_keyframe_trajectory.npz"))["tum"]
     parts = SM.split_trajectory(tum[:, 1:4])
@@ -163,7 +163,7 @@ def submap_window(part_id, n_kf=16, seed=0):
     lo, hi = ranges[k]
     idx = np.round(np.linspace(lo, hi, n_kf)).astype(int)
     poses = [_quat_pose(tum[i, 1:4], tum[i, 4:8]) for i in idx]
-    scale, shift = SM.world_cube_from_poses(tum[lo:hi + 1, 1:4], SENSORS["forest"]["ray_range"])
+    scale, shift = SM.world_cube_from_poses(SM.poses_from_tum(tum[lo:hi + 1]), SENSORS["forest"]["ray_range"])
     wc = R.WorldCube(torch.tensor([scale], dtype=torch.float32), torch.from_numpy(shift))
     info = dict(part=k, n_parts=len(parts), core=list(parts[k]), padded=[lo, hi], cube_scale=scale)
     return make_window("forest", n_kf, seed=seed, poses=poses), wc, info

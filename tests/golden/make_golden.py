@@ -23,7 +23,10 @@ import torch
 REF = os.environ.get("LONER_REFERENCE", "/root/reference")
 OUT = os.path.dirname(os.path.abspath(__file__))
 STUBS = ("tinycudann", "torchviz", "open3d", "pytorch3d", "kornia", "attrdict", "cv2", "rosbag",
-         "rospy", "cv_bridge", "sensor_msgs", "ros_numpy", "tf2_msgs", "geometry_msgs", "std_msgs")
+         "rospy", "cv_bridge", "sensor_msgs", "ros_numpy", "tf2_msgs", "geometry_msgs", "std_msgs", "tf2_py",
+         "nav_msgs")
+# modules the reference imports that do not exist in its own tree (analysis.fdt_common_utils)
+STUB_PREFIXES = ("analysis.fdt_common_utils",)
 
 
 class _Anything(types.ModuleType):
@@ -40,7 +43,7 @@ class _Anything(types.ModuleType):
 
 class _StubFinder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
     def find_spec(self, name, path, target=None):
-        if name.split(".")[0] in STUBS:
+        if name.split(".")[0] in STUBS or name.startswith(STUB_PREFIXES):
             return importlib.machinery.ModuleSpec(name, self, is_package=True)
         return None
 
@@ -479,9 +482,101 @@ def main_r2():
     json.dump(keys, open(f"{OUT}/ckpt_keys.json", "w"), indent=1, sort_keys=True)
     print("round-2 golden vectors written to", OUT)
 
+# ---------------------------------------------------------------------------------------------
+# Round-3 fixtures (``python tests/golden/make_golden.py r3``): the C5 submap pipeline.  The
+# reference's own examples/fdt_segment_and_optimize_submaps.py is imported (ROS / open3d stubbed)
+# and run on the committed haveri keyframe trajectory: its split + padding loop writes one trajectory
+# CSV per submap and calls optimize_implicit_map, which is replaced by a recorder.  Each written CSV
+# then goes through the driver's own world-cube branch for submaps
+# (examples/fdt_optimize_implicit_map.py:208-233): build_poses_from_df(df, False) and
+# compute_world_cube(camera_to_lidar=None, ..., padding=0.3, submap=name) (the hpk dataset family has no
+# calibration object: examples/utils.py:119-123).  A second, synthetic trajectory whose middle part is
+# shorter than the 30-pose padding records that the reference raises there.
+
+class _SettingsStub(dict):
+    """Settings.load_from_file / augment stand-in for the segmentation loop, which only reads
+    experiment_name and system.log_dir_prefix (fdt_segment_and_optimize_submaps.py:52-67)."""
+    log_dir = None
+
+    @classmethod
+    def load_from_file(cls, path):
+        return cls()
+
+    def augment(self, changes):
+        pass
+
+    def __getattr__(self, k):
+        if k == "system":
+            return NS(log_dir_prefix=_SettingsStub.log_dir)
+        return self[k]
+
+
+def _run_reference_segmentation(seg, tum, workdir, tag):
+    import shutil
+    import yaml
+    d = os.path.join(workdir, tag)
+    shutil.rmtree(d, ignore_errors=True)
+    os.makedirs(d)
+    traj = os.path.join(d, "gt.txt")
+    with open(traj, "w") as f:
+        for row in tum:
+            f.write(" ".join(repr(float(v)) for v in row) + "\n")
+    cfg = os.path.join(d, "run.yaml")
+    yaml.safe_dump(dict(baseline="defaults.yaml", changes=None, experiment_name=tag, groundtruth_traj=traj), open(cfg, "w"))
+    _SettingsStub.log_dir = d
+    calls = []
+    seg.Settings = _SettingsStub
+    seg.optimize_implicit_map = lambda exp_dir, cfg_path, submap=None: calls.append(submap)
+    err = None
+    try:
+        seg.optimize_and_segment_implicit_map(cfg)
+    except IndexError as e:  # a neighbouring part shorter than the padding
+        err = repr(e)
+    files = sorted(os.listdir(os.path.join(d, tag, "trajectories"))) if os.path.isdir(os.path.join(d, tag, "trajectories")) else []
+    return d, tag, calls, files, err
+
+
+def main_r3():
+    import pandas as pd
+    ref = import_reference()
+    sys.path.insert(0, os.path.join(REF, "analysis"))
+    import examples.fdt_segment_and_optimize_submaps as seg
+    work = os.path.join(os.path.dirname(os.path.dirname(OUT)), "scratch", "golden_r3")
+    tum = np.load(f"{OUT}/haveri_keyframe_trajectory.npz")["tum"]
+    d, tag, calls, files, err = _run_reference_segmentation(seg, tum, work, "haveri")
+    assert err is None, err
+    tdir = os.path.join(d, tag, "trajectories")
+    names, rows, scales, shifts, mid = [], [], [], [], []
+    ts_index = {float(t): i for i, t in enumerate(tum[:, 0])}
+    for fn in files:
+        df = pd.read_csv(os.path.join(tdir, fn), names=["timestamp", "x", "y", "z", "q_x", "q_y", "q_z", "q_w"],
+                         delimiter=" ")
+        idx = np.array([ts_index[float(t)] for t in df["timestamp"]])
+        poses, _ = ref.pose_utils.build_poses_from_df(df, False)
+        wc = ref.pose_utils.compute_world_cube(None, None, None, poses, (2.5, 45.0), padding=0.3, submap=fn[:-4])
+        names.append(fn[:-4])
+        rows.append(idx)
+        scales.append(float(wc.scale_factor.reshape(-1)[0]))
+        shifts.append(wc.shift.numpy().reshape(3))
+    mids = np.load(os.path.join(d, tag, "submaps_middlepoints.npy"))
+    offsets = np.cumsum([0] + [len(r) for r in rows])
+    # a trajectory whose second part is shorter than the padding: 0.9 m steps, then 2.6 m steps
+    steps = np.concatenate([np.full(55, 0.9), np.full(25, 2.6), np.full(70, 0.9)])
+    xyz = np.stack([np.concatenate([[0.0], np.cumsum(steps)]), np.zeros(len(steps) + 1), np.zeros(len(steps) + 1)], 1)
+    short = np.concatenate([np.arange(len(xyz))[:, None] * 0.1, xyz, np.tile([0.0, 0.0, 0.0, 1.0], (len(xyz), 1))], 1)
+    _, _, calls_s, files_s, err_s = _run_reference_segmentation(seg, short, work, "short")
+    np.savez_compressed(f"{OUT}/submaps.npz", names=np.array(names), row_index=np.concatenate(rows),
+                        row_offsets=offsets, scale=np.float32(scales), shift=np.float32(shifts), middle_points=mids,
+                        ray_range=np.float32([2.5, 45.0]), short_tum=short, short_raises=np.bool_(err_s is not None),
+                        short_files_written=np.int64(len(files_s)), short_calls=np.int64(len(calls_s)))
+    print("round-3 golden vectors written to", OUT, names, scales, err_s, files_s, calls_s)
+
+
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "r2":
         main_r2()
+    elif len(sys.argv) > 1 and sys.argv[1] == "r3":
+        main_r3()
     else:
         main()

@@ -1,19 +1,27 @@
-"""C5 trajectory segmentation (loner_amd.submaps), restated from
-examples/fdt_segment_and_optimize_submaps.py:24-25,86-147 and pose_utils.py:222-314 on the committed
-haveri keyframe trajectory.  The script is not importable here (ROS / open3d imports): its split is
-pinned by the properties its loop guarantees and by the boundaries it yields on this trajectory
-(parity unpinned: restated from the text).  CPU only."""
+"""C5 trajectory segmentation and per-submap world cubes (loner_amd.submaps) against
+tests/golden/submaps.npz: tests/golden/make_golden.py (``r3``) ran the reference's own
+examples/fdt_segment_and_optimize_submaps.py:39-162 on the committed haveri keyframe trajectory and then,
+per written submap trajectory, pose_utils.build_poses_from_df(df, False) + compute_world_cube(..., submap=)
+as examples/fdt_optimize_implicit_map.py:208-233 does.  CPU only."""
 import os
 
 import numpy as np
+import pytest
 
 from loner_amd import submaps as SM
 
-TUM = np.load(os.path.join(os.path.dirname(__file__), "golden", "haveri_keyframe_trajectory.npz"))["tum"]
+G = os.path.join(os.path.dirname(__file__), "golden")
+TUM = np.load(os.path.join(G, "haveri_keyframe_trajectory.npz"))["tum"]
+SUB = np.load(os.path.join(G, "submaps.npz"))
 
 
 def _steps(p):
     return np.linalg.norm(np.diff(p, axis=0), axis=1)
+
+
+def _golden_rows():
+    off = SUB["row_offsets"]
+    return [SUB["row_index"][off[k]:off[k + 1]] for k in range(len(off) - 1)]
 
 
 def test_split_boundaries_and_properties():
@@ -27,22 +35,41 @@ def test_split_boundaries_and_properties():
             assert parts[k + 1][0] == e  # the next part starts with this part's last pose
             assert d[s:e + 1].sum() > SM.MAX_LENGTH  # one more step would have passed 50 m
     assert parts[0][0] == 0 and parts[-1][1] == len(pos) - 1
+    np.testing.assert_allclose(SM.middle_points(pos, parts), SUB["middle_points"], rtol=0, atol=1e-12)
 
 
-def test_padding_and_world_cubes():
-    parts = SM.split_trajectory(TUM[:, 1:4])
-    ranges = SM.padded_ranges(parts, len(TUM))
-    # previous part's poses [-30, -1) before, next part's [1, 30) after (29 each)
-    assert ranges == [(0, 311 + 29), (311 - 29, 622 + 29), (622 - 29, 934 + 29), (934 - 29, 1093)]
-    for lo, hi in ranges:
-        scale, shift = SM.world_cube_from_poses(TUM[lo:hi + 1, 1:4], (2.5, 45.0))
-        p = TUM[lo:hi + 1, 1:4]
-        # every pose's +-45 m box lies inside the cube [-1, 1]^3 after (x + shift) / scale
-        q = (np.concatenate([p - 45.0, p + 45.0]) + shift) / scale
+def test_padded_ranges_match_reference_files():
+    """The poses each reference submap file holds, in order, are the padded index range."""
+    ranges = SM.padded_ranges(SM.split_trajectory(TUM[:, 1:4]), len(TUM))
+    rows = _golden_rows()
+    assert len(ranges) == len(rows) == len(SUB["names"])
+    for (lo, hi), idx in zip(ranges, rows):
+        np.testing.assert_array_equal(idx, np.arange(lo, hi + 1))
+
+
+def test_world_cubes_match_reference():
+    """compute_world_cube with the corners rotated by every pose (pose_utils.py:296-298)."""
+    ranges = SM.padded_ranges(SM.split_trajectory(TUM[:, 1:4]), len(TUM))
+    for k, (lo, hi) in enumerate(ranges):
+        scale, shift = SM.world_cube_from_poses(SM.poses_from_tum(TUM[lo:hi + 1]), tuple(SUB["ray_range"]))
+        np.testing.assert_allclose(scale, SUB["scale"][k], rtol=1e-6)
+        np.testing.assert_allclose(shift, SUB["shift"][k], rtol=1e-6, atol=1e-5)
+        # every pose's rotated +-45 m cube lies inside [-1, 1]^3 after (x + shift) / scale
+        P = SM.poses_from_tum(TUM[lo:hi + 1]).astype(np.float64)
+        c = np.array([[sx, sy, sz] for sx in (-45, 45) for sy in (-45, 45) for sz in (-45, 45)], np.float64)
+        q = (np.einsum("nij,kj->nki", P[:, :3, :3], c) + P[:, None, :3, 3] + shift) / scale
         assert np.abs(q).max() <= 1.0
-        # the cube is the padded bounding sphere of those boxes (pose_utils.py:306-314)
-        ext = (p.max(0) + 45.0) - (p.min(0) - 45.0)
-        assert np.isclose(scale, np.linalg.norm(ext) / (2 * np.sqrt(3)) * 1.3, rtol=1e-5)
+
+
+def test_short_neighbour_raises_like_reference():
+    """A part with fewer poses than the padding: the reference's part_next[k] / part_previous[-30]
+    raise IndexError (fdt_segment_and_optimize_submaps.py:139,146), before any submap is optimised."""
+    assert bool(SUB["short_raises"]) and int(SUB["short_calls"]) == 0
+    short = SUB["short_tum"]
+    parts = SM.split_trajectory(short[:, 1:4])
+    assert min(e - s + 1 for s, e in parts) < SM.PADDING
+    with pytest.raises(IndexError):
+        SM.padded_ranges(parts, len(short))
 
 
 def test_submap_window_is_its_segment():
@@ -53,3 +80,5 @@ def test_submap_window_is_its_segment():
     np.testing.assert_allclose(t[0], TUM[282, 1:4], atol=1e-5)
     np.testing.assert_allclose(t[-1], TUM[651, 1:4], atol=1e-5)
     assert float(cube.scale_factor[0]) == info["cube_scale"]
+    np.testing.assert_allclose(info["cube_scale"], SUB["scale"][1], rtol=1e-6)
+    np.testing.assert_allclose(cube.shift.numpy(), SUB["shift"][1], rtol=1e-6, atol=1e-5)

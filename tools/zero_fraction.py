@@ -27,7 +27,7 @@ eng.step(rays[:n], inten[:n])
 torch.cuda.synchronize()
 w = eng.weights[:n]
 print("w==0 frac", float((w == 0).float().mean()))
-de = eng.d_enc[:, :n * S]
+de = eng.denc_f32()[:, :n * S]
 print("d_enc zero frac per level", [round(float(((de[l] == 0).all(-1)).float().mean()), 3) for l in range(16)])
 tiles = (w.reshape(-1, 16) == 0).all(-1).float().mean()
 print("all-zero 16-tiles", float(tiles))
