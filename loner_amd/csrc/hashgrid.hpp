@@ -448,7 +448,6 @@ struct BwdWorkspace {
   uint64_t* seg_start;   // [kMaxBuckets + 1]
   long long* partial;    // [2 kAccumGroups][2 * kChunk] int64 fixed-point partial sums of cut buckets
   uint2* rec;            // [8 * N * L] records {word, half2} (see "Backward records")
-  uint8_t* ovf;          // [L][n_sb] 1 where the level-looped scatter left (row, level) to k_bwd_scatter_overflow
   int64_t n_sb;
   int64_t n_chunks;
 };
@@ -459,7 +458,7 @@ inline int64_t bwd_n_chunks(int64_t n) { return (bwd_n_sb(n) + kRowsPerChunk - 1
 inline int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
 
 struct WsLayout {
-  int64_t hist, chunk_sum, level_max, counts, seg_start, partial, rec, ovf, total;
+  int64_t hist, chunk_sum, level_max, counts, seg_start, partial, rec, total;
 };
 
 inline WsLayout ws_layout(const lnr_grid_desc* d, const GridArgs& a, int64_t n) {
@@ -474,7 +473,6 @@ inline WsLayout ws_layout(const lnr_grid_desc* d, const GridArgs& a, int64_t n) 
   w.partial = b;   b += align256((int64_t)2 * kAccumGroups * 2 * kChunk * 8);
   // +2 records: the accumulate loads records in pairs
   w.rec = b;       b += align256((8 * n * (int64_t)d->n_levels + 2) * 8);
-  w.ovf = b;       b += align256(nsb * (int64_t)d->n_levels);
   w.total = b;
   return w;
 }
@@ -492,7 +490,6 @@ inline BwdWorkspace carve_workspace(void* base, const GridArgs& a, const lnr_gri
   w.seg_start = reinterpret_cast<uint64_t*>(p + L.seg_start);
   w.partial = reinterpret_cast<long long*>(p + L.partial);
   w.rec = reinterpret_cast<uint2*>(p + L.rec);
-  w.ovf = reinterpret_cast<uint8_t*>(p + L.ovf);
   w.n_sb = bwd_n_sb(n);
   w.n_chunks = bwd_n_chunks(n);
   return w;

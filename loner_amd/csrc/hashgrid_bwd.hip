@@ -3,15 +3,20 @@
 // Measured on MI355X: scattered fp32 global atomics run at ~20 G lane-ops/s (memory-side
 // execution) and LDS ds_add_f32 at only 0.33 lanes/clk/CU whatever the address pattern, while
 // ds_add_u64 runs at 4.8 lanes/clk/CU.  So the backward is
-//   count   per (kSB-sample row, level) record histogram per 4096-entry table chunk
-//           (emitted by the training forward, or by k_bwd_count)
-//   scan    column prefix over rows -> exact record offsets (no global atomics, no capacity guess)
-//   scatter 12-byte records (hashgrid.hpp: one per x-pair of corners at fine levels, one per
-//           merged corner at coherent levels) staged in LDS in bucket order and written as
-//           coalesced runs; per-row max |value| for the fixed-point scale
-//   accum   one workgroup per (bucket, slice): int64 fixed-point sums in a 64 KB LDS chunk with
-//           ds_add_u64, converted back to fp32 and stored; a bucket split over several slices
-//           stores per-slice int64 partial chunks that k_bwd_finalize adds exactly
+//   count    per (512-sample row, level) record histogram over the level's 4096-entry table chunks
+//            (buckets), emitted by the training forward (k_hashgrid_fwd<..., true>) or by k_bwd_count
+//   scan     k_bwd_chunk_sums + k_bwd_scan_rows (column prefix over 64-row chunks) + k_bwd_scan_buckets:
+//            exact per-row record offsets in every bucket (no global atomics, no capacity guess)
+//   scatter  k_bwd_scatter_rows: one workgroup per row walks all 16 levels; 8-byte records {word,
+//            fp16 value pair at the level's power-of-two scale} (hashgrid.hpp "Backward records": one
+//            per x-pair of corners at fine levels, one per corner of a run of lanes in one cell at the
+//            coherent levels) are ranked with LDS atomics, staged in bucket order and copied out as
+//            runs; a (row, level) with more records than the stage holds writes each to its slot
+//   accum    k_bwd_accum: the records of a bucket range split evenly over 512 workgroups, each adding
+//            its pieces into a 64 KB LDS chunk of int64 fixed point (ds_add_u64) and storing fp32 (a
+//            whole bucket) or an int64 partial chunk (a bucket its range boundaries cut) that
+//            k_bwd_finalize adds in workgroup order.  Small batches take k_bwd_accum_buckets instead:
+//            one workgroup per whole bucket, no partials and no finalize (accum_buckets_max_n).
 // No float atomics anywhere: the result is bitwise reproducible, and d_table is overwritten.
 #include "hashgrid.hpp"
 
@@ -347,34 +352,6 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
   scatter_row_level<PosFn, GradFn, KIND>(a, pos, n, grad, ws, l, sb, skip_zero, smem);
 }
 
-// The (row, level) items the level-looped scatter could not stage (more than kCap records: rows of
-// coherent levels whose runs did not merge, or pathological split pairs), each as above.
-template <class PosFn, class GradFn>
-__global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter_overflow(GridArgs a, PosFn pos, int64_t n,
-                                                                                      GradFn grad, BwdWorkspace ws,
-                                                                                      bool skip_zero) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ unsigned long long masks[kSB / 64];
-  // workgroup b checks items b, b + G, b + 2G, ... (G = gridDim.x, item = level * n_sb + row), kSB at
-  // a time: flagged items are runs of rows of one level, and the stride deals them over the grid
-  const int64_t items = ws.n_sb * a.n_levels, G = gridDim.x;
-  for (int64_t base = blockIdx.x; base < items; base += G * kSB) {
-    const int64_t it = base + G * threadIdx.x;
-    const unsigned long long m = __ballot(it < items && ws.ovf[it] != 0);
-    if ((threadIdx.x & 63) == 0) masks[threadIdx.x >> 6] = m;
-    __syncthreads();
-    for (int w = 0; w < kSB / 64; ++w) {
-      for (unsigned long long mm = masks[w]; mm; mm &= mm - 1) {
-        const int64_t q = base + G * (64 * w + __ffsll((long long)mm) - 1);
-        scatter_row_level<PosFn, GradFn, kLevelsAny>(a, pos, n, grad, ws, (uint32_t)(q / ws.n_sb), q % ws.n_sb,
-                                                     skip_zero, smem);
-        lds_barrier();
-      }
-    }
-    __syncthreads();  // masks are rewritten
-  }
-}
-
 // Level-looped scatter: one workgroup per histogram row walks every level, so a sample's position is
 // loaded and decoded once (not once per level), the next level's d_enc and histogram row are in
 // flight while this level ranks and places, and the copy-out of level l - 1 overlaps the ranking of
@@ -389,7 +366,8 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter_o
 //    operations and the copy-out stores, so nothing in it ever waits on global memory.
 //  * Each record is ranked (returning LDS atomic) and placed at once, 16 B {word, global slot, v0,
 //    v1} in bucket order; then the level's stage is copied out (kRowsStages).
-//  * A (row, level) with more than kRowsCap records is flagged and left to k_bwd_scatter_overflow.
+//  * A (row, level) with more than kRowsCap records (coherent rows whose runs did not merge) writes
+//    every record straight to its global slot instead (same slots, unstaged).
 // Same records, counts and blockmax as k_bwd_scatter.
 constexpr int kRowsCap = 2176;  // 4.25 records per sample: fine rows hold 4 + the rare split pairs
 // Stages: 1, one stage with the copy-out after each level's placement: 44 KB of LDS and 80 VGPRs
@@ -407,9 +385,6 @@ constexpr int rows_stages() {
 }
 template <class GradFn, int NB>
 constexpr int rows_waves() { return rows_stages<GradFn, NB>() == 1 ? 6 : 4; }
-#ifndef LNR_STAGE_SPLIT_WRITE
-#define LNR_STAGE_SPLIT_WRITE 1
-#endif
 #ifndef LNR_PRESCALE
 #define LNR_PRESCALE 1
 #endif
@@ -490,10 +465,7 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
       const uint32_t ex = inc - c0 - c1;
       if (2 * lane < nb) sm.sg[l][2 * lane] = make_uint2(ex, (uint32_t)(seg[p][0] + h0[p][0]));
       if (2 * lane + 1 < nb) sm.sg[l][2 * lane + 1] = make_uint2(ex + c0, (uint32_t)(seg[p][1] + h0[p][1]));
-      if (lane == 63) {
-        sm.total[l] = inc;
-        ws.ovf[(int64_t)l * ws.n_sb + sb] = inc > (uint32_t)kRowsCap;  // unstaged: k_bwd_scatter_overflow's item
-      }
+      if (lane == 63) sm.total[l] = inc;
     }
   }
   lds_barrier();
@@ -544,8 +516,7 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
 #else
     const float2 gv = in ? gl : make_float2(0.f, 0.f);
 #endif
-    const bool inr = staged && in;  // an unstaged row emits nothing here: k_bwd_scatter_overflow redoes it
-    const bool act = inr && (!skip_zero || gv.x != 0.f || gv.y != 0.f);
+    const bool act = in && (!skip_zero || gv.x != 0.f || gv.y != 0.f);
     const float rs = LNR_PRESCALE ? 1.0f : rsc[l];
     // rank (returning LDS atomics) and place: all start reads, then all atomics, then all writes
     // (one lane-level branch for the 4 records: they share their validity)
@@ -558,17 +529,18 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
 #pragma unroll
         for (int k = 0; k < 4; ++k) rank[k] = atomicAdd(&ctr[bk[k]], 1u);
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-#if LNR_STAGE_SPLIT_WRITE
-        {  // three 32-bit fields (ds_write2_b32 + ds_write_b32: no register moves to build a b128 quad)
-          uint32_t* q = reinterpret_cast<uint32_t*>(&sm.stage[stg][s4[k].x + rank[k]]);
-          q[0] = word[k];
-          q[1] = s4[k].y + rank[k];
-          q[2] = rec_half2(val[k].x, val[k].y, rs);
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t slot = s4[k].y + rank[k];
+          const uint32_t h = rec_half2(val[k].x, val[k].y, rs);
+          if (staged) {  // three 32-bit fields (ds_write2_b32 + ds_write_b32: no register moves for a b128 quad)
+            uint32_t* q = reinterpret_cast<uint32_t*>(&sm.stage[stg][s4[k].x + rank[k]]);
+            q[0] = word[k];
+            q[1] = slot;
+            q[2] = h;
+          } else {  // (block-uniform) more records than the stage holds: each straight to its global slot
+            ws.rec[slot < spare ? slot : spare] = make_uint2(word[k], h);
+          }
         }
-#else
-          sm.stage[stg][s4[k].x + rank[k]] = make_uint4(word[k], s4[k].y + rank[k], rec_half2(val[k].x, val[k].y, rs), 0u);
-#endif
       }
     };
     uint32_t bk4[4], w4[4];
@@ -606,7 +578,7 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
       RunInfo ri;
       float v[16];
       coherent_run_values(c, in, gv.x, gv.y, ri, v);
-      const bool valid = inr && ri.tail;
+      const bool valid = in && ri.tail;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -688,6 +660,9 @@ __device__ __forceinline__ unsigned long long fixed_i64(float x) {
   return bits - 0x4338000000000000ull;
 }
 
+#ifndef LNR_ACCUM_BUCKETS_MAX_N
+#define LNR_ACCUM_BUCKETS_MAX_N (1 << 17)  // C1 (32 K samples): 103 -> 76 us for the backward stage; the C4 shard of 8 GPUs (590 K): 219 -> 229 us
+#endif
 #ifndef LNR_ACCUM_WAVES_PER_EU
 #define LNR_ACCUM_WAVES_PER_EU 8
 #endif
@@ -717,13 +692,91 @@ __device__ __forceinline__ uint32_t level_of_bucket(const GridArgs& a, uint32_t 
   return l;
 }
 
-#ifdef LNR_EXP_WG_TIMES
-// diagnostic (experiment builds): per accumulate workgroup {start, end, records, first level}
-static __device__ unsigned long long g_wg[kAccumGroups][4];
-extern "C" int lnr_debug_accum_wg(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg), sizeof(g_wg)) == hipSuccess ? 0 : -1;
-}
+
+// The records [beg, end) of one bucket, added into the workgroup's LDS chunk (zeroed before).
+// Tiles of kTile records pass through LDS: each thread loads 2 consecutive records (one 16-B load,
+// coalesced) and stores them to the tile stage; then lane L of wave w takes records 32 L + 2 w and
+// + 1 of the tile, so one atomic instruction holds records 32 apart.  Adjacent records of a bucket
+// are one ray's consecutive samples (equal or neighbouring corners), and equal addresses
+// serialise within one LDS instruction; this way they meet in one only by a hash collision.
+// The stage is XOR-swizzled (stage_pos) so those strided reads spread over the banks.
+// Loads run kAccumTrip tiles ahead (registers).
+// A pair record (p > 0) adds (1 - tx) v to corner e0 and tx v to e1 = e0 ^ (2^p - 1), a single
+// record (p = 0, tx = 0) adds v to e0.  int64 sums: the result does not depend on the order.
+// fs = 2^k2, the bucket's fixed-point scale (the records carry 2^k_l already).
+__device__ __forceinline__ void accum_records(unsigned long long* acc, uint2* stage, const BwdWorkspace& ws,
+                                              uint64_t beg, uint64_t end, float fs) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t beg2 = beg & ~1ull;
+  const float ftx = fs * kInvU16;
+  const uint64_t n_tiles = (end - beg2 + kTile - 1) / kTile;
+  auto load_tile = [&](uint64_t tile) {  // this thread's 2 records of a tile: {w0, v0, w1, v1}
+    const uint64_t rr = beg2 + (tile < n_tiles ? tile : 0) * kTile + 2 * threadIdx.x;
+    const uint64_t rc = rr < end ? rr : beg2;  // unconditional loads
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(&ws.rec[rc]));
+  };
+  const uint32_t q0 = 32u * lane + 2u * (threadIdx.x >> 6);  // this lane's records in a tile
+  auto run_tile = [&](uint64_t tile, const u32x4& cur) {
+    lds_barrier();  // the previous tile's stage reads are done
+    *reinterpret_cast<u32x4*>(&stage[stage_pos(2 * threadIdx.x)]) = cur;
+    lds_barrier();
+    const uint64_t base = beg2 + tile * kTile;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const uint2 rec = stage[stage_pos(q0 + r)];
+      const uint64_t rr = base + q0 + r;
+      if (rr >= beg && rr < end) {
+        const uint32_t w = rec.x;
+        const float v0 = rec_v0(rec.y), v1 = rec_v1(rec.y);
+        const uint32_t e0 = w & (kChunk - 1);
+        const uint32_t p = (w >> kChunkLog2) & 15u;
+        const float tx = (float)(w >> 16) * ftx;  // 0 for single-corner records; pre-scaled
+        const float s0 = fs - tx;
+        atomicAdd(&acc[e0], fixed_i64(s0 * v0));
+        atomicAdd(&acc[kChunk + e0], fixed_i64(s0 * v1));
+        if (p) {
+          // Invariant: the scatter writes p <= 12 (kChunkLog2) for every record, so e1 stays inside
+          // this chunk.  A corrupted record with p in 13..15 would put e1 up to 32767, which still
+          // lands inside this workgroup's LDS (the second feature array or the tile stage) and
+          // would corrupt sums silently; the mask is not applied in the product build because it
+          // cost 10 % of the kernel (408 -> 450 us at C2).  -DLNR_BWD_CHECK traps instead.
+#ifdef LNR_BWD_CHECK
+          if (p > kChunkLog2) __builtin_trap();
 #endif
+          const uint32_t e1 = e0 ^ ((1u << p) - 1u);
+          atomicAdd(&acc[e1], fixed_i64(tx * v0));
+          atomicAdd(&acc[kChunk + e1], fixed_i64(tx * v1));
+        }
+      }
+    }
+  };
+  // kAccumTrip tiles per trip, each in a register set of its own (the unrolled loop indexes them
+  // statically), its next load issued as soon as it is staged: the loads of the following
+  // kAccumTrip tiles are in flight while these accumulate
+  u32x4 buf[kAccumTrip];
+#pragma unroll
+  for (int d = 0; d < kAccumTrip; ++d) buf[d] = load_tile(d);
+  for (uint64_t tile = 0; tile < n_tiles; tile += kAccumTrip) {
+#pragma unroll
+    for (int d = 0; d < kAccumTrip; ++d) {
+      if (tile + d < n_tiles) {  // block-uniform
+        const u32x4 c = buf[d];
+        buf[d] = load_tile(tile + d + kAccumTrip);
+        run_tile(tile + d, c);
+      }
+    }
+  }
+}
+
+// A whole bucket's final fp32 values from its LDS chunk.
+__device__ __forceinline__ void store_bucket(const unsigned long long* acc, const GridArgs& a, const BwdWorkspace& ws,
+                                             float* __restrict__ d_table, uint32_t l, uint32_t ent0, uint32_t nent,
+                                             int k2) {
+  const double inv = unit_back(a, ws, l, k2);
+  float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0);
+  for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x)
+    dst[t] = (float)((double)(long long)acc[(t & 1) * kChunk + (t >> 1)] * inv);
+}
 
 // One workgroup per kAccumGroups-th of the records of buckets [b_begin, b_end).  Per bucket piece:
 // int64 fixed-point sums in a 64 KB LDS chunk with ds_add_u64, then the fp32 gradient (a whole
@@ -734,19 +787,10 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
   __shared__ unsigned long long acc[2 * kChunk];  // int64 fixed point, one array per feature (8-B atomics
                                                   // on random entries spread over twice the bank pairs)
   __shared__ __attribute__((aligned(16))) uint2 stage[kTile];  // the tile's records, swizzled
-  const int lane = threadIdx.x & 63;
   const uint64_t r0 = ws.seg_start[b_begin], R = ws.seg_start[b_end] - r0;
-#ifdef LNR_ACCUM_PAIR_REVERSE
-  const uint32_t gi = blockIdx.x < kAccumGroups / 2 ? blockIdx.x : (3 * kAccumGroups / 2 - 1) - blockIdx.x;
-#else
   const uint32_t gi = blockIdx.x;
-#endif
   const uint64_t rbeg = range_at(r0, R, gi), rend = range_at(r0, R, gi + 1);
   if (rbeg >= rend) return;
-#ifdef LNR_EXP_WG_TIMES
-  unsigned long long wg_t0 = 0;
-  if (threadIdx.x == 0) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(wg_t0)::"memory");
-#endif
   uint32_t lo = b_begin, hi = b_end;  // the bucket holding record rbeg: seg_start[lo] <= rbeg < seg_start[lo + 1]
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
@@ -761,112 +805,50 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
     const uint32_t l = level_of_bucket(a, b);
     const uint32_t ent0 = (b - a.bucket_base[l]) * kChunk;
     const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
-    LNR_STAMP(t0);
     for (int t = threadIdx.x; t < 2 * kChunk; t += blockDim.x) acc[t] = 0ull;
     lds_barrier();
-    LNR_STAMP(t1);
-    // Tiles of kTile records pass through LDS: each thread loads 2 consecutive records (one 16-B load,
-    // coalesced) and stores them to the tile stage; then lane L of wave w takes records 32 L + 2 w and
-    // + 1 of the tile, so one atomic instruction holds records 32 apart.  Adjacent records of a bucket
-    // are one ray's consecutive samples (equal or neighbouring corners), and equal addresses
-    // serialise within one LDS instruction; this way they meet in one only by a hash collision.
-    // The stage is XOR-swizzled (stage_pos) so those strided reads spread over the banks.
-    // Loads run kAccumTrip tiles ahead (registers).
-    // A pair record (p > 0) adds (1 - tx) v to corner e0 and tx v to e1 = e0 ^ (2^p - 1), a single
-    // record (p = 0, tx = 0) adds v to e0.  int64 sums: the result does not depend on the order.
-    const uint64_t beg2 = beg & ~1ull;
-    // one scale per bucket (the pieces' partials add exactly); the records carry 2^k_l already
+    // one scale per bucket (the pieces' partials add exactly)
     const int k2 = bucket_k2(ws, b);
-    const float fs = ldexpf(1.f, k2);
-    const float ftx = fs * kInvU16;
-    const uint64_t n_tiles = (end - beg2 + kTile - 1) / kTile;
-    auto load_tile = [&](uint64_t tile) {  // this thread's 2 records of a tile: {w0, v0, w1, v1}
-      const uint64_t rr = beg2 + (tile < n_tiles ? tile : 0) * kTile + 2 * threadIdx.x;
-      const uint64_t rc = rr < end ? rr : beg2;  // unconditional loads
-      return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(&ws.rec[rc]));
-    };
-    const uint32_t q0 = 32u * lane + 2u * (threadIdx.x >> 6);  // this lane's records in a tile
-    auto run_tile = [&](uint64_t tile, const u32x4& cur) {
-      lds_barrier();  // the previous tile's stage reads are done
-      *reinterpret_cast<u32x4*>(&stage[stage_pos(2 * threadIdx.x)]) = cur;
-      lds_barrier();
-      const uint64_t base = beg2 + tile * kTile;
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        const uint2 rec = stage[stage_pos(q0 + r)];
-        const uint64_t rr = base + q0 + r;
-        if (rr >= beg && rr < end) {
-          const uint32_t w = rec.x;
-          const float v0 = rec_v0(rec.y), v1 = rec_v1(rec.y);
-          const uint32_t e0 = w & (kChunk - 1);
-          const uint32_t p = (w >> kChunkLog2) & 15u;
-          const float tx = (float)(w >> 16) * ftx;  // 0 for single-corner records; pre-scaled
-          const float s0 = fs - tx;
-          atomicAdd(&acc[e0], fixed_i64(s0 * v0));
-          atomicAdd(&acc[kChunk + e0], fixed_i64(s0 * v1));
-          if (p) {
-            // Invariant: the scatter writes p <= 12 (kChunkLog2) for every record, so e1 stays inside
-            // this chunk.  A corrupted record with p in 13..15 would put e1 up to 32767, which still
-            // lands inside this workgroup's LDS (the second feature array or the tile stage) and
-            // would corrupt sums silently; the mask is not applied in the product build because it
-            // cost 10 % of the kernel (408 -> 450 us at C2).  -DLNR_BWD_CHECK traps instead.
-#ifdef LNR_BWD_CHECK
-            if (p > kChunkLog2) __builtin_trap();
-#endif
-            const uint32_t e1 = e0 ^ ((1u << p) - 1u);
-            atomicAdd(&acc[e1], fixed_i64(tx * v0));
-            atomicAdd(&acc[kChunk + e1], fixed_i64(tx * v1));
-          }
-        }
-      }
-    };
-    // kAccumTrip tiles per trip, each in a register set of its own (the unrolled loop indexes them
-    // statically), its next load issued as soon as it is staged: the loads of the following
-    // kAccumTrip tiles are in flight while these accumulate
-    u32x4 buf[kAccumTrip];
-#pragma unroll
-    for (int d = 0; d < kAccumTrip; ++d) buf[d] = load_tile(d);
-    for (uint64_t tile = 0; tile < n_tiles; tile += kAccumTrip) {
-#pragma unroll
-      for (int d = 0; d < kAccumTrip; ++d) {
-        if (tile + d < n_tiles) {  // block-uniform
-          const u32x4 c = buf[d];
-          buf[d] = load_tile(tile + d + kAccumTrip);
-          run_tile(tile + d, c);
-        }
-      }
-    }
-    LNR_STAMP(t2);
+    accum_records(acc, stage, ws, beg, end, ldexpf(1.f, k2));
     lds_barrier();
-    LNR_STAMP(t3);
     if (beg == s0 && end == s1) {  // the whole bucket: the final values
-      const double inv = unit_back(a, ws, l, k2);
-      float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0);
-      for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x)
-        dst[t] = (float)((double)(long long)acc[(t & 1) * kChunk + (t >> 1)] * inv);
+      store_bucket(acc, a, ws, d_table, l, ent0, nent, k2);
     } else {  // this piece's int64 partial chunk
       long long* dst = ws.partial + (int64_t)(2 * gi + (beg > s0 ? 0 : 1)) * (2 * kChunk);
       for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) dst[t] = (long long)acc[(t & 1) * kChunk + (t >> 1)];
     }
     lds_barrier();
-    LNR_STAMP(t4);
-    LNR_PHASE(16, t1, t0);
-    LNR_PHASE(17, t2, t1);
-    LNR_PHASE(18, t3, t2);
-    LNR_PHASE(19, t4, t3);
-    LNR_PHASE(20, 1ull, 0ull);
-    LNR_PHASE(21, end - beg, 0ull);
   }
-#ifdef LNR_EXP_WG_TIMES
-  if (threadIdx.x == 0) {
-    unsigned long long t1;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
-    g_wg[gi][0] = wg_t0;
-    g_wg[gi][1] = t1;
-    g_wg[gi][2] = rend - rbeg;
-    g_wg[gi][3] = level_of_bucket(a, lo);
+}
+
+// Small batches (few records per bucket): one workgroup per whole bucket, the finest level's
+// first (the dispatcher hands workgroups out in launch order as slots free, so the large fine-level
+// buckets start first and the small coherent ones fill in).  No bucket is cut, so there are no
+// partial chunks and no k_bwd_finalize; an empty bucket stores its zeros.  The same per-bucket
+// fixed-point unit as k_bwd_accum: bitwise the same gradient.  The record-balanced k_bwd_accum
+// instead pays two 64 KB partial chunks per workgroup and a finalize pass over every cut bucket,
+// which dominates when a bucket holds a tile or two of records.
+__global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_accum_buckets(GridArgs a, BwdWorkspace ws,
+                                                                                                float* __restrict__ d_table,
+                                                                                                uint32_t b_begin, uint32_t b_end) {
+  __shared__ unsigned long long acc[2 * kChunk];
+  __shared__ __attribute__((aligned(16))) uint2 stage[kTile];
+  const uint32_t b = b_end - 1 - blockIdx.x;
+  const uint64_t s0 = ws.seg_start[b], s1 = ws.seg_start[b + 1];
+  const uint32_t l = level_of_bucket(a, b);
+  const uint32_t ent0 = (b - a.bucket_base[l]) * kChunk;
+  const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
+  if (s0 == s1) {
+    float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0);
+    for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) dst[t] = 0.f;
+    return;
   }
-#endif
+  for (int t = threadIdx.x; t < 2 * kChunk; t += blockDim.x) acc[t] = 0ull;
+  lds_barrier();
+  const int k2 = bucket_k2(ws, b);
+  accum_records(acc, stage, ws, s0, s1, ldexpf(1.f, k2));
+  lds_barrier();
+  store_bucket(acc, a, ws, d_table, l, ent0, nent, k2);
 }
 
 // Buckets the accumulation did not finish: cut buckets = the sum of their pieces' partial chunks in
@@ -919,12 +901,23 @@ __global__ void __launch_bounds__(kFinalizeThreads) k_bwd_finalize(GridArgs a, B
   }
 }
 
+// Samples up to which the accumulation takes whole buckets (k_bwd_accum_buckets) instead of the
+// record-balanced split; LONER_ACCUM_BUCKETS_MAX_N overrides it (measurements: DESIGN.md section 4).
+// (read at every launch, so a process can switch between the two: tests/test_gpu_fullsize.py)
+static int64_t accum_buckets_max_n() {
+  const char* e = getenv("LONER_ACCUM_BUCKETS_MAX_N");
+  return e ? (int64_t)atoll(e) : (int64_t)LNR_ACCUM_BUCKETS_MAX_N;
+}
+
 // Accumulate + finalize the buckets of levels [l0, l1): their slice of d_table becomes final.
 static void launch_accum(const GridArgs& a, const BwdWorkspace& w, const lnr_grid_desc* d, int64_t n, uint32_t l0,
                          uint32_t l1, float* d_table, hipStream_t st) {
   const uint32_t b0 = a.bucket_base[l0], b1 = a.bucket_base[l1];
   if (b1 <= b0) return;
-  (void)n;
+  if (n <= accum_buckets_max_n()) {  // small batches: whole buckets, no partials, no finalize
+    hipLaunchKernelGGL(k_bwd_accum_buckets, dim3(b1 - b0), dim3(kAccumThreads), 0, st, a, w, d_table, b0, b1);
+    return;
+  }
   hipLaunchKernelGGL(k_bwd_accum, dim3(kAccumGroups), dim3(kAccumThreads), 0, st,
                      a, w, d_table, b0, b1);
   hipLaunchKernelGGL(k_bwd_finalize, dim3(b1 - b0), dim3(kFinalizeThreads), 0, st, a, w, d_table, b0, b1);
@@ -967,7 +960,6 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, Gra
   // plus the pass over the rows it could not stage; other grids (the colour grid's 2^19 levels have
   // 128 chunks): one workgroup per (row, level)
   const bool rows = L == 16 && all_fine && pow2 && 8 * n * (int64_t)L + 2 < (int64_t(1) << 32);
-  bool looped = true;
   if (rows && m >= 3 && m <= 7 && maxnb <= 64) {
     auto kern = m == 3   ? k_bwd_scatter_rows<PosFn, GradFn, 16, 3, 64>
                 : m == 4 ? k_bwd_scatter_rows<PosFn, GradFn, 16, 4, 64>
@@ -983,14 +975,8 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, Gra
     hipLaunchKernelGGL(kern, dim3((unsigned)w.n_sb), dim3(kSB), 0, st, a, pos, n, grad, w, skip_zero);
 #endif
   } else {
-    looped = false;
     hipLaunchKernelGGL((k_bwd_scatter<PosFn, GradFn, kLevelsAny>), dim3((unsigned)(w.n_sb * L)), dim3(kSB), kScatterLds,
                        st, a, pos, n, grad, w, 0u, skip_zero);
-  }
-  if (looped) {  // the (row, level) items the level-looped scatter could not stage
-    const int64_t items = w.n_sb * L;
-    hipLaunchKernelGGL((k_bwd_scatter_overflow<PosFn, GradFn>), dim3((unsigned)(items < 2048 ? items : 2048)),
-                       dim3(kSB), kScatterLds, st, a, pos, n, grad, w, skip_zero);
   }
   if (flags & LNR_BWD_NO_ACCUM) LNR_RETURN_LAUNCH(who);  // accumulate later, by level range
   launch_accum(a, w, d, n, 0, d->n_levels, d_table, st);

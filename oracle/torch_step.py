@@ -161,3 +161,60 @@ def render_step(field, rays, S=2048):
         T = torch.cumprod(torch.cat([torch.ones(R, 1), 1 - alpha + 1e-10], -1), -1)
         hit = (T[:, 1:] <= 0.5) & (T[:, :-1] > 0.5)
         return torch.where(hit.any(-1), z.gather(1, hit.float().argmax(-1, keepdim=True))[:, 0], torch.zeros(R))
+
+
+def _sh4_torch(d):
+    """tcnn SphericalHarmonics degree 4 of unit directions d (R,3) (oracle/render.py sh4, in torch)."""
+    x, y, z = d[:, 0], d[:, 1], d[:, 2]
+    return torch.stack([torch.full_like(x, 0.28209479177387814), -0.48860251190291987 * y, 0.48860251190291987 * z,
+                        -0.48860251190291987 * x, 1.0925484305920792 * x * y, -1.0925484305920792 * y * z,
+                        0.94617469575755997 * z * z - 0.31539156525251999, -1.0925484305920792 * x * z,
+                        0.54627421529603959 * (x * x - y * y), 0.59004358992664352 * y * (-3 * x * x + y * y),
+                        2.8906114426405538 * x * y * z, 0.45704579946446572 * y * (1 - 5 * z * z),
+                        0.3731763325901154 * z * (5 * z * z - 3), 0.45704579946446572 * x * (1 - 5 * z * z),
+                        1.4453057213202769 * z * (x * x - y * y), 0.59004358992664352 * x * (-x * x + 3 * y * y)], 1)
+
+
+class TorchColor:
+    """The colour head (nerf_tcnn.py:40-52,80-95): HashGrid L16 T=2^19 + SH4 -> 48->64x4->3 MLP, sigmoid,
+    with torch.optim.Adam over its parameters (optimizer.py:541-688)."""
+
+    def __init__(self, n_hidden=4, table_init=1e-4, seed=1):
+        g = torch.Generator().manual_seed(seed)
+        self.grid = TorchField(log2_hashmap_size=19, table_init=table_init, seed=seed)
+        dims = [48] + [64] * n_hidden + [16]
+        self.mats = []
+        for i in range(len(dims) - 1):
+            a = math.sqrt(6.0 / (dims[i] + dims[i + 1]))
+            self.mats.append(((torch.rand(dims[i + 1], dims[i], generator=g) * 2 - 1) * a).requires_grad_())
+        self.opt = torch.optim.Adam([self.grid.table] + self.mats, lr=0.01)
+
+    def color(self, pos01, dirs):
+        h = torch.cat([self.grid.encode(pos01), _sh4_torch(dirs)], -1)
+        for m in self.mats[:-1]:
+            h = torch.relu(h @ m.t())
+        return torch.sigmoid((h @ self.mats[-1].t())[:, :3])
+
+
+def camera_step(field, color, rays, rgb_gt, S=512):
+    """One colour-head iteration (optimizer.py:541-688,861-894) in torch: OGM samples, the frozen sigma
+    field's compositing weights (no grad), the colour head on every sample, rgb = sum w c + 1 - sum w,
+    L1 loss, autograd backward through the colour MLP and colour grid, Adam.  Returns the loss."""
+    R = rays.shape[0]
+    with torch.no_grad():
+        z = sample_ogm(field, rays, S)
+        xyz = rays[:, None, 0:3] + rays[:, None, 3:6] * z[..., None]
+        pos = ((xyz + 1) / 2).reshape(-1, 3)
+        sig = field.sigma(pos).reshape(R, S)
+        d = torch.cat([z[:, 1:] - z[:, :-1], torch.full((R, 1), 1e10)], -1) * rays[:, 3:6].norm(dim=-1, keepdim=True)
+        alpha = 1 - torch.exp(-d * torch.relu(sig + torch.randn(R, S)))
+        T = torch.cumprod(torch.cat([torch.ones(R, 1), 1 - alpha + 1e-10], -1), -1)[:, :-1]
+        w = alpha * T
+    dirs = rays[:, 3:6].repeat_interleave(S, 0)
+    col = color.color(pos, dirs).reshape(R, S, 3)
+    rgb = (w[..., None] * col).sum(1) + (1 - w.sum(1, keepdim=True))
+    loss = (rgb - rgb_gt).abs().mean()
+    color.opt.zero_grad(set_to_none=True)
+    loss.backward()
+    color.opt.step()
+    return float(loss.detach())

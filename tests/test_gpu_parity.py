@@ -355,3 +355,66 @@ def test_adam_matches_torch_semantics(L):
         L.call("lnr_adam_step", (tq), None, (cu(gr)), (tm2), (tv2), 64, step, 0.01, 0.9, 0.999,
                1e-8, L.stream())
     np.testing.assert_allclose(host(tq), q.detach().numpy(), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("lvl", [3, 10])
+def test_hashgrid_bwd_record_dynamic_range(L, lvl):
+    """fp16 record values over a wide dynamic range (hashgrid.hpp "Record values").
+    One level's encoding gradient spans 2^-30 .. 1 (log-uniform, random signs) on unsorted positions (one
+    or two contributions per entry: no averaging).  The records hold w g 2^k in fp16 with 2^k = 2^9 / 2^E
+    (level max < 2^E), so a contribution above 2^-23 of the level maximum is a normal fp16 (relative
+    rounding 2^-11), below it a subnormal (absolute step 2^-24 scaled units) and below 2^-34 of it zero.
+    Per entry, against the fp64 oracle (oracle/hashgrid.encode_backward):
+      err <= 2^-11 sum|w g| + 2^-16 sum wyz |g| (tx as unorm16) + count 2^-25 2^-k (subnormal steps);
+    entries whose every contribution lies below the flush threshold are exactly 0, and entries above
+    2^-23 of the maximum meet the relative bar alone."""
+    rng = np.random.default_rng(40 + lvl)
+    n = 24000
+    pos = rng.uniform(0.0, 1.0, (n, 3)).astype(np.float32)
+    lay = ohg.GridLayout(16, 2, 18, 16)
+    d = L.grid_desc(16, 2, 18, 16)
+    denc = rng.normal(0, 1, (n, 32)).astype(np.float32)
+    mag = np.exp2(rng.uniform(-30.0, 0.0, (n, 2))) * rng.choice([-1.0, 1.0], (n, 2))
+    denc[:, 2 * lvl:2 * lvl + 2] = mag.astype(np.float32)
+    denc_lm = np.ascontiguousarray(denc.reshape(n, 16, 2).transpose(1, 0, 2))
+    nb = int(L.lib().lnr_hashgrid_bwd_workspace_bytes(ctypes.byref(d), n))
+    ws = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    gt = torch.zeros(lay.n_entries * 2, dtype=torch.float32, device="cuda")
+    L.call("lnr_hashgrid_bwd", ctypes.byref(d), cu(pos), n, cu(denc_lm), n, gt, ws, nb, 0, L.stream())
+    got = host(gt).reshape(-1, 2)
+    g = denc[:, 2 * lvl:2 * lvl + 2].astype(np.float64)
+    E = int(np.frexp(np.float32(np.abs(g).max()))[1])
+    k = 9 - E
+    w, idx = ohg.corner_weights_indices(pos, lay, lvl)
+    _, frac = ohg._corners(pos, lay, lvl)
+    size, off = lay.sizes[lvl], lay.offsets[lvl]
+    ref = np.zeros((size, 2))
+    ref_abs = np.zeros((size, 2))
+    yz_abs = np.zeros((size, 2))
+    cnt = np.zeros(size)
+    for c in range(8):
+        e = idx[:, c] - off
+        wyz = (frac[:, 1] if c & 2 else 1 - frac[:, 1]) * (frac[:, 2] if c & 4 else 1 - frac[:, 2])
+        np.add.at(ref, e, w[:, c:c + 1].astype(np.float64) * g)
+        np.add.at(ref_abs, e, w[:, c:c + 1].astype(np.float64) * np.abs(g))
+        np.add.at(yz_abs, e, wyz[:, None].astype(np.float64) * np.abs(g))
+        np.add.at(cnt, e, 1.0)
+    got_l = got[off:off + size].astype(np.float64)
+    bound = 1.01 * 2.0 ** -11 * ref_abs + 2.0 ** -16 * yz_abs + cnt[:, None] * 2.0 ** (-25 - k) + 1e-300
+    err = np.abs(got_l - ref)
+    assert np.all(err <= bound), (float((err / bound).max()), int((err > bound).sum()))
+    top = np.abs(g).max()
+    # every record value below the flush threshold (scaled value < 2^-25 rounds to fp16 zero): exactly 0.
+    # A fine level's pair record holds wyz g (the x weight applies in the accumulation): yz_abs bounds it
+    below = (ref_abs > 0) & (yz_abs * 2.0 ** k < 2.0 ** -25)
+    assert np.all(got_l[below] == 0.0)
+    # entries above 2^-23 of the level maximum: relative (fp16 rounding + tx quantisation) bar alone
+    big = ref_abs > 2.0 ** -23 * top
+    assert np.all(err[big] <= 1.01 * 2.0 ** -11 * ref_abs[big] + 2.0 ** -16 * yz_abs[big] + cnt[:, None].repeat(2, 1)[big]
+                  * 2.0 ** (-25 - k))
+    assert big.sum() > 1000 and ((ref_abs > 0) & ~big).sum() > 100 and below.sum() > 10  # every regime occurs
+    # other levels are untouched by the wide range: the usual relative L2 bar
+    gall = ohg.encode_backward(pos, denc, lay)
+    mask = np.ones(lay.n_entries, bool)
+    mask[off:off + size] = False
+    assert np.linalg.norm(got[mask] - gall[mask]) / np.linalg.norm(gall[mask]) < TABLE_GRAD_RTOL
