@@ -38,6 +38,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 TB/s measured copy)
 MFMA_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA (MI355X_MICROARCH.md; sparsity figures excluded)
 MLP_FLOP_PER_SAMPLE = 12672  # sigma MLP 32->64->1(16): fwd 2*(32*64 + 64*1) = 4224, bwd 2x
+PROF_STEPS = 20  # untimed steps with per-stage HIP events, after the timed region (two OGM updates)
 
 
 def parse():
@@ -325,9 +326,12 @@ def bench_render(args):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        run(args.warmup + i, True)
+        run(args.warmup + i, False)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    for i in range(PROF_STEPS):  # per-stage events, untimed
+        run(args.warmup + args.steps + i, True)
+    torch.cuda.synchronize()
     stage_ms = {k: float(np.mean([v[j].elapsed_time(v[j + 1]) for j in range(0, len(v), 2)])) for k, v in ev.items()}
     N = R * S
     # dominant kernel: the sigma-grid encode, 512 B/sample of gathers (the colour-grid encode skips
@@ -437,9 +441,11 @@ def bench_camera(args):
     t0 = time.perf_counter()
     n_tot = 0
     for i in range(args.steps):
-        n_tot += run(args.warmup + i, True)
+        n_tot += run(args.warmup + i, False)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    for i in range(PROF_STEPS):  # whole-iteration events, untimed
+        run(args.warmup + args.steps + i, True)
     # one extra profiled iteration split by stage (events between the engine's launches)
     stage_ms = _camera_stages(eng, fr, rays, inten, L)
     N = n_tot * S
@@ -641,11 +647,21 @@ def main():
                         loss=S_.LossConfig.from_dict(LOSS_PRESETS[preset]))
     state = S_.FieldState(cfg, device=dev)
     allreduce = None
+    zero, hooks = None, {}
+    # the sharded optimiser (ZeRO-1: reduce-scatter, Adam on 1/N of the parameters, all-gather of the fp16
+    # shadow) for the data-parallel step; LONER_ZERO=0 keeps the all-reduce + replicated Adam
+    use_zero = os.environ.get("LONER_ZERO", "1") != "0"
     if dist is not None and not replicas:
         def allreduce(t, async_op=False):
             return dist.all_reduce(t, async_op=async_op)
+        if use_zero and world in (2, 4, 8):
+            zero = (rank, world)
+            hooks = dict(reduce_scatter=lambda o, i, async_op=False: dist.reduce_scatter_tensor(o, i, async_op=async_op),
+                         all_gather=lambda o, i, async_op=False: dist.all_gather_into_tensor(o, i, async_op=async_op))
+    elif args.shard_of and use_zero:
+        zero = (0, args.shard_of)  # one rank's share of the sharded Adam, no exchange (world size 1)
     eng = S_.StepEngine(state, R, seed=12345 + (rank if replicas else 0), allreduce=allreduce,
-                        ray_offset=0 if replicas else rank * R)
+                        ray_offset=0 if replicas else rank * R, zero=zero, **hooks)
     r_glob = R if replicas else R * world
     if args.shard_of:
         r_glob = R * args.shard_of
@@ -663,10 +679,9 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    prof = {}
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
-        out = run(i, prof)
+        out = run(i)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist is not None:
@@ -677,6 +692,12 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     loss = out.cpu().numpy()
+    # per-stage HIP events in a separate pass after the timed region (recording them costs host time:
+    # 47 us per step at C1, where the host issues the step faster than the GPU runs it only without them)
+    prof = {}
+    for i in range(args.warmup + args.steps, args.warmup + args.steps + PROF_STEPS):
+        run(i, prof)
+    torch.cuda.synchronize()
     stage_ms = {k: float(np.mean([v[j].elapsed_time(v[j + 1]) for j in range(0, len(v), 2)])) for k, v in prof.items()}
 
     if rank != 0:
@@ -716,8 +737,9 @@ def main():
                                + f"L=16 T=2^18 hash grid + 64-wide sigma MLP, {preset} loss (L1_JS)",
                    "rays_per_gpu": R, "samples_per_ray": n_samples, "global_rays": R * world,
                    "parallelism": (f"replicas{world}" if replicas else f"dp{world}") if world > 1 else
-                   (f"shard 0 of {args.shard_of} (one rank's strong-scaling step, no collective)" if args.shard_of
-                    else "single"),
+                   (f"shard 0 of {args.shard_of} (one rank's strong-scaling step: its rays, its 1/{args.shard_of} "
+                    f"of the sharded Adam; no collective)" if args.shard_of else "single"),
+                   "optimizer": "sharded (ZeRO-1)" if zero is not None else "replicated",
                    **({"submap_rank0": submap} if submap is not None else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,

@@ -198,7 +198,11 @@ typedef struct lnr_loss_params {
                                 lnr_build_lidar_rays writes it) */
   uint32_t* dev_status;      /* optional DEVICE word: LNR_STATUS_* bits are OR-ed in (no host sync; the
                                 caller reads it when it chooses, e.g. once per window) */
+  float* dev_loss_out;       /* optional DEVICE [8]: lnr_field_train also writes lnr_loss_finalize's output
+                                here, in its last launch (one launch less per step) */
+  int32_t flags;             /* LNR_LP_* */
 } lnr_loss_params;
+#define LNR_LP_DW_OVERWRITE 1  /* lnr_field_train STORES d_w (the MLP gradient) instead of adding to it */
 
 /* Status bits (replace the reference's per-step host checks):
  *   LNR_STATUS_NAN_LOSS     loss is NaN: optimizer.py:854 asserts "NaN Loss Encountered"

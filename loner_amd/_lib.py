@@ -47,7 +47,10 @@ class LossParams(ctypes.Structure):
                 ("min_js", ctypes.c_float), ("max_js", ctypes.c_float), ("js_alpha", ctypes.c_float),
                 ("los_eps", ctypes.c_float), ("far_ref", ctypes.c_float), ("inv_n_opaque", ctypes.c_float),
                 ("inv_rs", ctypes.c_float), ("dev_n_opaque", ctypes.c_void_p), ("dev_far_ref", ctypes.c_void_p),
-                ("dev_status", ctypes.c_void_p)]
+                ("dev_status", ctypes.c_void_p), ("dev_loss_out", ctypes.c_void_p), ("flags", ctypes.c_int32)]
+
+
+LP_DW_OVERWRITE = 1
 
 
 STATUS_NAN_LOSS, STATUS_INF_LOSS, STATUS_SIGMA_CLIPPED, STATUS_NONFINITE_OUTPUT = 1, 2, 4, 8

@@ -391,7 +391,7 @@ __device__ __forceinline__ void mlp_forward_ray(const FieldArgs& a, const RaySha
   for (int tb = wid * per_wave; tb < (wid + 1) * per_wave; tb += 16) {
     const int64_t n = r * a.S + tb + c;
     half8_t b = load_enc_operand(a.enc, a.enc_stride, n, true);
-    float h[16];
+    SigmaHidden h;
     const float sg = sigma_tile_fwd(sw, b, h);
     if (g == 0) sh.sig[tb + c] = sigma_to_f16(sg);
     if (a.lp.dev_status && __any(!isfinite(round_f16(sg))) && lane == 0) atomicOr(a.lp.dev_status, LNR_STATUS_SIGMA_CLIPPED);
@@ -406,7 +406,7 @@ __device__ __forceinline__ void mlp_backward_ray(const FieldArgs& a, const RaySh
   _Float16* lds = sh.mlp + wid * (64 * 32 + 32 * 32);
   float2* denc = reinterpret_cast<float2*>(a.d_enc);
   for (int tb = wid * per_wave; tb < (wid + 1) * per_wave; tb += 32) {
-    float h0[16], h1[16];
+    SigmaHidden h0, h1;
     half8_t e0, e1;
     float ds0, ds1;
     {
@@ -729,7 +729,7 @@ __global__ void __launch_bounds__(NT) k_field_wave(FieldArgs a) {
   for (int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + wid; r < a.n_rays; r += (int64_t)gridDim.x * kWavesPerBlock) {
 #pragma unroll 8
     for (int tb = 0; tb < S; tb += 16) {
-      float h[16];
+      SigmaHidden h;
       const float sgm = sigma_tile_fwd(sw, load_enc_operand(a.enc, a.enc_stride, r * S + tb + c, true), h);
       if (g == 0) sig[tb + c] = sigma_to_f16(sgm);
       if (a.lp.dev_status && __any(!isfinite(round_f16(sgm))) && lane == 0) atomicOr(a.lp.dev_status, LNR_STATUS_SIGMA_CLIPPED);
@@ -760,7 +760,7 @@ __global__ void __launch_bounds__(NT) k_sigma_fwd_tiles(FieldArgs a) {
     for (int t = 0; t < 4; ++t) b[t] = load_enc_operand(a.enc, a.enc_stride, n0 + 16 * t + c, true);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      float h[16];
+      SigmaHidden h;
       const float sgm = sigma_tile_fwd(sw, b[t], h);
       if (g == 0) a.d_sigma[n0 + 16 * t + c] = sigma_to_f16(sgm);
       if (a.lp.dev_status && __any(!isfinite(round_f16(sgm))) && lane == 0) atomicOr(a.lp.dev_status, LNR_STATUS_SIGMA_CLIPPED);
@@ -797,57 +797,54 @@ __device__ __forceinline__ uint32_t pack_h2(float x, float y) {
 // Phase 2, tile-parallel: sigma MLP backward over 32-sample tile pairs (no per-ray structure):
 // d_enc (level-major float2) and the per-block dW slab.
 // (2 waves per SIMD at its 242 VGPRs; forcing 3 or 4 spills 45 / 116 VGPRs: 0.18 -> 0.56 / 0.76 ms)
+#ifndef LNR_MLP_BWD_WAVES
+#define LNR_MLP_BWD_WAVES 2  // waves per SIMD (3 spills 113 registers)
+#endif
 template <bool JAC>  // JAC: write d sigma / d enc (fp16 pairs) instead of d_enc
-__global__ void __launch_bounds__(NT) k_mlp_bwd_tiles(FieldArgs a) {
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(LNR_MLP_BWD_WAVES, LNR_MLP_BWD_WAVES))) k_mlp_bwd_tiles(FieldArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   _Float16* lds = reinterpret_cast<_Float16*>(smem) + wid * (64 * 32 + 32 * 32);
   SigmaWeights sw;
   load_sigma_weights(a.w, sw);
-  DW0Acc acc;
+  DW0Mfma acc;
+  acc.init();
   float dw1[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) dw1[k] = 0.f;
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) acc.v[t][m][q] = 0.f;
   float2* denc = reinterpret_cast<float2*>(a.d_enc);
   float lmax[4] = {0.f, 0.f, 0.f, 0.f};  // max |d_enc| of this lane's levels 2g, 2g + 1, 8 + 2g, 9 + 2g
   const int64_t N = a.n_rays * (int64_t)a.S;  // a multiple of 64
-  // software-pipelined: the next tile pair's enc / dsigma loads are in flight while this one computes
-  // (2 waves per SIMD at this register count: latency is hidden by ILP, not by occupancy)
+  // software-pipelined two tile pairs deep: the loads of the next two pairs (enc, dsigma) are in flight
+  // while this one computes (2 waves per SIMD at this register count: latency is hidden by ILP)
   const int64_t step = (int64_t)gridDim.x * kWavesPerBlock * 32;
   int64_t n0 = ((int64_t)blockIdx.x * kWavesPerBlock + wid) * 32;
-  const int gq = g;
-  uint32_t nx0[4], nx1[4];
-  float nds0 = 0.f, nds1 = 0.f;
-  auto prefetch = [&](int64_t m) {
+  struct Pre {
+    uint32_t x0[4], x1[4];
+    float d0, d1;
+  };
+  auto prefetch = [&](int64_t m, Pre& p) {
     const bool v = m < N;
     const int64_t mm = v ? m : 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      nx0[q] = a.enc[(int64_t)(4 * gq + q) * a.enc_stride + mm + c];
-      nx1[q] = a.enc[(int64_t)(4 * gq + q) * a.enc_stride + mm + 16 + c];
+      p.x0[q] = a.enc[(int64_t)(4 * g + q) * a.enc_stride + mm + c];
+      p.x1[q] = a.enc[(int64_t)(4 * g + q) * a.enc_stride + mm + 16 + c];
     }
-    nds0 = a.d_sigma[mm + c];
-    nds1 = a.d_sigma[mm + 16 + c];
+    p.d0 = a.d_sigma[mm + c];
+    p.d1 = a.d_sigma[mm + 16 + c];
   };
-  prefetch(n0);
-  for (; n0 < N; n0 += step) {
-    float h0[16], h1[16];
+  auto pair = [&](int64_t n0, const Pre& p) {
+    SigmaHidden h0, h1;
     half8_t e0, e1;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      e0[2 * q + 0] = __builtin_bit_cast(_Float16, (uint16_t)(nx0[q] & 0xFFFFu));
-      e0[2 * q + 1] = __builtin_bit_cast(_Float16, (uint16_t)(nx0[q] >> 16));
-      e1[2 * q + 0] = __builtin_bit_cast(_Float16, (uint16_t)(nx1[q] & 0xFFFFu));
-      e1[2 * q + 1] = __builtin_bit_cast(_Float16, (uint16_t)(nx1[q] >> 16));
+      e0[2 * q + 0] = __builtin_bit_cast(_Float16, (uint16_t)(p.x0[q] & 0xFFFFu));
+      e0[2 * q + 1] = __builtin_bit_cast(_Float16, (uint16_t)(p.x0[q] >> 16));
+      e1[2 * q + 0] = __builtin_bit_cast(_Float16, (uint16_t)(p.x1[q] & 0xFFFFu));
+      e1[2 * q + 1] = __builtin_bit_cast(_Float16, (uint16_t)(p.x1[q] >> 16));
     }
-    const float ds0 = nds0, ds1 = nds1;
-    prefetch(n0 + step);
+    const float ds0 = p.d0, ds1 = p.d1;
     (void)sigma_tile_fwd(sw, e0, h0);
     (void)sigma_tile_fwd(sw, e1, h1);
     float mx = 0.f;
@@ -858,7 +855,7 @@ __global__ void __launch_bounds__(NT) k_mlp_bwd_tiles(FieldArgs a) {
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fmaxf(fabsf((float)e0[j] * ds0), fabsf((float)e1[j] * ds1)));
-    const float scale = grad_scale(wave_max(mx));
+    const float pair_max = wave_max(mx);
     float d[2][4];
     sigma_tile_bwd_denc(sw, h0, d);
 #pragma unroll
@@ -890,10 +887,29 @@ __global__ void __launch_bounds__(NT) k_mlp_bwd_tiles(FieldArgs a) {
       lmax[2 * m] = fmaxf(lmax[2 * m], fmaxf(fabsf(q0.x), fabsf(q0.y)));
       lmax[2 * m + 1] = fmaxf(lmax[2 * m + 1], fmaxf(fabsf(q1.x), fabsf(q1.y)));
     }
-    dw0_pair(lds, sw, h0, h1, e0, e1, ds0, ds1, scale, acc);
+    dw0_pair_mfma(lds, h0, h1, e0, e1, ds0, ds1, pair_max, acc);
+  };
+  Pre pa, pb;
+  prefetch(n0, pa);
+  prefetch(n0 + step, pb);
+  for (; n0 < N; n0 += 2 * step) {
+    {
+      const Pre cur = pa;
+      prefetch(n0 + 2 * step, pa);
+      pair(n0, cur);
+    }
+    if (n0 + step < N) {  // (wave-uniform)
+      const Pre cur = pb;
+      prefetch(n0 + 3 * step, pb);
+      pair(n0 + step, cur);
+    }
   }
   __syncthreads();
-  write_dw_slab<NT>(reinterpret_cast<float*>(smem), acc, dw1, a.dw_slab + (int64_t)blockIdx.x * LNR_SIGMA_MLP_PARAMS);
+  {
+    DW0Acc out;
+    acc.finish(sw, out);
+    write_dw_slab<NT>(reinterpret_cast<float*>(smem), out, dw1, a.dw_slab + (int64_t)blockIdx.x * LNR_SIGMA_MLP_PARAMS);
+  }
   if (a.denc_max) {  // the level maxima (hash-grid backward record scales): 16-lane row max, then the block's
     __shared__ float bm[kWavesPerBlock][kSigmaLevels];
 #pragma unroll
@@ -937,15 +953,11 @@ static size_t bwd_tiles_smem_bytes() {
   return b < LNR_SIGMA_MLP_PARAMS * 4 ? LNR_SIGMA_MLP_PARAMS * 4 : b;
 }
 
-// dW += the per-workgroup slabs, fixed summation order (mlp.hpp reduce_slabs_fixed)
-__global__ void __launch_bounds__(64 * kSlabWaves) k_reduce_slabs(const float* __restrict__ slab, int nb, float* __restrict__ dw) {
-  reduce_slabs_fixed(slab, nb, dw);
-}
-
 constexpr int kReduceThreads = 1024;  // single-workgroup reductions over rays: latency, not bandwidth
 
-__global__ void __launch_bounds__(kReduceThreads) k_loss_finalize(const float* __restrict__ st, int64_t n,
-                                                                  lnr_loss_params lp, float* out) {
+// lnr_loss_finalize's body (one workgroup of kReduceThreads): per-ray partials -> the loss scalars
+__device__ __forceinline__ void loss_finalize_block(const float* __restrict__ st, int64_t n, const lnr_loss_params& lp,
+                                                    float* out) {
   __shared__ float red[5 * kReduceThreads / 64];
   double a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0;
   for (int64_t r = threadIdx.x; r < n; r += blockDim.x) {
@@ -974,6 +986,24 @@ __global__ void __launch_bounds__(kReduceThreads) k_loss_finalize(const float* _
     out[4] = oterm;
     out[5] = v[4];
   }
+}
+
+// dW (+)= the per-workgroup slabs, fixed summation order (mlp.hpp reduce_slabs_fixed).  With
+// lp.dev_loss_out, one more workgroup (the last) finalizes the loss from the per-ray partials.
+static_assert(64 * kSlabWaves == kReduceThreads, "the loss-finalize workgroup shares the launch shape");
+__global__ void __launch_bounds__(64 * kSlabWaves) k_reduce_slabs(const float* __restrict__ slab, int nb, float* __restrict__ dw,
+                                                                  bool overwrite, const float* __restrict__ ray_stats,
+                                                                  int64_t n_rays, lnr_loss_params lp) {
+  if (blockIdx.x == (LNR_SIGMA_MLP_PARAMS + 63) / 64) {
+    loss_finalize_block(ray_stats, n_rays, lp, lp.dev_loss_out);
+    return;
+  }
+  reduce_slabs_fixed(slab, nb, dw, overwrite);
+}
+
+__global__ void __launch_bounds__(kReduceThreads) k_loss_finalize(const float* __restrict__ st, int64_t n,
+                                                                  lnr_loss_params lp, float* out) {
+  loss_finalize_block(st, n, lp, out);
 }
 
 static int chunk_for(int S) {
@@ -1161,7 +1191,9 @@ extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t e
                          enc_stride, n_rays * (int64_t)n_samples, d_enc_level_max);
     }
   }
-  hipLaunchKernelGGL(k_reduce_slabs, dim3((LNR_SIGMA_MLP_PARAMS + 63) / 64), dim3(64 * kSlabWaves), 0, st, workspace, nb, d_w);
+  const int nred = (LNR_SIGMA_MLP_PARAMS + 63) / 64 + (lp->dev_loss_out ? 1 : 0);
+  hipLaunchKernelGGL(k_reduce_slabs, dim3(nred), dim3(64 * kSlabWaves), 0, st, workspace, nb, d_w,
+                     (lp->flags & LNR_LP_DW_OVERWRITE) != 0, ray_stats, n_rays, *lp);
   LNR_RETURN_LAUNCH("lnr_field_train(reduce)");
 }
 

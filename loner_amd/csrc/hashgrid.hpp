@@ -24,7 +24,8 @@ constexpr int kMaxBuckets = 2048;
 // The accumulation splits the records of a bucket range evenly over kAccumGroups workgroups (two
 // 64 KB-LDS workgroups per CU of the 256): each walks its own record range bucket by bucket, so
 // every CU does the same work whatever the bucket sizes.  A bucket cut by a range boundary leaves an
-// int64 partial chunk per piece (at most two per workgroup) that k_bwd_finalize adds exactly.
+// int64 partial chunk per piece (at most two per workgroup), added exactly by the last piece's
+// workgroup to arrive (or by k_bwd_finalize).
 constexpr int kAccumGroups = 512;
 
 struct GridArgs {
@@ -447,6 +448,7 @@ struct BwdWorkspace {
   uint32_t* counts;      // [kMaxBuckets]
   uint64_t* seg_start;   // [kMaxBuckets + 1]
   long long* partial;    // [2 kAccumGroups][2 * kChunk] int64 fixed-point partial sums of cut buckets
+  uint32_t* bucket_done; // [kMaxBuckets] pieces of a cut bucket accumulated so far (k_bwd_accum<true>)
   uint2* rec;            // [8 * N * L] records {word, half2} (see "Backward records")
   int64_t n_sb;
   int64_t n_chunks;
@@ -458,7 +460,7 @@ inline int64_t bwd_n_chunks(int64_t n) { return (bwd_n_sb(n) + kRowsPerChunk - 1
 inline int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
 
 struct WsLayout {
-  int64_t hist, chunk_sum, level_max, counts, seg_start, partial, rec, total;
+  int64_t hist, chunk_sum, level_max, counts, seg_start, partial, bucket_done, rec, total;
 };
 
 inline WsLayout ws_layout(const lnr_grid_desc* d, const GridArgs& a, int64_t n) {
@@ -471,6 +473,7 @@ inline WsLayout ws_layout(const lnr_grid_desc* d, const GridArgs& a, int64_t n) 
   w.counts = b;    b += align256(kMaxBuckets * 4);
   w.seg_start = b; b += align256((kMaxBuckets + 1) * 8);
   w.partial = b;   b += align256((int64_t)2 * kAccumGroups * 2 * kChunk * 8);
+  w.bucket_done = b; b += align256(kMaxBuckets * 4);
   // +2 records: the accumulate loads records in pairs
   w.rec = b;       b += align256((8 * n * (int64_t)d->n_levels + 2) * 8);
   w.total = b;
@@ -489,6 +492,7 @@ inline BwdWorkspace carve_workspace(void* base, const GridArgs& a, const lnr_gri
   w.counts = reinterpret_cast<uint32_t*>(p + L.counts);
   w.seg_start = reinterpret_cast<uint64_t*>(p + L.seg_start);
   w.partial = reinterpret_cast<long long*>(p + L.partial);
+  w.bucket_done = reinterpret_cast<uint32_t*>(p + L.bucket_done);
   w.rec = reinterpret_cast<uint2*>(p + L.rec);
   w.n_sb = bwd_n_sb(n);
   w.n_chunks = bwd_n_chunks(n);

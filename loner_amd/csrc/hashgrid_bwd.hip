@@ -79,7 +79,18 @@ __global__ void __launch_bounds__(kMaxChunksPerLevel) k_bwd_scan_rows(GridArgs a
   if (c >= nb) return;
   const uint32_t* cs = ws.chunk_sum + (int64_t)l * ws.n_chunks * kMaxChunksPerLevel + c;
   uint32_t base = 0, tot = 0;  // the preceding chunks' sum; all chunks' (the bucket total, chunk 0)
-  const int64_t kend = ch == 0 ? ws.n_chunks : ch;
+  // one chunk (a small batch): no k_bwd_chunk_sums launch, the total is this chunk's own column sum
+  const int64_t kend = ws.n_chunks == 1 ? 0 : ch == 0 ? ws.n_chunks : ch;
+  if (ws.n_chunks == 1) {
+    const uint32_t* col = ws.hist + (int64_t)a.bucket_base[l] * ws.n_sb + c;
+    for (int64_t r = 0; r < ws.n_sb; r += 16) {
+      uint32_t v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = r + u < ws.n_sb ? col[(r + u) * nb] : 0u;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) tot += v[u];
+    }
+  }
   for (int64_t k = 0; k < kend; k += 16) {  // 16 loads in flight (L2 hits)
     uint32_t v[16];
 #pragma unroll
@@ -125,6 +136,8 @@ __global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint
   for (int w = 0; w < wid; ++w) bseg += w_seg[w];
   uint64_t e_seg = bseg + iseg - seg[0] - seg[1];  // exclusive value at this thread's first bucket
   if (t == 1023) ws.seg_start[n_buckets] = bseg + iseg;  // total (n_buckets may equal 2 * blockDim)
+  ws.bucket_done[2 * t] = 0u;  // k_bwd_accum<true>'s arrival counters (kMaxBuckets = 2 * blockDim)
+  ws.bucket_done[2 * t + 1] = 0u;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     if (2 * t + q < (int)n_buckets) ws.seg_start[2 * t + q] = e_seg;
@@ -660,6 +673,9 @@ __device__ __forceinline__ unsigned long long fixed_i64(float x) {
   return bits - 0x4338000000000000ull;
 }
 
+#ifndef LNR_SCATTER_ROWS_MIN
+#define LNR_SCATTER_ROWS_MIN 256
+#endif
 #ifndef LNR_ACCUM_BUCKETS_MAX_N
 #define LNR_ACCUM_BUCKETS_MAX_N (1 << 17)  // C1 (32 K samples): 103 -> 76 us for the backward stage; the C4 shard of 8 GPUs (590 K): 219 -> 229 us
 #endif
@@ -782,26 +798,51 @@ __device__ __forceinline__ void store_bucket(const unsigned long long* acc, cons
 // int64 fixed-point sums in a 64 KB LDS chunk with ds_add_u64, then the fp32 gradient (a whole
 // bucket) or the piece's int64 partial chunk (a bucket the range boundaries cut; partial slot 2i for
 // a piece cut at its start, 2i + 1 for one cut only at its end).
+// FINISH: a cut bucket is finished inside this kernel by the last of its pieces' workgroups to get
+// there (a per-bucket arrival counter, ws.bucket_done): it adds the other pieces' partial chunks into
+// its own LDS sums (int64: exact, so the arrival order does not matter) and stores the fp32 values;
+// the workgroup whose range holds an empty bucket's position stores its zeros.  Without FINISH,
+// k_bwd_finalize does both in a second launch.
+__device__ __forceinline__ void store_zero_bucket(const GridArgs& a, float* __restrict__ d_table, uint32_t b) {
+  const uint32_t l = level_of_bucket(a, b);
+  const uint32_t ent0 = (b - a.bucket_base[l]) * kChunk;
+  const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
+  float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0);
+  for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) dst[t] = 0.f;
+}
+
+template <bool FINISH>
 __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_accum(GridArgs a, BwdWorkspace ws, float* __restrict__ d_table,
                                                                                         uint32_t b_begin, uint32_t b_end) {
   __shared__ unsigned long long acc[2 * kChunk];  // int64 fixed point, one array per feature (8-B atomics
                                                   // on random entries spread over twice the bank pairs)
   __shared__ __attribute__((aligned(16))) uint2 stage[kTile];  // the tile's records, swizzled
-  const uint64_t r0 = ws.seg_start[b_begin], R = ws.seg_start[b_end] - r0;
+  const uint64_t r0 = ws.seg_start[b_begin], rtot = ws.seg_start[b_end], R = rtot - r0;
   const uint32_t gi = blockIdx.x;
+  if (FINISH && R == 0) {  // no records at all: workgroup 0 stores every bucket's zeros
+    if (gi == 0)
+      for (uint32_t b = b_begin; b < b_end; ++b) store_zero_bucket(a, d_table, b);
+    return;
+  }
   const uint64_t rbeg = range_at(r0, R, gi), rend = range_at(r0, R, gi + 1);
   if (rbeg >= rend) return;
-  uint32_t lo = b_begin, hi = b_end;  // the bucket holding record rbeg: seg_start[lo] <= rbeg < seg_start[lo + 1]
-  while (hi - lo > 1) {
+  // first bucket to visit: the one holding record rbeg, or (FINISH) the first empty one sitting at rbeg
+  uint32_t lo = b_begin, hi = b_end;  // FINISH: first b with seg_start[b] >= rbeg; else last with <= rbeg
+  while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (ws.seg_start[mid] <= rbeg) lo = mid;
+    if (FINISH ? ws.seg_start[mid] < rbeg : ws.seg_start[mid + 1] <= rbeg) lo = mid + 1;
     else hi = mid;
   }
+  if (FINISH && lo > b_begin && ws.seg_start[lo] > rbeg) --lo;  // rbeg strictly inside bucket lo - 1
   for (uint32_t b = lo; b < b_end; ++b) {
     const uint64_t s0 = ws.seg_start[b], s1 = ws.seg_start[b + 1];
-    if (s0 >= rend) break;
+    if (s0 >= rend && !(FINISH && s0 == rend && rend == rtot)) break;  // (the last range owns trailing empties)
+    if (s0 == s1) {  // empty bucket
+      if (FINISH) store_zero_bucket(a, d_table, b);  // owned: rbeg <= s0 < rend, or trailing
+      continue;
+    }
     const uint64_t beg = s0 > rbeg ? s0 : rbeg, end = s1 < rend ? s1 : rend;
-    if (beg >= end) continue;  // empty bucket: k_bwd_finalize writes its zeros
+    if (beg >= end) continue;
     const uint32_t l = level_of_bucket(a, b);
     const uint32_t ent0 = (b - a.bucket_base[l]) * kChunk;
     const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
@@ -813,9 +854,45 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
     lds_barrier();
     if (beg == s0 && end == s1) {  // the whole bucket: the final values
       store_bucket(acc, a, ws, d_table, l, ent0, nent, k2);
-    } else {  // this piece's int64 partial chunk
-      long long* dst = ws.partial + (int64_t)(2 * gi + (beg > s0 ? 0 : 1)) * (2 * kChunk);
-      for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) dst[t] = (long long)acc[(t & 1) * kChunk + (t >> 1)];
+      lds_barrier();
+      continue;
+    }
+    // this piece's int64 partial chunk
+    long long* dst = ws.partial + (int64_t)(2 * gi + (beg > s0 ? 0 : 1)) * (2 * kChunk);
+    for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) dst[t] = (long long)acc[(t & 1) * kChunk + (t >> 1)];
+    if (FINISH) {
+      // in-launch hand-off (cdna_hip_programming.md, split-K reduction recipe): every storing wave
+      // drains its stores, the workgroup meets, ONE lane releases at agent scope and takes a ticket;
+      // the last arriver's lane acquires at agent scope before its workgroup reads the other chunks
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const uint32_t g0 = group_of(r0, R, s0), g1 = group_of(r0, R, s1 - 1);
+      if (threadIdx.x == 0) {
+        uint32_t pieces = 0;  // groups with a non-empty range inside the bucket
+        for (uint32_t g = g0; g <= g1; ++g) pieces += range_at(r0, R, g) < range_at(r0, R, g + 1) ? 1u : 0u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t old = __hip_atomic_fetch_add(&ws.bucket_done[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = old + 1 == pieces;
+        if (last) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        stage[0].x = last ? 1u : 0u;  // (the tile stage is idle here: no second LDS object, which would
+                                      // push the workgroup past 80 KB and halve the residency)
+      }
+      __syncthreads();
+      if (stage[0].x) {  // the last piece: add the others' partial chunks, store the fp32 values
+        for (uint32_t g = g0; g <= g1; ++g) {
+          const uint64_t gb = range_at(r0, R, g);
+          if (g == gi || gb >= range_at(r0, R, g + 1)) continue;
+          const long long* src = ws.partial + (int64_t)(2 * g + (gb > s0 ? 0 : 1)) * (2 * kChunk);
+          for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x)
+            acc[(t & 1) * kChunk + (t >> 1)] += (unsigned long long)src[t];
+        }
+        lds_barrier();
+        store_bucket(acc, a, ws, d_table, l, ent0, nent, k2);
+      }
     }
     lds_barrier();
   }
@@ -909,6 +986,19 @@ static int64_t accum_buckets_max_n() {
   return e ? (int64_t)atoll(e) : (int64_t)LNR_ACCUM_BUCKETS_MAX_N;
 }
 
+// Rows (512-sample histogram rows) from which the scatter takes the level-looped kernel;
+// LONER_SCATTER_ROWS_MIN overrides it (read at every launch).
+static int64_t scatter_rows_min() {
+  const char* e = getenv("LONER_SCATTER_ROWS_MIN");
+  return e ? (int64_t)atoll(e) : (int64_t)LNR_SCATTER_ROWS_MIN;
+}
+
+// 1 (default): cut buckets are finished inside k_bwd_accum; 0: by k_bwd_finalize (LONER_ACCUM_FINISH)
+static bool accum_finish() {
+  const char* e = getenv("LONER_ACCUM_FINISH");
+  return e ? atoi(e) != 0 : true;
+}
+
 // Accumulate + finalize the buckets of levels [l0, l1): their slice of d_table becomes final.
 static void launch_accum(const GridArgs& a, const BwdWorkspace& w, const lnr_grid_desc* d, int64_t n, uint32_t l0,
                          uint32_t l1, float* d_table, hipStream_t st) {
@@ -918,8 +1008,11 @@ static void launch_accum(const GridArgs& a, const BwdWorkspace& w, const lnr_gri
     hipLaunchKernelGGL(k_bwd_accum_buckets, dim3(b1 - b0), dim3(kAccumThreads), 0, st, a, w, d_table, b0, b1);
     return;
   }
-  hipLaunchKernelGGL(k_bwd_accum, dim3(kAccumGroups), dim3(kAccumThreads), 0, st,
-                     a, w, d_table, b0, b1);
+  if (accum_finish()) {  // cut buckets finished by their last piece's workgroup: no finalize launch
+    hipLaunchKernelGGL(k_bwd_accum<true>, dim3(kAccumGroups), dim3(kAccumThreads), 0, st, a, w, d_table, b0, b1);
+    return;
+  }
+  hipLaunchKernelGGL(k_bwd_accum<false>, dim3(kAccumGroups), dim3(kAccumThreads), 0, st, a, w, d_table, b0, b1);
   hipLaunchKernelGGL(k_bwd_finalize, dim3(b1 - b0), dim3(kFinalizeThreads), 0, st, a, w, d_table, b0, b1);
 }
 
@@ -945,7 +1038,8 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, Gra
                 who);
     hipLaunchKernelGGL(k_denc_level_max<GradFn>, dim3(kMaxBlocks, d->n_levels), dim3(256), 0, st, grad, n, w);
   }
-  hipLaunchKernelGGL(k_bwd_chunk_sums, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
+  if (w.n_chunks > 1)
+    hipLaunchKernelGGL(k_bwd_chunk_sums, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
   hipLaunchKernelGGL(k_bwd_scan_rows, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
   hipLaunchKernelGGL(k_bwd_scan_buckets, dim3(1), dim3(1024), 0, st, w, a.n_buckets);
   const uint32_t m = a.merge_levels, L = d->n_levels;
@@ -959,7 +1053,10 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, Gra
   // the reference's sigma grid (16 levels, base 16, scale 2, 2^18 entries): the level-looped scatter
   // plus the pass over the rows it could not stage; other grids (the colour grid's 2^19 levels have
   // 128 chunks): one workgroup per (row, level)
-  const bool rows = L == 16 && all_fine && pow2 && 8 * n * (int64_t)L + 2 < (int64_t(1) << 32);
+  // A small batch has too few rows for the level-looped kernel to fill the chip (C1: 64 rows, one
+  // workgroup each walking 16 levels in sequence): one workgroup per (row, level) instead.
+  const bool rows = L == 16 && all_fine && pow2 && 8 * n * (int64_t)L + 2 < (int64_t(1) << 32) &&
+                    w.n_sb >= scatter_rows_min();
   if (rows && m >= 3 && m <= 7 && maxnb <= 64) {
     auto kern = m == 3   ? k_bwd_scatter_rows<PosFn, GradFn, 16, 3, 64>
                 : m == 4 ? k_bwd_scatter_rows<PosFn, GradFn, 16, 4, 64>

@@ -17,7 +17,7 @@ __global__ void __launch_bounds__(256) k_sigma_mlp_fwd(const uint16_t* __restric
     const int64_t s = tile * 16 + c;
     const bool valid = s < n;
     half8_t b = load_enc_operand(enc, stride, s, valid);
-    float h[16];
+    SigmaHidden h;
     const float sg = sigma_tile_fwd(sw, b, h);
     if (g == 0 && valid) sigma[s] = f2h(sigma_to_f16(sg));
   }
@@ -51,7 +51,7 @@ __global__ void __launch_bounds__(256) k_sigma_mlp_bwd(const uint16_t* __restric
     const bool v0 = s0 < n, v1 = s1 < n;
     half8_t e0 = load_enc_operand(enc, stride, s0, v0);
     half8_t e1 = load_enc_operand(enc, stride, s1, v1);
-    float h0[16], h1[16];
+    SigmaHidden h0, h1;
     (void)sigma_tile_fwd(sw, e0, h0);
     (void)sigma_tile_fwd(sw, e1, h1);
     const float ds0 = v0 ? dsig[s0] : 0.f, ds1 = v1 ? dsig[s1] : 0.f;

@@ -18,7 +18,15 @@ namespace lnr {
 struct SigmaWeights {
   half8_t a0[4];     // layer-0 A operand per hid tile t: W0[16t + (l&15)][8g + j]
   half8_t bt[2][2];  // backward A operand [in tile m][k-step s]: W0[hid(s,g,j)][16m + (l&15)]
-  float w1[16];      // W1[0][16t + 4g + r] at index 4t + r
+  half8_t w1h[2];    // W1[0][16t + 4g + r] at index k = 4t + r, as fp16 (the weight's own precision)
+  __device__ __forceinline__ float w1(int k) const { return (float)w1h[k >> 3][k & 7]; }
+};
+
+// The hidden layer of one 16-sample tile, fp16 (tcnn stores it so): h[k] = relu(H)[hid 16t + 4g + r][sample
+// l&15] at k = 4t + r, as packed halves (8 registers, not 16)
+struct SigmaHidden {
+  half8_t q[2];
+  __device__ __forceinline__ float operator[](int k) const { return (float)q[k >> 3][k & 7]; }
 };
 
 __device__ __forceinline__ int hid_perm(int s, int g, int j) { return 32 * s + 16 * (j >> 2) + 4 * g + (j & 3); }
@@ -42,7 +50,8 @@ __device__ __forceinline__ void load_sigma_weights(const uint16_t* __restrict__ 
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) sw.w1[4 * t + r] = h2f(w1[16 * t + 4 * g + r]);
+    for (int r = 0; r < 4; ++r)
+      sw.w1h[(4 * t + r) >> 3][(4 * t + r) & 7] = __builtin_bit_cast(_Float16, w1[16 * t + 4 * g + r]);
 }
 
 // B operand of the forward product for sample n (lane column): features 8g..8g+7 = levels 4g..4g+3.
@@ -61,7 +70,7 @@ __device__ __forceinline__ half8_t load_enc_operand(const uint32_t* __restrict__
 
 // Forward of one 16-sample tile.  h[4t+r] = fp16(relu(H))[hid 16t+4g+r][sample l&15];
 // returns sigma for sample l&15 (fp32 accumulate of fp16 operands, NOT yet rounded).
-__device__ __forceinline__ float sigma_tile_fwd(const SigmaWeights& sw, const half8_t& benc, float (&h)[16]) {
+__device__ __forceinline__ float sigma_tile_fwd(const SigmaWeights& sw, const half8_t& benc, SigmaHidden& h) {
   float part = 0.f;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -69,9 +78,9 @@ __device__ __forceinline__ float sigma_tile_fwd(const SigmaWeights& sw, const ha
     acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(sw.a0[t], benc, acc, 0, 0, 0);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float v = round_f16(fmaxf(acc[r], 0.f));
-      h[4 * t + r] = v;
-      part = fmaf(sw.w1[4 * t + r], v, part);
+      const _Float16 v16 = (_Float16)fmaxf(acc[r], 0.f);
+      h.q[(4 * t + r) >> 3][(4 * t + r) & 7] = v16;
+      part = fmaf(sw.w1(4 * t + r), (float)v16, part);
     }
   }
   part += __shfl_xor(part, 16, 64);
@@ -101,15 +110,12 @@ __device__ __forceinline__ float grad_scale(float maxabs) {
 // Backward of one tile for d_sigma = 1: dH^T[hid][s] = w1[hid] * (h > 0) is exact in fp16, so the
 // MFMA result is exact up to fp32 accumulation; the caller multiplies by the sample's d_sigma.
 // d[m][r] = dEnc[sample l&15][in 16m + 4g + r] / d_sigma.
-__device__ __forceinline__ void sigma_tile_bwd_denc(const SigmaWeights& sw, const float (&h)[16], float (&d)[2][4]) {
-  half8_t b[2];
+__device__ __forceinline__ void sigma_tile_bwd_denc(const SigmaWeights& sw, const SigmaHidden& h, float (&d)[2][4]) {
+  half8_t b[2];  // (k-step s, j) holds hidden unit k = 8 s + j: mask * w1 in one select per half
 #pragma unroll
   for (int s = 0; s < 2; ++s)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 4 * (2 * s + (j >> 2)) + (j & 3);
-      b[s][j] = (_Float16)((h[k] > 0.f) ? sw.w1[k] : 0.f);
-    }
+    for (int j = 0; j < 8; ++j) b[s][j] = h.q[s][j] > (_Float16)0.f ? sw.w1h[s][j] : (_Float16)0.f;
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     float4_t acc = {0.f, 0.f, 0.f, 0.f};
@@ -126,8 +132,8 @@ struct DW0Acc {
   float v[4][2][4];
 };
 
-__device__ __forceinline__ void dw0_pair(_Float16* __restrict__ lds, const SigmaWeights& sw, const float (&h0)[16],
-                                         const float (&h1)[16], const half8_t& e0, const half8_t& e1, float ds0,
+__device__ __forceinline__ void dw0_pair(_Float16* __restrict__ lds, const SigmaWeights& sw, const SigmaHidden& h0,
+                                         const SigmaHidden& h1, const half8_t& e0, const half8_t& e1, float ds0,
                                          float ds1, float scale, DW0Acc& acc) {
   // dW0[hid][in] = w1[hid] * sum_s mask[hid][s] * (ds_s * Enc[s][in]); the mask operand is exact,
   // ds_s * Enc is lifted by a per-pair power of two for the fp16 operand.
@@ -163,8 +169,86 @@ __device__ __forceinline__ void dw0_pair(_Float16* __restrict__ lds, const Sigma
       float4_t d = {0.f, 0.f, 0.f, 0.f};
       d = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[t], b[m], d, 0, 0, 0);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc.v[t][m][r] = fmaf(d[r], sw.w1[4 * t + r] * inv, acc.v[t][m][r]);
+      for (int r = 0; r < 4; ++r) acc.v[t][m][r] = fmaf(d[r], sw.w1(4 * t + r) * inv, acc.v[t][m][r]);
     }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+}
+
+// dW0 accumulated in the MFMA accumulators themselves (C operand), at a running power-of-two operand
+// scale 2^kc that only decreases: a pair whose ds * Enc needs a smaller scale first rescales the sums
+// (exact: a power of two).  No per-pair fp32 FMAs and no per-pair result registers; w1 and 2^-kc are
+// applied once, in finish().  Pairs whose ds are all zero add nothing and are skipped.
+struct DW0Mfma {
+  float4_t v[4][2];
+  int kc;  // running exponent (kUnset before the first non-zero pair)
+  static constexpr int kUnset = 1 << 20;
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int m = 0; m < 2; ++m) v[t][m] = float4_t{0.f, 0.f, 0.f, 0.f};
+    kc = kUnset;
+  }
+  // acc.v[t][m][r] * w1[4t + r] * 2^-kc: dW0[16t + 4g + r][16m + (l&15)], as DW0Acc for write_dw_slab
+  __device__ __forceinline__ void finish(const SigmaWeights& sw, DW0Acc& out) const {
+    const float inv = kc == kUnset ? 0.f : ldexpf(1.f, -kc);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out.v[t][m][r] = v[t][m][r] * (sw.w1(4 * t + r) * inv);
+  }
+};
+
+__device__ __forceinline__ void dw0_pair_mfma(_Float16* __restrict__ lds, const SigmaHidden& h0, const SigmaHidden& h1,
+                                              const half8_t& e0, const half8_t& e1, float ds0, float ds1, float maxabs,
+                                              DW0Mfma& acc) {
+  if (!(maxabs > 0.f) || !isfinite(maxabs)) return;  // (wave-uniform) nothing to add
+  int e;
+  frexpf(maxabs, &e);
+  int k = 13 - e;
+  k = k > 100 ? 100 : (k < -100 ? -100 : k);
+  if (k < acc.kc) {  // a larger pair: the sums so far move to the smaller scale
+    if (acc.kc != DW0Mfma::kUnset) {
+      const float f = ldexpf(1.f, k - acc.kc);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) acc.v[t][m] *= f;
+    }
+    acc.kc = k;
+  }
+  const float scale = ldexpf(1.f, acc.kc);
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  _Float16* mk = lds;             // [64 hid][32 samples] ReLU mask
+  _Float16* ens = lds + 64 * 32;  // [32 in][32 samples] scaled ds * Enc
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kk = 8 * q + j, hid = 16 * (kk >> 2) + 4 * g + (kk & 3);
+      mk[hid * 32 + c] = h0.q[q][j] > (_Float16)0.f ? (_Float16)1.f : (_Float16)0.f;
+      mk[hid * 32 + 16 + c] = h1.q[q][j] > (_Float16)0.f ? (_Float16)1.f : (_Float16)0.f;
+    }
+  const float s0 = ds0 * scale, s1 = ds1 * scale;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ens[(8 * g + j) * 32 + c] = (_Float16)((float)e0[j] * s0);
+    ens[(8 * g + j) * 32 + 16 + c] = (_Float16)((float)e1[j] * s1);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-local hand-off through LDS
+  __builtin_amdgcn_wave_barrier();
+  half8_t a[4], b[2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) a[t] = *reinterpret_cast<const half8_t*>(mk + (16 * t + c) * 32 + 8 * g);
+#pragma unroll
+  for (int m = 0; m < 2; ++m) b[m] = *reinterpret_cast<const half8_t*>(ens + (16 * m + c) * 32 + 8 * g);
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int m = 0; m < 2; ++m) acc.v[t][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[t], b[m], acc.v[t][m], 0, 0, 0);
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
 }
@@ -208,11 +292,12 @@ __device__ __forceinline__ void write_dw_slab(float* __restrict__ red, const DW0
 }
 
 
-// dW[i] += sum over the nb per-workgroup slabs of slab[b][i], in a FIXED order (bitwise
+// dW[i] += (or, overwrite, =) the sum over the nb per-workgroup slabs of slab[b][i], in a FIXED order (bitwise
 // reproducible): workgroup x owns 64 consecutive i, each of its kSlabWaves waves sums a contiguous
 // range of slabs (256-B coalesced rows), then the wave partials are added in wave order.
 constexpr int kSlabWaves = 16;
-__device__ __forceinline__ void reduce_slabs_fixed(const float* __restrict__ slab, int nb, float* __restrict__ dw) {
+__device__ __forceinline__ void reduce_slabs_fixed(const float* __restrict__ slab, int nb, float* __restrict__ dw,
+                                                   bool overwrite = false) {
   __shared__ float part[kSlabWaves][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + lane;
@@ -236,7 +321,7 @@ __device__ __forceinline__ void reduce_slabs_fixed(const float* __restrict__ sla
     float t = 0.f;
 #pragma unroll
     for (int w = 0; w < kSlabWaves; ++w) t += part[w][lane];
-    dw[i] += t;
+    dw[i] = overwrite ? t : dw[i] + t;
   }
 }
 

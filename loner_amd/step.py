@@ -159,7 +159,7 @@ class StepEngine:
     """Preallocated workspaces for a fixed ray-batch size; ``step`` runs one optimiser step."""
 
     def __init__(self, state: FieldState, n_rays: int, seed: int = 0, allreduce=None, ray_offset: int = 0,
-                 count_in_forward: bool = True):
+                 count_in_forward: bool = True, zero=None, reduce_scatter=None, all_gather=None):
         self.state = state
         self.cfg = state.cfg
         self.n_rays = n_rays
@@ -195,6 +195,31 @@ class StepEngine:
         # semantics), or None
         self.allreduce = allreduce
         dev = state.device
+        # Sharded optimiser (ZeRO-1): zero = (rank, world).  Each level range's gradient slice is
+        # reduce-scattered instead of all-reduced (reduce_scatter(out, inp, async_op), the semantics of
+        # torch.distributed.reduce_scatter_tensor), the rank runs Adam on its 1/world chunk of every range,
+        # and the updated fp16 shadow chunks are all-gathered (all_gather(out, inp, async_op), as
+        # all_gather_into_tensor).  The fp32 master and the moments stay current only on each chunk's
+        # owner: sync_master() all-gathers the master (checkpoints).  With zero but no collectives (one
+        # process), the step does one rank's share of Adam and nothing else: the per-rank work of an
+        # N-GPU run, for measuring it on one GPU (bench.py --shard-of).
+        self.zero = None
+        if zero is not None:
+            zr, zw = int(zero[0]), int(zero[1])
+            if not 0 <= zr < zw:
+                raise ValueError(f"zero=(rank, world) out of range: {zero}")
+            self.zero = (zr, zw)
+            self.reduce_scatter, self.all_gather = reduce_scatter, all_gather
+            if zw > 1 and allreduce is not None and (reduce_scatter is None or all_gather is None):
+                raise ValueError("a sharded optimiser over ranks needs reduce_scatter and all_gather hooks")
+            self.zero_chunks = []  # per level range: (a0, a1, chunk), this rank owning [a0 + r c, a0 + (r+1) c)
+            for l0, l1 in self.ar_groups:
+                a0, a1 = self._ar_range(l0, l1)
+                if (a1 - a0) % (4 * zw):
+                    raise ValueError(f"levels [{l0}, {l1}) hold {a1 - a0} parameters, not a multiple of 4 x {zw} ranks "
+                                     "(the sharded optimiser needs equal, 16-B aligned chunks)")
+                self.zero_chunks.append((a0, a1, (a1 - a0) // zw))
+            self.zero_grad = [torch.empty(c, dtype=torch.float32, device=dev) for _, _, c in self.zero_chunks]
         self.z = torch.empty(n_rays, self.S, dtype=torch.float32, device=dev)
         self.enc = torch.empty(self.cfg.n_levels, self.N, dtype=torch.int32, device=dev)
         self.ws = torch.empty(L.lib().lnr_field_train_workspace_words(n_rays, self.S), dtype=torch.float32, device=dev)
@@ -241,6 +266,10 @@ class StepEngine:
         lp.dev_n_opaque = self.n_opaque.data_ptr()
         lp.dev_far_ref = None if dev_far_ref is None else dev_far_ref.data_ptr()
         lp.dev_status = self.status.data_ptr()
+        # lnr_field_train stores the MLP gradient (no zeroing launch) and finalizes the loss scalars
+        # into loss_out in its last launch (no lnr_loss_finalize launch)
+        lp.dev_loss_out = self.loss_out.data_ptr()
+        lp.flags = L.LP_DW_OVERWRITE
         return lp
 
     def check_status(self, clear=True):
@@ -257,6 +286,22 @@ class StepEngine:
         if bits & L.STATUS_NAN_LOSS:
             raise RuntimeError("NaN Loss Encountered")
         return bits
+
+    def _ar_range(self, l0, l1):
+        """[a0, a1) of level range [l0, l1) in the flat parameter buffer (range 0 also holds the MLP)."""
+        st = self.state
+        a0 = 0 if l0 == 0 else st.n_mlp + 2 * int(st.desc.offset[l0])
+        return a0, st.n_mlp + 2 * int(st.desc.offset[l1])
+
+    def sync_master(self):
+        """Sharded optimiser: all-gather the fp32 master (and the Adam moments) chunks so every rank holds
+        the whole current state (e.g. before a checkpoint).  A no-op otherwise."""
+        if self.zero is None or self.zero[1] == 1 or self.all_gather is None:
+            return
+        st, (zr, zw) = self.state, self.zero
+        for a0, a1, c in self.zero_chunks:
+            for buf in (st.params, st.m, st.v):
+                self.all_gather(buf[a0:a1], buf[a0 + zr * c:a0 + (zr + 1) * c])
 
     def _allreduce_async(self, t):
         """``allreduce(t, async_op=True)`` when the hook supports it (torch.distributed's
@@ -316,8 +361,8 @@ class StepEngine:
             L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(st.desc), rays, self.z, R, S, st.table_f16, self.enc, N,
                    None, 0, s)
         m(prof, "encode")
-        # 4. fused field + loss + backward through compositing and MLP
-        st.grad_mlp.zero_()  # the MLP gradient accumulates; the table gradient is overwritten below
+        # 4. fused field + loss + backward through compositing and MLP (stores the MLP gradient, and the
+        # loss scalars into loss_out)
         if pending is not None:
             pending.wait()  # orders the current stream after the collective (no host sync)
         m(prof, "field")
@@ -329,6 +374,8 @@ class StepEngine:
         # 5. hash-grid backward
         m(prof, "grid_bwd")
         flags = (L.BWD_COUNTS_READY if self.count_in_forward else 0) | L.BWD_LEVEL_MAX_READY
+        if self.zero is not None:
+            return self._step_zero(rays, depth_gt, R, S, N, flags, s, scale, update_ogm, global_step, prof)
         if self.allreduce is None:
             self._grid_bwd(rays, R, S, N, flags, s)
             m(prof, "grid_bwd")
@@ -341,8 +388,7 @@ class StepEngine:
             for l0, l1 in self.ar_groups:
                 L.call("lnr_hashgrid_bwd_accum", L.ctypes.byref(st.desc), R * S, self.bwd_ws, self.bwd_ws_bytes, l0,
                        l1, st.grad_table, s)
-                a0 = 0 if l0 == 0 else st.n_mlp + 2 * int(st.desc.offset[l0])
-                a1 = st.n_mlp + 2 * int(st.desc.offset[l1])
+                a0, a1 = self._ar_range(l0, l1)
                 pending.append(self._allreduce_async(st.grad[a0:a1]))
             m(prof, "grid_bwd")
             m(prof, "allreduce")
@@ -356,9 +402,54 @@ class StepEngine:
         L.call("lnr_adam_step", st.params, st.shadow, st.grad, st.m, st.v, st.n_padded, st.adam_step,
                cfg.lr * self.lr_factor, 0.9, 0.999, 1e-8, s)
         m(prof, "adam")
-        # 8. loss scalars (device)
-        L.call("lnr_loss_finalize", self.stats, R, L.ctypes.byref(lp), self.loss_out, s)
-        # 9. OGM every N_iters_acc global steps (optimizer.py:466-469)
+        # 8. OGM every N_iters_acc global steps (optimizer.py:466-469)
+        if update_ogm is None:
+            update_ogm = (global_step % cfg.n_iters_acc == 0)
+        if update_ogm:
+            m(prof, "ogm")
+            self.ogm_update(rays, depth_gt, scale)
+            m(prof, "ogm")
+        return self.loss_out
+
+    def _step_zero(self, rays, depth_gt, R, S, N, flags, s, scale, update_ogm, global_step, prof):
+        """The step's tail with the sharded optimiser (see __init__): per level range, accumulate, then
+        reduce-scatter the range's gradient (asynchronous: the next range accumulates meanwhile); Adam on
+        this rank's chunk of every range; all-gather the fp16 shadow chunks."""
+        st, cfg, m = self.state, self.cfg, self._mark
+        zr, zw = self.zero
+        comm = self.allreduce is not None and zw > 1
+        if comm:
+            self._grid_bwd(rays, R, S, N, flags | L.BWD_NO_ACCUM, s)
+            pending = []
+            for (l0, l1), (a0, a1, c), out in zip(self.ar_groups, self.zero_chunks, self.zero_grad):
+                L.call("lnr_hashgrid_bwd_accum", L.ctypes.byref(st.desc), R * S, self.bwd_ws, self.bwd_ws_bytes, l0,
+                       l1, st.grad_table, s)
+                pending.append(self.reduce_scatter(out, st.grad[a0:a1], async_op=True))
+            m(prof, "grid_bwd")
+            m(prof, "allreduce")
+            for w in pending:
+                if w is not None:
+                    w.wait()
+            m(prof, "allreduce")
+        else:  # one process: this rank's share of the work only (no exchange)
+            self._grid_bwd(rays, R, S, N, flags, s)
+            m(prof, "grid_bwd")
+        st.adam_step += 1
+        m(prof, "adam")
+        for (a0, a1, c), g in zip(self.zero_chunks, self.zero_grad):
+            o = a0 + zr * c
+            grad = g if comm else st.grad[o:o + c]
+            L.call("lnr_adam_step", st.params[o:o + c], st.shadow[o:o + c], grad, st.m[o:o + c], st.v[o:o + c], c,
+                   st.adam_step, cfg.lr * self.lr_factor, 0.9, 0.999, 1e-8, s)
+        m(prof, "adam")
+        if comm:
+            m(prof, "allgather")
+            pending = [self.all_gather(st.shadow[a0:a1], st.shadow[a0 + zr * c:a0 + (zr + 1) * c], async_op=True)
+                       for a0, a1, c in self.zero_chunks]
+            for w in pending:
+                if w is not None:
+                    w.wait()
+            m(prof, "allgather")
         if update_ogm is None:
             update_ogm = (global_step % cfg.n_iters_acc == 0)
         if update_ogm:

@@ -81,3 +81,75 @@ def test_gloo_two_ranks_bucketed_async_allreduce(tmp_path):
     for a, b in [(0, st.n_mlp)] + [(st.n_mlp + 2 * int(st.desc.offset[l0]), st.n_mlp + 2 * int(st.desc.offset[l1]))
                                    for l0, l1 in eng.ar_groups]:
         assert np.linalg.norm(g0[a:b] - g_ref[a:b]) <= 1e-4 * np.linalg.norm(g_ref[a:b]) + 1e-12
+
+
+def _zero_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from loner_amd.shard import shard_range
+
+    def allreduce(t, async_op=False):
+        return dist.all_reduce(t, async_op=async_op)
+
+    hooks = dict(reduce_scatter=lambda o, i, async_op=False: dist.reduce_scatter_tensor(o, i, async_op=async_op),
+                 all_gather=lambda o, i, async_op=False: dist.all_gather_into_tensor(o, i, async_op=async_op))
+    for tag, zero in (("ar", None), ("zero", (rank, world))):
+        S_, syn, rays, dgt, st = _setup()
+        R = rays.shape[0]
+        s0, s1 = shard_range(R, rank, world)
+        eng = S_.StepEngine(st, s1 - s0, seed=9, allreduce=allreduce, ray_offset=s0, zero=zero,
+                            **(hooks if zero else {}))
+        for k in range(3):
+            eng.step(rays[s0:s1].contiguous(), dgt[s0:s1].contiguous(), global_step=9 + k, scale=syn.CUBES["forest"][0],
+                     far_ref=float(rays[0, -1]), n_rays_global=R)
+        eng.sync_master()
+        torch.cuda.synchronize()
+        np.save(os.path.join(out, f"{tag}_params{rank}.npy"), st.params.cpu().numpy())
+        np.save(os.path.join(out, f"{tag}_shadow{rank}.npy"), st.shadow.cpu().numpy())
+        np.save(os.path.join(out, f"{tag}_m{rank}.npy"), st.m.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_two_ranks_sharded_optimizer(tmp_path):
+    """ZeRO-1 (reduce-scatter of each level range's gradient, Adam on each rank's half, all-gather of the
+    fp16 shadow) gives the all-reduce path's parameters bit for bit, on both ranks, over 3 steps (one an
+    OGM step); after sync_master the fp32 master and the moments agree too."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_zero_worker, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=100)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    for what in ("params", "shadow", "m"):
+        ref = np.load(tmp_path / f"ar_{what}0.npy")
+        assert np.array_equal(ref, np.load(tmp_path / f"ar_{what}1.npy"))
+        for r in range(2):
+            assert np.array_equal(ref, np.load(tmp_path / f"zero_{what}{r}.npy")), (what, r)
+
+
+def test_sharded_optimizer_emulation_single_process():
+    """One process with zero=(0, N) and no collectives (bench.py --shard-of): Adam touches exactly this
+    rank's chunk of every level range, identically to the full Adam there."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    S_, syn, rays, dgt, st = _setup()
+    p0 = st.params.clone()
+    eng = S_.StepEngine(st, rays.shape[0], seed=9, zero=(0, 4))
+    eng.step(rays, dgt, global_step=3, scale=syn.CUBES["forest"][0], far_ref=float(rays[0, -1]))
+    S2, _, _, _, st2 = _setup()
+    eng2 = S2.StepEngine(st2, rays.shape[0], seed=9)
+    eng2.step(rays, dgt, global_step=3, scale=syn.CUBES["forest"][0], far_ref=float(rays[0, -1]))
+    torch.cuda.synchronize()
+    for a0, a1, c in eng.zero_chunks:
+        assert torch.equal(st.params[a0:a0 + c], st2.params[a0:a0 + c])
+        assert torch.equal(st.params[a0 + c:a1], p0[a0 + c:a1])  # the other ranks' chunks: untouched here

@@ -199,24 +199,29 @@ def _assert_accum_paths_equal(L, st, rays, eng, R, Sn, g_ref=None):
     gradient (and g_ref, when given); returns it."""
     import os
     s = L.stream()
-    old = os.environ.get("LONER_ACCUM_BUCKETS_MAX_N")
+    keys = ("LONER_ACCUM_BUCKETS_MAX_N", "LONER_ACCUM_FINISH")
+    old = {k: os.environ.get(k) for k in keys}
     out = []
     try:
-        for thr in ("0", str(1 << 40)):
-            os.environ["LONER_ACCUM_BUCKETS_MAX_N"] = thr
+        # record-balanced with in-kernel finishing (twice: arrival order varies), with k_bwd_finalize,
+        # and whole buckets
+        for thr, fin in (("0", "1"), ("0", "1"), ("0", "0"), (str(1 << 40), "1")):
+            os.environ["LONER_ACCUM_BUCKETS_MAX_N"], os.environ["LONER_ACCUM_FINISH"] = thr, fin
             g = torch.full((2 * st.n_entries,), float("nan"), dtype=torch.float32, device="cuda")  # all written
             L.call("lnr_hashgrid_bwd_rays_jac", L.ctypes.byref(st.desc), rays, eng.z, R, Sn, eng.d_jac, eng.d_sigma(),
                    R * Sn, g, eng.bwd_ws, eng.bwd_ws_bytes, 0, s)
             out.append(g)
-        assert torch.equal(out[0], out[1])
+        for g in out[1:]:
+            assert torch.equal(out[0], g)
         if g_ref is not None:
             assert torch.equal(out[0], g_ref)
         return out[0]
     finally:
-        if old is None:
-            os.environ.pop("LONER_ACCUM_BUCKETS_MAX_N", None)
-        else:
-            os.environ["LONER_ACCUM_BUCKETS_MAX_N"] = old
+        for k in keys:
+            if old[k] is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = old[k]
 
 
 def test_accum_paths_small_batch(L):

@@ -1,5 +1,5 @@
 # GPU box: A/B of an environment switch of tools/exp_kernels.py under rocprofv3 --stats.
-#   bash tools/exp_ab.sh VAR   -> gpurun_out/exp/VAR0, gpurun_out/exp/VAR1
+#   bash tools/experiments/exp_ab.sh VAR   -> gpurun_out/exp/VAR0, gpurun_out/exp/VAR1
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp

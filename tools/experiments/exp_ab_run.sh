@@ -1,9 +1,9 @@
-# GPU box: tools/exp_variants.sh, then the average time of the named kernels per variant.
-# Usage: bash tools/exp_ab_run.sh k_bwd_accum k_bwd_scatter_rows ...
+# GPU box: tools/experiments/exp_variants.sh, then the average time of the named kernels per variant.
+# Usage: bash tools/experiments/exp_ab_run.sh k_bwd_accum k_bwd_scatter_rows ...
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 rm -rf $R/gpurun_out/exp
-bash $R/tools/exp_variants.sh || exit 1
+bash $R/tools/experiments/exp_variants.sh || exit 1
 for d in $R/gpurun_out/exp/*/; do
   F=$(find $d -name '*kernel_stats.csv' | head -1)
   echo "== $(basename $d)"

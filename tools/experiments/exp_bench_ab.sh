@@ -1,6 +1,6 @@
 # GPU box: the bench (default config unless BENCH_ARGS) under rocprofv3 --kernel-trace --stats for the
 # default library and every variant under loner_amd/_lib/variants/, then the named kernels' average
-# time and the bench's ms/step per variant.  Usage: bash tools/exp_bench_ab.sh k_bwd_accum ...
+# time and the bench's ms/step per variant.  Usage: bash tools/experiments/exp_bench_ab.sh k_bwd_accum ...
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 rm -rf $R/gpurun_out/bab

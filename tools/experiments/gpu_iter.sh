@@ -1,5 +1,5 @@
 # GPU box, one iteration: the gpu suite (or the pytest selection given), the default bench, and the
-# bench under rocprofv3 --kernel-trace --stats (top kernels printed).  Usage: bash tools/gpu_iter.sh [TAG] [pytest args]
+# bench under rocprofv3 --kernel-trace --stats (top kernels printed).  Usage: bash tools/experiments/gpu_iter.sh [TAG] [pytest args]
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
