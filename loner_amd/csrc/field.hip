@@ -789,6 +789,16 @@ __global__ void __launch_bounds__(NT) k_composite_wave(FieldArgs a) {
   }
 }
 
+// Element access at a 32-bit byte offset from a (uniform) base pointer
+template <class T>
+__device__ __forceinline__ T ld_off(const T* base, uint32_t byte_off) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
+}
+template <class T>
+__device__ __forceinline__ void st_off(T* base, uint32_t byte_off, T v) {
+  *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + byte_off) = v;
+}
+
 // fp16 pair (round to nearest) in one word, low half first
 __device__ __forceinline__ uint32_t pack_h2(float x, float y) {
   return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)x) | ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)y) << 16);
@@ -797,16 +807,32 @@ __device__ __forceinline__ uint32_t pack_h2(float x, float y) {
 // Phase 2, tile-parallel: sigma MLP backward over 32-sample tile pairs (no per-ray structure):
 // d_enc (level-major float2) and the per-block dW slab.
 // (2 waves per SIMD at its 242 VGPRs; forcing 3 or 4 spills 45 / 116 VGPRs: 0.18 -> 0.56 / 0.76 ms)
+#ifndef LNR_MLP_PREFETCH
+#define LNR_MLP_PREFETCH 2  // tile pairs loaded ahead in k_mlp_bwd_tiles (1 or 2)
+#endif
+#ifndef LNR_MLP_W_LDS
+#define LNR_MLP_W_LDS 0  // the layer-0 weight operands in LDS instead of registers (k_mlp_bwd_tiles)
+#endif
 #ifndef LNR_MLP_BWD_WAVES
-#define LNR_MLP_BWD_WAVES 2  // waves per SIMD (3 spills 113 registers)
+#define LNR_MLP_BWD_WAVES 2  // waves per SIMD (3 spills 113 registers with the weights in registers)
 #endif
 template <bool JAC>  // JAC: write d sigma / d enc (fp16 pairs) instead of d_enc
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(LNR_MLP_BWD_WAVES, LNR_MLP_BWD_WAVES))) k_mlp_bwd_tiles(FieldArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   _Float16* lds = reinterpret_cast<_Float16*>(smem) + wid * (64 * 32 + 32 * 32);
+#if LNR_MLP_W_LDS
+  SigmaWeightsLds sw;
+  {
+    SigmaWeights swr;
+    load_sigma_weights(a.w, swr);
+    sw.stage(reinterpret_cast<half8_t*>(reinterpret_cast<_Float16*>(smem) + kWavesPerBlock * (64 * 32 + 32 * 32)), swr);
+  }
+  __syncthreads();
+#else
   SigmaWeights sw;
   load_sigma_weights(a.w, sw);
+#endif
   DW0Mfma acc;
   acc.init();
   float dw1[16];
@@ -823,16 +849,19 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(LNR_MLP
     uint32_t x0[4], x1[4];
     float d0, d1;
   };
+  // 32-bit byte offsets from uniform bases (the launcher checks 16 levels x stride x 4 B < 4 GB): one
+  // register per address instead of a 64-bit pair, and no hoisted per-level 64-bit row addresses
+  const uint32_t st4 = (uint32_t)a.enc_stride * 4u;
+  const uint32_t row_e = 4u * (uint32_t)g * st4, row_j = 2u * (uint32_t)g * st4;  // this lane group's rows
   auto prefetch = [&](int64_t m, Pre& p) {
-    const bool v = m < N;
-    const int64_t mm = v ? m : 0;
+    const uint32_t mb = (uint32_t)((m < N ? m : 0) + c) * 4u;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      p.x0[q] = a.enc[(int64_t)(4 * g + q) * a.enc_stride + mm + c];
-      p.x1[q] = a.enc[(int64_t)(4 * g + q) * a.enc_stride + mm + 16 + c];
+      p.x0[q] = ld_off(a.enc, row_e + (uint32_t)q * st4 + mb);
+      p.x1[q] = ld_off(a.enc, row_e + (uint32_t)q * st4 + mb + 64u);
     }
-    p.d0 = a.d_sigma[mm + c];
-    p.d1 = a.d_sigma[mm + 16 + c];
+    p.d0 = ld_off(a.d_sigma, mb);
+    p.d1 = ld_off(a.d_sigma, mb + 64u);
   };
   auto pair = [&](int64_t n0, const Pre& p) {
     SigmaHidden h0, h1;
@@ -863,8 +892,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(LNR_MLP
       const int lvl = 8 * m + 2 * g;
       const float2 q0 = make_float2(d[m][0] * ds0, d[m][1] * ds0), q1 = make_float2(d[m][2] * ds0, d[m][3] * ds0);
       if (JAC) {
-        a.d_jac[(int64_t)lvl * a.enc_stride + n0 + c] = pack_h2(d[m][0], d[m][1]);
-        a.d_jac[(int64_t)(lvl + 1) * a.enc_stride + n0 + c] = pack_h2(d[m][2], d[m][3]);
+        const uint32_t o = row_j + 8u * (uint32_t)m * st4 + (uint32_t)(n0 + c) * 4u;
+        st_off(a.d_jac, o, pack_h2(d[m][0], d[m][1]));
+        st_off(a.d_jac, o + st4, pack_h2(d[m][2], d[m][3]));
       } else {
         denc[(int64_t)lvl * a.enc_stride + n0 + c] = q0;
         denc[(int64_t)(lvl + 1) * a.enc_stride + n0 + c] = q1;
@@ -878,8 +908,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(LNR_MLP
       const int lvl = 8 * m + 2 * g;
       const float2 q0 = make_float2(d[m][0] * ds1, d[m][1] * ds1), q1 = make_float2(d[m][2] * ds1, d[m][3] * ds1);
       if (JAC) {
-        a.d_jac[(int64_t)lvl * a.enc_stride + n0 + 16 + c] = pack_h2(d[m][0], d[m][1]);
-        a.d_jac[(int64_t)(lvl + 1) * a.enc_stride + n0 + 16 + c] = pack_h2(d[m][2], d[m][3]);
+        const uint32_t o = row_j + 8u * (uint32_t)m * st4 + (uint32_t)(n0 + 16 + c) * 4u;
+        st_off(a.d_jac, o, pack_h2(d[m][0], d[m][1]));
+        st_off(a.d_jac, o + st4, pack_h2(d[m][2], d[m][3]));
       } else {
         denc[(int64_t)lvl * a.enc_stride + n0 + 16 + c] = q0;
         denc[(int64_t)(lvl + 1) * a.enc_stride + n0 + 16 + c] = q1;
@@ -889,6 +920,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(LNR_MLP
     }
     dw0_pair_mfma(lds, h0, h1, e0, e1, ds0, ds1, pair_max, acc);
   };
+#if LNR_MLP_PREFETCH == 2
   Pre pa, pb;
   prefetch(n0, pa);
   prefetch(n0 + step, pb);
@@ -904,6 +936,15 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(LNR_MLP
       pair(n0 + step, cur);
     }
   }
+#else
+  Pre pa;
+  prefetch(n0, pa);
+  for (; n0 < N; n0 += step) {
+    const Pre cur = pa;
+    prefetch(n0 + step, pa);
+    pair(n0, cur);
+  }
+#endif
   __syncthreads();
   {
     DW0Acc out;
@@ -949,7 +990,8 @@ __global__ void __launch_bounds__(256) k_denc_max(const float2* __restrict__ d_e
 
 static size_t wave_smem_bytes(int S) { return (size_t)kWavesPerBlock * S * 4; }
 static size_t bwd_tiles_smem_bytes() {
-  const size_t b = (size_t)kWavesPerBlock * (64 * 32 + 32 * 32) * 2;
+  // per-wave dW0 staging, then (LNR_MLP_W_LDS) the 8 weight operands x 64 lanes x 16 B
+  const size_t b = (size_t)kWavesPerBlock * (64 * 32 + 32 * 32) * 2 + (LNR_MLP_W_LDS ? 8 * 64 * 16 : 0);
   return b < LNR_SIGMA_MLP_PARAMS * 4 ? LNR_SIGMA_MLP_PARAMS * 4 : b;
 }
 
@@ -1136,6 +1178,8 @@ extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t e
               "lnr_field_train: null pointer");
   LNR_REQUIRE(!d_enc_jac || n_samples == 64 || n_samples == 128 || n_samples == 256 || n_samples == 512,
               "lnr_field_train: d_enc_jac needs n_samples in {64, 128, 256, 512} (got %d)", n_samples);
+  LNR_REQUIRE(enc_stride < (int64_t(1) << 26), "lnr_field_train: enc_stride=%lld over 2^26 (32-bit level offsets)",
+              (long long)enc_stride);
   FieldArgs a{};
   a.w = w; a.enc = enc; a.enc_stride = enc_stride; a.rays = rays; a.z = z; a.depth_gt = depth_gt;
   a.n_rays = n_rays; a.S = n_samples; a.noise_std = noise_std; a.noise = noise; a.key = key;

@@ -20,6 +20,21 @@ struct SigmaWeights {
   half8_t bt[2][2];  // backward A operand [in tile m][k-step s]: W0[hid(s,g,j)][16m + (l&15)]
   half8_t w1h[2];    // W1[0][16t + 4g + r] at index k = 4t + r, as fp16 (the weight's own precision)
   __device__ __forceinline__ float w1(int k) const { return (float)w1h[k >> 3][k & 7]; }
+  __device__ __forceinline__ half8_t A0(int t) const { return a0[t]; }
+  __device__ __forceinline__ half8_t BT(int m, int s) const { return bt[m][s]; }
+};
+
+// The same operands kept in LDS (one copy per workgroup, [operand][64 lanes] of 16 B: conflict-free
+// ds_read_b128) and read where used: 32 fewer registers per lane for a register-bound kernel.
+struct SigmaWeightsLds {
+  const half8_t* a0;  // [4][64]
+  const half8_t* bt;  // [2 m][2 s][64]
+  half8_t w1h[2];
+  __device__ __forceinline__ float w1(int k) const { return (float)w1h[k >> 3][k & 7]; }
+  __device__ __forceinline__ half8_t A0(int t) const { return a0[t * 64 + (threadIdx.x & 63)]; }
+  __device__ __forceinline__ half8_t BT(int m, int s) const { return bt[(2 * m + s) * 64 + (threadIdx.x & 63)]; }
+  // stage from registers (every wave writes the same values: wave 0's write suffices; the caller syncs)
+  __device__ __forceinline__ void stage(half8_t* lds, const struct SigmaWeights& sw);
 };
 
 // The hidden layer of one 16-sample tile, fp16 (tcnn stores it so): h[k] = relu(H)[hid 16t + 4g + r][sample
@@ -54,6 +69,22 @@ __device__ __forceinline__ void load_sigma_weights(const uint16_t* __restrict__ 
       sw.w1h[(4 * t + r) >> 3][(4 * t + r) & 7] = __builtin_bit_cast(_Float16, w1[16 * t + 4 * g + r]);
 }
 
+__device__ __forceinline__ void SigmaWeightsLds::stage(half8_t* lds, const SigmaWeights& sw) {
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x < 64) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) lds[t * 64 + lane] = sw.a0[t];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) lds[(4 + 2 * m + q) * 64 + lane] = sw.bt[m][q];
+  }
+  a0 = lds;
+  bt = lds + 4 * 64;
+  w1h[0] = sw.w1h[0];
+  w1h[1] = sw.w1h[1];
+}
+
 // B operand of the forward product for sample n (lane column): features 8g..8g+7 = levels 4g..4g+3.
 __device__ __forceinline__ half8_t load_enc_operand(const uint32_t* __restrict__ enc, int64_t stride, int64_t n,
                                                     bool valid) {
@@ -70,12 +101,13 @@ __device__ __forceinline__ half8_t load_enc_operand(const uint32_t* __restrict__
 
 // Forward of one 16-sample tile.  h[4t+r] = fp16(relu(H))[hid 16t+4g+r][sample l&15];
 // returns sigma for sample l&15 (fp32 accumulate of fp16 operands, NOT yet rounded).
-__device__ __forceinline__ float sigma_tile_fwd(const SigmaWeights& sw, const half8_t& benc, SigmaHidden& h) {
+template <class W>
+__device__ __forceinline__ float sigma_tile_fwd(const W& sw, const half8_t& benc, SigmaHidden& h) {
   float part = 0.f;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     float4_t acc = {0.f, 0.f, 0.f, 0.f};
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(sw.a0[t], benc, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(sw.A0(t), benc, acc, 0, 0, 0);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const _Float16 v16 = (_Float16)fmaxf(acc[r], 0.f);
@@ -110,7 +142,8 @@ __device__ __forceinline__ float grad_scale(float maxabs) {
 // Backward of one tile for d_sigma = 1: dH^T[hid][s] = w1[hid] * (h > 0) is exact in fp16, so the
 // MFMA result is exact up to fp32 accumulation; the caller multiplies by the sample's d_sigma.
 // d[m][r] = dEnc[sample l&15][in 16m + 4g + r] / d_sigma.
-__device__ __forceinline__ void sigma_tile_bwd_denc(const SigmaWeights& sw, const SigmaHidden& h, float (&d)[2][4]) {
+template <class W>
+__device__ __forceinline__ void sigma_tile_bwd_denc(const W& sw, const SigmaHidden& h, float (&d)[2][4]) {
   half8_t b[2];  // (k-step s, j) holds hidden unit k = 8 s + j: mask * w1 in one select per half
 #pragma unroll
   for (int s = 0; s < 2; ++s)
@@ -119,8 +152,8 @@ __device__ __forceinline__ void sigma_tile_bwd_denc(const SigmaWeights& sw, cons
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     float4_t acc = {0.f, 0.f, 0.f, 0.f};
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(sw.bt[m][0], b[0], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(sw.bt[m][1], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(sw.BT(m, 0), b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(sw.BT(m, 1), b[1], acc, 0, 0, 0);
 #pragma unroll
     for (int r = 0; r < 4; ++r) d[m][r] = acc[r];
   }
@@ -191,7 +224,8 @@ struct DW0Mfma {
     kc = kUnset;
   }
   // acc.v[t][m][r] * w1[4t + r] * 2^-kc: dW0[16t + 4g + r][16m + (l&15)], as DW0Acc for write_dw_slab
-  __device__ __forceinline__ void finish(const SigmaWeights& sw, DW0Acc& out) const {
+  template <class W>
+  __device__ __forceinline__ void finish(const W& sw, DW0Acc& out) const {
     const float inv = kc == kUnset ? 0.f : ldexpf(1.f, -kc);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
