@@ -744,7 +744,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "hash-grid backward stage (k_bwd_chunk_sums, k_bwd_scan_*, k_bwd_scatter_rows, "
-                               "k_bwd_scatter_overflow, k_bwd_accum, k_bwd_finalize)",
+                               "k_bwd_accum_units, k_bwd_finalize_units)",
                      "algorithmic_bytes_per_launch": 1024 * N, "ms_per_launch": bwd_ms,
                      "step_algorithmic_bytes": step_bytes,
                      "step_frac": step_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,

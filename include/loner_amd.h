@@ -374,6 +374,21 @@ int lnr_ogm_grad(const float* rays, const float* z, const float* depth_gt, int64
                  float scale, float* grad_ws, int64_t ws_words, int32_t occ_res, void* stream);
 int lnr_sgd_step(float* param, const float* grad, int64_t n, float lr, void* stream);
 
+/* OccupancyGridModel.interpolate (src/models/model_tcnn.py:126-134) as an operator of its own, for the
+ * module-level drop-in (Optimizer._step_occupancy_grid, src/mapping/optimizer.py:897-908, calls it and
+ * backpropagates through it).  Replaces torch.nn.functional.grid_sample on a (1, 1, res, res, res) grid
+ * with (n, 3) points in [-1, 1]: trilinear, align_corners=False, zeros padding.
+ *   lnr_grid_sample3d      out[i] = grid_sample(grid, pts[i])
+ *   lnr_grid_sample3d_bwd  dgrid = sum_i dout[i] d out[i] / d grid (overwritten; the points get no
+ *                          gradient: the reference's points are detached).  Deterministic: int64
+ *                          fixed point with a unit from max |dout| and n (about 2^-42 of max |dout|
+ *                          per point at n = 10^6); ws: lnr_grid_sample3d_bwd_workspace_words(res)
+ *                          fp32 words, 8-byte aligned (2 + 2 res^3 at least). */
+int lnr_grid_sample3d(const float* grid, int32_t res, const float* pts, int64_t n, float* out, void* stream);
+int64_t lnr_grid_sample3d_bwd_workspace_words(int32_t res);
+int lnr_grid_sample3d_bwd(const float* pts, const float* dout, int64_t n, int32_t res, float* dgrid, float* ws,
+                          int64_t ws_words, void* stream);
+
 /* ---------------------------------------------------------------- per-keyframe scan preprocessing */
 /* LidarScan.motion_compensate (src/common/sensors.py:169-231).  Host-computed per scan: the start pose
  * rotation (row-major) and translation, end - start translation, axis/angle of R_start^T R_end

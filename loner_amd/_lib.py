@@ -152,6 +152,9 @@ _SIGNATURES = {
     "lnr_ogm_workspace_words": (c_i64, [c_i32]),
     "lnr_ogm_update": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_f, c_f, c_p, c_p, c_i64, c_i32, c_p]),
     "lnr_ogm_grad": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_i64, c_i32, c_p]),
+    "lnr_grid_sample3d": (ctypes.c_int, [c_p, c_i32, c_p, c_i64, c_p, c_p]),
+    "lnr_grid_sample3d_bwd_workspace_words": (c_i64, [c_i32]),
+    "lnr_grid_sample3d_bwd": (ctypes.c_int, [c_p, c_p, c_i64, c_i32, c_p, c_p, c_i64, c_p]),
     "lnr_sgd_step": (ctypes.c_int, [c_p, c_p, c_i64, c_f, c_p]),
     "lnr_fill_uniform": (ctypes.c_int, [c_p, c_i64, c_u32, c_f, c_f, c_i64, c_p]),
     "lnr_f32_to_f16": (ctypes.c_int, [c_p, c_p, c_i64, c_p]),

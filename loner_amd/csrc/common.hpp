@@ -176,4 +176,27 @@ __device__ __forceinline__ unsigned long long stamp() {
 #define LNR_PHASE_EXPORT(tu)
 #endif
 
+// OccupancyGridModel.interpolate (src/models/model_tcnn.py:126-134): grid_sample of the (R, R, R) grid
+// at (x, y, z) in [-1, 1] (x the fastest axis), trilinear, align_corners=False, zeros padding.  Its
+// corner order and weights are those of the grid-gradient splat (optim.hip).
+__device__ __forceinline__ float occ_grid_sample(const float* __restrict__ occ, int R, float x, float y, float z) {
+  const float ix = ((x + 1.f) * (float)R - 1.f) / 2.f;
+  const float iy = ((y + 1.f) * (float)R - 1.f) / 2.f;
+  const float iz = ((z + 1.f) * (float)R - 1.f) / 2.f;
+  const float fx = floorf(ix), fy = floorf(iy), fz = floorf(iz);
+  const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
+  const float wx[2] = {(float)(x0 + 1) - ix, ix - (float)x0};
+  const float wy[2] = {(float)(y0 + 1) - iy, iy - (float)y0};
+  const float wz[2] = {(float)(z0 + 1) - iz, iz - (float)z0};
+  float acc = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int bx = c & 1, by = (c >> 1) & 1, bz = (c >> 2) & 1;
+    const int cx = x0 + bx, cy = y0 + by, cz = z0 + bz;
+    const float w = wx[bx] * wy[by] * wz[bz];
+    if (cx >= 0 && cx < R && cy >= 0 && cy < R && cz >= 0 && cz < R) acc += occ[((int64_t)cz * R + cy) * R + cx] * w;
+  }
+  return acc;
+}
+
 }  // namespace lnr

@@ -808,7 +808,7 @@ __device__ __forceinline__ uint32_t pack_h2(float x, float y) {
 // d_enc (level-major float2) and the per-block dW slab.
 // (2 waves per SIMD at its 242 VGPRs; forcing 3 or 4 spills 45 / 116 VGPRs: 0.18 -> 0.56 / 0.76 ms)
 #ifndef LNR_MLP_PREFETCH
-#define LNR_MLP_PREFETCH 2  // tile pairs loaded ahead in k_mlp_bwd_tiles (1 or 2)
+#define LNR_MLP_PREFETCH 1  // tile pairs loaded ahead in k_mlp_bwd_tiles (1 or 2; C2: 271 against 279 us)
 #endif
 #ifndef LNR_MLP_W_LDS
 #define LNR_MLP_W_LDS 0  // the layer-0 weight operands in LDS instead of registers (k_mlp_bwd_tiles)

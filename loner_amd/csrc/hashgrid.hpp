@@ -27,6 +27,18 @@ constexpr int kMaxBuckets = 2048;
 // int64 partial chunk per piece (at most two per workgroup), added exactly by the last piece's
 // workgroup to arrive (or by k_bwd_finalize).
 constexpr int kAccumGroups = 512;
+// Unit accumulation (k_bwd_accum_units, mid-size batches): each bucket is one work unit when it holds at
+// most T = max(R / kAccumGroups, one tile) records, else ceil(n / T) equal pieces.  Only the large
+// buckets (the coarse levels' few chunks) leave partial chunks, and a finalize workgroup per such
+// bucket adds them.  Sum of the pieces <= kMaxBuckets + kAccumGroups; cut buckets < kAccumGroups;
+// their pieces <= 2 kAccumGroups (the partial chunks).
+constexpr int kMaxUnits = kMaxBuckets + kAccumGroups;
+struct UnitTable {
+  uint32_t n_units, n_cut, pad0, pad1;
+  uint2 unit[kMaxUnits];       // {bucket, piece << 16 | pieces}, bucket order
+  uint32_t slot[kMaxBuckets];  // a cut bucket's first partial chunk
+  uint2 cut[kAccumGroups];     // {bucket, pieces} of the cut buckets, bucket order
+};
 
 struct GridArgs {
   LevelParams lv[LNR_MAX_LEVELS];
@@ -449,6 +461,7 @@ struct BwdWorkspace {
   uint64_t* seg_start;   // [kMaxBuckets + 1]
   long long* partial;    // [2 kAccumGroups][2 * kChunk] int64 fixed-point partial sums of cut buckets
   uint32_t* bucket_done; // [kMaxBuckets] pieces of a cut bucket accumulated so far (k_bwd_accum<true>)
+  UnitTable* units;      // the unit accumulation's work list (k_bwd_scan_buckets / k_bwd_units)
   uint2* rec;            // [8 * N * L] records {word, half2} (see "Backward records")
   int64_t n_sb;
   int64_t n_chunks;
@@ -460,7 +473,7 @@ inline int64_t bwd_n_chunks(int64_t n) { return (bwd_n_sb(n) + kRowsPerChunk - 1
 inline int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
 
 struct WsLayout {
-  int64_t hist, chunk_sum, level_max, counts, seg_start, partial, bucket_done, rec, total;
+  int64_t hist, chunk_sum, level_max, counts, seg_start, partial, bucket_done, units, rec, total;
 };
 
 inline WsLayout ws_layout(const lnr_grid_desc* d, const GridArgs& a, int64_t n) {
@@ -474,6 +487,7 @@ inline WsLayout ws_layout(const lnr_grid_desc* d, const GridArgs& a, int64_t n) 
   w.seg_start = b; b += align256((kMaxBuckets + 1) * 8);
   w.partial = b;   b += align256((int64_t)2 * kAccumGroups * 2 * kChunk * 8);
   w.bucket_done = b; b += align256(kMaxBuckets * 4);
+  w.units = b;     b += align256(sizeof(UnitTable));
   // +2 records: the accumulate loads records in pairs
   w.rec = b;       b += align256((8 * n * (int64_t)d->n_levels + 2) * 8);
   w.total = b;
@@ -493,6 +507,7 @@ inline BwdWorkspace carve_workspace(void* base, const GridArgs& a, const lnr_gri
   w.seg_start = reinterpret_cast<uint64_t*>(p + L.seg_start);
   w.partial = reinterpret_cast<long long*>(p + L.partial);
   w.bucket_done = reinterpret_cast<uint32_t*>(p + L.bucket_done);
+  w.units = reinterpret_cast<UnitTable*>(p + L.units);
   w.rec = reinterpret_cast<uint2*>(p + L.rec);
   w.n_sb = bwd_n_sb(n);
   w.n_chunks = bwd_n_chunks(n);

@@ -16,7 +16,9 @@
 //            its pieces into a 64 KB LDS chunk of int64 fixed point (ds_add_u64) and storing fp32 (a
 //            whole bucket) or an int64 partial chunk (a bucket its range boundaries cut) that
 //            k_bwd_finalize adds in workgroup order.  Small batches take k_bwd_accum_buckets instead:
-//            one workgroup per whole bucket, no partials and no finalize (accum_buckets_max_n).
+//            one workgroup per whole bucket, no partials and no finalize (accum_buckets_max_n); mid-size
+//            ones (a data-parallel shard) k_bwd_accum_units: a work list of whole buckets and equal
+//            pieces of the large ones, so only those leave partial chunks (accum_units).
 // No float atomics anywhere: the result is bitwise reproducible, and d_table is overwritten.
 #include "hashgrid.hpp"
 
@@ -117,9 +119,57 @@ __global__ void __launch_bounds__(kMaxChunksPerLevel) k_bwd_scan_rows(GridArgs a
   }
 }
 
-// Bucket segment starts: exclusive prefix of the bucket totals (records are laid out bucket-major).
+// The unit accumulation's work list for buckets [b0, b0 + nb) holding R records (see UnitTable):
+// thread t's buckets are b0 + 2t and b0 + 2t + 1, with record counts cnt.  One 1024-thread block.
+constexpr uint64_t kUnitMinRecords = 2048;  // one accumulate tile (kTile): no smaller pieces
+__device__ __forceinline__ void build_units(UnitTable* ut, uint32_t b0, uint32_t nb, const uint64_t (&cnt)[2],
+                                            uint64_t R, uint64_t* scratch /* LDS [16] */) {
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const uint64_t T0 = (R + kAccumGroups - 1) / kAccumGroups;
+  const uint64_t T = T0 > kUnitMinRecords ? T0 : kUnitMinRecords;
+  uint32_t P[2];
+  uint64_t pk[2];  // packed counters: units (bits 0-20), partial chunks (21-41), cut buckets (42-)
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    P[q] = 2 * t + q < (int)nb ? (cnt[q] <= T ? 1u : (uint32_t)((cnt[q] + T - 1) / T)) : 0u;
+    pk[q] = (uint64_t)P[q] | ((uint64_t)(P[q] > 1 ? P[q] : 0u) << 21) | ((uint64_t)(P[q] > 1 ? 1u : 0u) << 42);
+  }
+  uint64_t inc = pk[0] + pk[1];
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
+  }
+  if (lane == 63) scratch[wid] = inc;
+  lds_barrier();
+  uint64_t ex = inc - pk[0] - pk[1], tot = 0;
+  for (int w = 0; w < 16; ++w) {
+    if (w < wid) ex += scratch[w];
+    tot += scratch[w];
+  }
+  constexpr uint64_t m21 = (1ull << 21) - 1;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if (P[q]) {
+      const uint32_t b = b0 + 2 * t + q, u0 = (uint32_t)(ex & m21), s0 = (uint32_t)((ex >> 21) & m21);
+      for (uint32_t k = 0; k < P[q]; ++k) ut->unit[u0 + k] = make_uint2(b, (k << 16) | P[q]);
+      if (P[q] > 1) {
+        ut->slot[b] = s0;
+        ut->cut[ex >> 42] = make_uint2(b, P[q]);
+      }
+    }
+    ex += pk[q];
+  }
+  if (t == 0) {
+    ut->n_units = (uint32_t)(tot & m21);
+    ut->n_cut = (uint32_t)(tot >> 42);
+  }
+}
+
+// Bucket segment starts: exclusive prefix of the bucket totals (records are laid out bucket-major),
+// and the unit accumulation's work list over all buckets.
 __global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint32_t n_buckets) {
-  __shared__ uint64_t w_seg[16];
+  __shared__ uint64_t w_seg[16], w_units[16];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   uint64_t seg[2];  // two buckets per thread (n_buckets <= kMaxBuckets = 2048)
 #pragma unroll
@@ -132,8 +182,11 @@ __global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint
   }
   if (lane == 63) w_seg[wid] = iseg;
   lds_barrier();
-  uint64_t bseg = 0;
-  for (int w = 0; w < wid; ++w) bseg += w_seg[w];
+  uint64_t bseg = 0, total = 0;
+  for (int w = 0; w < 16; ++w) {
+    if (w < wid) bseg += w_seg[w];
+    total += w_seg[w];
+  }
   uint64_t e_seg = bseg + iseg - seg[0] - seg[1];  // exclusive value at this thread's first bucket
   if (t == 1023) ws.seg_start[n_buckets] = bseg + iseg;  // total (n_buckets may equal 2 * blockDim)
   ws.bucket_done[2 * t] = 0u;  // k_bwd_accum<true>'s arrival counters (kMaxBuckets = 2 * blockDim)
@@ -143,6 +196,26 @@ __global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint
     if (2 * t + q < (int)n_buckets) ws.seg_start[2 * t + q] = e_seg;
     e_seg += seg[q];
   }
+  build_units(ws.units, 0, n_buckets, seg, total, w_units);
+}
+
+// The work list for a sub-range [b0, b1) of the buckets (the accumulation by level range, for the
+// bucketed gradient exchange); k_bwd_scan_buckets made the whole range's.
+__global__ void __launch_bounds__(1024) k_bwd_units(BwdWorkspace ws, uint32_t b0, uint32_t b1) {
+  __shared__ uint64_t w_r[16], w_units[16];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const uint32_t nb = b1 - b0;
+  uint64_t cnt[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) cnt[q] = 2 * t + q < (int)nb ? ws.counts[b0 + 2 * t + q] : 0u;
+  uint64_t r = cnt[0] + cnt[1];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) r += __shfl_xor(r, o, 64);
+  if (lane == 0) w_r[wid] = r;
+  lds_barrier();
+  uint64_t R = 0;
+  for (int w = 0; w < 16; ++w) R += w_r[w];
+  build_units(ws.units, b0, nb, cnt, R, w_units);
 }
 
 // One workgroup per (histogram row, level): kSB samples, up to 8 records each (hashgrid.hpp).
@@ -416,32 +489,31 @@ struct RowsLds {  // the small tables first: their addresses fit the 16-bit LDS 
 // NL levels, the first NM coherent (run-merging) and the rest fine, at most NB buckets per level:
 // compile-time, so the level loop unrolls into straight-line code.  Record slots are 32-bit (the
 // launcher checks 8 N L < 2^32).
-template <class PosFn, class GradFn, int NL, int NM, int NB>
-__global__ void __launch_bounds__(kSB)
-__attribute__((amdgpu_waves_per_eu(rows_waves<GradFn, NB>(), rows_waves<GradFn, NB>())))
-k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace ws, bool skip_zero) {
+// The body walks levels [LB, LB + NL) of histogram row sb (local level l is level LB + l).
+template <class PosFn, class GradFn, int LB, int NL, int NM, int NB, int kRowsStages>
+__device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& sm, const GridArgs& a, const PosFn& pos,
+                                                  int64_t n, const GradFn& grad, const BwdWorkspace& ws, bool skip_zero,
+                                                  int64_t sb) {
   static_assert(NL <= 2 * (kSB / 64), "wave w prepares levels 2w and 2w + 1");
   static_assert(NB <= 128, "two buckets per lane");
-  constexpr int kRowsStages = rows_stages<GradFn, NB>();
   static_assert(kRowsStages == 1 || kRowsStages == 2, "one or two stages");
-  __shared__ RowsLds<NL, NB, kRowsStages> sm;
-  const int64_t sb = xcd_row(blockIdx.x, gridDim.x);
+  static_assert(NM <= NL, "coherent levels come first");
   const int64_t i = sb * kSB + threadIdx.x;
   const bool in = i < n;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const bool last = sb + 1 >= ws.n_sb;
   const int64_t ic = in ? i : n - 1;
-  const uint32_t spare = (uint32_t)(8 * n * (int64_t)NL);  // one of the 2 slack records past the last slot
+  const uint32_t spare = (uint32_t)(8 * n * (int64_t)a.n_levels);  // one of the 2 slack records past the last slot
 
   // prologue 1: the level table and zero rank counters
   if (threadIdx.x < NL * (sizeof(LevelParams) / 4))
-    reinterpret_cast<uint32_t*>(sm.lv)[threadIdx.x] = reinterpret_cast<const uint32_t*>(a.lv)[threadIdx.x];
+    reinterpret_cast<uint32_t*>(sm.lv)[threadIdx.x] = reinterpret_cast<const uint32_t*>(a.lv + LB)[threadIdx.x];
   if (threadIdx.x < 2 * NB) (&sm.ctr[0][0])[threadIdx.x] = 0u;
   // prologue 2: every global load of the kernel
   const typename PosFn::Raw raw = pos.load(ic);
   typename GradFn::Raw g[NL];  // (GradJac: the fp16 pair, scaled by d sigma at use: half the registers)
 #pragma unroll
-  for (int l = 0; l < NL; ++l) g[l] = grad.load_raw_nt(l, ic);  // read once: nontemporal, so they do not
+  for (int l = 0; l < NL; ++l) g[l] = grad.load_raw_nt(LB + l, ic);  // read once: nontemporal, so they do not
                                                                 // displace the runs' L2 lines
   const float gsc = grad.scale(ic);
   uint32_t h0[2][2], h1[2][2];
@@ -450,7 +522,7 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
   for (int p = 0; p < 2; ++p) {
     const uint32_t l = 2 * wid + p;
     if (l < (uint32_t)NL) {
-      const uint32_t b0 = a.bucket_base[l], nb = a.bucket_base[l + 1] - b0;
+      const uint32_t b0 = a.bucket_base[LB + l], nb = a.bucket_base[LB + l + 1] - b0;
       const uint32_t* row = ws.hist + (int64_t)b0 * ws.n_sb + sb * nb;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
@@ -463,7 +535,7 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
   }
   float rsc[NL];  // per-level record scales (uniform: scalar loads)
 #pragma unroll
-  for (int l = 0; l < NL; ++l) rsc[l] = ldexpf(1.f, rec_exp_for(ws.level_max[l]));
+  for (int l = 0; l < NL; ++l) rsc[l] = ldexpf(1.f, rec_exp_for(ws.level_max[LB + l]));
   float x = 0.f, y = 0.f, z = 0.f;
   pos.eval(raw, x, y, z);
   // prologue 3: wave w's levels' bucket starts (a wave prefix over the buckets, two per lane)
@@ -471,7 +543,7 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
   for (int p = 0; p < 2; ++p) {
     const uint32_t l = 2 * wid + p;
     if (l < (uint32_t)NL) {
-      const uint32_t nb = a.bucket_base[l + 1] - a.bucket_base[l];
+      const uint32_t nb = a.bucket_base[LB + l + 1] - a.bucket_base[LB + l];
       const uint32_t c0 = 2 * lane < nb ? h1[p][0] - h0[p][0] : 0u;
       const uint32_t c1 = 2 * lane + 1 < nb ? h1[p][1] - h0[p][1] : 0u;
       const uint32_t inc = wave_incl_scan_u32(c0 + c1);
@@ -616,6 +688,14 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
     }
   }
   if (kRowsStages == 2) copy_out(NL - 1);
+}
+
+template <class PosFn, class GradFn, int NL, int NM, int NB>
+__global__ void __launch_bounds__(kSB)
+__attribute__((amdgpu_waves_per_eu(rows_waves<GradFn, NB>(), rows_waves<GradFn, NB>())))
+k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace ws, bool skip_zero) {
+  __shared__ RowsLds<NL, NB, rows_stages<GradFn, NB>()> sm;
+  scatter_rows_body<PosFn, GradFn, 0, NL, NM, NB>(sm, a, pos, n, grad, ws, skip_zero, xcd_row(blockIdx.x, gridDim.x));
 }
 
 constexpr size_t kScatterLds = (size_t)kCap * 4 + kMaxChunksPerLevel * 8 + (size_t)kCap * 4 + kMaxChunksPerLevel * 4 +
@@ -928,6 +1008,40 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
   store_bucket(acc, a, ws, d_table, l, ent0, nent, k2);
 }
 
+// One workgroup per unit of the work list (UnitTable): a whole bucket (its fp32 values, or its zeros
+// when empty) or one of the equal pieces of a large bucket (its int64 partial chunk, added by
+// k_bwd_finalize_units).  The grid is the list's bound; workgroups past n_units return at once.
+static_assert(kUnitMinRecords == (uint64_t)kTile, "pieces of at least one tile");
+__global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_accum_units(GridArgs a, BwdWorkspace ws,
+                                                                                              float* __restrict__ d_table) {
+  __shared__ unsigned long long acc[2 * kChunk];
+  __shared__ __attribute__((aligned(16))) uint2 stage[kTile];
+  const UnitTable* ut = ws.units;
+  if (blockIdx.x >= ut->n_units) return;
+  const uint2 e = ut->unit[blockIdx.x];
+  const uint32_t b = e.x, k = e.y >> 16, P = e.y & 0xFFFFu;
+  const uint64_t s0 = ws.seg_start[b], s1 = ws.seg_start[b + 1];
+  const uint32_t l = level_of_bucket(a, b);
+  const uint32_t ent0 = (b - a.bucket_base[l]) * kChunk;
+  const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
+  if (s0 == s1) {
+    store_zero_bucket(a, d_table, b);
+    return;
+  }
+  const uint64_t n = s1 - s0, beg = s0 + n * k / P, end = s0 + n * (k + 1) / P;
+  for (int t = threadIdx.x; t < 2 * kChunk; t += blockDim.x) acc[t] = 0ull;
+  lds_barrier();
+  const int k2 = bucket_k2(ws, b);
+  accum_records(acc, stage, ws, beg, end, ldexpf(1.f, k2));
+  lds_barrier();
+  if (P == 1) {
+    store_bucket(acc, a, ws, d_table, l, ent0, nent, k2);
+    return;
+  }
+  long long* dst = ws.partial + (int64_t)(ut->slot[b] + k) * (2 * kChunk);
+  for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) dst[t] = (long long)acc[(t & 1) * kChunk + (t >> 1)];
+}
+
 // Buckets the accumulation did not finish: cut buckets = the sum of their pieces' partial chunks in
 // workgroup order (deterministic), empty buckets = 0.  One workgroup per bucket of [b_begin, b_end).
 constexpr int kFinalizeThreads = 1024;  // 8 consecutive values per thread: 2 kChunk in one pass
@@ -978,6 +1092,47 @@ __global__ void __launch_bounds__(kFinalizeThreads) k_bwd_finalize(GridArgs a, B
   }
 }
 
+// The cut buckets of the unit accumulation: the sum of their pieces' partial chunks in piece order.
+// One workgroup per cut bucket (the grid is the bound kAccumGroups; the rest return at once).
+__global__ void __launch_bounds__(kFinalizeThreads) k_bwd_finalize_units(GridArgs a, BwdWorkspace ws,
+                                                                         float* __restrict__ d_table) {
+  typedef long long i64x2 __attribute__((ext_vector_type(2)));
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  const UnitTable* ut = ws.units;
+  if (blockIdx.x >= ut->n_cut) return;
+  const uint2 cb = ut->cut[blockIdx.x];
+  const uint32_t b = cb.x, P = cb.y, slot0 = ut->slot[b];
+  const uint32_t l = level_of_bucket(a, b);
+  const uint32_t ent0 = (b - a.bucket_base[l]) * kChunk;
+  const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
+  const double inv = unit_back(a, ws, l, bucket_k2(ws, b));
+  const uint32_t t0 = 8 * threadIdx.x;
+  if (t0 >= 2 * nent) return;
+  long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (uint32_t k = 0; k < P; ++k) {
+    const i64x2* src = reinterpret_cast<const i64x2*>(ws.partial + (int64_t)(slot0 + k) * (2 * kChunk) + t0);
+    i64x2 q[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) q[j] = src[j];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[2 * j] += q[j].x;
+      v[2 * j + 1] += q[j].y;
+    }
+  }
+  float o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (float)((double)v[j] * inv);
+  float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0) + t0;
+  if (t0 + 8 <= 2 * nent && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0)) {
+    reinterpret_cast<f32x4v*>(dst)[0] = f32x4v{o[0], o[1], o[2], o[3]};
+    reinterpret_cast<f32x4v*>(dst)[1] = f32x4v{o[4], o[5], o[6], o[7]};
+  } else {
+    for (int j = 0; j < 8; ++j)
+      if (t0 + j < 2 * nent) dst[j] = o[j];
+  }
+}
+
 // Samples up to which the accumulation takes whole buckets (k_bwd_accum_buckets) instead of the
 // record-balanced split; LONER_ACCUM_BUCKETS_MAX_N overrides it (measurements: DESIGN.md section 4).
 // (read at every launch, so a process can switch between the two: tests/test_gpu_fullsize.py)
@@ -993,10 +1148,28 @@ static int64_t scatter_rows_min() {
   return e ? (int64_t)atoll(e) : (int64_t)LNR_SCATTER_ROWS_MIN;
 }
 
-// 1 (default): cut buckets are finished inside k_bwd_accum; 0: by k_bwd_finalize (LONER_ACCUM_FINISH)
+// The unit accumulation (k_bwd_accum_units + k_bwd_finalize_units) for mid-size batches: above the
+// whole-bucket kernel's range, up to LNR_ACCUM_UNITS_MAX_N samples.  Measured (r03, backward stage):
+// C4 shard 1/8 (0.59 M samples) 214 -> 188 us and shard 1/4 321 -> 312 us (the record-balanced split's
+// ~1000 partial chunks and its finalize pass are a fixed ~35 us); C2 (4.7 M) 964 -> 984 us (equal
+// record ranges balance the chip better than whole buckets there).  LONER_ACCUM_UNITS=1 / 0 forces
+// it on / off (read at every launch).
+#ifndef LNR_ACCUM_UNITS_MAX_N
+#define LNR_ACCUM_UNITS_MAX_N (int64_t(1) << 21)
+#endif
+static bool accum_units(int64_t n) {
+  const char* e = getenv("LONER_ACCUM_UNITS");
+  if (e) return atoi(e) != 0;
+  return n > accum_buckets_max_n() && n <= LNR_ACCUM_UNITS_MAX_N;
+}
+
+// 1: cut buckets are finished inside k_bwd_accum by their last piece's workgroup; 0 (default): by
+// k_bwd_finalize, one workgroup per bucket (LONER_ACCUM_FINISH).  Measured (r03): the in-kernel
+// finishing serialises a workgroup's cut buckets behind its own accumulation, the finalize launch
+// spreads them over the chip: C4 shard 1/8 backward 280 against 213 us, C2 972 against 966 us.
 static bool accum_finish() {
   const char* e = getenv("LONER_ACCUM_FINISH");
-  return e ? atoi(e) != 0 : true;
+  return e ? atoi(e) != 0 : false;
 }
 
 // Accumulate + finalize the buckets of levels [l0, l1): their slice of d_table becomes final.
@@ -1004,6 +1177,14 @@ static void launch_accum(const GridArgs& a, const BwdWorkspace& w, const lnr_gri
                          uint32_t l1, float* d_table, hipStream_t st) {
   const uint32_t b0 = a.bucket_base[l0], b1 = a.bucket_base[l1];
   if (b1 <= b0) return;
+  if (accum_units(n)) {  // the work list: whole buckets and equal pieces of the large ones
+    if (b0 != 0 || b1 != a.n_buckets)  // (a level range: its own list; the whole range's is the scan's)
+      hipLaunchKernelGGL(k_bwd_units, dim3(1), dim3(1024), 0, st, w, b0, b1);
+    hipLaunchKernelGGL(k_bwd_accum_units, dim3(b1 - b0 + kAccumGroups), dim3(kAccumThreads), 0, st, a, w, d_table);
+    hipLaunchKernelGGL(k_bwd_finalize_units, dim3(std::min<uint32_t>(b1 - b0, kAccumGroups)), dim3(kFinalizeThreads), 0,
+                       st, a, w, d_table);
+    return;
+  }
   if (n <= accum_buckets_max_n()) {  // small batches: whole buckets, no partials, no finalize
     hipLaunchKernelGGL(k_bwd_accum_buckets, dim3(b1 - b0), dim3(kAccumThreads), 0, st, a, w, d_table, b0, b1);
     return;

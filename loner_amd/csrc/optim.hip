@@ -63,32 +63,68 @@ __device__ __forceinline__ float logits_grad(float x) {
   return 0.25f * fr - 2.5f * oc;
 }
 
-// The splat accumulates in int64 fixed point (2^28 units: a sample adds |w g| <= 2.5, so 2^31 samples
-// stay below 2^63), so the grid gradient does not depend on the atomics' order: bitwise
-// reproducible.  Workspace (floats): [0, V) the float result, then n_rep int64 replicas.
+// The splat accumulates in int64 fixed point, so the grid gradient does not depend on the atomics'
+// order: bitwise reproducible.  The OGM update's unit is 2^-28 (a sample adds |w g| <= 2.5, so 2^31
+// samples stay below 2^63); the generic grid_sample backward (lnr_grid_sample3d_bwd) takes its unit
+// from max |dout| and the point count (fix_exp below).  Workspace (floats): [0, V) the float result,
+// then n_rep int64 replicas.
 constexpr int32_t kOgmReplicas = 3;
-constexpr float kOgmFix = 268435456.0f;  // 2^28
+constexpr int kOgmFixExp = 28;
 
-__global__ void __launch_bounds__(256) k_ogm_grad(const float* __restrict__ rays, const float* __restrict__ z,
-                                                  const float* __restrict__ dgt, int64_t n_rays, int32_t S,
-                                                  float scale, unsigned long long* __restrict__ grad, int32_t R,
-                                                  int32_t n_rep) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  // replica of the grid this workgroup adds into: the rays of one keyframe share their first
-  // voxels, so one copy would serialise hundreds of same-address atomics at the memory side
-  grad += (int64_t)(blockIdx.x % (uint32_t)n_rep) * R * R * R;
-  const int lane = threadIdx.x & 63;
-  const bool valid = i < n_rays * (int64_t)S;
-  float gval = 0.f, px = 0.f, py = 0.f, pz = 0.f;
-  if (valid) {
+// The OGM update's points: sample i of ray r, xyz = o + d z, logits gradient of its depth error.
+struct OgmRaySamples {
+  const float* rays;
+  const float* z;
+  const float* dgt;
+  int32_t S;
+  float scale;
+  __device__ __forceinline__ void at(int64_t i, float& px, float& py, float& pz, float& g) const {
     const int64_t r = i / S;
     const float* ry = rays + 13 * r;
     const float t = z[i];
     px = ry[0] + ry[3] * t;
     py = ry[1] + ry[4] * t;
     pz = ry[2] + ry[5] * t;
-    gval = logits_grad(t * scale - dgt[r] * scale);
+    g = logits_grad(t * scale - dgt[r] * scale);
   }
+};
+
+// grid_sample's backward for given points and output gradients (OccupancyGridModel.interpolate).
+struct PointGrads {
+  const float* pts;   // (n, 3)
+  const float* dout;  // (n)
+  __device__ __forceinline__ void at(int64_t i, float& px, float& py, float& pz, float& g) const {
+    px = pts[3 * i];
+    py = pts[3 * i + 1];
+    pz = pts[3 * i + 2];
+    g = dout[i];
+  }
+};
+
+// Fixed-point exponent of the generic backward: every per-voxel sum of |w g| <= n max|g| < 2^62.
+__device__ __forceinline__ int fix_exp(const uint32_t* amax_bits, int64_t n) {
+  if (amax_bits == nullptr) return kOgmFixExp;
+  const float m = __uint_as_float(*amax_bits);
+  if (!(m > 0.f)) return 0;  // (nothing to add, or non-finite: the sums are garbage either way)
+  int em, en = 0;
+  frexpf(m, &em);  // m < 2^em
+  while ((int64_t(1) << en) < n && en < 62) ++en;
+  const int e = 62 - em - en;
+  return e < -120 ? -120 : (e > 120 ? 120 : e);
+}
+
+template <class Src>
+__global__ void __launch_bounds__(256) k_ogm_grad(Src src, int64_t n, unsigned long long* __restrict__ grad,
+                                                  int32_t R, int32_t n_rep, const uint32_t* amax_bits) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // replica of the grid this workgroup adds into: the rays of one keyframe share their first
+  // voxels, so one copy would serialise hundreds of same-address atomics at the memory side
+  grad += (int64_t)(blockIdx.x % (uint32_t)n_rep) * R * R * R;
+  const float fix = ldexpf(1.f, fix_exp(amax_bits, n));
+  const int lane = threadIdx.x & 63;
+  const bool valid = i < n;
+  float gval = 0.f, px = 0.f, py = 0.f, pz = 0.f;
+  if (valid) src.at(i, px, py, pz, gval);
   const float ix = ((px + 1.f) * (float)R - 1.f) / 2.f;
   const float iy = ((py + 1.f) * (float)R - 1.f) / 2.f;
   const float iz = ((pz + 1.f) * (float)R - 1.f) / 2.f;
@@ -115,18 +151,33 @@ __global__ void __launch_bounds__(256) k_ogm_grad(const float* __restrict__ rays
       if (lane - o >= head_lane) p += q;
     }
     const bool tail = (lane == 63) || ((heads >> (lane + 1)) & 1ull);
-    if (tail && idx >= 0) atomicAdd(&grad[idx], (unsigned long long)__float2ll_rn(p * kOgmFix));
+    if (tail && idx >= 0) atomicAdd(&grad[idx], (unsigned long long)__float2ll_rn(p * fix));
   }
 }
 
-// out = (sum of the int64 replicas) / 2^28 (exact integer sum, one rounding)
+// out = (sum of the int64 replicas) / 2^e (exact integer sum, one rounding)
 __global__ void k_sum_replicas(const unsigned long long* __restrict__ g, int64_t nv, int32_t n_rep,
-                               float* __restrict__ out) {
+                               float* __restrict__ out, const uint32_t* amax_bits, int64_t n_pts) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nv) return;
   long long s = 0;
   for (int k = 0; k < n_rep; ++k) s += (long long)g[(int64_t)k * nv + i];
-  out[i] = (float)((double)s * (1.0 / 268435456.0));
+  out[i] = (float)ldexp((double)s, -fix_exp(amax_bits, n_pts));
+}
+
+// max |x| of n floats into *amax_bits (zeroed before; non-negative floats order as their bits)
+__global__ void __launch_bounds__(256) k_abs_max(const float* __restrict__ x, int64_t n, uint32_t* amax_bits) {
+  float m = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf(x[i]));
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(amax_bits, __float_as_uint(m));
+}
+
+__global__ void __launch_bounds__(256) k_grid_sample3d(const float* __restrict__ grid, int32_t R,
+                                                       const float* __restrict__ pts, int64_t n, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = occ_grid_sample(grid, R, pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]);
 }
 
 static int ogm_grad_launch(const float* rays, const float* z, const float* depth_gt, int64_t n_rays, int32_t n_samples,
@@ -146,10 +197,12 @@ static int ogm_grad_launch(const float* rays, const float* z, const float* depth
   const int64_t n = n_rays * (int64_t)n_samples;
   if (n > 0) {
     LNR_REQUIRE(rays && z && depth_gt, "%s: null pointer", who);
-    hipLaunchKernelGGL(k_ogm_grad, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rays, z, depth_gt, n_rays,
-                       n_samples, scale, g64, occ_res, n_rep);
+    const OgmRaySamples src{rays, z, depth_gt, n_samples, scale};
+    hipLaunchKernelGGL(k_ogm_grad<OgmRaySamples>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, n, g64,
+                       occ_res, n_rep, (const uint32_t*)nullptr);
   }
-  hipLaunchKernelGGL(k_sum_replicas, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, g64, nv, n_rep, grad_ws);
+  hipLaunchKernelGGL(k_sum_replicas, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, g64, nv, n_rep, grad_ws,
+                     (const uint32_t*)nullptr, n);
   return LNR_OK;
 }
 
@@ -237,6 +290,51 @@ extern "C" int lnr_ogm_grad(const float* rays, const float* z, const float* dept
                               as_stream(stream), "lnr_ogm_grad"))
     return e;
   LNR_RETURN_LAUNCH("lnr_ogm_grad");
+}
+
+extern "C" int lnr_grid_sample3d(const float* grid, int32_t res, const float* pts, int64_t n, float* out,
+                                 void* stream) {
+  LNR_REQUIRE(res >= 1 && n >= 0, "lnr_grid_sample3d: bad sizes");
+  if (n == 0) return LNR_OK;
+  LNR_REQUIRE(grid && pts && out, "lnr_grid_sample3d: null pointer");
+  hipLaunchKernelGGL(k_grid_sample3d, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), grid, res, pts,
+                     n, out);
+  LNR_RETURN_LAUNCH("lnr_grid_sample3d");
+}
+
+extern "C" int64_t lnr_grid_sample3d_bwd_workspace_words(int32_t res) {
+  if (res < 1) return -1;
+  return 2 + 2 * (int64_t)kOgmReplicas * res * res * res;  // max |dout| (8-B slot) + int64 replicas
+}
+
+extern "C" int lnr_grid_sample3d_bwd(const float* pts, const float* dout, int64_t n, int32_t res, float* dgrid,
+                                     float* ws, int64_t ws_words, void* stream) {
+  LNR_REQUIRE(res >= 1 && n >= 0, "lnr_grid_sample3d_bwd: bad sizes");
+  LNR_REQUIRE(n < (int64_t(1) << 40), "lnr_grid_sample3d_bwd: n=%lld too large", (long long)n);
+  LNR_REQUIRE(dgrid && ws, "lnr_grid_sample3d_bwd: null pointer");
+  LNR_REQUIRE(n == 0 || (pts && dout), "lnr_grid_sample3d_bwd: null pointer");
+  LNR_REQUIRE(((uintptr_t)ws & 7) == 0, "lnr_grid_sample3d_bwd: workspace must be 8-byte aligned");
+  const int64_t nv = (int64_t)res * res * res;
+  const int64_t rep = (ws_words - 2) / (2 * nv);
+  LNR_REQUIRE(rep >= 1, "lnr_grid_sample3d_bwd: workspace holds %lld words, needs >= %lld", (long long)ws_words,
+              (long long)(2 + 2 * nv));
+  const int32_t n_rep = (int32_t)(rep > kOgmReplicas ? kOgmReplicas : rep);
+  uint32_t* amax = reinterpret_cast<uint32_t*>(ws);
+  unsigned long long* g64 = reinterpret_cast<unsigned long long*>(ws + 2);
+  hipStream_t st = as_stream(stream);
+  if (hipMemsetAsync(ws, 0, (size_t)(2 + 2 * n_rep * nv) * sizeof(float), st) != hipSuccess) {
+    set_error("lnr_grid_sample3d_bwd: hipMemsetAsync failed");
+    return LNR_ERR_HIP;
+  }
+  if (n > 0) {
+    hipLaunchKernelGGL(k_abs_max, dim3(grid1d(n, 1024)), dim3(256), 0, st, dout, n, amax);
+    const PointGrads src{pts, dout};
+    hipLaunchKernelGGL(k_ogm_grad<PointGrads>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, n, g64, res,
+                       n_rep, (const uint32_t*)amax);
+  }
+  hipLaunchKernelGGL(k_sum_replicas, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, g64, nv, n_rep, dgrid,
+                     (const uint32_t*)amax, n);
+  LNR_RETURN_LAUNCH("lnr_grid_sample3d_bwd");
 }
 
 extern "C" int lnr_sgd_step(float* param, const float* grad, int64_t n, float lr, void* stream) {

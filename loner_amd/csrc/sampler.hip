@@ -19,26 +19,6 @@ __device__ __forceinline__ float linspace01(int i, int n) {
   return (i < n / 2) ? (0.0f + step * (float)i) : (1.0f - step * (float)(n - 1 - i));
 }
 
-__device__ __forceinline__ float grid_sample(const float* __restrict__ occ, int R, float x, float y, float z) {
-  const float ix = ((x + 1.f) * (float)R - 1.f) / 2.f;
-  const float iy = ((y + 1.f) * (float)R - 1.f) / 2.f;
-  const float iz = ((z + 1.f) * (float)R - 1.f) / 2.f;
-  const float fx = floorf(ix), fy = floorf(iy), fz = floorf(iz);
-  const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
-  const float wx[2] = {(float)(x0 + 1) - ix, ix - (float)x0};
-  const float wy[2] = {(float)(y0 + 1) - iy, iy - (float)y0};
-  const float wz[2] = {(float)(z0 + 1) - iz, iz - (float)z0};
-  float acc = 0.f;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const int bx = c & 1, by = (c >> 1) & 1, bz = (c >> 2) & 1;
-    const int cx = x0 + bx, cy = y0 + by, cz = z0 + bz;
-    const float w = wx[bx] * wy[by] * wz[bz];
-    if (cx >= 0 && cx < R && cy >= 0 && cy < R && cz >= 0 && cz < R) acc += occ[((int64_t)cz * R + cy) * R + cx] * w;
-  }
-  return acc;
-}
-
 struct SamplerArgs {
   const float* rays;
   int64_t n_rays;
@@ -108,7 +88,7 @@ __global__ void __launch_bounds__(SNT) k_sampler(SamplerArgs a) {
     for (int i = t; i < H; i += SNT) {
       const float z = zs[i];
       const float px = ry[0] + ry[3] * z, py = ry[1] + ry[4] * z, pz = ry[2] + ry[5] * z;
-      const float l = grid_sample(a.occ, a.occ_res, px, py, pz);
+      const float l = occ_grid_sample(a.occ, a.occ_res, px, py, pz);
       float p = 1.0f / (1.0f + expf(-l));
       p = 2.0f * (fminf(fmaxf(p, 0.5f), 1.0f) - 0.5f);
       prob[i] = p;
@@ -275,7 +255,7 @@ __global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_wave(SamplerArgs
       zq[q] = z;
       buf[i] = z;
       // 2. occupancy probability (ray_sampling.py:74-81)
-      const float l = grid_sample(a.occ, a.occ_res, ox + dx * z, oy + dy * z, oz + dz * z);
+      const float l = occ_grid_sample(a.occ, a.occ_res, ox + dx * z, oy + dy * z, oz + dz * z);
       float p = 1.0f / (1.0f + expf(-l));
       p = 2.0f * (fminf(fmaxf(p, 0.5f), 1.0f) - 0.5f);
       pq[q] = p;

@@ -1,8 +1,9 @@
 """The north-star driver's LiDAR phase (examples/fdt_optimize_implicit_map.py) as host logic over the
 reference-shaped surface: which scans train and which evaluate, the shuffled keyframe windows, the
 optimiser schedule edits, and the repetition / checkpoint / stop rule.  Scan I/O (rosbag), pose
-interpolation and the metric CSV files stay with the caller: ``run_lidar_phase`` takes the training
-keyframes and two evaluation callables and returns what happened per repetition.
+interpolation stay with the caller: ``run_lidar_phase`` takes the training keyframes and two
+evaluation callables and returns what happened per repetition; given an ``L1MetricsLog``
+(loner_amd/metrics.py) it also writes the reference's metric CSV and YAML files.
 
     DriverSettings        the module constants of fdt_optimize_implicit_map.py:62-74
     split_indices         test / train / eval scan indices (:427-431, :496)
@@ -10,6 +11,9 @@ keyframes and two evaluation callables and returns what happened per repetition.
     repetition_windows    one repetition's shuffled keyframe windows (:574-613)
     StopRule              the repetition loop's checkpoint and stop decisions (:650-727)
     run_lidar_phase       the whole loop (:568-727)
+    PoseInterpolator      ground-truth poses -> scan / image poses (:370-425, :768-783)
+    configure_optimizer_camera, camera_windows, run_camera_phase
+                          the camera phase (:736-757, :834-887; off in the reference, ITERATE_CAMERA)
 
 The random draws use a ``numpy.random.RandomState`` seeded like the reference's ``np.random.seed(8)``:
 the legacy global generator and a RandomState with the same seed produce the same ``choice`` stream,
@@ -139,7 +143,8 @@ def _stats(l1s):
     return dict(min=float(a.min()), max=float(a.max()), mean=float(a.mean()), rmse=float(np.sqrt(np.mean(a * a))))
 
 
-def run_lidar_phase(opt, keyframes, eval_test, eval_eval, cfg: DriverSettings = None, rng=None, save=None):
+def run_lidar_phase(opt, keyframes, eval_test, eval_eval, cfg: DriverSettings = None, rng=None, save=None,
+                    metrics=None):
     """The LiDAR iteration loop (:568-727).
 
     opt        an ``Optimizer`` (loner_amd.optimizer), already configured (``configure_optimizer``)
@@ -149,6 +154,7 @@ def run_lidar_phase(opt, keyframes, eval_test, eval_eval, cfg: DriverSettings = 
     rng        the generator the caller split the scans with (``split_indices``); the shuffles
                continue its stream, as the reference's global generator does
     save       ``save(name, global_step)``, called for every checkpoint the reference writes
+    metrics    an ``L1MetricsLog``: each repetition's test and eval L1s go to its files (:645-677)
     Returns one record per repetition: global step, test and eval L1 statistics, saved
     checkpoint names and the stop reason.
     """
@@ -161,7 +167,11 @@ def run_lidar_phase(opt, keyframes, eval_test, eval_eval, cfg: DriverSettings = 
         losses = []
         for win in repetition_windows(len(keyframes), cfg, rng):
             losses.append(opt.iterate_optimizer([kfs[i] for i in win]))
-        test, ev = _stats(eval_test()), _stats(eval_eval())
+        if metrics is not None:
+            test = metrics.write("test", int(opt._global_step), eval_test())
+            ev = metrics.write("eval", int(opt._global_step), eval_eval())
+        else:
+            test, ev = _stats(eval_test()), _stats(eval_eval())
         saves, reason = rule.after_repetition(ev["mean"], opt._global_step)
         for name in saves:
             if save is not None:
@@ -170,3 +180,134 @@ def run_lidar_phase(opt, keyframes, eval_test, eval_eval, cfg: DriverSettings = 
                             global_step=int(opt._global_step), windows=len(losses), loss=losses,
                             l1_test=test, l1_eval=ev, saved=saves, stop=reason))
     return history
+
+
+# ----------------------------------------------------------------------------- poses
+
+def pose6_to_matrix(p6):
+    """Pose(pose_tensor=[t, axis-angle]).get_transformation_matrix() (pose.py:45-48, pose_utils.py:354-368):
+    (N, 6) or (6,) -> (N, 4, 4) / (4, 4) float32."""
+    from scipy.spatial.transform import Rotation
+    p = np.asarray(p6, dtype=np.float64)
+    one = p.ndim == 1
+    p = p.reshape(-1, 6)
+    T = np.zeros((p.shape[0], 4, 4))
+    T[:, :3, :3] = Rotation.from_rotvec(p[:, 3:]).as_matrix()
+    T[:, :3, 3] = p[:, :3]
+    T[:, 3, 3] = 1.0
+    T = T.astype(np.float32)
+    return T[0] if one else T
+
+
+class PoseInterpolator:
+    """The driver's pose interpolation (fdt_optimize_implicit_map.py:370-425 and :768-783).
+
+    gt_ts          ground-truth timestamps (seconds, absolute)
+    gt_transforms  (N, 4, 4) ground-truth poses; re-expressed relative to the first one
+                   (``inv(T_0) @ T_i``) unless ``submap`` (a submap's poses are already world-frame)
+    Translations interpolate linearly per axis (``np.interp``), rotations by ``Slerp`` over the
+    keyframe rotations; poses come back as (N, 6) [t, axis-angle] rows (``pose6_to_matrix``)."""
+
+    def __init__(self, gt_ts, gt_transforms, submap=False):
+        from scipy.spatial.transform import Rotation, Slerp
+        T = np.asarray(gt_transforms, dtype=np.float64)
+        if not submap:
+            T = np.linalg.inv(T[0])[None] @ T
+        self.first_ts = float(gt_ts[0])
+        self.last_ts = float(gt_ts[-1])
+        self.ts = np.asarray(gt_ts, dtype=np.float64) - self.first_ts
+        self.t = T[:, :3, 3]
+        self.transforms = T
+        self._slerp = Slerp(self.ts, Rotation.from_quat(Rotation.from_matrix(T[:, :3, :3]).as_quat()))
+
+    def at(self, ts_rel):
+        """(N, 6) poses at timestamps relative to the first ground-truth pose."""
+        ts_rel = np.asarray(ts_rel, dtype=np.float64)
+        t = np.stack([np.interp(ts_rel, self.ts, self.t[:, k]) for k in range(3)], axis=1)
+        return np.hstack((t, self._slerp(ts_rel).as_rotvec()))
+
+    def lidar(self, lidar_ts):
+        """:403-425: the scan period (mean spacing, rounded to 10 ms), the scans inside the ground
+        truth (a scan's start, ts - period, at or after the first pose; its end at or before the last),
+        their relative timestamps, poses at the scan ends and at the scan starts (motion compensation)."""
+        lidar_ts = np.asarray(lidar_ts, dtype=np.float64)
+        scan_time = np.round((lidar_ts[-1] - lidar_ts[0]) / len(lidar_ts), 2)
+        keep = (self.first_ts <= lidar_ts - scan_time) * (lidar_ts <= self.last_ts)
+        ts = lidar_ts[keep] - self.first_ts
+        return dict(scan_time=scan_time, ts=ts, poses=self.at(ts), poses_motion_comp=self.at(ts - scan_time))
+
+    def camera(self, camera_ts, scan_time, start=None, end=None, skip=None):
+        """:768-781: the images inside [first pose, last pose - scan period], their relative
+        timestamps and poses, then ``[start:end:skip]`` of both."""
+        camera_ts = np.asarray(camera_ts, dtype=np.float64)
+        keep = (self.first_ts <= camera_ts) * (camera_ts <= self.last_ts - scan_time)
+        ts = camera_ts[keep] - self.first_ts
+        poses = self.at(ts)[start:end:skip, :]
+        return ts[start:end:skip], poses
+
+
+# ----------------------------------------------------------------------------- camera phase
+
+@dataclass
+class CameraPhaseSettings:
+    """fdt_optimize_implicit_map.py:78-90 (camera phase)."""
+    iterate: bool = False  # ITERATE_CAMERA: the reference driver leaves the camera phase off
+    max_window_length: int = 6
+    repetitions: int = 1
+    shuffle: bool = True
+    strategy: str = "FIXED"
+    num_iterations: int = 2 ** 5
+
+
+def configure_optimizer_camera(opt, cfg: CameraPhaseSettings):
+    """:736-757: ground-truth poses, poses and the sigma MLP frozen, the colour MLP trained, camera
+    rays used, no sky segmentation, rays drawn with ``cfg.strategy`` ('FIXED'), and every window
+    running ``num_iterations`` steps."""
+    opt._use_gt_poses = True
+    s = opt._optimization_settings
+    s.freeze_poses, s.freeze_sigma_mlp, s.freeze_rgb_mlp, s.lidar_only = True, True, False, False
+    s.num_iterations = cfg.num_iterations
+    opt._enable_sky_segmentation = False
+    rs = opt._settings.get("rays_selection") if hasattr(opt._settings, "get") else None
+    if rs is not None:
+        rs["strategy"] = cfg.strategy
+    opt._keyframe_count = 1
+    empty = copy.deepcopy(opt._keyframe_schedule[0])
+    empty["num_keyframes"] = -1
+    empty["iteration_schedule"][0].update(num_iterations=cfg.num_iterations, freeze_poses=True,
+                                          freeze_sigma_mlp=True, freeze_rgb_mlp=False)
+    opt._keyframe_schedule = [empty]
+
+
+def camera_windows(n_images, cfg: CameraPhaseSettings, rng):
+    """One repetition's image windows (:835-873): a shuffled order (``choice(n, n, replace=False)``),
+    a window closed at ``max_window_length`` images or at the order's last image."""
+    order = rng.choice(n_images, n_images, replace=False) if cfg.shuffle else np.arange(n_images)
+    order = [int(i) for i in order]
+    wins, win = [], []
+    for i in order:
+        win.append(i)
+        if len(win) == cfg.max_window_length or i == order[-1]:
+            wins.append(win)
+            win = []
+    if win:
+        wins.append(win)
+    return wins
+
+
+def run_camera_phase(opt, frames_of, n_images, cfg: CameraPhaseSettings = None, rng=None, save=None):
+    """The camera loop (:834-887): ``repetitions`` passes over the images in shuffled windows, each
+    window one ``opt.iterate_optimizer_camera(frames_of(indices))`` (``frames_of`` builds the
+    window's ``camera.CameraFrames`` from image indices), then one checkpoint
+    ``reiterate_camera_<global_step>.tar``.  Returns the per-window losses per repetition; nothing
+    runs unless ``cfg.iterate``."""
+    cfg = cfg or CameraPhaseSettings()
+    if not cfg.iterate:
+        return []
+    rng = rng if rng is not None else np.random.RandomState(8)
+    losses = []
+    for _ in range(cfg.repetitions):
+        losses.append([opt.iterate_optimizer_camera(frames_of(w)) for w in camera_windows(n_images, cfg, rng)])
+    if save is not None:
+        save(f"reiterate_camera_{opt._global_step}.tar", opt._global_step)
+    return losses

@@ -91,9 +91,40 @@ class Model(nn.Module):
         return results
 
 
+class _GridSample3d(torch.autograd.Function):
+    """grid_sample on a (1, 1, R, R, R) grid at (..., 3) points on the HIP path (lnr_grid_sample3d and
+    its deterministic backward): the values, and the grid's gradient on backward."""
+
+    @staticmethod
+    def forward(ctx, grid, pts):
+        from . import _lib as L
+        R = grid.shape[-1]
+        p = pts.detach().reshape(-1, 3).contiguous()
+        out = torch.empty(p.shape[0], dtype=torch.float32, device=grid.device)
+        L.call("lnr_grid_sample3d", grid.detach().contiguous(), R, p, p.shape[0], out, L.stream(grid.device))
+        ctx.save_for_backward(p)
+        ctx.res = R
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from . import _lib as L
+        if ctx.needs_input_grad[1]:
+            raise NotImplementedError("OccupancyGridModel.interpolate: no gradient for the points "
+                                      "(the reference's points are detached)")
+        (p,) = ctx.saved_tensors
+        R = ctx.res
+        ws = torch.empty(int(L.lib().lnr_grid_sample3d_bwd_workspace_words(R)), dtype=torch.float32, device=p.device)
+        dgrid = torch.empty(1, 1, R, R, R, dtype=torch.float32, device=p.device)
+        L.call("lnr_grid_sample3d_bwd", p, dout.reshape(-1).contiguous().float(), p.shape[0], R, dgrid, ws, ws.numel(),
+               L.stream(p.device))
+        return dgrid, None
+
+
 class OccupancyGridModel(nn.Module):
-    """model_tcnn.py:111-134.  ``interpolate`` is torch's grid_sample (the OGM update's autograd
-    uses it); the sampler's own lookup is fused into the HIP sampler kernel."""
+    """model_tcnn.py:111-134.  ``interpolate`` runs lnr_grid_sample3d (forward) and
+    lnr_grid_sample3d_bwd (the grid's gradient, what _step_occupancy_grid backpropagates,
+    optimizer.py:897-908); the sampler's own lookup is fused into the HIP sampler kernel."""
 
     def __init__(self, cfg, device=None):
         super().__init__()
@@ -106,7 +137,16 @@ class OccupancyGridModel(nn.Module):
 
     @staticmethod
     def interpolate(occupancy_grid, ray_bin_centers, mode='bilinear'):
+        """grid_sample(occupancy_grid, points, mode, align_corners=False) -> (n_rays, n_bins), for a
+        (1, 1, R, R, R) fp32 device grid and (n_rays, n_bins, 3) points; ``mode`` 'bilinear' (the
+        reference's only use).  Anything else raises: there is no host fallback."""
         n_rays, n_bins, _ = ray_bin_centers.shape
-        grid_values = ray_bin_centers.reshape(1, 1, n_rays, n_bins, 3)
-        return nn.functional.grid_sample(occupancy_grid, grid_values, mode=mode,
-                                         align_corners=False).reshape(n_rays, n_bins)
+        g = occupancy_grid
+        if mode != 'bilinear':
+            raise NotImplementedError(f"OccupancyGridModel.interpolate: mode={mode!r} (only 'bilinear')")
+        if not (g.is_cuda and ray_bin_centers.is_cuda and g.dtype == torch.float32 and
+                ray_bin_centers.dtype == torch.float32 and g.dim() == 5 and g.shape[:2] == (1, 1) and
+                g.shape[2] == g.shape[3] == g.shape[4]):
+            raise ValueError("OccupancyGridModel.interpolate: needs a (1, 1, R, R, R) fp32 device grid and "
+                             "fp32 device points")
+        return _GridSample3d.apply(g, ray_bin_centers).reshape(n_rays, n_bins)

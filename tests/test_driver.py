@@ -124,3 +124,110 @@ def test_run_lidar_phase_schedule():
     assert saved == [("final.tar", 12), ("final_24.tar", 24), ("final_36.tar", 36)]
     assert hist[-1]["stop"] == "worse_than_previous"  # saved for reaching the maximum, then found worse
     assert hist[0]["l1_test"]["mean"] == 1.5 and math.isclose(hist[0]["l1_test"]["rmse"], math.sqrt(2.5))
+
+
+def test_metric_files_in_reference_format(tmp_path):
+    """The files fdt_optimize_implicit_map.py:548-562,645-677 writes: both CSVs created with their
+    header before the loop, one row per repetition, and a YAML per (kind, global step) holding the
+    0-d tensors' format (the float32 value, in Python's repr), without a trailing newline."""
+    import csv
+
+    import torch
+
+    from loner_amd.metrics import L1MetricsLog
+    cfg = D.DriverSettings(repetitions_max=2, num_iterations=4)
+    opt = _FakeOpt()
+    D.configure_optimizer(opt, cfg)
+    rng = np.random.RandomState(cfg.seed)
+    _, train, _ = D.split_indices(40, cfg, rng)
+    log = L1MetricsLog(tmp_path)
+    for kind in ("test", "eval"):
+        assert (tmp_path / "metrics" / f"l1_{kind}.csv").read_text() == "global_step,min,max,mean,rmse\n"
+    evals = iter([[torch.tensor([1.5, 2.5])], [torch.tensor([0.25]), torch.tensor([0.75])]])
+    hist = D.run_lidar_phase(opt, [f"kf{i}" for i in train], lambda: torch.tensor([1.0, 2.0, 4.0]),
+                             lambda: next(evals), cfg, rng, metrics=log)
+    assert [h["global_step"] for h in hist] == [12, 24]
+    t = torch.tensor([1.0, 2.0, 4.0])
+    rmse = torch.sqrt(torch.mean(t ** 2))
+    assert (tmp_path / "metrics_test" / "l1_12.yaml").read_text() == \
+        f"min: {t.min()}\nmax: {t.max()}\nmean: {t.mean()}\nrmse: {rmse}"
+    assert (tmp_path / "metrics_test" / "l1_12.yaml").read_text().startswith("min: 1.0\nmax: 4.0\nmean: 2.3333332538604736")
+    rows = list(csv.reader(open(tmp_path / "metrics" / "l1_test.csv")))
+    assert rows[0] == ["global_step", "min", "max", "mean", "rmse"]
+    assert [r[0] for r in rows[1:]] == ["12", "24"]
+    assert rows[1][1:4] == ["1.0", "4.0", str(np.float32(7.0 / 3.0))]
+    ev = list(csv.reader(open(tmp_path / "metrics" / "l1_eval.csv")))
+    assert ev[2][1:4] == ["0.25", "0.75", "0.5"]  # the per-scan tensors joined (torch.hstack)
+    assert hist[1]["l1_eval"]["mean"] == 0.5
+
+
+def _rand_transforms(rng, n):
+    from scipy.spatial.transform import Rotation
+    T = np.tile(np.eye(4), (n, 1, 1))
+    T[:, :3, :3] = Rotation.from_rotvec(rng.normal(0, 0.4, (n, 3))).as_matrix()
+    T[:, :3, 3] = np.cumsum(rng.normal(0, 1.0, (n, 3)), axis=0)
+    return T
+
+
+def test_pose_interpolator():
+    """fdt_optimize_implicit_map.py:370-425,768-783: relative to the first pose (not for submaps), exact
+    at the ground-truth stamps, linear translation / slerp rotation between them, the scan-period rule
+    for which scans and images are kept, [start:end:skip] of the images."""
+    from scipy.spatial.transform import Rotation
+    rng = np.random.default_rng(3)
+    ts = 100.0 + np.cumsum(rng.uniform(0.05, 0.15, 30))
+    T = _rand_transforms(rng, 30)
+    pi = D.PoseInterpolator(ts, T)
+    rel = np.linalg.inv(T[0]) @ T
+    P = D.pose6_to_matrix(pi.at(ts - ts[0]))
+    np.testing.assert_allclose(P, rel, atol=2e-6)
+    assert P.dtype == np.float32
+    np.testing.assert_allclose(D.pose6_to_matrix(D.PoseInterpolator(ts, T, submap=True).at(ts - ts[0])), T, atol=2e-5)
+    mid = 0.5 * (ts[4] + ts[5]) - ts[0]
+    p = pi.at([mid])[0]
+    np.testing.assert_allclose(p[:3], 0.5 * (rel[4, :3, 3] + rel[5, :3, 3]), atol=1e-9)
+    r4, r5 = Rotation.from_matrix(rel[4, :3, :3]), Rotation.from_matrix(rel[5, :3, :3])
+    half = r4 * Rotation.from_rotvec(0.5 * (r4.inv() * r5).as_rotvec())
+    np.testing.assert_allclose(Rotation.from_rotvec(p[3:]).as_matrix(), half.as_matrix(), atol=1e-9)
+    lidar_ts = np.arange(ts[0] - 0.3, ts[-1] + 0.3, 0.1)
+    out = pi.lidar(lidar_ts)
+    assert out["scan_time"] == np.round((lidar_ts[-1] - lidar_ts[0]) / len(lidar_ts), 2)
+    st = out["scan_time"]
+    keep = lidar_ts[(lidar_ts - st >= ts[0]) & (lidar_ts <= ts[-1])]
+    np.testing.assert_allclose(out["ts"], keep - ts[0])
+    np.testing.assert_allclose(out["poses_motion_comp"], pi.at(keep - ts[0] - st))
+    cam_ts = np.arange(ts[0] - 0.2, ts[-1] + 0.2, 0.07)
+    cts, cposes = pi.camera(cam_ts, st, start=1, end=None, skip=2)
+    inside = cam_ts[(cam_ts >= ts[0]) & (cam_ts <= ts[-1] - st)] - ts[0]
+    np.testing.assert_allclose(cts, inside[1::2])
+    np.testing.assert_allclose(cposes, pi.at(inside)[1::2])
+
+
+def test_camera_phase():
+    """:736-757 schedule edits; :834-887 windows of 6 closed at the order's last image, one
+    iterate_optimizer_camera per window, `reiterate_camera_<step>.tar` at the end; off by default."""
+    cfg = D.CameraPhaseSettings(iterate=True, repetitions=2, num_iterations=3)
+    opt = _FakeOpt()
+    opt._optimization_settings = type("S", (), {})()
+    D.configure_optimizer_camera(opt, cfg)
+    s = opt._optimization_settings
+    assert (s.freeze_poses, s.freeze_sigma_mlp, s.freeze_rgb_mlp, s.lidar_only, s.num_iterations) == \
+        (True, True, False, False, 3)
+    assert opt._use_gt_poses and opt._settings["rays_selection"]["strategy"] == "FIXED"
+    it = opt._keyframe_schedule[0]["iteration_schedule"][0]
+    assert opt._keyframe_schedule[0]["num_keyframes"] == -1 and it["freeze_sigma_mlp"] and not it["freeze_rgb_mlp"]
+    rng = np.random.RandomState(8)
+    wins = D.camera_windows(15, cfg, np.random.RandomState(8))
+    assert [len(w) for w in wins] == [6, 6, 3] and sorted(sum(wins, [])) == list(range(15))
+    calls, saved = [], []
+
+    def cam(frames):
+        calls.append(frames)
+        opt._global_step += 3
+        return 0.5
+
+    opt.iterate_optimizer_camera = cam
+    losses = D.run_camera_phase(opt, lambda w: list(w), 15, cfg, rng, save=lambda n, st: saved.append(n))
+    assert [len(x) for x in losses] == [3, 3] and len(calls) == 6
+    assert saved == [f"reiterate_camera_{opt._global_step}.tar"]
+    assert D.run_camera_phase(opt, list, 15, D.CameraPhaseSettings()) == []  # ITERATE_CAMERA = False

@@ -299,3 +299,67 @@ def test_render_rays_sigma_only_vs_oracle(tc):
     # rendered-depth L1 in metres (BASELINE.json metric), GPU vs oracle on identical rays/draws
     l1 = np.abs(host(res["depth_fine"]) - ro["depth"]).mean() * 121.426537
     assert l1 < 1e-3, l1
+
+
+# ----------------------------------------------------------------- OccupancyGridModel.interpolate
+def test_occupancy_interpolate_golden_and_backward(tc):
+    """OccupancyGridModel.interpolate on the HIP path (lnr_grid_sample3d / _bwd): the values against
+    the reference's own interpolate (samplers.npz, make_golden.py:260-262); _step_occupancy_grid's
+    pattern (optimizer.py:897-908: backward with the logits gradient, then SGD) against the
+    reference's occupancy update (loss_l1js_default.npz); a deterministic backward; and the grid
+    gradient for arbitrary points and output gradients against torch's fp64 grid_sample backward."""
+    from loner_amd import model as M
+    from oracle import loss as oloss
+    s = np.load("tests/golden/samplers.npz")
+    occ = torch.from_numpy(s["occ"]).reshape(1, 1, 100, 100, 100).cuda()
+    v = M.OccupancyGridModel.interpolate(occ, torch.from_numpy(s["pts"]).cuda())
+    assert v.shape == s["interp"].shape
+    np.testing.assert_allclose(host(v), s["interp"], rtol=1e-6, atol=1e-6)
+    g = np.load("tests/golden/loss_l1js_default.npz")
+    rays, z, dgt, scale = g["rays"], g["z"], g["depth_gt"], np.float32(g["scale"])
+    pts = (rays[:, None, 0:3] + rays[:, None, 3:6] * z[:, :, None]).astype(np.float32)
+    lg = oloss.logits_grad((z * scale).astype(np.float32), (dgt * scale).astype(np.float32))
+    model = M.OccupancyGridModel(dict(voxel_size=100), device="cuda")
+    with torch.no_grad():
+        model.occupancy_grid.copy_(occ)
+    opt = torch.optim.SGD(model.parameters(), lr=float(g["occ_lr"]))
+    grads = []
+    for _ in range(2):
+        model.occupancy_grid.grad = None
+        logits = M.OccupancyGridModel.interpolate(model(), torch.from_numpy(pts).cuda())
+        logits.backward(gradient=torch.from_numpy(lg).cuda())
+        grads.append(model.occupancy_grid.grad.clone())
+    assert torch.equal(grads[0], grads[1])  # int64 fixed point: the atomics' order does not matter
+    opt.step()
+    delta = host(model.occupancy_grid).reshape(-1) - s["occ"].reshape(-1)
+    idx = g["occ_delta_idx"]
+    np.testing.assert_allclose(delta[idx], g["occ_delta"], rtol=1e-3, atol=2e-7)
+    mask = np.ones(delta.size, bool)
+    mask[idx] = False
+    assert np.abs(delta[mask]).max() < 1e-7
+    # arbitrary points (some outside the grid) and gradients spanning six decades
+    rng = np.random.default_rng(4)
+    P = rng.uniform(-1.1, 1.1, (64, 97, 3)).astype(np.float32)
+    P[:, :40] = P[:, :1] + rng.normal(0, 0.004, (64, 40, 3)).astype(np.float32)  # clustered: shared voxels
+    dout = (rng.normal(size=(64, 97)) * 10.0 ** rng.uniform(-3, 3, (64, 97))).astype(np.float32)
+    gcpu = torch.from_numpy(s["occ"]).double().reshape(1, 1, 100, 100, 100).requires_grad_(True)
+    ref_v = torch.nn.functional.grid_sample(gcpu, torch.from_numpy(P).double().reshape(1, 1, 64, 97, 3),
+                                            mode="bilinear", align_corners=False).reshape(64, 97)
+    ref_v.backward(torch.from_numpy(dout).double())
+    gdev = occ.clone().requires_grad_(True)
+    got_v = M.OccupancyGridModel.interpolate(gdev, torch.from_numpy(P).cuda())
+    got_v.backward(torch.from_numpy(dout).cuda())
+    # fp32 source coordinates: ix = ((x + 1) R - 1) / 2 rounds to ~1e-5 voxels, times grid slopes of up to
+    # 20 per voxel: torch's own fp32 grid_sample differs from fp64 by 2e-4 here, so the values are
+    # checked against torch fp32 (same arithmetic) and the gradient against fp64 at 2e-5 of its max
+    # (torch fp32's own error: 6.7e-6)
+    v32 = torch.nn.functional.grid_sample(torch.from_numpy(s["occ"]).reshape(1, 1, 100, 100, 100),
+                                          torch.from_numpy(P).reshape(1, 1, 64, 97, 3), mode="bilinear",
+                                          align_corners=False).reshape(64, 97).numpy()
+    np.testing.assert_allclose(host(got_v), v32, rtol=1e-6, atol=4e-6)
+    assert np.abs(host(got_v) - ref_v.detach().numpy()).max() < 5e-4
+    ref_g = gcpu.grad.numpy().reshape(-1)
+    got_g = host(gdev.grad).reshape(-1)
+    assert np.abs(got_g - ref_g).max() <= 2e-5 * np.abs(ref_g).max(), np.abs(got_g - ref_g).max()
+    with pytest.raises(ValueError):
+        M.OccupancyGridModel.interpolate(occ.cpu(), torch.from_numpy(P))

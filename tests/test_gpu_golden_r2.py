@@ -70,6 +70,48 @@ def test_colour_render_weights_golden(L):
     np.testing.assert_allclose(rgb, g["rgb"], rtol=1e-5, atol=1e-5)
 
 
+def _passthrough_colour_mlp(n_hidden_layers=4):
+    """tcnn-flat weights of a colour network that hands its first three inputs through: W0 puts relu(x_j)
+    and relu(-x_j) on hidden units 2j and 2j + 1, the hidden layers are identities on them and the output
+    layer takes their difference, so the network's output j is x_j exactly (every value fp16, every
+    product by +-1)."""
+    mats = [np.zeros((64, 48), np.float32)] + [np.eye(64, dtype=np.float32)] * (n_hidden_layers - 1) + \
+        [np.zeros((16, 64), np.float32)]
+    for j in range(3):
+        mats[0][2 * j, j], mats[0][2 * j + 1, j] = 1.0, -1.0
+        mats[-1][j, 2 * j], mats[-1][j, 2 * j + 1] = 1.0, -1.0
+    return np.concatenate([m.reshape(-1) for m in mats]).astype(np.float16)
+
+
+def test_colour_map_golden_through_rgb_render(L):
+    """lnr_rgb_render's own colour map (rgb = sum w c + 1 - sum w, rendering_tcnn.py:283-289) on the
+    fixture's colours: the colour-grid encodings carry the colours' logits into a pass-through network
+    (_passthrough_colour_mlp), so the kernel's sigmoid gives back the reference's colours (to fp16) and
+    its compositing runs on the HIP weights of the fixture's sigma, z and noise."""
+    g = np.load(os.path.join(GOLDEN, "camera_loss.npz"))
+    rays, z, sig, noise, col = g["rays"], g["z"], g["sigma"], g["noise"], g["colors"].astype(np.float64)
+    R, S = z.shape
+    w = torch.empty(R, S, dtype=torch.float32, device="cuda")
+    d = torch.empty(R, dtype=torch.float32, device="cuda")
+    L.call("lnr_composite", cu(rays), cu(z), cu(sig), R, S, 0, 1.0, cu(noise), 0, 0, w, d, None, None, L.stream())
+    c = np.clip(col, 1e-7, 1 - 1e-7)
+    logit = np.clip(np.log(c) - np.log1p(-c), -15.0, 15.0).astype(np.float16).reshape(R * S, 3)
+    feats = np.zeros((16, R * S, 2), np.float16)  # level-major half2: level l holds features 2l, 2l + 1
+    feats[0, :, 0], feats[0, :, 1], feats[1, :, 0] = logit[:, 0], logit[:, 1], logit[:, 2]
+    enc = cu(feats.view(np.uint32).reshape(16, R * S))
+    mlp = cu(_passthrough_colour_mlp().view(np.uint16))
+    rgb = torch.empty(R, 3, dtype=torch.float32, device="cuda")
+    L.call("lnr_rgb_render", mlp, 4, enc, R * S, cu(rays), w, R, S, rgb, L.stream())
+    got, wg = host(rgb), host(w).astype(np.float64)
+    # the kernel's arithmetic: colour = fp16(sigmoid(fp16 logit)), fp32 sums of w c
+    col16 = (1.0 / (1.0 + np.exp(-logit.astype(np.float32)))).astype(np.float16).astype(np.float64).reshape(R, S, 3)
+    emu = (wg[..., None] * col16).sum(1) + (1 - wg.sum(1, keepdims=True))
+    np.testing.assert_allclose(got, emu, rtol=1e-5, atol=2e-6)
+    # and the reference's rgb: the colours differ from the fixture's by the fp16 logit and colour roundings
+    # (|dc| <= 0.23 * 2^-11 + 2^-12)
+    np.testing.assert_allclose(got, g["rgb"], rtol=0, atol=5e-4)
+
+
 def test_adam_with_tcnn_fp16_gradients_golden(L):
     """lnr_adam_step fed the fp16-rounded gradients tcnn's binding hands back, against torch.optim.Adam on
     an fp32 parameter (the reference's literal fp16-parameter Adam is non-finite after one step at these

@@ -195,27 +195,40 @@ def test_step_engine_one_step_vs_oracle(L):
 
 
 def _assert_accum_paths_equal(L, st, rays, eng, R, Sn, g_ref=None):
-    """Both accumulation paths (LONER_ACCUM_BUCKETS_MAX_N switches them at each launch) give the same
-    gradient (and g_ref, when given); returns it."""
+    """Every accumulation path (LONER_ACCUM_UNITS, LONER_ACCUM_BUCKETS_MAX_N and LONER_ACCUM_FINISH
+    switch them at each launch) gives the same gradient bitwise, behind each scatter kernel: the level-looped one and one
+    workgroup per (row, level) (LONER_SCATTER_ROWS_MIN switches them), whose coherent-level run sums
+    may group their fp32 additions differently (close, not bitwise).  g_ref, when given, is bitwise one of the
+    two; returns both (level-looped, per (row, level))."""
     import os
     s = L.stream()
-    keys = ("LONER_ACCUM_BUCKETS_MAX_N", "LONER_ACCUM_FINISH")
+    keys = ("LONER_ACCUM_UNITS", "LONER_ACCUM_BUCKETS_MAX_N", "LONER_ACCUM_FINISH", "LONER_SCATTER_ROWS_MIN")
     old = {k: os.environ.get(k) for k in keys}
-    out = []
+    big = str(1 << 40)
+    # the unit work list (default), record-balanced with in-kernel finishing (twice: arrival order
+    # varies), with k_bwd_finalize, and whole buckets
+    accums = (("1", "0", "0"), ("0", "0", "1"), ("0", "0", "1"), ("0", "0", "0"), ("0", big, "0"))
+    groups = {"rows": [a + ("0",) for a in accums], "row_level": [a + (big,) for a in accums]}
+    out = {}
     try:
-        # record-balanced with in-kernel finishing (twice: arrival order varies), with k_bwd_finalize,
-        # and whole buckets
-        for thr, fin in (("0", "1"), ("0", "1"), ("0", "0"), (str(1 << 40), "1")):
-            os.environ["LONER_ACCUM_BUCKETS_MAX_N"], os.environ["LONER_ACCUM_FINISH"] = thr, fin
-            g = torch.full((2 * st.n_entries,), float("nan"), dtype=torch.float32, device="cuda")  # all written
-            L.call("lnr_hashgrid_bwd_rays_jac", L.ctypes.byref(st.desc), rays, eng.z, R, Sn, eng.d_jac, eng.d_sigma(),
-                   R * Sn, g, eng.bwd_ws, eng.bwd_ws_bytes, 0, s)
-            out.append(g)
-        for g in out[1:]:
-            assert torch.equal(out[0], g)
+        for name, settings in groups.items():
+            out[name] = []
+            for setting in settings:
+                for k, v in zip(keys, setting):
+                    os.environ[k] = v
+                g = torch.full((2 * st.n_entries,), float("nan"), dtype=torch.float32, device="cuda")  # all written
+                L.call("lnr_hashgrid_bwd_rays_jac", L.ctypes.byref(st.desc), rays, eng.z, R, Sn, eng.d_jac,
+                       eng.d_sigma(), R * Sn, g, eng.bwd_ws, eng.bwd_ws_bytes, 0, s)
+                out[name].append(g)
+        for name, gs in out.items():
+            bad = [(groups[name][i], float((g - gs[0]).abs().max())) for i, g in enumerate(gs) if not torch.equal(g, gs[0])]
+            assert not bad, (name, bad)
+        a, b = out["rows"][0], out["row_level"][0]
+        # a differently grouped run sum can round its fp16 record the other way: measured 1.1e-6 at C1
+        assert float((a - b).norm() / b.norm()) < 2e-5
         if g_ref is not None:
-            assert torch.equal(out[0], g_ref)
-        return out[0]
+            assert torch.equal(a, g_ref) or torch.equal(b, g_ref)
+        return a, b
     finally:
         for k in keys:
             if old[k] is None:
@@ -235,7 +248,7 @@ def test_accum_paths_small_batch(L):
     st = S_.FieldState(S_.StepConfig(n_samples=64), device="cuda:0", table_init=0.5)
     eng = S_.StepEngine(st, rays.shape[0], seed=4)
     eng.step(rays, dgt, global_step=1, scale=syn.CUBES["quad"][0], far_ref=float(rays[0, -1]))
-    g = _assert_accum_paths_equal(L, st, rays, eng, rays.shape[0], 64)
+    _, g = _assert_accum_paths_equal(L, st, rays, eng, rays.shape[0], 64)  # (C1's scatter: per (row, level))
     assert int((g != 0).sum()) > 0 and int((g == 0).sum()) > 0
     # the step's own gradient (histogram counted in the forward) agrees to the fixed-point unit
     torch.testing.assert_close(st.grad_table, g, rtol=1e-6, atol=1e-12)

@@ -22,7 +22,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BWD_KERNELS = ("k_bwd_chunk_sums", "k_bwd_scan_rows", "k_bwd_scan_buckets", "k_bwd_scatter_rows",
-               "k_bwd_scatter_overflow", "k_bwd_scatter", "k_denc_level_max", "k_bwd_accum", "k_bwd_finalize")
+               "k_bwd_scatter", "k_denc_level_max", "k_bwd_accum", "k_bwd_finalize", "k_bwd_accum_units",
+               "k_bwd_finalize_units", "k_bwd_accum_buckets", "k_bwd_units")
 
 
 def per_dispatch(path):
