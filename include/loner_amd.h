@@ -360,6 +360,19 @@ int lnr_rgb_train(const uint16_t* w_rgb, int32_t n_hidden_layers, const uint32_t
 /* torch.optim.Adam (no weight decay); step is 1-based.  shadow (fp16) may be NULL. */
 int lnr_adam_step(float* param, uint16_t* shadow, const float* grad, float* m, float* v, int64_t n, int32_t step,
                   double lr, double beta1, double beta2, double eps, void* stream);
+/* The same step over up to LNR_ADAM_MAX_RANGES independent ranges in one launch (the sharded
+ * optimiser's per-level-range chunks, loner_amd.step.StepEngine(zero=...)). */
+#define LNR_ADAM_MAX_RANGES 8
+typedef struct lnr_adam_range {
+  float* param;
+  uint16_t* shadow; /* may be NULL */
+  const float* grad;
+  float* m;
+  float* v;
+  int64_t n;
+} lnr_adam_range;
+int lnr_adam_step_ranges(const lnr_adam_range* ranges, int32_t n_ranges, int32_t step, double lr, double beta1,
+                         double beta2, double eps, void* stream);
 /* OGM update: occ (res^3) -= lr * grid_sample^T(logits_grad(z*scale - depth_gt*scale)).  grad_ws is
  * workspace of ws_words fp32 (lnr_ogm_workspace_words(occ_res) for full speed; at least 3 res^3):
  * the splat accumulates in int64 fixed point in replicas of the grid that spread same-voxel

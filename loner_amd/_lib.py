@@ -41,6 +41,15 @@ class GridDesc(ctypes.Structure):
                 ("size", ctypes.c_uint32 * MAX_LEVELS), ("offset", ctypes.c_uint32 * (MAX_LEVELS + 1))]
 
 
+class AdamRange(ctypes.Structure):
+    """lnr_adam_range (include/loner_amd.h)."""
+    _fields_ = [("param", ctypes.c_void_p), ("shadow", ctypes.c_void_p), ("grad", ctypes.c_void_p),
+                ("m", ctypes.c_void_p), ("v", ctypes.c_void_p), ("n", ctypes.c_int64)]
+
+
+ADAM_MAX_RANGES = 8
+
+
 class LossParams(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int32), ("scale", ctypes.c_float), ("los_lambda", ctypes.c_float),
                 ("depthloss_lambda", ctypes.c_float), ("min_depth_eps", ctypes.c_float),
@@ -149,6 +158,7 @@ _SIGNATURES = {
     "lnr_build_lidar_rays": (ctypes.c_int, [ctypes.POINTER(RayWindowDesc), c_i32, c_p, c_u32, c_i64, c_i64, c_p, c_p,
                                             c_p, c_p, c_p, c_p]),
     "lnr_adam_step": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i32, c_d, c_d, c_d, c_d, c_p]),
+    "lnr_adam_step_ranges": (ctypes.c_int, [c_p, c_i32, c_i32, c_d, c_d, c_d, c_d, c_p]),
     "lnr_ogm_workspace_words": (c_i64, [c_i32]),
     "lnr_ogm_update": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_f, c_f, c_p, c_p, c_i64, c_i32, c_p]),
     "lnr_ogm_grad": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_i64, c_i32, c_p]),

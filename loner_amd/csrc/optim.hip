@@ -10,13 +10,13 @@
 
 namespace lnr {
 
-__global__ void __launch_bounds__(256) k_adam(float* __restrict__ p, uint16_t* __restrict__ shadow,
-                                              const float* __restrict__ g, float* __restrict__ m,
-                                              float* __restrict__ v, int64_t n, float one_minus_b1, float b2,
-                                              float one_minus_b2, float step_size, float bc2_sqrt, float eps) {
+__device__ __forceinline__ void adam_range(float* __restrict__ p, uint16_t* __restrict__ shadow,
+                                           const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+                                           int64_t n, float one_minus_b1, float b2, float one_minus_b2,
+                                           float step_size, float bc2_sqrt, float eps, uint32_t bx, uint32_t nbx) {
   const int64_t n4 = n / 4;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+  const int64_t stride = (int64_t)nbx * blockDim.x;
+  for (int64_t i = (int64_t)bx * blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 pp = reinterpret_cast<float4*>(p)[i];
     const float4 gg = reinterpret_cast<const float4*>(g)[i];
     float4 mm = reinterpret_cast<float4*>(m)[i];
@@ -43,7 +43,7 @@ __global__ void __launch_bounds__(256) k_adam(float* __restrict__ p, uint16_t* _
     }
   }
   // tail
-  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+  if (bx == 0 && threadIdx.x < (n & 3)) {
     const int64_t i = n4 * 4 + threadIdx.x;
     float mk = m[i] + one_minus_b1 * (g[i] - m[i]);
     float vk = v[i] * b2 + one_minus_b2 * g[i] * g[i];
@@ -53,6 +53,25 @@ __global__ void __launch_bounds__(256) k_adam(float* __restrict__ p, uint16_t* _
     p[i] = pk;
     if (shadow) shadow[i] = f2h(pk);
   }
+}
+
+__global__ void __launch_bounds__(256) k_adam(float* __restrict__ p, uint16_t* __restrict__ shadow,
+                                              const float* __restrict__ g, float* __restrict__ m,
+                                              float* __restrict__ v, int64_t n, float one_minus_b1, float b2,
+                                              float one_minus_b2, float step_size, float bc2_sqrt, float eps) {
+  adam_range(p, shadow, g, m, v, n, one_minus_b1, b2, one_minus_b2, step_size, bc2_sqrt, eps, blockIdx.x, gridDim.x);
+}
+
+// Several ranges in one launch (the sharded optimiser's chunks, one per level range): blockIdx.y
+// is the range.
+struct AdamRanges {
+  lnr_adam_range r[LNR_ADAM_MAX_RANGES];
+};
+__global__ void __launch_bounds__(256) k_adam_ranges(AdamRanges rs, float one_minus_b1, float b2, float one_minus_b2,
+                                                     float step_size, float bc2_sqrt, float eps) {
+  const lnr_adam_range& r = rs.r[blockIdx.y];
+  adam_range(r.param, r.shadow, r.grad, r.m, r.v, r.n, one_minus_b1, b2, one_minus_b2, step_size, bc2_sqrt, eps,
+             blockIdx.x, gridDim.x);
 }
 
 // logits "gradient" of losses.py:54-62 with eps=2, l_free=0.25, l_occ=2.5; H(0)=0.
@@ -260,6 +279,33 @@ extern "C" int lnr_adam_step(float* param, uint16_t* shadow, const float* grad, 
   hipLaunchKernelGGL(k_adam, dim3(grid1d(n / 4, 8192)), dim3(256), 0, as_stream(stream), param, shadow, grad, m, v, n,
                      (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), step_size, bc2_sqrt, (float)eps);
   LNR_RETURN_LAUNCH("lnr_adam_step");
+}
+
+extern "C" int lnr_adam_step_ranges(const lnr_adam_range* ranges, int32_t n_ranges, int32_t step, double lr,
+                                    double beta1, double beta2, double eps, void* stream) {
+  LNR_REQUIRE(n_ranges >= 0 && n_ranges <= LNR_ADAM_MAX_RANGES && step >= 1,
+              "lnr_adam_step_ranges: n_ranges=%d (at most %d) step=%d", n_ranges, LNR_ADAM_MAX_RANGES, step);
+  if (n_ranges == 0) return LNR_OK;
+  LNR_REQUIRE(ranges != nullptr, "lnr_adam_step_ranges: null ranges");
+  AdamRanges rs{};
+  int64_t nmax = 0;
+  for (int i = 0; i < n_ranges; ++i) {
+    const lnr_adam_range& r = ranges[i];
+    LNR_REQUIRE(r.n >= 0, "lnr_adam_step_ranges: range %d: n < 0", i);
+    LNR_REQUIRE(r.n == 0 || (r.param && r.grad && r.m && r.v), "lnr_adam_step_ranges: range %d: null pointer", i);
+    LNR_REQUIRE(((uintptr_t)r.param | (uintptr_t)r.grad | (uintptr_t)r.m | (uintptr_t)r.v) % 16 == 0 &&
+                    (r.shadow == nullptr || (uintptr_t)r.shadow % 8 == 0),
+                "lnr_adam_step_ranges: range %d: buffers must be 16-byte aligned", i);
+    rs.r[i] = r;
+    nmax = r.n > nmax ? r.n : nmax;
+  }
+  if (nmax == 0) return LNR_OK;
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);  // (as lnr_adam_step)
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  hipLaunchKernelGGL(k_adam_ranges, dim3(grid1d(nmax / 4, 8192), n_ranges), dim3(256), 0, as_stream(stream), rs,
+                     (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)(lr / bc1), (float)std::sqrt(bc2),
+                     (float)eps);
+  LNR_RETURN_LAUNCH("lnr_adam_step_ranges");
 }
 
 extern "C" int64_t lnr_ogm_workspace_words(int32_t occ_res) {

@@ -219,6 +219,8 @@ class StepEngine:
                     raise ValueError(f"levels [{l0}, {l1}) hold {a1 - a0} parameters, not a multiple of 4 x {zw} ranks "
                                      "(the sharded optimiser needs equal, 16-B aligned chunks)")
                 self.zero_chunks.append((a0, a1, (a1 - a0) // zw))
+            if len(self.zero_chunks) > L.ADAM_MAX_RANGES:
+                raise ValueError(f"{len(self.zero_chunks)} level ranges: at most {L.ADAM_MAX_RANGES} (one Adam launch)")
             self.zero_grad = [torch.empty(c, dtype=torch.float32, device=dev) for _, _, c in self.zero_chunks]
         self.z = torch.empty(n_rays, self.S, dtype=torch.float32, device=dev)
         self.enc = torch.empty(self.cfg.n_levels, self.N, dtype=torch.int32, device=dev)
@@ -436,11 +438,15 @@ class StepEngine:
             m(prof, "grid_bwd")
         st.adam_step += 1
         m(prof, "adam")
-        for (a0, a1, c), g in zip(self.zero_chunks, self.zero_grad):
+        # this rank's chunk of every level range, one launch (lnr_adam_step_ranges)
+        rng = (L.AdamRange * len(self.zero_chunks))()
+        for i, ((a0, a1, c), g) in enumerate(zip(self.zero_chunks, self.zero_grad)):
             o = a0 + zr * c
             grad = g if comm else st.grad[o:o + c]
-            L.call("lnr_adam_step", st.params[o:o + c], st.shadow[o:o + c], grad, st.m[o:o + c], st.v[o:o + c], c,
-                   st.adam_step, cfg.lr * self.lr_factor, 0.9, 0.999, 1e-8, s)
+            rng[i] = L.AdamRange(L.ptr(st.params[o:o + c]), L.ptr(st.shadow[o:o + c]), L.ptr(grad),
+                                 L.ptr(st.m[o:o + c]), L.ptr(st.v[o:o + c]), c)
+        L.call("lnr_adam_step_ranges", rng, len(self.zero_chunks), st.adam_step, cfg.lr * self.lr_factor, 0.9, 0.999,
+               1e-8, s)
         m(prof, "adam")
         if comm:
             m(prof, "allgather")

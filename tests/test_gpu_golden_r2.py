@@ -139,3 +139,29 @@ def test_checkpoint_matches_reference_keys(L):
     d = ck.build_ckpt(st, 7, other_params=ck.color_params(cs))
     assert {k: list(v.shape) for k, v in d["network_state_dict"].items()} == keys["network_state_dict"]
     assert {k: list(v.shape) for k, v in d["occ_model_state_dict"].items()} == keys["occ_model_state_dict"]
+
+
+def test_adam_ranges_match_single_launches(L):
+    """lnr_adam_step_ranges (the sharded optimiser's chunks in one launch) is bitwise lnr_adam_step on
+    each range, tails (n not a multiple of 4) and a NULL shadow included."""
+    g = np.load(os.path.join(GOLDEN, "adam_fp16.npz"))
+    p0, gr = g["p0"].astype(np.float32), g["grad_f16"][0].astype(np.float32)
+    cuts = [(0, 1000), (1024, 1024 + 777), (2048, 4096)]
+    a = [cu(p0.copy()) for _ in range(2)]
+    m = [torch.zeros(len(p0), device="cuda") for _ in range(2)]
+    v = [torch.zeros(len(p0), device="cuda") for _ in range(2)]
+    sh = [torch.zeros(len(p0), dtype=torch.float16, device="cuda") for _ in range(2)]
+    gd = cu(gr)
+    for step in (1, 2):
+        for k, (o, e) in enumerate(cuts):
+            L.call("lnr_adam_step", a[0][o:e], sh[0][o:e] if k else None, gd[o:e], m[0][o:e], v[0][o:e], e - o, step,
+                   1e-3, 0.9, 0.999, 1e-8, L.stream())
+        rng = (L.AdamRange * len(cuts))()
+        for k, (o, e) in enumerate(cuts):
+            rng[k] = L.AdamRange(L.ptr(a[1][o:e]), L.ptr(sh[1][o:e]) if k else None, L.ptr(gd[o:e]), L.ptr(m[1][o:e]),
+                                 L.ptr(v[1][o:e]), e - o)
+        L.call("lnr_adam_step_ranges", rng, len(cuts), step, 1e-3, 0.9, 0.999, 1e-8, L.stream())
+    torch.cuda.synchronize()
+    for x, y in ((a[0], a[1]), (m[0], m[1]), (v[0], v[1]), (sh[0], sh[1])):
+        assert torch.equal(x, y)
+    assert not torch.equal(a[1], cu(p0))
