@@ -244,6 +244,10 @@ class StepEngine:
         self.opacity = torch.empty(n_rays, dtype=torch.float32, device=dev)
         self.loss_out = torch.zeros(8, dtype=torch.float32, device=dev)
         self.n_opaque = torch.zeros(1, dtype=torch.float32, device=dev)
+        # the opaque count (and its all-reduce) runs on a side stream, off the critical path: only the
+        # field kernel needs it (forked after the rays exist, joined before the field kernel)
+        self._side = torch.cuda.Stream(device=dev)
+        self._fork, self._join = torch.cuda.Event(), torch.cuda.Event()
         # on-device ray building (step_window)
         self.rays = torch.empty(n_rays, 13, dtype=torch.float32, device=dev)
         self.depth_gt = torch.empty(n_rays, dtype=torch.float32, device=dev)
@@ -341,10 +345,16 @@ class StepEngine:
         far_h = None if dev_far is not None else float(far_ref)
         n_glob = R if n_rays_global is None else n_rays_global
         m = self._mark
-        # 1. opaque count (global): local count + all-reduce
-        L.call("lnr_count_opaque", depth_gt, R, 0.0 if far_h is None else far_h, dev_far, self.n_opaque, s)
-        # the count is first needed by the field kernel: its all-reduce overlaps sampling + encode
-        pending = self._allreduce_async(self.n_opaque) if self.allreduce is not None else None
+        # 1. opaque count (global): local count + all-reduce, on the side stream; the count is first
+        # needed by the field kernel, so both overlap sampling + encode
+        main = torch.cuda.current_stream(st.device)
+        self._fork.record(main)
+        with torch.cuda.stream(self._side):
+            self._side.wait_event(self._fork)
+            L.call("lnr_count_opaque", depth_gt, R, 0.0 if far_h is None else far_h, dev_far, self.n_opaque,
+                   L.stream(st.device))
+            pending = self._allreduce_async(self.n_opaque) if self.allreduce is not None else None
+            self._join.record(self._side)
         lp = self.loss_params(global_step, iteration_idx, scale, far_h, n_glob, dev_far)
         # 2. sampling
         m(prof, "sample")
@@ -365,6 +375,7 @@ class StepEngine:
         m(prof, "encode")
         # 4. fused field + loss + backward through compositing and MLP (stores the MLP gradient, and the
         # loss scalars into loss_out)
+        main.wait_event(self._join)
         if pending is not None:
             pending.wait()  # orders the current stream after the collective (no host sync)
         m(prof, "field")
