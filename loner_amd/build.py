@@ -73,10 +73,12 @@ def build(jobs=8, force=False, verbose=False, defines=(), out=None):
                 print(f"[{os.path.basename(o)}]\n{err}", file=sys.stderr)
     if os.path.exists(lib_path) and os.path.getmtime(lib_path) >= max(os.path.getmtime(o) for o in objs):
         return lib_path
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib_path, *objs]
+    tmp = lib_path + ".tmp"  # linked aside, then renamed: a reader never sees a half-written library
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
+    os.replace(tmp, lib_path)
     return lib_path
 
 

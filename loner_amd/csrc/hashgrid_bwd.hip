@@ -1011,7 +1011,12 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
 // One workgroup per unit of the work list (UnitTable): a whole bucket (its fp32 values, or its zeros
 // when empty) or one of the equal pieces of a large bucket (its int64 partial chunk, added by
 // k_bwd_finalize_units).  The grid is the list's bound; workgroups past n_units return at once.
+// FINISH: the last of a cut bucket's pieces to arrive adds the others' partial chunks and stores the
+// bucket (the split-K hand-off of k_bwd_accum<true>; counters zeroed by k_bwd_scan_buckets), so no
+// k_bwd_finalize_units launch.  The cut buckets are the coarse levels', first in the list, so their
+// finishing overlaps the fine levels' units.
 static_assert(kUnitMinRecords == (uint64_t)kTile, "pieces of at least one tile");
+template <bool FINISH>
 __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_accum_units(GridArgs a, BwdWorkspace ws,
                                                                                               float* __restrict__ d_table) {
   __shared__ unsigned long long acc[2 * kChunk];
@@ -1038,8 +1043,33 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
     store_bucket(acc, a, ws, d_table, l, ent0, nent, k2);
     return;
   }
-  long long* dst = ws.partial + (int64_t)(ut->slot[b] + k) * (2 * kChunk);
+  const uint32_t slot0 = ut->slot[b];
+  long long* dst = ws.partial + (int64_t)(slot0 + k) * (2 * kChunk);
   for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) dst[t] = (long long)acc[(t & 1) * kChunk + (t >> 1)];
+  if (!FINISH) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's partial stores are done
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(&ws.bucket_done[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = old + 1 == P;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    stage[0].x = last ? 1u : 0u;  // (the tile stage is idle here)
+  }
+  __syncthreads();
+  if (!stage[0].x) return;
+  for (uint32_t q = 0; q < P; ++q) {  // the other pieces' partial chunks (int64: exact in any order)
+    if (q == k) continue;
+    const long long* src = ws.partial + (int64_t)(slot0 + q) * (2 * kChunk);
+    for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x)
+      acc[(t & 1) * kChunk + (t >> 1)] += (unsigned long long)src[t];
+  }
+  lds_barrier();
+  store_bucket(acc, a, ws, d_table, l, ent0, nent, k2);
 }
 
 // Buckets the accumulation did not finish: cut buckets = the sum of their pieces' partial chunks in
@@ -1154,6 +1184,12 @@ static int64_t scatter_rows_min() {
 // ~1000 partial chunks and its finalize pass are a fixed ~35 us); C2 (4.7 M) 964 -> 984 us (equal
 // record ranges balance the chip better than whole buckets there).  LONER_ACCUM_UNITS=1 / 0 forces
 // it on / off (read at every launch).
+// The unit accumulation's cut buckets finished by their last piece (1, default) or by
+// k_bwd_finalize_units (0): LONER_UNITS_FINISH, read at every launch.
+static bool units_finish() {
+  const char* e = getenv("LONER_UNITS_FINISH");
+  return e ? atoi(e) != 0 : true;
+}
 #ifndef LNR_ACCUM_UNITS_MAX_N
 #define LNR_ACCUM_UNITS_MAX_N (int64_t(1) << 21)
 #endif
@@ -1180,7 +1216,13 @@ static void launch_accum(const GridArgs& a, const BwdWorkspace& w, const lnr_gri
   if (accum_units(n)) {  // the work list: whole buckets and equal pieces of the large ones
     if (b0 != 0 || b1 != a.n_buckets)  // (a level range: its own list; the whole range's is the scan's)
       hipLaunchKernelGGL(k_bwd_units, dim3(1), dim3(1024), 0, st, w, b0, b1);
-    hipLaunchKernelGGL(k_bwd_accum_units, dim3(b1 - b0 + kAccumGroups), dim3(kAccumThreads), 0, st, a, w, d_table);
+    if (units_finish()) {
+      hipLaunchKernelGGL(k_bwd_accum_units<true>, dim3(b1 - b0 + kAccumGroups), dim3(kAccumThreads), 0, st, a, w,
+                         d_table);
+      return;
+    }
+    hipLaunchKernelGGL(k_bwd_accum_units<false>, dim3(b1 - b0 + kAccumGroups), dim3(kAccumThreads), 0, st, a, w,
+                       d_table);
     hipLaunchKernelGGL(k_bwd_finalize_units, dim3(std::min<uint32_t>(b1 - b0, kAccumGroups)), dim3(kFinalizeThreads), 0,
                        st, a, w, d_table);
     return;

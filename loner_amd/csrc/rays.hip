@@ -154,10 +154,43 @@ __device__ __forceinline__ SlotPoint slot_point(const lnr_ray_window& w, int32_t
   return p;
 }
 
+// The per-keyframe tables (offsets, counts, poses) of windows of up to kKfLds keyframes are copied to
+// LDS once per workgroup: a slot's keyframe search and its table reads then cost LDS latency, not a
+// chain of dependent global loads (the kernel is latency-bound: a few thousand slots).
+constexpr int kKfLds = 64;
+struct KfTables {
+  int32_t ray_off[kKfLds + 1], scan_off[kKfLds + 1], sky_off[kKfLds + 1];
+  int32_t n_sel[kKfLds], n_trunk[kKfLds], n_sel_trunk[kKfLds];
+  float poses[12 * kKfLds];
+};
+
 __global__ void __launch_bounds__(256) k_build_rays(lnr_ray_window w, int32_t select, const int32_t* __restrict__ given,
                                                     uint32_t key, int64_t slot0, int64_t n, float* __restrict__ rays,
                                                     float* __restrict__ depth, uint8_t* __restrict__ valid,
                                                     int32_t* __restrict__ point_index, float* __restrict__ far_ref) {
+  __shared__ KfTables tb;
+  if (w.n_kf <= kKfLds) {  // (uniform)
+    const int K = w.n_kf;
+    for (int i = threadIdx.x; i <= K; i += blockDim.x) {
+      tb.ray_off[i] = w.ray_off[i];
+      tb.scan_off[i] = w.scan_off[i];
+      if (w.sky_off) tb.sky_off[i] = w.sky_off[i];
+      if (i < K) {
+        tb.n_sel[i] = w.n_sel[i];
+        if (w.n_trunk) tb.n_trunk[i] = w.n_trunk[i];
+        if (w.n_sel_trunk) tb.n_sel_trunk[i] = w.n_sel_trunk[i];
+      }
+    }
+    for (int i = threadIdx.x; i < 12 * K; i += blockDim.x) tb.poses[i] = w.poses[i];
+    __syncthreads();
+    w.ray_off = tb.ray_off;
+    w.scan_off = tb.scan_off;
+    w.n_sel = tb.n_sel;
+    w.poses = tb.poses;
+    if (w.sky_off) w.sky_off = tb.sky_off;
+    if (w.n_trunk) w.n_trunk = tb.n_trunk;
+    if (w.n_sel_trunk) w.n_sel_trunk = tb.n_sel_trunk;
+  }
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (far_ref != nullptr && t == 0) {
     // far bound of the first valid ray of the whole batch (global ray 0 after the validity filter;

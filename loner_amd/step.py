@@ -253,6 +253,18 @@ class StepEngine:
         self.depth_gt = torch.empty(n_rays, dtype=torch.float32, device=dev)
         self.ray_valid = torch.empty(n_rays, dtype=torch.uint8, device=dev)
         self.far_ref = torch.empty(1, dtype=torch.float32, device=dev)
+        # step_window on windows whose rays can fail the 1 m filter: two ray buffers, the next step's
+        # build + compaction prefetched on a side stream (``prefetch``)
+        self.prefetch = os.environ.get("LONER_PREFETCH", "1") != "0"
+        self._pf, self._pf_parity = None, 0
+        self._pf_stream = torch.cuda.Stream(device=dev)
+        self._pf_fork = torch.cuda.Event()
+        self._pf_bufs = [dict(rays=self.rays if i == 0 else torch.empty_like(self.rays),
+                              dgt=self.depth_gt if i == 0 else torch.empty_like(self.depth_gt),
+                              valid=self.ray_valid if i == 0 else torch.empty_like(self.ray_valid),
+                              far=self.far_ref if i == 0 else torch.empty_like(self.far_ref),
+                              rays_c=torch.empty_like(self.rays), dgt_c=torch.empty_like(self.depth_gt))
+                         for i in range(2)]
 
     def loss_params(self, global_step, iteration_idx, scale, far_ref, n_rays_global, dev_far_ref=None):
         lc = self.cfg.loss
@@ -526,22 +538,56 @@ class StepEngine:
         if not 0 <= n <= self.n_rays or self.ray_offset + n > window.n_slots:
             raise ValueError(f"slots [{self.ray_offset}, {self.ray_offset + n}) outside the window "
                              f"({window.n_slots}) or the engine capacity ({self.n_rays})")
-        key = L.step_key(self.seed, global_step)
         m = self._mark
-        m(prof, "rays")
-        window.build(key, self.ray_offset, n, self.rays[:n], self.depth_gt[:n], self.ray_valid[:n], None,
-                     self.far_ref)
-        m(prof, "rays")
-        rays, dgt = self.rays[:n], self.depth_gt[:n]
-        if n_rays_global is None:
-            n_rays_global = window.n_slots
-        if not window.all_valid:
-            keep = self.ray_valid[:n].bool()
-            rays, dgt = rays[keep].contiguous(), dgt[keep].contiguous()
-            cnt = torch.tensor([float(rays.shape[0])], device=self.state.device)
+        if window.all_valid:
+            m(prof, "rays")
+            window.build(L.step_key(self.seed, global_step), self.ray_offset, n, self.rays[:n], self.depth_gt[:n],
+                         self.ray_valid[:n], None, self.far_ref)
+            m(prof, "rays")
+            return self.step(self.rays[:n], self.depth_gt[:n], global_step, iteration_idx, scale=window.scale,
+                             far_ref=self.far_ref, n_rays_global=window.n_slots if n_rays_global is None else n_rays_global,
+                             prof=prof, **kw)
+        # Windows with rays the 1 m filter drops: the batch size must reach the host (one sync per step).
+        # The build and compaction of step k + 1 run on a side stream while step k runs, so that sync
+        # never waits for the main stream: the host stays a step ahead of the GPU (double-buffered).
+        main = torch.cuda.current_stream(self.state.device)
+        want = (id(window), global_step, n, self.ray_offset, n_rays_global)
+        pf, self._pf = self._pf, None
+        if pf is None or pf["want"] != want:
+            m(prof, "rays")
+            pf = self._build_compact(window, global_step, n, n_rays_global, self._pf_parity, main)
+            m(prof, "rays")
+        else:
+            main.wait_event(pf["done"])
+        self._pf_parity = pf["parity"]
+        self._pf_fork.record(main)  # the other buffer is free once everything enqueued so far is done
+        out = self.step(pf["rays"], pf["dgt"], global_step, iteration_idx, scale=window.scale, far_ref=pf["far"],
+                        n_rays_global=pf["n_glob"], prof=prof, **kw)
+        if self.prefetch:
+            nxt = None if n_rays_global is None else n_rays_global
+            with torch.cuda.stream(self._pf_stream):
+                self._pf_stream.wait_event(self._pf_fork)
+                self._pf = self._build_compact(window, global_step + 1, n, nxt, 1 - self._pf_parity, self._pf_stream)
+        return out
+
+    def _build_compact(self, window, global_step, n, n_rays_global, parity, stream):
+        """Build slots [ray_offset, ray_offset + n) of ``window`` for ``global_step`` into ray buffer
+        ``parity`` on ``stream`` and drop the invalid rays (order kept; one host sync on that stream);
+        the global count is all-reduced when data-parallel."""
+        b = self._pf_bufs[parity]
+        with torch.cuda.stream(stream):
+            window.build(L.step_key(self.seed, global_step), self.ray_offset, n, b["rays"][:n], b["dgt"][:n],
+                         b["valid"][:n], None, b["far"])
+            idx = torch.nonzero(b["valid"][:n]).squeeze(1)
+            k = int(idx.numel())  # (the sync)
+            torch.index_select(b["rays"][:n], 0, idx, out=b["rays_c"][:k])
+            torch.index_select(b["dgt"][:n], 0, idx, out=b["dgt_c"][:k])
+            cnt = torch.tensor([float(k)], device=self.state.device)
             if self.allreduce is not None:
                 self.allreduce(cnt)
-            n_rays_global = int(cnt.item())
-        return self.step(rays, dgt, global_step, iteration_idx, scale=window.scale, far_ref=self.far_ref,
-                         n_rays_global=n_rays_global, prof=prof, **kw)
+            n_glob = int(cnt.item())
+            done = torch.cuda.Event()
+            done.record(stream)
+        return dict(want=(id(window), global_step, n, self.ray_offset, n_rays_global), rays=b["rays_c"][:k],
+                    dgt=b["dgt_c"][:k], far=b["far"], n_glob=n_glob, done=done, parity=parity)
 

@@ -144,3 +144,31 @@ def test_step_window_equals_step_on_built_rays(L):
         grads.append(host(st.grad).copy())
     np.testing.assert_array_equal(outs[0], outs[1])
     np.testing.assert_array_equal(grads[0], grads[1])
+
+
+def test_prefetched_compaction_equals_synchronous(L):
+    """step_window on a window with invalid rays: the next step's build + compaction prefetched on a
+    side stream (double-buffered) gives bitwise the synchronous path's losses and parameters, over
+    consecutive steps, a skipped step (the prefetch is discarded) and an OGM step."""
+    from loner_amd import step as S_
+    from loner_amd.rays import RayWindow
+    scans, wc, rr = _window("quad", 2, seed=4)
+    scale, shift = float(wc.scale_factor[0]), wc.shift.numpy()
+    s1 = dict(scans[1])
+    pose = s1["pose"].clone()
+    pose[0, 3] = float(0.9995 * scale - shift[0])
+    s1["pose"] = pose
+    win = RayWindow([scans[0], s1], wc, rr, n_lidar=256, strategy="RANDOM")
+    assert not win.all_valid
+    res = []
+    for prefetch in (True, False):
+        st = S_.FieldState(S_.StepConfig(n_samples=64, occ_lr=1e-3), device="cuda:0", table_init=0.5)
+        eng = S_.StepEngine(st, win.n_slots, seed=3)
+        eng.prefetch = prefetch
+        outs = [host(eng.step_window(win, global_step=g)).copy() for g in (8, 9, 10, 12, 13)]
+        torch.cuda.synchronize()
+        res.append((outs, host(st.params).copy(), host(st.occ).copy()))
+    for a, b in zip(res[0][0], res[1][0]):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(res[0][1], res[1][1])
+    np.testing.assert_array_equal(res[0][2], res[1][2])

@@ -195,19 +195,22 @@ def test_step_engine_one_step_vs_oracle(L):
 
 
 def _assert_accum_paths_equal(L, st, rays, eng, R, Sn, g_ref=None):
-    """Every accumulation path (LONER_ACCUM_UNITS, LONER_ACCUM_BUCKETS_MAX_N and LONER_ACCUM_FINISH
-    switch them at each launch) gives the same gradient bitwise, behind each scatter kernel: the level-looped one and one
+    """Every accumulation path (LONER_ACCUM_UNITS, LONER_ACCUM_BUCKETS_MAX_N, LONER_ACCUM_FINISH and
+    LONER_UNITS_FINISH switch them at each launch) gives the same gradient bitwise, behind each scatter kernel: the level-looped one and one
     workgroup per (row, level) (LONER_SCATTER_ROWS_MIN switches them), whose coherent-level run sums
     may group their fp32 additions differently (close, not bitwise).  g_ref, when given, is bitwise one of the
     two; returns both (level-looped, per (row, level))."""
     import os
     s = L.stream()
-    keys = ("LONER_ACCUM_UNITS", "LONER_ACCUM_BUCKETS_MAX_N", "LONER_ACCUM_FINISH", "LONER_SCATTER_ROWS_MIN")
+    keys = ("LONER_ACCUM_UNITS", "LONER_ACCUM_BUCKETS_MAX_N", "LONER_ACCUM_FINISH", "LONER_UNITS_FINISH",
+            "LONER_SCATTER_ROWS_MIN")
     old = {k: os.environ.get(k) for k in keys}
     big = str(1 << 40)
-    # the unit work list (default), record-balanced with in-kernel finishing (twice: arrival order
-    # varies), with k_bwd_finalize, and whole buckets
-    accums = (("1", "0", "0"), ("0", "0", "1"), ("0", "0", "1"), ("0", "0", "0"), ("0", big, "0"))
+    # the unit work list with in-kernel finishing (twice: arrival order varies) and with
+    # k_bwd_finalize_units, record-balanced with in-kernel finishing (twice) and with k_bwd_finalize,
+    # and whole buckets
+    accums = (("1", "0", "0", "1"), ("1", "0", "0", "1"), ("1", "0", "0", "0"), ("0", "0", "1", "1"),
+              ("0", "0", "1", "1"), ("0", "0", "0", "1"), ("0", big, "0", "1"))
     groups = {"rows": [a + ("0",) for a in accums], "row_level": [a + (big,) for a in accums]}
     out = {}
     try:
