@@ -259,11 +259,23 @@ class StepEngine:
         self._pf, self._pf_parity = None, 0
         self._pf_stream = torch.cuda.Stream(device=dev)
         self._pf_fork = torch.cuda.Event()
-        self._pf_bufs = [dict(rays=self.rays if i == 0 else torch.empty_like(self.rays),
+        self._pf_bufs = [dict(rays=torch.empty_like(self.rays), dgt=torch.empty_like(self.depth_gt),
+                              valid=torch.empty_like(self.ray_valid), far=torch.empty_like(self.far_ref),
+                              rays_c=torch.empty_like(self.rays), dgt_c=torch.empty_like(self.depth_gt))
+                         for i in range(2)]
+        # step_window on windows whose rays all pass the filter: step k + 1's ray build and sampling
+        # enqueued on a side stream right after step k (two ray / depth buffers), so they run in the
+        # holes step k leaves (the scatter's last round, the accumulate's tail) instead of at the head
+        # of step k + 1 (``pipeline``; not when step k updates the OGM, which the sampler reads)
+        self.pipeline = os.environ.get("LONER_PIPELINE", "1") != "0"
+        self._pp, self._pp_parity = None, 0
+        self._pp_stream = torch.cuda.Stream(device=dev)
+        self._pp_fork = torch.cuda.Event()
+        self._pp_bufs = [dict(rays=self.rays if i == 0 else torch.empty_like(self.rays),
                               dgt=self.depth_gt if i == 0 else torch.empty_like(self.depth_gt),
                               valid=self.ray_valid if i == 0 else torch.empty_like(self.ray_valid),
                               far=self.far_ref if i == 0 else torch.empty_like(self.far_ref),
-                              rays_c=torch.empty_like(self.rays), dgt_c=torch.empty_like(self.depth_gt))
+                              z=self.z if i == 0 else torch.empty_like(self.z))
                          for i in range(2)]
 
     def loss_params(self, global_step, iteration_idx, scale, far_ref, n_rays_global, dev_far_ref=None):
@@ -340,7 +352,7 @@ class StepEngine:
             prof.setdefault(stage, []).append(ev)
 
     def step(self, rays, depth_gt, global_step, iteration_idx=0, scale=1.0, far_ref=None, n_rays_global=None,
-             u_jitter=None, u_pdf=None, noise=None, update_ogm=None, prof=None):
+             u_jitter=None, u_pdf=None, noise=None, update_ogm=None, prof=None, presampled=False):
         """rays (R,13) fp32, depth_gt (R,) fp32 normalised, both on this GPU, R <= the engine's
         capacity.  Returns the device loss buffer [loss, mean_eps, depth_term, los_term, opacity_term,
         n_opaque] (no host sync).  ``far_ref``: the far bound of global ray 0, a float or a 1-element
@@ -368,9 +380,11 @@ class StepEngine:
             pending = self._allreduce_async(self.n_opaque) if self.allreduce is not None else None
             self._join.record(self._side)
         lp = self.loss_params(global_step, iteration_idx, scale, far_h, n_glob, dev_far)
-        # 2. sampling
+        # 2. sampling (``presampled``: step_window's pipeline already drew self.z for these rays)
         m(prof, "sample")
-        if cfg.sampler == "OGM":
+        if presampled:
+            pass
+        elif cfg.sampler == "OGM":
             L.call("lnr_sample_ogm", rays, R, S, st.occ, cfg.occ_res, cfg.perturb, u_jitter, u_pdf, key,
                    self.ray_offset, self.z, s)
         else:
@@ -540,13 +554,7 @@ class StepEngine:
                              f"({window.n_slots}) or the engine capacity ({self.n_rays})")
         m = self._mark
         if window.all_valid:
-            m(prof, "rays")
-            window.build(L.step_key(self.seed, global_step), self.ray_offset, n, self.rays[:n], self.depth_gt[:n],
-                         self.ray_valid[:n], None, self.far_ref)
-            m(prof, "rays")
-            return self.step(self.rays[:n], self.depth_gt[:n], global_step, iteration_idx, scale=window.scale,
-                             far_ref=self.far_ref, n_rays_global=window.n_slots if n_rays_global is None else n_rays_global,
-                             prof=prof, **kw)
+            return self._step_window_pipelined(window, global_step, iteration_idx, n, n_rays_global, prof, kw)
         # Windows with rays the 1 m filter drops: the batch size must reach the host (one sync per step).
         # The build and compaction of step k + 1 run on a side stream while step k runs, so that sync
         # never waits for the main stream: the host stays a step ahead of the GPU (double-buffered).
@@ -568,6 +576,57 @@ class StepEngine:
             with torch.cuda.stream(self._pf_stream):
                 self._pf_stream.wait_event(self._pf_fork)
                 self._pf = self._build_compact(window, global_step + 1, n, nxt, 1 - self._pf_parity, self._pf_stream)
+        return out
+
+    def _step_window_pipelined(self, window, global_step, iteration_idx, n, n_rays_global, prof, kw):
+        """step_window for windows with no invalid rays (fixed batch size, no host sync), with step
+        k + 1's build + sampling prefetched (``pipeline``)."""
+        m = self._mark
+        main = torch.cuda.current_stream(self.state.device)
+        want = (id(window), global_step, n, self.ray_offset)
+        pp, self._pp = self._pp, None
+        if pp is not None and pp["want"] == want:
+            main.wait_event(pp["done"])
+            parity, presampled = pp["parity"], pp["sampled"]
+            b = self._pp_bufs[parity]
+        else:
+            parity, presampled = self._pp_parity, False
+            b = self._pp_bufs[parity]
+            m(prof, "rays")
+            window.build(L.step_key(self.seed, global_step), self.ray_offset, n, b["rays"][:n], b["dgt"][:n],
+                         b["valid"][:n], None, b["far"])
+            m(prof, "rays")
+        self._pp_parity = parity
+        # (the buffers of the step in flight: rays, depth_gt, ray_valid, far_ref and z as step() uses them)
+        self.z, self.rays, self.depth_gt, self.ray_valid, self.far_ref = b["z"], b["rays"], b["dgt"], b["valid"], b["far"]
+        self._pp_fork.record(main)  # the other buffers are free once everything enqueued so far is done
+        out = self.step(b["rays"][:n], b["dgt"][:n], global_step, iteration_idx, scale=window.scale, far_ref=b["far"],
+                        n_rays_global=window.n_slots if n_rays_global is None else n_rays_global, prof=prof,
+                        presampled=presampled, **kw)
+        if not self.pipeline or prof is not None or "u_jitter" in kw or "u_pdf" in kw:
+            return out  # (a profiled step keeps its stages apart)
+        cfg = self.cfg
+        ogm_now = kw.get("update_ogm")
+        if ogm_now is None:
+            ogm_now = global_step % cfg.n_iters_acc == 0
+        q = 1 - parity
+        bq = self._pp_bufs[q]
+        key = L.step_key(self.seed, global_step + 1)
+        sample = cfg.sampler != "OGM" or not ogm_now  # the OGM sampler reads the grid step k may update
+        with torch.cuda.stream(self._pp_stream):
+            self._pp_stream.wait_event(self._pp_fork)
+            window.build(key, self.ray_offset, n, bq["rays"][:n], bq["dgt"][:n], bq["valid"][:n], None, bq["far"])
+            if sample:
+                s = L.stream(self.state.device)
+                if cfg.sampler == "OGM":
+                    L.call("lnr_sample_ogm", bq["rays"][:n], n, self.S, self.state.occ, cfg.occ_res, cfg.perturb, None,
+                           None, key, self.ray_offset, bq["z"], s)
+                else:
+                    L.call("lnr_sample_uniform", bq["rays"][:n], n, self.S, cfg.perturb, None, key, self.ray_offset,
+                           bq["z"], s)
+            done = torch.cuda.Event()
+            done.record(self._pp_stream)
+        self._pp = dict(want=(id(window), global_step + 1, n, self.ray_offset), parity=q, sampled=sample, done=done)
         return out
 
     def _build_compact(self, window, global_step, n, n_rays_global, parity, stream):
