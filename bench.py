@@ -743,8 +743,10 @@ def main():
                    **({"submap_rank0": submap} if submap is not None else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": "hash-grid backward stage (k_bwd_chunk_sums, k_bwd_scan_*, k_bwd_scatter_rows, "
-                               "k_bwd_accum_units, k_bwd_finalize_units)",
+                     "kernel": "hash-grid backward stage (k_bwd_chunk_sums, k_bwd_scan_*, k_bwd_scatter_rows, " + (
+                         "k_bwd_accum_buckets)" if N <= (1 << 17) else
+                         "k_bwd_accum_units: whole buckets and pieces of the large ones)" if N <= (1 << 21) else
+                         "k_bwd_accum: record-balanced, k_bwd_finalize)"),
                      "algorithmic_bytes_per_launch": 1024 * N, "ms_per_launch": bwd_ms,
                      "step_algorithmic_bytes": step_bytes,
                      "step_frac": step_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
