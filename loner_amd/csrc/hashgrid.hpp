@@ -348,15 +348,55 @@ __device__ __forceinline__ RunInfo cell_runs_dpp(bool in, uint32_t cx, uint32_t 
   return ri;
 }
 
+// One step of a segmented sum as ONE instruction per value: v += dpp(v) * f, with f = 1.0 where this
+// lane's run reaches back over the shift and 0.0 elsewhere (v_fmac_f32 with a DPP source operand;
+// the compiler does not fold a DPP move into fmac, so it is written out).  x * 1.0 is exact, so each
+// add rounds exactly as the conditional add it replaces; where f = 0 the value is unchanged (up to
+// the sign of a zero).  Every row enabled and bound_ctrl: a source lane outside the shift reads 0.
+// The leading s_nop 1 covers the DPP source hazard (2 wait states after a VALU write of the source,
+// e.g. a copy the compiler places before the block); inside the block value k is last written 16
+// instructions back.
+#define LNR_FMAC_DPP_16(DPP, v, f)                                                                        \
+  asm volatile(                                                                                          \
+      "s_nop 1\n\t"                                                                                      \
+      "v_fmac_f32_dpp %0, %0, %16 " DPP "\n\tv_fmac_f32_dpp %1, %1, %16 " DPP "\n\t"                    \
+      "v_fmac_f32_dpp %2, %2, %16 " DPP "\n\tv_fmac_f32_dpp %3, %3, %16 " DPP "\n\t"                    \
+      "v_fmac_f32_dpp %4, %4, %16 " DPP "\n\tv_fmac_f32_dpp %5, %5, %16 " DPP "\n\t"                    \
+      "v_fmac_f32_dpp %6, %6, %16 " DPP "\n\tv_fmac_f32_dpp %7, %7, %16 " DPP "\n\t"                    \
+      "v_fmac_f32_dpp %8, %8, %16 " DPP "\n\tv_fmac_f32_dpp %9, %9, %16 " DPP "\n\t"                    \
+      "v_fmac_f32_dpp %10, %10, %16 " DPP "\n\tv_fmac_f32_dpp %11, %11, %16 " DPP "\n\t"                \
+      "v_fmac_f32_dpp %12, %12, %16 " DPP "\n\tv_fmac_f32_dpp %13, %13, %16 " DPP "\n\t"                \
+      "v_fmac_f32_dpp %14, %14, %16 " DPP "\n\tv_fmac_f32_dpp %15, %15, %16 " DPP                       \
+      : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]), \
+        "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]),        \
+        "+v"(v[15])                                                                                      \
+      : "v"(f))
+#ifndef LNR_SEG_FMAC
+#define LNR_SEG_FMAC 1  // the segmented sums as v_fmac_f32_dpp (1) or DPP move + masked add (0)
+#endif
+
 // Segmented inclusive sum of N values over runs sharing one RunInfo: the run's tail lane ends with
-// the run totals.  Each step's lane condition is computed once for all N values, and only the steps
-// the wave's runs need are taken: row shifts up to the longest within-row run prefix, the row
-// broadcasts only when a run crosses a 16-lane row boundary.  Fixed order: deterministic.
+// the run totals.  Each step's lane condition is computed once for all N values.  Fixed order:
+// deterministic.  N = 16 (the coherent levels' 8 corners x 2 features) takes every step as one
+// v_fmac_f32_dpp per value; otherwise each step is a DPP move and a masked add per value, and only
+// the steps the wave's runs need are taken: row shifts up to the longest within-row run prefix, the
+// row broadcasts only when a run crosses a 16-lane row boundary.
 template <int N>
 __device__ __forceinline__ void run_sum_dpp_n(const RunInfo& ri, float (&v)[N]) {
   const int lane = threadIdx.x & 63;
   const int h = ri.head_lane;
   const int rs = lane & ~15;
+  if constexpr (LNR_SEG_FMAC && N == 16) {
+    // (branching around a step would cost the register copies the compiler places at the joins; a
+    // step no run needs multiplies by 0 everywhere)
+    LNR_FMAC_DPP_16("row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1", v, (lane - 1 >= h) ? 1.f : 0.f);
+    LNR_FMAC_DPP_16("row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1", v, (lane - 2 >= h) ? 1.f : 0.f);
+    LNR_FMAC_DPP_16("row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1", v, (lane - 4 >= h) ? 1.f : 0.f);
+    LNR_FMAC_DPP_16("row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1", v, (lane - 8 >= h) ? 1.f : 0.f);
+    LNR_FMAC_DPP_16("row_bcast:15 row_mask:0xf bank_mask:0xf bound_ctrl:1", v, ((lane & 16) && h < rs) ? 1.f : 0.f);
+    LNR_FMAC_DPP_16("row_bcast:31 row_mask:0xf bank_mask:0xf bound_ctrl:1", v, (lane >= 32 && h < 32) ? 1.f : 0.f);
+    return;
+  }
   // longest distance from a lane back to its run's first lane in the same row (0..15), wave-uniform
   int d = lane - (h > rs ? h : rs);
   d = max(d, __builtin_amdgcn_update_dpp(0, d, 0x111, 0xF, 0xF, true));
