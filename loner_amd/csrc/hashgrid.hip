@@ -17,19 +17,24 @@ namespace lnr {
 // nontemporal store keeps it out of the way of the table slices in L2 (step -0.01 ms at C2)
 __device__ __forceinline__ void store_enc(uint32_t* p, uint32_t v) { __builtin_nontemporal_store(v, p); }
 
-template <class PosFn, bool COUNT>
+// One kernel for the training encode (ws.hist set: also the backward's record histogram) and the
+// eval encode (ws.hist null; ``live`` optional).  The flag is a runtime, block-uniform one on
+// purpose: a separate no-count instantiation compiles to a shape whose fine and dense gathers share
+// one load block, and that runs 14 % slower (C2: 838 against 722 us; tools/exp_overlap.py).
+template <class PosFn>
 __global__ void __launch_bounds__(1024) k_hashgrid_fwd(GridArgs a, PosFn pos, int64_t n, const uint32_t* __restrict__ table,
                                                       uint32_t* __restrict__ enc, int64_t stride, BwdWorkspace ws,
                                                       const float* __restrict__ live) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t l = blockIdx.y;
+  const bool count = ws.hist != nullptr;
   const bool in = i < n;
-  // live (forward only, never with COUNT): samples whose weight is exactly 0 get a zero encoding and
-  // issue no gathers
-  const bool use = in && (COUNT || live == nullptr || live[i] != 0.f);
-  if (!COUNT && !in) return;
-  __shared__ uint32_t hist[COUNT ? kMaxChunksPerLevel : 1];
-  if (COUNT) {
+  // live (eval only, never when counting): samples whose weight is exactly 0 get a zero encoding
+  // and issue no gathers
+  const bool use = in && (live == nullptr || live[i] != 0.f);
+  if (!count && !in) return;
+  __shared__ uint32_t hist[kMaxChunksPerLevel];
+  if (count) {
     for (int b = threadIdx.x; b < kMaxChunksPerLevel; b += blockDim.x) hist[b] = 0;
   }
   float x = 0.f, y = 0.f, z = 0.f;
@@ -38,35 +43,15 @@ __global__ void __launch_bounds__(1024) k_hashgrid_fwd(GridArgs a, PosFn pos, in
   if (lv.fine) {  // block-uniform
     FineCell c;
     fine_cell(lv, x, y, z, c);
-    if (!COUNT && in && !use) enc[(int64_t)l * stride + i] = 0u;
+    if (in && !use) enc[(int64_t)l * stride + i] = 0u;
     if (use) {
       const uint32_t* tl = table + lv.offset;
       uint32_t v[8];
-#ifdef LNR_FWD_X4
-      // one 16-B load per x-pair: the partner e ^ d lies in the same aligned 4-entry group when
-      // d <= 3 (x even or x = 1 mod 4); the rest take a second, sparser gather
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-      u32x4 q[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) q[j] = *reinterpret_cast<const u32x4*>(tl + (c.e[j] & ~3u));
-      const bool near = c.d <= 3u;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t s0 = c.e[j] & 3u, s1 = (c.e[j] ^ c.d) & 3u;
-        v[2 * j] = s0 == 0 ? q[j].x : s0 == 1 ? q[j].y : s0 == 2 ? q[j].z : q[j].w;
-        v[2 * j + 1] = s1 == 0 ? q[j].x : s1 == 1 ? q[j].y : s1 == 2 ? q[j].z : q[j].w;
-      }
-      if (!near) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[2 * j + 1] = tl[c.e[j] ^ c.d];
-      }
-#else
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         v[2 * j] = tl[c.e[j]];
         v[2 * j + 1] = tl[c.e[j] ^ c.d];
       }
-#endif
       float f0 = 0.f, f1 = 0.f;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -77,7 +62,7 @@ __global__ void __launch_bounds__(1024) k_hashgrid_fwd(GridArgs a, PosFn pos, in
       }
       store_enc(enc + (int64_t)l * stride + i, (uint32_t)f2h(f0) | ((uint32_t)f2h(f1) << 16));
     }
-    if (COUNT) {
+    if (count) {
       lds_barrier();
       count_block_records_fine(a, l, c, in, hist, ws);
     }
@@ -85,7 +70,7 @@ __global__ void __launch_bounds__(1024) k_hashgrid_fwd(GridArgs a, PosFn pos, in
   }
   Corners c;
   level_corners(lv, x, y, z, c);
-  if (!COUNT && in && !use) enc[(int64_t)l * stride + i] = 0u;
+  if (in && !use) enc[(int64_t)l * stride + i] = 0u;
   if (use) {
     uint32_t v[8];
 #pragma unroll
@@ -99,7 +84,7 @@ __global__ void __launch_bounds__(1024) k_hashgrid_fwd(GridArgs a, PosFn pos, in
     }
     store_enc(enc + (int64_t)l * stride + i, (uint32_t)f2h(f0) | ((uint32_t)f2h(f1) << 16));
   }
-  if (COUNT) {
+  if (count) {
     lds_barrier();
     count_block_records(a, l, c, in, in, hist, ws);
   }
@@ -224,7 +209,6 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
                       const float* live = nullptr) {
   GridArgs a = make_args(d, pos.samples_per_ray());
   LNR_REQUIRE(n < (int64_t(1) << 31), "%s: n=%lld samples exceeds 2^31", who, (long long)n);
-  dim3 grid((unsigned)((n + 255) / 256), d->n_levels);
   if (bwd_ws) {
     LNR_REQUIRE(bwd_ws_bytes >= bwd_workspace_bytes(d, n), "%s: backward workspace too small", who);
     LNR_REQUIRE(a.n_buckets <= (uint32_t)kMaxBuckets, "%s: too many table chunks (%u)", who, a.n_buckets);
@@ -234,11 +218,13 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
     BwdWorkspace w = carve_workspace(bwd_ws, a, d, n);
     // one workgroup per histogram row (kSB samples) so the row is written whole
     dim3 gridc((unsigned)w.n_sb, d->n_levels);
-    hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, true>), gridc, dim3(kSB), 0, st, a, pos, n,
-                       reinterpret_cast<const uint32_t*>(table), enc, enc_stride, w, nullptr);
+    hipLaunchKernelGGL(k_hashgrid_fwd<PosFn>, gridc, dim3(kSB), 0, st, a, pos, n, reinterpret_cast<const uint32_t*>(table),
+                       enc, enc_stride, w, nullptr);
   } else {
-    hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, false>), grid, dim3(256), 0, st, a, pos, n,
-                       reinterpret_cast<const uint32_t*>(table), enc, enc_stride, BwdWorkspace{}, live);
+    // kSB-sample workgroups as in training (C2-size eval launch: 1011 us at 256 threads, 836 at 512)
+    dim3 grid((unsigned)((n + kSB - 1) / kSB), d->n_levels);
+    hipLaunchKernelGGL(k_hashgrid_fwd<PosFn>, grid, dim3(kSB), 0, st, a, pos, n, reinterpret_cast<const uint32_t*>(table),
+                       enc, enc_stride, BwdWorkspace{}, live);
   }
   LNR_RETURN_LAUNCH(who);
 }

@@ -4,7 +4,7 @@
 // execution) and LDS ds_add_f32 at only 0.33 lanes/clk/CU whatever the address pattern, while
 // ds_add_u64 runs at 4.8 lanes/clk/CU.  So the backward is
 //   count    per (512-sample row, level) record histogram over the level's 4096-entry table chunks
-//            (buckets), emitted by the training forward (k_hashgrid_fwd<..., true>) or by k_bwd_count
+//            (buckets), emitted by the training forward (k_hashgrid_fwd given the workspace) or by k_bwd_count
 //   scan     k_bwd_chunk_sums + k_bwd_scan_rows (column prefix over 64-row chunks) + k_bwd_scan_buckets:
 //            exact per-row record offsets in every bucket (no global atomics, no capacity guess)
 //   scatter  k_bwd_scatter_rows: one workgroup per row walks all 16 levels; 8-byte records {word,
