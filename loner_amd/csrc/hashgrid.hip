@@ -17,76 +17,126 @@ namespace lnr {
 // nontemporal store keeps it out of the way of the table slices in L2 (step -0.01 ms at C2)
 __device__ __forceinline__ void store_enc(uint32_t* p, uint32_t v) { __builtin_nontemporal_store(v, p); }
 
+// The 8 corners of a fine (hashed, power-of-two) level: the x-pairs e, e ^ d of the four y/z edges.
+// What bounds this gather is the texture addresser: TA busy 85 % of the launch at C2, about 40
+// TA cycles per wave-wide gather of scattered entries (profiles/r03_l2req_C2.txt).  Reading an
+// x-pair through one 16-B load of its aligned quad (3/4 of the pairs; tried) cut the vector-L1 line
+// accesses from 426 M to 288 M per launch but left TA busy where it was (0.743 against 0.720 ms);
+// 8-B pair loads ran 0.86 ms.  Plain dword gathers it is.
+__device__ __forceinline__ void fine_gather(const uint32_t* __restrict__ tl, const FineCell& c, uint32_t (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[2 * j] = tl[c.e[j]];
+    v[2 * j + 1] = tl[c.e[j] ^ c.d];
+  }
+}
+
+#ifndef LNR_ENC_SPT2_MIN_N
+#define LNR_ENC_SPT2_MIN_N (1 << 18)  // two samples per thread from this many samples (C2 encode 0.745-0.770 ->
+                                      // 0.720 ms); below it one (C1: 19 against 25 us: half the waves)
+#endif
+
 // One kernel for the training encode (ws.hist set: also the backward's record histogram) and the
 // eval encode (ws.hist null; ``live`` optional).  The flag is a runtime, block-uniform one on
 // purpose: a separate no-count instantiation compiles to a shape whose fine and dense gathers share
 // one load block, and that runs 14 % slower (C2: 838 against 722 us; tools/exp_overlap.py).
-template <class PosFn>
-__global__ void __launch_bounds__(1024) k_hashgrid_fwd(GridArgs a, PosFn pos, int64_t n, const uint32_t* __restrict__ table,
-                                                      uint32_t* __restrict__ enc, int64_t stride, BwdWorkspace ws,
-                                                      const float* __restrict__ live) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// One workgroup per histogram row (kSB samples) and level, kEncSpt samples per thread: thread t
+// takes samples t and t + kSB / 2 of the row, so each wave still covers 64-sample groups (the
+// coherent levels' run merging sees the lanes the scatter sees), and a fine level's gathers of both
+// samples are in flight together.
+#ifndef LNR_ENC_WAVES
+#define LNR_ENC_WAVES 8  // waves per SIMD asked of the encode (68 registers would allow 7)
+#endif
+template <class PosFn, int kEncSpt>
+__global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per_eu(LNR_ENC_WAVES, LNR_ENC_WAVES))) k_hashgrid_fwd(GridArgs a, PosFn pos, int64_t n,
+                                                               const uint32_t* __restrict__ table,
+                                                               uint32_t* __restrict__ enc, int64_t stride,
+                                                               BwdWorkspace ws, const float* __restrict__ live) {
+  constexpr int H = kSB / kEncSpt;
+  const int64_t i0 = (int64_t)blockIdx.x * kSB + threadIdx.x;
   const uint32_t l = blockIdx.y;
   const bool count = ws.hist != nullptr;
-  const bool in = i < n;
-  // live (eval only, never when counting): samples whose weight is exactly 0 get a zero encoding
-  // and issue no gathers
-  const bool use = in && (live == nullptr || live[i] != 0.f);
-  if (!count && !in) return;
+  if (!count && i0 >= n) return;
   __shared__ uint32_t hist[kMaxChunksPerLevel];
   if (count) {
     for (int b = threadIdx.x; b < kMaxChunksPerLevel; b += blockDim.x) hist[b] = 0;
   }
-  float x = 0.f, y = 0.f, z = 0.f;
-  if (in) pos(i, x, y, z);
+  bool in[kEncSpt], use[kEncSpt];
+  float x[kEncSpt], y[kEncSpt], z[kEncSpt];
+#pragma unroll
+  for (int h = 0; h < kEncSpt; ++h) {
+    const int64_t i = i0 + h * H;
+    in[h] = i < n;
+    // live (eval only, never when counting): samples whose weight is exactly 0 get a zero encoding
+    // and issue no gathers
+    use[h] = in[h] && (live == nullptr || live[i] != 0.f);
+    x[h] = y[h] = z[h] = 0.f;
+    if (in[h]) pos(i, x[h], y[h], z[h]);
+  }
   const LevelParams& lv = a.lv[l];
   if (lv.fine) {  // block-uniform
-    FineCell c;
-    fine_cell(lv, x, y, z, c);
-    if (in && !use) enc[(int64_t)l * stride + i] = 0u;
-    if (use) {
-      const uint32_t* tl = table + lv.offset;
-      uint32_t v[8];
+    FineCell c[kEncSpt];
+    uint32_t v[kEncSpt][8];
+    const uint32_t* tl = table + lv.offset;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[2 * j] = tl[c.e[j]];
-        v[2 * j + 1] = tl[c.e[j] ^ c.d];
-      }
-      float f0 = 0.f, f1 = 0.f;
+    for (int h = 0; h < kEncSpt; ++h) {
+      fine_cell(lv, x[h], y[h], z[h], c[h]);
+      if (use[h]) fine_gather(tl, c[h], v[h]);
+    }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float w = fine_weight(c, k >> 1, k & 1);
-        const float2 t = half2_to_float2(v[k]);
-        f0 = fmaf(w, t.x, f0);
-        f1 = fmaf(w, t.y, f1);
+    for (int h = 0; h < kEncSpt; ++h) {
+      uint32_t* dst = enc + (int64_t)l * stride + i0 + h * H;
+      if (use[h]) {
+        float f0 = 0.f, f1 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float w = fine_weight(c[h], k >> 1, k & 1);
+          const float2 t = half2_to_float2(v[h][k]);
+          f0 = fmaf(w, t.x, f0);
+          f1 = fmaf(w, t.y, f1);
+        }
+        store_enc(dst, (uint32_t)f2h(f0) | ((uint32_t)f2h(f1) << 16));
+      } else if (in[h]) {
+        *dst = 0u;
       }
-      store_enc(enc + (int64_t)l * stride + i, (uint32_t)f2h(f0) | ((uint32_t)f2h(f1) << 16));
     }
     if (count) {
       lds_barrier();
-      count_block_records_fine(a, l, c, in, hist, ws);
+#pragma unroll
+      for (int h = 0; h < kEncSpt; ++h) count_fine_add(c[h], in[h], hist);
+      lds_barrier();
+      publish_block_counts(a, l, hist, ws);
     }
     return;
   }
-  Corners c;
-  level_corners(lv, x, y, z, c);
-  if (in && !use) enc[(int64_t)l * stride + i] = 0u;
-  if (use) {
-    uint32_t v[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = table[c.idx[k]];
-    float f0 = 0.f, f1 = 0.f;
+  for (int h = 0; h < kEncSpt; ++h) {
+    Corners c;
+    level_corners(lv, x[h], y[h], z[h], c);
+    uint32_t* dst = enc + (int64_t)l * stride + i0 + h * H;
+    if (use[h]) {
+      uint32_t v[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float2 t = half2_to_float2(v[k]);
-      f0 = fmaf(c.w[k], t.x, f0);
-      f1 = fmaf(c.w[k], t.y, f1);
+      for (int k = 0; k < 8; ++k) v[k] = table[c.idx[k]];
+      float f0 = 0.f, f1 = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float2 t = half2_to_float2(v[k]);
+        f0 = fmaf(c.w[k], t.x, f0);
+        f1 = fmaf(c.w[k], t.y, f1);
+      }
+      store_enc(dst, (uint32_t)f2h(f0) | ((uint32_t)f2h(f1) << 16));
+    } else if (in[h]) {
+      *dst = 0u;
     }
-    store_enc(enc + (int64_t)l * stride + i, (uint32_t)f2h(f0) | ((uint32_t)f2h(f1) << 16));
+    if (count) {
+      if (h == 0) lds_barrier();  // the zeroed histogram
+      count_add(a, l, c, in[h], in[h], hist);
+    }
   }
   if (count) {
     lds_barrier();
-    count_block_records(a, l, c, in, in, hist, ws);
+    publish_block_counts(a, l, hist, ws);
   }
 }
 
@@ -209,6 +259,7 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
                       const float* live = nullptr) {
   GridArgs a = make_args(d, pos.samples_per_ray());
   LNR_REQUIRE(n < (int64_t(1) << 31), "%s: n=%lld samples exceeds 2^31", who, (long long)n);
+  const bool spt2 = n >= (int64_t)LNR_ENC_SPT2_MIN_N;
   if (bwd_ws) {
     LNR_REQUIRE(bwd_ws_bytes >= bwd_workspace_bytes(d, n), "%s: backward workspace too small", who);
     LNR_REQUIRE(a.n_buckets <= (uint32_t)kMaxBuckets, "%s: too many table chunks (%u)", who, a.n_buckets);
@@ -218,13 +269,21 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
     BwdWorkspace w = carve_workspace(bwd_ws, a, d, n);
     // one workgroup per histogram row (kSB samples) so the row is written whole
     dim3 gridc((unsigned)w.n_sb, d->n_levels);
-    hipLaunchKernelGGL(k_hashgrid_fwd<PosFn>, gridc, dim3(kSB), 0, st, a, pos, n, reinterpret_cast<const uint32_t*>(table),
-                       enc, enc_stride, w, nullptr);
+    if (spt2)
+      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 2>), gridc, dim3(kSB / 2), 0, st, a, pos, n,
+                         reinterpret_cast<const uint32_t*>(table), enc, enc_stride, w, nullptr);
+    else
+      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1>), gridc, dim3(kSB), 0, st, a, pos, n,
+                         reinterpret_cast<const uint32_t*>(table), enc, enc_stride, w, nullptr);
   } else {
-    // kSB-sample workgroups as in training (C2-size eval launch: 1011 us at 256 threads, 836 at 512)
+    // kSB-sample workgroups as in training (C2-size eval launch: 1011 us at 256 one-sample threads, 836 at 512)
     dim3 grid((unsigned)((n + kSB - 1) / kSB), d->n_levels);
-    hipLaunchKernelGGL(k_hashgrid_fwd<PosFn>, grid, dim3(kSB), 0, st, a, pos, n, reinterpret_cast<const uint32_t*>(table),
-                       enc, enc_stride, BwdWorkspace{}, live);
+    if (spt2)
+      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 2>), grid, dim3(kSB / 2), 0, st, a, pos, n,
+                         reinterpret_cast<const uint32_t*>(table), enc, enc_stride, BwdWorkspace{}, live);
+    else
+      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1>), grid, dim3(kSB), 0, st, a, pos, n,
+                         reinterpret_cast<const uint32_t*>(table), enc, enc_stride, BwdWorkspace{}, live);
   }
   LNR_RETURN_LAUNCH(who);
 }

@@ -597,9 +597,9 @@ __device__ __forceinline__ void publish_block_counts(const GridArgs& a, uint32_t
   for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) row[b] = hist[b];
 }
 
-// Fine levels: one record per x-pair, two when the pair spans two chunks (d >= kChunk).
-__device__ __forceinline__ void count_block_records_fine(const GridArgs& a, uint32_t l, const FineCell& c, bool in,
-                                                         uint32_t* hist, const BwdWorkspace& ws) {
+// Fine levels: one record per x-pair, two when the pair spans two chunks (d >= kChunk).  The _add
+// forms only count (LDS atomics): the forward counts two samples per thread before publishing.
+__device__ __forceinline__ void count_fine_add(const FineCell& c, bool in, uint32_t* hist) {
   if (in) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -607,6 +607,10 @@ __device__ __forceinline__ void count_block_records_fine(const GridArgs& a, uint
       if (c.d >= (uint32_t)kChunk) atomicAdd(&hist[(c.e[j] ^ c.d) >> kChunkLog2], 1u);
     }
   }
+}
+__device__ __forceinline__ void count_block_records_fine(const GridArgs& a, uint32_t l, const FineCell& c, bool in,
+                                                         uint32_t* hist, const BwdWorkspace& ws) {
+  count_fine_add(c, in, hist);
   lds_barrier();
   publish_block_counts(a, l, hist, ws);
 }
@@ -614,8 +618,9 @@ __device__ __forceinline__ void count_block_records_fine(const GridArgs& a, uint
 // ``in``: the sample exists; ``act``: it has a non-zero gradient at this level (only the count
 // after the MLP backward knows; = in otherwise).  Coherent levels count every sample (zero lanes
 // merge into the runs harmlessly), the others only active ones: the scatter decides the same way.
-__device__ __forceinline__ void count_block_records(const GridArgs& a, uint32_t l, const Corners& c, bool in,
-                                                    bool act, uint32_t* hist, const BwdWorkspace& ws) {
+// Every lane of the wave must call it (the run ballot).
+__device__ __forceinline__ void count_add(const GridArgs& a, uint32_t l, const Corners& c, bool in, bool act,
+                                          uint32_t* hist) {
   const uint32_t off = a.lv[l].offset;
   if (l < a.merge_levels) {
     const RunInfo ri = cell_runs_dpp(in, c.cx, c.cy, c.cz);  // every lane must take part in the ballot
@@ -631,6 +636,10 @@ __device__ __forceinline__ void count_block_records(const GridArgs& a, uint32_t 
       if (!pairable(e0, e1)) atomicAdd(&hist[e1 >> kChunkLog2], 1u);
     }
   }
+}
+__device__ __forceinline__ void count_block_records(const GridArgs& a, uint32_t l, const Corners& c, bool in,
+                                                    bool act, uint32_t* hist, const BwdWorkspace& ws) {
+  count_add(a, l, c, in, act, hist);
   lds_barrier();
   publish_block_counts(a, l, hist, ws);
 }

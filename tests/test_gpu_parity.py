@@ -73,6 +73,41 @@ def test_hashgrid_fwd_bitexact_indices(L):
     assert np.all(np.abs(got - ref) <= 1.01 * ulp), np.abs(got - ref).max()
 
 
+@pytest.mark.parametrize("count", [False, True])
+@pytest.mark.parametrize("n", [3 * 4096 + 77, (1 << 18) + 77])
+def test_hashgrid_fwd_table_offset_and_ragged_rows(L, count, n):
+    """The encode (one sample per thread below 2^18 samples, else two: samples t and t + 256 of each
+    512-sample row) on a ragged last row, with the table at a 16-B aligned and at an unaligned (4 B past) address: the same
+    entries, so bit-identical encodings and training-launch record histograms, and both within one
+    fp16 ulp of the oracle.  Positions at the grid's upper edge exercise the x-pair wrap."""
+    rng = np.random.default_rng(7)
+    d = L.grid_desc(16, 2, 18, 16)
+    lay = ohg.GridLayout(16, 2, 18, 16)
+    pos = rng.uniform(0, 1, (n, 3)).astype(np.float32)
+    pos[:6] = [[0, 0, 0], [1, 1, 1], [0.999999, 0.5, 0.25], [1, 0, 1], [0.5, 0.999999, 0.999999], [0.25, 0.75, 1]]
+    table = rng.uniform(-1, 1, (lay.n_entries, 2)).astype(np.float16).view(np.int16).reshape(-1)
+    buf = torch.zeros(table.size + 8, dtype=torch.int16, device="cuda")
+    aligned = buf[:table.size]
+    shifted = buf[2:2 + table.size]  # 4 B past a 16-B boundary
+    outs = []
+    for t in (aligned, shifted):
+        t.copy_(torch.from_numpy(table))
+        enc = torch.empty(16, n, dtype=torch.int32, device="cuda")
+        ws = nb = None
+        if count:
+            nb = int(L.lib().lnr_hashgrid_bwd_workspace_bytes(ctypes.byref(d), n))
+            ws = torch.zeros(nb // 4 + 1, dtype=torch.int32, device="cuda")
+        L.call("lnr_hashgrid_fwd", ctypes.byref(d), cu(pos), n, t, enc, n, ws, nb or 0, L.stream())
+        torch.cuda.synchronize()
+        outs.append((enc.clone(), None if ws is None else ws.clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    if count:
+        assert torch.equal(outs[0][1], outs[1][1])
+    got = enc_levelmajor_to_aos(outs[0][0], n, 16).astype(np.float32)
+    ref = ohg.encode(pos, table.view(np.float16).reshape(-1, 2), lay).astype(np.float32)
+    assert np.all(np.abs(got - ref) <= 1.01 * (np.abs(ref) * 2.0 ** -10 + 2.0 ** -24))
+
+
 def test_hashgrid_fwd_rays_matches_positions(L):
     g = np.load("tests/golden/samplers.npz")
     rays, z = g["rays"], g["z_ogm"]
