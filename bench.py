@@ -751,6 +751,15 @@ def main():
                      "step_algorithmic_bytes": step_bytes,
                      "step_frac": step_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "traffic_step": traffic_step, "traffic_step_source": traffic_step_src},
+        # the longest single kernel, the training encode (k_hashgrid_fwd: 8 gathers per sample and level,
+        # 512 B/sample algorithmic), against HBM peak; what bounds it is the texture addresser, not bytes
+        # ("What bounds the forward encode")
+        "dominant_kernel": {"kernel": "k_hashgrid_fwd (training encode + record histogram)",
+                            "ms_per_launch": stage_ms["encode"], "algorithmic_bytes_per_launch": 512 * N,
+                            "achieved": 512.0 * N / (stage_ms["encode"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": 512.0 * N / (stage_ms["encode"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                            "bound": "texture addresser: TA busy 0.85 of the launch at C2 "
+                                     "(rocprofv3 TA_BUSY_avr, profiles/r03_l2req_C2.txt)"},
         # the sigma MLP (fwd 4224 + bwd 8448 FLOP/sample) over the field stage
         # (k_sigma_fwd_tiles + k_composite_wave + k_mlp_bwd_tiles), against the dense fp16 MFMA peak
         "mfma": {"achieved": mlp_tflops, "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": mlp_tflops / MFMA_PEAK_TFLOPS,
