@@ -22,7 +22,7 @@ __device__ __forceinline__ void store_enc(uint32_t* p, uint32_t v) { __builtin_n
 // TA cycles per wave-wide gather of scattered entries (profiles/r03_l2req_C2.txt).  Reading an
 // x-pair through one 16-B load of its aligned quad (3/4 of the pairs; tried) cut the vector-L1 line
 // accesses from 426 M to 288 M per launch but left TA busy where it was (0.743 against 0.720 ms);
-// 8-B pair loads ran 0.86 ms.  Plain dword gathers it is.
+// 8-B pair loads ran 0.86 ms.  Plain dword gathers (here, or lane-paired below).
 __device__ __forceinline__ void fine_gather(const uint32_t* __restrict__ tl, const FineCell& c, uint32_t (&v)[8]) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -31,9 +31,49 @@ __device__ __forceinline__ void fine_gather(const uint32_t* __restrict__ tl, con
   }
 }
 
+// The same 8 corners with lanes paired (2m, 2m + 1): in one instruction both lanes of a pair read
+// the two x-corners of one sample's edge (the even lane corner e, the odd lane e ^ d), so the pair
+// shares a cache line (94 % of the x-pairs do) and a wave-wide gather touches 32 lines instead of 64.
+// Slot 0 of each edge serves the even lane's sample, slot 1 the odd lane's; one DPP swap per edge
+// hands each lane the corner its partner read for it.  C2 encode 0.721 -> 0.691 ms: the texture
+// addresser does not charge purely by lines.  Every lane of the wave must take
+// part (the swaps): the loads, not the lanes, are predicated on ``use``, and a dead lane still gathers
+// for a live partner, which is why the live-masked eval launch keeps fine_gather.  Same entries in the
+// same corner order: the encoding is bit-identical to fine_gather's.
+#ifndef LNR_ENC_PAIRED
+#define LNR_ENC_PAIRED true  // the training / plain eval encode's fine gathers lane-paired (C2: 0.721 -> 0.691 ms)
+#endif
+__device__ __forceinline__ uint32_t dpp_pair_swap(uint32_t v) {  // quad_perm [1, 0, 3, 2]
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ void fine_gather_paired(const uint32_t* __restrict__ tl, const FineCell& c, bool use,
+                                                   uint32_t (&v)[8]) {
+  const bool odd = (threadIdx.x & 1) != 0;
+  const uint32_t pd = dpp_pair_swap(c.d);
+  const bool puse = dpp_pair_swap(use ? 1u : 0u) != 0u;
+  const uint32_t d_even = odd ? pd : c.d, d_odd = odd ? c.d : pd;
+  const bool use_even = odd ? puse : use, use_odd = odd ? use : puse;
+  uint32_t s0[4], s1[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t pe = dpp_pair_swap(c.e[j]);
+    const uint32_t e_even = odd ? pe : c.e[j], e_odd = odd ? c.e[j] : pe;
+    const uint32_t a0 = odd ? (e_even ^ d_even) : e_even;  // slot 0: the even lane's sample
+    const uint32_t a1 = odd ? (e_odd ^ d_odd) : e_odd;     // slot 1: the odd lane's sample
+    s0[j] = use_even ? tl[a0] : 0u;
+    s1[j] = use_odd ? tl[a1] : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t r = dpp_pair_swap(odd ? s0[j] : s1[j]);  // what the partner read for this lane
+    v[2 * j] = odd ? r : s0[j];
+    v[2 * j + 1] = odd ? s1[j] : r;
+  }
+}
+
 #ifndef LNR_ENC_SPT2_MIN_N
-#define LNR_ENC_SPT2_MIN_N (1 << 18)  // two samples per thread from this many samples (C2 encode 0.745-0.770 ->
-                                      // 0.720 ms); below it one (C1: 19 against 25 us: half the waves)
+#define LNR_ENC_SPT2_MIN_N (1 << 18)  // the live-masked eval encode: two samples per thread from this many
+                                      // samples (C3 colour encode 0.48 -> 0.43 ms); below it one
 #endif
 
 // One kernel for the training encode (ws.hist set: also the backward's record histogram) and the
@@ -47,7 +87,7 @@ __device__ __forceinline__ void fine_gather(const uint32_t* __restrict__ tl, con
 #ifndef LNR_ENC_WAVES
 #define LNR_ENC_WAVES 8  // waves per SIMD asked of the encode (68 registers would allow 7)
 #endif
-template <class PosFn, int kEncSpt>
+template <class PosFn, int kEncSpt, bool PAIRED>
 __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per_eu(LNR_ENC_WAVES, LNR_ENC_WAVES))) k_hashgrid_fwd(GridArgs a, PosFn pos, int64_t n,
                                                                const uint32_t* __restrict__ table,
                                                                uint32_t* __restrict__ enc, int64_t stride,
@@ -56,7 +96,7 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
   const int64_t i0 = (int64_t)blockIdx.x * kSB + threadIdx.x;
   const uint32_t l = blockIdx.y;
   const bool count = ws.hist != nullptr;
-  if (!count && i0 >= n) return;
+  if (!count && (i0 & ~(int64_t)1) >= n) return;  // (lane pairs leave together: fine_gather_paired)
   __shared__ uint32_t hist[kMaxChunksPerLevel];
   if (count) {
     for (int b = threadIdx.x; b < kMaxChunksPerLevel; b += blockDim.x) hist[b] = 0;
@@ -79,9 +119,14 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
     uint32_t v[kEncSpt][8];
     const uint32_t* tl = table + lv.offset;
 #pragma unroll
-    for (int h = 0; h < kEncSpt; ++h) {
-      fine_cell(lv, x[h], y[h], z[h], c[h]);
-      if (use[h]) fine_gather(tl, c[h], v[h]);
+    for (int h = 0; h < kEncSpt; ++h) fine_cell(lv, x[h], y[h], z[h], c[h]);
+    if constexpr (PAIRED) {
+#pragma unroll
+      for (int h = 0; h < kEncSpt; ++h) fine_gather_paired(tl, c[h], use[h], v[h]);
+    } else {
+#pragma unroll
+      for (int h = 0; h < kEncSpt; ++h)
+        if (use[h]) fine_gather(tl, c[h], v[h]);
     }
 #pragma unroll
     for (int h = 0; h < kEncSpt; ++h) {
@@ -259,6 +304,9 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
                       const float* live = nullptr) {
   GridArgs a = make_args(d, pos.samples_per_ray());
   LNR_REQUIRE(n < (int64_t(1) << 31), "%s: n=%lld samples exceeds 2^31", who, (long long)n);
+  // training and plain eval launches: one sample per thread, lane-paired fine gathers; the eval launch
+  // with a ``live`` mask (C3's colour encode, most samples dead): plain gathers, so dead lanes issue
+  // none, two samples per thread from LNR_ENC_SPT2_MIN_N samples
   const bool spt2 = n >= (int64_t)LNR_ENC_SPT2_MIN_N;
   if (bwd_ws) {
     LNR_REQUIRE(bwd_ws_bytes >= bwd_workspace_bytes(d, n), "%s: backward workspace too small", who);
@@ -269,21 +317,21 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
     BwdWorkspace w = carve_workspace(bwd_ws, a, d, n);
     // one workgroup per histogram row (kSB samples) so the row is written whole
     dim3 gridc((unsigned)w.n_sb, d->n_levels);
-    if (spt2)
-      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 2>), gridc, dim3(kSB / 2), 0, st, a, pos, n,
-                         reinterpret_cast<const uint32_t*>(table), enc, enc_stride, w, nullptr);
-    else
-      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1>), gridc, dim3(kSB), 0, st, a, pos, n,
-                         reinterpret_cast<const uint32_t*>(table), enc, enc_stride, w, nullptr);
+    hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED>), gridc, dim3(kSB), 0, st, a, pos, n,
+                       reinterpret_cast<const uint32_t*>(table), enc, enc_stride, w, nullptr);
   } else {
     // kSB-sample workgroups as in training (C2-size eval launch: 1011 us at 256 one-sample threads, 836 at 512)
     dim3 grid((unsigned)((n + kSB - 1) / kSB), d->n_levels);
-    if (spt2)
-      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 2>), grid, dim3(kSB / 2), 0, st, a, pos, n,
-                         reinterpret_cast<const uint32_t*>(table), enc, enc_stride, BwdWorkspace{}, live);
+    const uint32_t* tb = reinterpret_cast<const uint32_t*>(table);
+    if (live == nullptr)
+      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED>), grid, dim3(kSB), 0, st, a, pos, n, tb, enc,
+                         enc_stride, BwdWorkspace{}, live);
+    else if (spt2)
+      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 2, false>), grid, dim3(kSB / 2), 0, st, a, pos, n, tb, enc,
+                         enc_stride, BwdWorkspace{}, live);
     else
-      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1>), grid, dim3(kSB), 0, st, a, pos, n,
-                         reinterpret_cast<const uint32_t*>(table), enc, enc_stride, BwdWorkspace{}, live);
+      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, false>), grid, dim3(kSB), 0, st, a, pos, n, tb, enc,
+                         enc_stride, BwdWorkspace{}, live);
   }
   LNR_RETURN_LAUNCH(who);
 }

@@ -76,8 +76,8 @@ def test_hashgrid_fwd_bitexact_indices(L):
 @pytest.mark.parametrize("count", [False, True])
 @pytest.mark.parametrize("n", [3 * 4096 + 77, (1 << 18) + 77])
 def test_hashgrid_fwd_table_offset_and_ragged_rows(L, count, n):
-    """The encode (one sample per thread below 2^18 samples, else two: samples t and t + 256 of each
-    512-sample row) on a ragged last row, with the table at a 16-B aligned and at an unaligned (4 B past) address: the same
+    """The encode (lane-paired fine gathers: both lanes of a pair read one sample's x-pair, then swap)
+    on a ragged last row of odd length (the last sample's partner lane has no sample), with the table at a 16-B aligned and at an unaligned (4 B past) address: the same
     entries, so bit-identical encodings and training-launch record histograms, and both within one
     fp16 ulp of the oracle.  Positions at the grid's upper edge exercise the x-pair wrap."""
     rng = np.random.default_rng(7)
@@ -106,6 +106,32 @@ def test_hashgrid_fwd_table_offset_and_ragged_rows(L, count, n):
     got = enc_levelmajor_to_aos(outs[0][0], n, 16).astype(np.float32)
     ref = ohg.encode(pos, table.view(np.float16).reshape(-1, 2), lay).astype(np.float32)
     assert np.all(np.abs(got - ref) <= 1.01 * (np.abs(ref) * 2.0 ** -10 + 2.0 ** -24))
+
+
+@pytest.mark.parametrize("R", [24, 520])
+def test_hashgrid_fwd_live_mask_matches_full_encode(L, R):
+    """The live-masked eval encode (plain gathers, dead samples issue none; two samples per thread
+    from 2^18 samples) equals the full encode (lane-paired gathers) on live samples and is 0 on dead
+    ones, bit for bit: the same entries in the same corner order."""
+    rng = np.random.default_rng(11)
+    S = 512
+    d = L.grid_desc(16, 2, 19, 16)
+    lay = ohg.GridLayout(16, 2, 19, 16)
+    o = rng.uniform(-0.5, 0.5, (R, 3))
+    dr = rng.normal(0, 1, (R, 3))
+    dr /= np.linalg.norm(dr, axis=1, keepdims=True)
+    rays = np.zeros((R, 13), np.float32)
+    rays[:, 0:3], rays[:, 3:6] = o, dr
+    z = np.sort(rng.uniform(0.0, 0.45, (R, S)), 1).astype(np.float32)
+    live = (rng.uniform(0, 1, (R, S)) < 0.3).astype(np.float32)
+    table = cu(rng.uniform(-1, 1, (lay.n_entries, 2)).astype(np.float16).view(np.int16))
+    full = torch.empty(16, R * S, dtype=torch.int32, device="cuda")
+    part = torch.full((16, R * S), -1, dtype=torch.int32, device="cuda")
+    L.call("lnr_hashgrid_fwd_rays", ctypes.byref(d), cu(rays), cu(z), R, S, table, full, R * S, None, 0, L.stream())
+    L.call("lnr_hashgrid_fwd_rays_live", ctypes.byref(d), cu(rays), cu(z), R, S, table, cu(live), part, R * S,
+           L.stream())
+    mask = torch.from_numpy(live.reshape(1, -1) != 0).cuda()
+    assert torch.equal(part, torch.where(mask, full, torch.zeros_like(full)))
 
 
 def test_hashgrid_fwd_rays_matches_positions(L):
