@@ -271,6 +271,12 @@ class StepEngine:
         self._pp, self._pp_parity = None, 0
         self._pp_stream = torch.cuda.Stream(device=dev)
         self._pp_fork = torch.cuda.Event()
+        # where in step k the prefetch may start (LONER_PIPE_AT): "start" (beside the encode), "encode"
+        # (after the encode launch: beside the field and the backward) or "field" (beside the backward)
+        self.pipe_at = os.environ.get("LONER_PIPE_AT", "start")
+        if self.pipe_at not in ("start", "encode", "field"):
+            raise ValueError(f"LONER_PIPE_AT={self.pipe_at!r}: expected start, encode or field")
+        self._pp_mid = torch.cuda.Event()
         self._pp_bufs = [dict(rays=self.rays if i == 0 else torch.empty_like(self.rays),
                               dgt=self.depth_gt if i == 0 else torch.empty_like(self.depth_gt),
                               valid=self.ray_valid if i == 0 else torch.empty_like(self.ray_valid),
@@ -399,6 +405,8 @@ class StepEngine:
             L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(st.desc), rays, self.z, R, S, st.table_f16, self.enc, N,
                    None, 0, s)
         m(prof, "encode")
+        if self.pipe_at == "encode":
+            self._pp_mid.record(main)
         # 4. fused field + loss + backward through compositing and MLP (stores the MLP gradient, and the
         # loss scalars into loss_out)
         main.wait_event(self._join)
@@ -409,6 +417,8 @@ class StepEngine:
                self.ray_offset, L.ctypes.byref(lp), self.d_enc, st.grad_mlp, self.ws, self.stats, self.depth,
                self.opacity, None, self.level_max_ptr, self.d_jac if self.compact_denc else None, s)
         m(prof, "field")
+        if self.pipe_at == "field":
+            self._pp_mid.record(main)
         self._r_last = R
         # 5. hash-grid backward
         m(prof, "grid_bwd")
@@ -614,7 +624,7 @@ class StepEngine:
         key = L.step_key(self.seed, global_step + 1)
         sample = cfg.sampler != "OGM" or not ogm_now  # the OGM sampler reads the grid step k may update
         with torch.cuda.stream(self._pp_stream):
-            self._pp_stream.wait_event(self._pp_fork)
+            self._pp_stream.wait_event(self._pp_fork if self.pipe_at == "start" else self._pp_mid)
             window.build(key, self.ray_offset, n, bq["rays"][:n], bq["dgt"][:n], bq["valid"][:n], None, bq["far"])
             if sample:
                 s = L.stream(self.state.device)

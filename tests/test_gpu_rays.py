@@ -178,22 +178,23 @@ def test_pipelined_build_and_sampling_equals_plain(L):
     """step_window's pipeline (step k + 1's ray build and sampling enqueued on a side stream after
     step k, double-buffered; no sampling prefetch after an OGM step) gives bitwise the plain path's
     losses, parameters, occupancy grid and last samples, across OGM steps (global steps 10, 20) and a
-    skipped step (the prefetch is discarded)."""
+    skipped step (the prefetch is discarded), for every fork point of the prefetch (LONER_PIPE_AT)."""
     from loner_amd import step as S_
     from loner_amd.rays import RayWindow
     scans, wc, rr = _window("forest", 2, seed=8)
     win = RayWindow(scans, wc, rr, n_lidar=128, n_sky=16, strategy="MASK")
     assert win.all_valid
     res = []
-    for pipeline in (True, False):
+    for pipeline, at in ((False, "start"), (True, "start"), (True, "encode"), (True, "field")):
         st = S_.FieldState(S_.StepConfig(n_samples=128, occ_lr=1e-3), device="cuda:0", table_init=0.5)
         eng = S_.StepEngine(st, win.n_slots, seed=7)
-        eng.pipeline = pipeline
+        eng.pipeline, eng.pipe_at = pipeline, at
         outs = [eng.step_window(win, global_step=g).clone() for g in (8, 9, 10, 11, 13, 14, 19, 20, 21)]
         torch.cuda.synchronize()
         res.append(([host(o) for o in outs], host(st.params).copy(), host(st.occ).copy(), host(eng.z).copy(),
                     host(eng.rays).copy()))
-    for a, b in zip(res[0][0], res[1][0]):
-        np.testing.assert_array_equal(a, b)
-    for a, b in zip(res[0][1:], res[1][1:]):
-        np.testing.assert_array_equal(a, b)
+    for r in res[1:]:
+        for a, b in zip(res[0][0], r[0]):
+            np.testing.assert_array_equal(a, b)
+        for a, b in zip(res[0][1:], r[1:]):
+            np.testing.assert_array_equal(a, b)
