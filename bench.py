@@ -505,7 +505,7 @@ def _camera_stages(eng, fr, rays, inten, L):
            1.0 / (3.0 * R), eng.rgb, eng.loss, eng.d_enc, cs.grad_mlp, eng.ws, eng.ws_bytes, eng.level_max_ptr, s)
     mark("grid_bwd")
     L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(cs.desc), rays, eng.z, R, S, eng.d_enc, N, cs.grad_table,
-           eng.bwd_ws, eng.bwd_ws_bytes, (0 if eng.skip_zero else L.BWD_COUNTS_READY) | L.BWD_LEVEL_MAX_READY, s)
+           None, None, eng.bwd_ws, eng.bwd_ws_bytes, (0 if eng.skip_zero else L.BWD_COUNTS_READY) | L.BWD_LEVEL_MAX_READY, s)
     mark("adam")
     L.call("lnr_adam_step", cs.params, cs.shadow, cs.grad, cs.m, cs.v, cs.n_padded, 1, 0.0, 0.9, 0.999, 1e-8, s)
     mark("end")

@@ -101,8 +101,16 @@ int lnr_hashgrid_fwd_rays_live(const lnr_grid_desc* d, const float* rays, const 
 /* Backward: d_table (n_entries,2) fp32 = scatter of corner weights * d_enc, as an atomic-free
  * binned scatter of 8-byte records (fp16 values at a per-level power-of-two scale from max |d_enc|)
  * with int64 fixed-point accumulation.  d_table is OVERWRITTEN (every entry, zero where
- * no sample touches it) and the result is bitwise reproducible; `workspace` holds at least
- * lnr_hashgrid_bwd_workspace_bytes(d, N) bytes. */
+ * no sample touches it, all zero for N = 0) and the result is bitwise reproducible; `workspace` holds
+ * at least lnr_hashgrid_bwd_workspace_bytes(d, N) bytes.
+ * Input gradient (tcnn's backward w.r.t. the positions, src/models/nerf_tcnn.py:63,68-71 when pos
+ * requires grad, e.g. joint pose + map optimisation, src/mapping/optimizer.py:256-262): when d_pos is
+ * not NULL, d_pos (N,3) fp32 = dL/dpos01 (OVERWRITTEN): per sample, the sum over (level, feature) of
+ * d_enc * d enc / d pos01, the trilinear blend's derivative from the fp16 `table` (the forward's
+ * operand, 4-byte aligned): tcnn v1.7 kernel_grid's dy_dx + kernel_grid_backward_input.  The _rays
+ * forms give it per sample w.r.t. pos01 = (o + d z + 1) / 2.  Deterministic (one fixed-order sum per
+ * sample).  d_table may be NULL (no table gradient: workspace unused), d_pos may be NULL (table unused),
+ * not both.  The input gradient is its own launch, so a call without d_pos costs nothing extra. */
 #define LNR_BWD_COUNTS_READY 1
 #define LNR_BWD_NO_ACCUM 2      /* stop after the scatter: lnr_hashgrid_bwd_accum then finishes level ranges */
 #define LNR_BWD_LEVEL_MAX_READY 4 /* the caller stored max |d_enc| per level at lnr_hashgrid_bwd_level_max():
@@ -115,16 +123,18 @@ int64_t lnr_hashgrid_bwd_workspace_bytes(const lnr_grid_desc* d, int64_t n);
  * every n: the workspace's first bytes). */
 float* lnr_hashgrid_bwd_level_max(const lnr_grid_desc* d, int64_t n, void* workspace);
 int lnr_hashgrid_bwd(const lnr_grid_desc* d, const float* pos01, int64_t n, const float* d_enc,
-                     int64_t enc_stride, float* d_table, void* workspace, int64_t workspace_bytes, int32_t flags,
-                     void* stream);
+                     int64_t enc_stride, float* d_table, const uint16_t* table, float* d_pos, void* workspace,
+                     int64_t workspace_bytes, int32_t flags, void* stream);
 int lnr_hashgrid_bwd_rays(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
                           int32_t n_samples, const float* d_enc, int64_t enc_stride, float* d_table,
-                          void* workspace, int64_t workspace_bytes, int32_t flags, void* stream);
+                          const uint16_t* table, float* d_pos, void* workspace, int64_t workspace_bytes,
+                          int32_t flags, void* stream);
 /* The same, from lnr_field_train's compact encoding gradient: d_enc = d_sigma[n] * J[l][n] with J
  * level-major fp16 pairs (one uint32 per level and sample, level stride jac_stride). */
 int lnr_hashgrid_bwd_rays_jac(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
                               int32_t n_samples, const uint32_t* d_jac, const float* d_sigma, int64_t jac_stride,
-                              float* d_table, void* workspace, int64_t workspace_bytes, int32_t flags, void* stream);
+                              float* d_table, const uint16_t* table, float* d_pos, void* workspace,
+                              int64_t workspace_bytes, int32_t flags, void* stream);
 /* With flags & LNR_BWD_NO_ACCUM the three calls above stop after the scatter; this finishes the
  * levels [level_begin, level_end) (n = samples of that call, same workspace): their slice of
  * d_table is final on return, so a data-parallel caller can all-reduce it while the next range
@@ -231,11 +241,14 @@ int lnr_composite_loss_bwd(const float* rays, const float* z, const float* sigma
 /* Autograd backward of lnr_composite (the tcnn-compatible render_rays path, where the loss is the
  * caller's torch code): d_sigma (R,S) fp32 from upstream gradients of weights (R,S), depth, opacity
  * and variance (R); any of them may be NULL (= zero).  Same noise arguments as the forward, so the
- * noise is regenerated bit-identically instead of being stored. */
+ * noise is regenerated bit-identically instead of being stored.  d_ray (optional, (R,2)): the
+ * render's gradient w.r.t. the ray itself, [dL/d|d| (deltas are scaled by the direction's norm,
+ * rendering_tcnn.py:248), dL/dfar (the default depth's far term, :274-278; 0 for the adjusted
+ * strategy)] - what autograd returns when the rays require grad (poses under optimisation). */
 int lnr_composite_bwd(const float* rays, const float* z, const float* sigma, int64_t n_rays, int32_t n_samples,
                       int32_t strategy, float noise_std, const float* noise, uint32_t key, int64_t ray_offset,
                       const float* g_weights, const float* g_depth, const float* g_opacity, const float* g_variance,
-                      float* d_sigma, void* stream);
+                      float* d_sigma, float* d_ray, void* stream);
 /* Workspace (fp32 words) lnr_field_train needs: the dW slabs, then an (n_rays, n_samples) d_sigma
  * buffer between its ray phase and its tile-parallel MLP backward. */
 int64_t lnr_field_train_workspace_words(int64_t n_rays, int32_t n_samples);

@@ -109,12 +109,12 @@ _SIGNATURES = {
                                              c_i64, c_p]),
     "lnr_hashgrid_bwd_workspace_bytes": (c_i64, [ctypes.POINTER(GridDesc), c_i64]),
     "lnr_hashgrid_bwd_level_max": (c_p, [ctypes.POINTER(GridDesc), c_i64, c_p]),
-    "lnr_hashgrid_bwd": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_i32,
-                                        c_p]),
+    "lnr_hashgrid_bwd": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64,
+                                        c_i32, c_p]),
     "lnr_hashgrid_bwd_rays": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_p,
-                                             c_i64, c_i32, c_p]),
+                                             c_p, c_p, c_i64, c_i32, c_p]),
     "lnr_hashgrid_bwd_rays_jac": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_p, c_i64,
-                                                 c_p, c_p, c_i64, c_i32, c_p]),
+                                                 c_p, c_p, c_p, c_p, c_i64, c_i32, c_p]),
     "lnr_hashgrid_bwd_accum": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_i64, c_p, c_i64, c_u32, c_u32, c_p, c_p]),
     "lnr_hashgrid_bwd_atomic": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_i64, c_p, c_i64, c_p, c_p]),
     "lnr_hashgrid_bwd_rays_atomic": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_i64, c_p,
@@ -132,7 +132,7 @@ _SIGNATURES = {
     "lnr_composite": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_i32, c_f, c_p, c_u32, c_i64, c_p, c_p, c_p, c_p,
                                      c_p]),
     "lnr_composite_bwd": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_i32, c_f, c_p, c_u32, c_i64, c_p, c_p, c_p,
-                                         c_p, c_p, c_p]),
+                                         c_p, c_p, c_p, c_p]),
     "lnr_composite_loss_bwd": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_u32, c_i64,
                                               ctypes.POINTER(LossParams), c_p, c_p, c_p, c_p, c_p, c_p]),
     "lnr_field_train": (ctypes.c_int, [c_p, c_p, c_i64, c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_u32, c_i64,

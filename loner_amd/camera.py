@@ -262,7 +262,7 @@ class CameraStepEngine:
                S, 1.0 / (3.0 * n_glob), self.rgb, self.loss, self.d_enc, cs.grad_mlp, self.ws, self.ws_bytes,
                self.level_max_ptr, s)
         L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(cs.desc), rays, self.z, R, S, self.d_enc, N, cs.grad_table,
-               self.bwd_ws, self.bwd_ws_bytes, (0 if self.skip_zero else L.BWD_COUNTS_READY) | L.BWD_LEVEL_MAX_READY, s)
+               None, None, self.bwd_ws, self.bwd_ws_bytes, (0 if self.skip_zero else L.BWD_COUNTS_READY) | L.BWD_LEVEL_MAX_READY, s)
         if self.allreduce is not None:
             self.allreduce(cs.grad)
         cs.adam_step += 1

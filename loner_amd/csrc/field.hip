@@ -50,6 +50,7 @@ struct FieldArgs {
   const float* g_depth;     // (R)
   const float* g_opacity;   // (R)
   const float* g_variance;  // (R)
+  float* d_ray;             // optional (R,2): [dL/d|d|, dL/dfar] (the render's dependence on the ray itself)
 };
 
 // lnr_loss_params.kind for the plain autograd backward of the render (no loss inside the kernel)
@@ -125,16 +126,18 @@ __device__ void composite_ray(const FieldArgs& a, const RayShared& sh, int64_t r
   const float* zr = a.z + r * S;
   const int64_t gr = a.ray_offset + r;
 
-  float z[C], alpha[C], s[C], delta[C], x[C], w[C];
+  float z[C], alpha[C], s[C], delta[C], x[C], w[C], dlr[C];
   double tl[C];
   double P = 1.0;
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     const int i = i0 + c;
+    dlr[c] = 0.f;
     if (active && i < S) {
       z[c] = zr[i];
       const float zn = (i + 1 < S) ? zr[i + 1] : 0.f;
       const float dl = (i + 1 < S) ? (zn - z[c]) : 1e10f;
+      dlr[c] = dl;
       delta[c] = dl * dnorm;
       float nz = 0.f;
       if (!ADJ) {
@@ -257,15 +260,28 @@ __device__ void composite_ray(const FieldArgs& a, const RayShared& sh, int64_t r
       }
     }
     float X = block_suffix_affine(FA, FB, sh.fscan);
+    double acc_dn = 0.0;
 #pragma unroll
     for (int c = C - 1; c >= 0; --c) {
       if (active && i0 + c < S) {
         const float dA = T[c] * (G[c] - X);
         X = G[c] * alpha[c] + s[c] * X;
         const float sr = fmaxf(x[c], 0.f);
-        const float dsig = (x[c] > 0.f) ? dA * (delta[c] * expf(-(delta[c] * sr))) : 0.f;
+        const float ex = expf(-(delta[c] * sr));
+        const float dsig = (x[c] > 0.f) ? dA * (delta[c] * ex) : 0.f;
         sh.sig[i0 + c] = dsig;
         if (a.d_sigma) a.d_sigma[r * S + i0 + c] = dsig;
+        // deltas = dl * |d| (rendering_tcnn.py:248): d alpha / d |d| = dl * relu(sigma + noise) * exp(-delta sr)
+        acc_dn += (double)((dA * (ex * sr)) * dlr[c]);
+      }
+    }
+    if (a.d_ray) {  // (block-uniform branch)
+      float rd[1] = {(float)acc_dn};
+      block_sum<NT, 1>(rd, sh.red);
+      if (t == 0) {
+        a.d_ray[2 * r + 0] = rd[0];
+        // depth = sum w z + (1 - sum w) far (rendering_tcnn.py:274-278); the adjusted depth ignores far
+        a.d_ray[2 * r + 1] = ADJ ? 0.f : gd * (1.0f - wsum);
       }
     }
     __syncthreads();
@@ -1145,7 +1161,8 @@ extern "C" int lnr_composite_loss_bwd(const float* rays, const float* z, const f
 extern "C" int lnr_composite_bwd(const float* rays, const float* z, const float* sigma, int64_t n_rays,
                                  int32_t n_samples, int32_t strategy, float noise_std, const float* noise, uint32_t key,
                                  int64_t ray_offset, const float* g_weights, const float* g_depth,
-                                 const float* g_opacity, const float* g_variance, float* d_sigma, void* stream) {
+                                 const float* g_opacity, const float* g_variance, float* d_sigma, float* d_ray,
+                                 void* stream) {
   if (int e = check_rays(rays, z, n_rays, n_samples, "lnr_composite_bwd")) return e;
   LNR_REQUIRE(strategy == LNR_RENDER_DEFAULT || strategy == LNR_RENDER_ADJUSTED,
               "Unknown render strategy: %d", strategy);
@@ -1157,6 +1174,7 @@ extern "C" int lnr_composite_bwd(const float* rays, const float* z, const float*
   a.lp.kind = kLossExternal;
   a.g_weights = g_weights; a.g_depth = g_depth; a.g_opacity = g_opacity; a.g_variance = g_variance;
   a.d_sigma = d_sigma;
+  a.d_ray = d_ray;
   const int nb = field_blocks(n_rays);
   if (strategy == LNR_RENDER_ADJUSTED)
     return launch_field<true, true, kSigmaGiven>(a, nb, as_stream(stream), "lnr_composite_bwd");
@@ -1173,7 +1191,21 @@ extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t e
   if (int e = check_lp(lp, "lnr_field_train")) return e;
   LNR_REQUIRE(n_samples % 64 == 0, "lnr_field_train: n_samples=%d must be a multiple of 64", n_samples);
   LNR_REQUIRE(enc_stride >= n_rays * (int64_t)n_samples, "lnr_field_train: enc_stride too small");
-  if (n_rays == 0) return LNR_OK;
+  if (n_rays == 0) {
+    // an empty batch (e.g. one rank's share of a tiny global batch) still has outputs: the stored MLP
+    // gradient is zero, the level maxima are zero, and the loss scalars are finalized (loss 0)
+    hipStream_t st = as_stream(stream);
+    if (d_w && (lp->flags & LNR_LP_DW_OVERWRITE))
+      LNR_REQUIRE(hipMemsetAsync(d_w, 0, LNR_SIGMA_MLP_PARAMS * sizeof(float), st) == hipSuccess,
+                  "lnr_field_train: memset failed");
+    if (d_enc_level_max)
+      LNR_REQUIRE(hipMemsetAsync(d_enc_level_max, 0, kSigmaLevels * sizeof(float), st) == hipSuccess,
+                  "lnr_field_train: memset failed");
+    if (lp->dev_loss_out)
+      hipLaunchKernelGGL(k_loss_finalize, dim3(1), dim3(kReduceThreads), 0, st, ray_stats, (int64_t)0, *lp,
+                         lp->dev_loss_out);
+    LNR_RETURN_LAUNCH("lnr_field_train(empty)");
+  }
   LNR_REQUIRE(w && enc && depth_gt && (d_enc || d_enc_jac) && d_w && workspace && ray_stats,
               "lnr_field_train: null pointer");
   LNR_REQUIRE(!d_enc_jac || n_samples == 64 || n_samples == 128 || n_samples == 256 || n_samples == 512,

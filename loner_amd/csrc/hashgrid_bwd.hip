@@ -1309,6 +1309,98 @@ static int check_desc_bwd(const lnr_grid_desc* d, const char* who) {
   return LNR_OK;
 }
 
+// ---------------------------------------------------------------- input gradient (K3)
+// dL/dpos01 of the encoding, tcnn v1.7 grid.h: kernel_grid's dy_dx branch (per level and feature the
+// derivative of the trilinear blend along each axis: over the 4 cell edges along that axis, the
+// product of the other two axes' weights times scale_l times (value at the edge's upper corner -
+// value at its lower corner), the other axes in increasing order) followed by
+// kernel_grid_backward_input (dL/dx[dim] = sum over (level, feature) in output order of
+// dL/dy * dy/dx[dim]).  Table values are the fp16 forward operand; the arithmetic is fp32.
+// One thread per sample walks every level, so each sample's gradient is one fixed-order sum (no
+// atomics): deterministic.  The 8 corner gathers of a level are issued before any arithmetic.
+// Only launched when the caller asks for d_pos: the training step (which holds the poses fixed)
+// never pays for it.
+constexpr int kDposThreads = 256;
+template <class PosFn, class GradFn>
+__global__ void __launch_bounds__(kDposThreads) k_hashgrid_dpos(GridArgs a, PosFn pos, int64_t n,
+                                                                const uint32_t* __restrict__ table, GradFn grad,
+                                                                float* __restrict__ d_pos) {
+  const int64_t i = (int64_t)blockIdx.x * kDposThreads + threadIdx.x;
+  if (i >= n) return;
+  float x, y, z;
+  pos(i, x, y, z);
+  float r0 = 0.f, r1 = 0.f, r2 = 0.f;
+  for (uint32_t l = 0; l < a.n_levels; ++l) {
+    const LevelParams& p = a.lv[l];
+    Corners c;
+    level_corners(p, x, y, z, c);
+    uint32_t raw[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) raw[k] = table[c.idx[k]];
+    const float2 g = grad.load(l, i);
+    float2 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = half2_to_float2(raw[k]);
+    const float t[3] = {c.tx, c.ty, c.tz};
+    float dy[2][3];
+#pragma unroll
+    for (int dim = 0; dim < 3; ++dim) {
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float w = p.scale;
+        int k = 0, nd = 0;
+#pragma unroll
+        for (int od = 0; od < 3; ++od) {
+          if (od == dim) continue;
+          const int bit = (e >> nd) & 1;
+          w *= bit ? t[od] : 1.0f - t[od];
+          k |= bit << od;
+          ++nd;
+        }
+        const float2 lo = v[k], hi = v[k | (1 << dim)];
+        s0 += w * (hi.x - lo.x);
+        s1 += w * (hi.y - lo.y);
+      }
+      dy[0][dim] = s0;
+      dy[1][dim] = s1;
+    }
+    r0 += g.x * dy[0][0];
+    r1 += g.x * dy[0][1];
+    r2 += g.x * dy[0][2];
+    r0 += g.y * dy[1][0];
+    r1 += g.y * dy[1][1];
+    r2 += g.y * dy[1][2];
+  }
+  d_pos[3 * i + 0] = r0;
+  d_pos[3 * i + 1] = r1;
+  d_pos[3 * i + 2] = r2;
+}
+
+template <class PosFn, class GradFn>
+static int launch_dpos(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16_t* table, GradFn grad,
+                       float* d_pos, hipStream_t st, const char* who) {
+  LNR_REQUIRE(table != nullptr, "%s: d_pos needs the fp16 table", who);
+  LNR_REQUIRE((reinterpret_cast<uintptr_t>(table) & 3) == 0, "%s: table must be 4-byte aligned", who);
+  const GridArgs a = make_args(d, pos.samples_per_ray());
+  const int64_t nb = (n + kDposThreads - 1) / kDposThreads;
+  LNR_REQUIRE(nb < (int64_t(1) << 31), "%s: n=%lld too large", who, (long long)n);
+  hipLaunchKernelGGL((k_hashgrid_dpos<PosFn, GradFn>), dim3((unsigned)nb), dim3(kDposThreads), 0, st, a, pos, n,
+                     reinterpret_cast<const uint32_t*>(table), grad, d_pos);
+  LNR_RETURN_LAUNCH(who);
+}
+
+// An empty batch still overwrites its outputs: the table gradient (or the level range's slice of it)
+// is zero.
+static int zero_table_levels(const lnr_grid_desc* d, float* d_table, uint32_t l0, uint32_t l1, hipStream_t st,
+                             const char* who) {
+  if (!d_table || l1 <= l0) return LNR_OK;
+  const size_t e0 = d->offset[l0], e1 = d->offset[l1];
+  LNR_REQUIRE(hipMemsetAsync(d_table + 2 * e0, 0, (e1 - e0) * 2 * sizeof(float), st) == hipSuccess,
+              "%s: memset failed", who);
+  return LNR_OK;
+}
+
 }  // namespace lnr
 
 using namespace lnr;
@@ -1323,16 +1415,31 @@ extern "C" float* lnr_hashgrid_bwd_level_max(const lnr_grid_desc* d, int64_t n, 
   return carve_workspace(workspace, make_args(d), d, n).level_max;
 }
 
+// The three backward entry points: d_table (optional: NULL = no table gradient) through the binned
+// scatter, d_pos (optional: NULL = no input gradient) through k_hashgrid_dpos.
+template <class PosFn, class GradFn>
+static int bwd_entry(const lnr_grid_desc* d, PosFn pos, int64_t n, GradFn grad, float* d_table, const uint16_t* table,
+                     float* d_pos, void* workspace, int64_t workspace_bytes, int32_t flags, hipStream_t st,
+                     const char* who) {
+  if (n == 0) {
+    if (flags & LNR_BWD_NO_ACCUM) return LNR_OK;  // lnr_hashgrid_bwd_accum zeroes each range
+    if (int e = zero_table_levels(d, d_table, 0, d->n_levels, st, who)) return e;
+    LNR_RETURN_LAUNCH(who);
+  }
+  if (d_pos)
+    if (int e = launch_dpos(d, pos, n, table, grad, d_pos, st, who)) return e;
+  if (!d_table) return LNR_OK;
+  return launch_bwd_bucketed(d, pos, n, grad, d_table, workspace, workspace_bytes, flags, st, who);
+}
+
 extern "C" int lnr_hashgrid_bwd(const lnr_grid_desc* d, const float* pos01, int64_t n, const float* d_enc,
-                                int64_t enc_stride, float* d_table, void* workspace, int64_t workspace_bytes,
-                                int32_t flags, void* stream) {
+                                int64_t enc_stride, float* d_table, const uint16_t* table, float* d_pos,
+                                void* workspace, int64_t workspace_bytes, int32_t flags, void* stream) {
   if (int e = check_desc_bwd(d, "lnr_hashgrid_bwd")) return e;
   LNR_REQUIRE(n >= 0 && enc_stride >= n, "lnr_hashgrid_bwd: bad sizes");
-  if (n == 0) return LNR_OK;
-  LNR_REQUIRE(pos01 && d_enc && d_table, "lnr_hashgrid_bwd: null pointer");
-  return launch_bwd_bucketed(d, PosFromArray{pos01}, n, GradF32{reinterpret_cast<const float2*>(d_enc), enc_stride},
-                             d_table, workspace, workspace_bytes, flags,
-                             as_stream(stream), "lnr_hashgrid_bwd");
+  LNR_REQUIRE(n == 0 || (pos01 && d_enc && (d_table || d_pos)), "lnr_hashgrid_bwd: null pointer");
+  return bwd_entry(d, PosFromArray{pos01}, n, GradF32{reinterpret_cast<const float2*>(d_enc), enc_stride}, d_table,
+                   table, d_pos, workspace, workspace_bytes, flags, as_stream(stream), "lnr_hashgrid_bwd");
 }
 
 extern "C" int lnr_hashgrid_bwd_accum(const lnr_grid_desc* d, int64_t n, void* workspace, int64_t workspace_bytes,
@@ -1341,7 +1448,11 @@ extern "C" int lnr_hashgrid_bwd_accum(const lnr_grid_desc* d, int64_t n, void* w
   LNR_REQUIRE(level_begin <= level_end && level_end <= d->n_levels, "lnr_hashgrid_bwd_accum: bad level range");
   LNR_REQUIRE(n >= 0 && workspace && workspace_bytes >= bwd_workspace_bytes(d, n) && d_table,
               "lnr_hashgrid_bwd_accum: bad workspace / pointers");
-  if (n == 0) return LNR_OK;
+  if (n == 0) {
+    if (int e = zero_table_levels(d, d_table, level_begin, level_end, as_stream(stream), "lnr_hashgrid_bwd_accum"))
+      return e;
+    LNR_RETURN_LAUNCH("lnr_hashgrid_bwd_accum");
+  }
   const GridArgs a = make_args(d);
   launch_accum(a, carve_workspace(workspace, a, d, n), d, n, level_begin, level_end, d_table, as_stream(stream));
   LNR_RETURN_LAUNCH("lnr_hashgrid_bwd_accum");
@@ -1349,28 +1460,28 @@ extern "C" int lnr_hashgrid_bwd_accum(const lnr_grid_desc* d, int64_t n, void* w
 
 extern "C" int lnr_hashgrid_bwd_rays(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
                                      int32_t n_samples, const float* d_enc, int64_t enc_stride, float* d_table,
-                                     void* workspace, int64_t workspace_bytes, int32_t flags, void* stream) {
+                                     const uint16_t* table, float* d_pos, void* workspace, int64_t workspace_bytes,
+                                     int32_t flags, void* stream) {
   if (int e = check_desc_bwd(d, "lnr_hashgrid_bwd_rays")) return e;
   const int64_t n = n_rays * (int64_t)n_samples;
   LNR_REQUIRE(n_rays >= 0 && n_samples > 0 && enc_stride >= n, "lnr_hashgrid_bwd_rays: bad sizes");
-  if (n == 0) return LNR_OK;
-  LNR_REQUIRE(rays && z && d_enc && d_table, "lnr_hashgrid_bwd_rays: null pointer");
-  return launch_bwd_bucketed(d, PosFromRays{rays, z, n_samples}, n,
-                             GradF32{reinterpret_cast<const float2*>(d_enc), enc_stride}, d_table, workspace,
-                             workspace_bytes, flags, as_stream(stream), "lnr_hashgrid_bwd_rays");
+  LNR_REQUIRE(n == 0 || (rays && z && d_enc && (d_table || d_pos)), "lnr_hashgrid_bwd_rays: null pointer");
+  return bwd_entry(d, PosFromRays{rays, z, n_samples}, n, GradF32{reinterpret_cast<const float2*>(d_enc), enc_stride},
+                   d_table, table, d_pos, workspace, workspace_bytes, flags, as_stream(stream),
+                   "lnr_hashgrid_bwd_rays");
 }
 
 extern "C" int lnr_hashgrid_bwd_rays_jac(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
                                          int32_t n_samples, const uint32_t* d_jac, const float* d_sigma,
-                                         int64_t jac_stride, float* d_table, void* workspace, int64_t workspace_bytes,
-                                         int32_t flags, void* stream) {
+                                         int64_t jac_stride, float* d_table, const uint16_t* table, float* d_pos,
+                                         void* workspace, int64_t workspace_bytes, int32_t flags, void* stream) {
   if (int e = check_desc_bwd(d, "lnr_hashgrid_bwd_rays_jac")) return e;
   const int64_t n = n_rays * (int64_t)n_samples;
   LNR_REQUIRE(n_rays >= 0 && n_samples > 0 && jac_stride >= n, "lnr_hashgrid_bwd_rays_jac: bad sizes");
-  if (n == 0) return LNR_OK;
-  LNR_REQUIRE(rays && z && d_jac && d_sigma && d_table, "lnr_hashgrid_bwd_rays_jac: null pointer");
-  return launch_bwd_bucketed(d, PosFromRays{rays, z, n_samples}, n, GradJac{d_jac, d_sigma, jac_stride}, d_table,
-                             workspace, workspace_bytes, flags, as_stream(stream), "lnr_hashgrid_bwd_rays_jac");
+  LNR_REQUIRE(n == 0 || (rays && z && d_jac && d_sigma && (d_table || d_pos)),
+              "lnr_hashgrid_bwd_rays_jac: null pointer");
+  return bwd_entry(d, PosFromRays{rays, z, n_samples}, n, GradJac{d_jac, d_sigma, jac_stride}, d_table, table, d_pos,
+                   workspace, workspace_bytes, flags, as_stream(stream), "lnr_hashgrid_bwd_rays_jac");
 }
 
 LNR_PHASE_EXPORT(hashgrid_bwd)

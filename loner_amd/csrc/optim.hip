@@ -89,6 +89,7 @@ __device__ __forceinline__ float logits_grad(float x) {
 // then n_rep int64 replicas.
 constexpr int32_t kOgmReplicas = 3;
 constexpr int kOgmFixExp = 28;
+constexpr uint32_t kInfBits = 0x7F800000u;  // +inf's bits: k_abs_max's value at or above it = non-finite
 
 // The OGM update's points: sample i of ray r, xyz = o + d z, logits gradient of its depth error.
 struct OgmRaySamples {
@@ -123,8 +124,9 @@ struct PointGrads {
 // Fixed-point exponent of the generic backward: every per-voxel sum of |w g| <= n max|g| < 2^62.
 __device__ __forceinline__ int fix_exp(const uint32_t* amax_bits, int64_t n) {
   if (amax_bits == nullptr) return kOgmFixExp;
+  if (*amax_bits >= kInfBits) return 0;  // non-finite: k_sum_replicas writes NaN
   const float m = __uint_as_float(*amax_bits);
-  if (!(m > 0.f)) return 0;  // (nothing to add, or non-finite: the sums are garbage either way)
+  if (!(m > 0.f)) return 0;  // nothing to add
   int em, en = 0;
   frexpf(m, &em);  // m < 2^em
   while ((int64_t(1) << en) < n && en < 62) ++en;
@@ -174,23 +176,32 @@ __global__ void __launch_bounds__(256) k_ogm_grad(Src src, int64_t n, unsigned l
   }
 }
 
-// out = (sum of the int64 replicas) / 2^e (exact integer sum, one rounding)
+// out = (sum of the int64 replicas) / 2^e (exact integer sum, one rounding).  A non-finite output
+// gradient (k_abs_max's bits >= +inf's) cannot be carried in fixed point: the whole grid gradient is
+// then NaN, so the non-finite value propagates (torch's grid_sample backward would give NaN / inf at the
+// voxels the point touches) instead of turning into arbitrary integers.
 __global__ void k_sum_replicas(const unsigned long long* __restrict__ g, int64_t nv, int32_t n_rep,
                                float* __restrict__ out, const uint32_t* amax_bits, int64_t n_pts) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nv) return;
+  if (amax_bits && *amax_bits >= kInfBits) {
+    out[i] = __builtin_nanf("");
+    return;
+  }
   long long s = 0;
   for (int k = 0; k < n_rep; ++k) s += (long long)g[(int64_t)k * nv + i];
   out[i] = (float)ldexp((double)s, -fix_exp(amax_bits, n_pts));
 }
 
-// max |x| of n floats into *amax_bits (zeroed before; non-negative floats order as their bits)
+// max |x| of n floats into *amax_bits (zeroed before), as bits: non-negative floats order as their bits,
+// +inf is 0x7F800000 and every NaN (sign cleared) lies above it, so a non-finite x is never skipped (fmaxf
+// would drop a NaN)
 __global__ void __launch_bounds__(256) k_abs_max(const float* __restrict__ x, int64_t n, uint32_t* amax_bits) {
-  float m = 0.f;
+  uint32_t m = 0u;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    m = fmaxf(m, fabsf(x[i]));
-  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(amax_bits, __float_as_uint(m));
+    m = max(m, __float_as_uint(x[i]) & 0x7FFFFFFFu);
+  for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+  if ((threadIdx.x & 63) == 0 && m > 0u) atomicMax(amax_bits, m);
 }
 
 __global__ void __launch_bounds__(256) k_grid_sample3d(const float* __restrict__ grid, int32_t R,

@@ -205,6 +205,7 @@ class Optimizer:
                                       n_rays_global=window.n_slots, n_slots=n_local)
             self._global_step += 1
         eng.lr_factor = 1.0
+        eng.drop_prefetch()  # the next window is a new object: this one's prefetched step never runs
         return out
 
     # ------------------------------------------------------------------ camera phase

@@ -45,6 +45,7 @@ class _Composite(torch.autograd.Function):
         depth = torch.empty(n, dtype=torch.float32, device=dev)
         opacity = torch.empty(n, dtype=torch.float32, device=dev)
         var = torch.empty(n, dtype=torch.float32, device=dev)
+        rays13 = rays13.detach().contiguous()
         L.call("lnr_composite", rays13, z, sig, n, s, strategy, noise_std, None, key, 0, w, depth, opacity, var,
                L.stream(dev))
         ctx.save_for_backward(sig, z, rays13)
@@ -61,9 +62,19 @@ class _Composite(torch.autograd.Function):
         def c(t):
             return None if t is None else t.float().contiguous()
 
+        want_ray = ctx.needs_input_grad[2]
+        d_ray = torch.empty(n, 2, dtype=torch.float32, device=z.device) if want_ray else None
         L.call("lnr_composite_bwd", rays13, z, sig, n, s, strategy, noise_std, None, key, 0, c(g_w), c(g_depth),
-               c(g_opacity), c(g_var), d_sigma, L.stream(z.device))
-        return d_sigma.to(dtype), None, None, None, None, None
+               c(g_opacity), c(g_var), d_sigma, d_ray, L.stream(z.device))
+        d_rays13 = None
+        if want_ray:
+            # rays that require grad (poses under optimisation): the deltas' direction norm
+            # (rendering_tcnn.py:248) and the far term of the default depth (:274-278)
+            d = rays13[:, 3:6]
+            d_rays13 = torch.zeros_like(rays13)
+            d_rays13[:, 3:6] = d_ray[:, 0:1] * d / d.norm(dim=-1, keepdim=True)
+            d_rays13[:, 12] = d_ray[:, 1]
+        return d_sigma.to(dtype), None, d_rays13, None, None, None
 
 
 def _composite(raw, z_vals, rays_d, raw_noise_std, white_bkgd, sigma_only, num_colors, far, ret_var, strategy,

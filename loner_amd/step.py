@@ -531,10 +531,10 @@ class StepEngine:
         st = self.state
         if self.compact_denc:
             L.call("lnr_hashgrid_bwd_rays_jac", L.ctypes.byref(st.desc), rays, self.z, R, S, self.d_jac,
-                   self.d_sigma(R), N, st.grad_table, self.bwd_ws, self.bwd_ws_bytes, flags, s)
+                   self.d_sigma(R), N, st.grad_table, None, None, self.bwd_ws, self.bwd_ws_bytes, flags, s)
         else:
             L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(st.desc), rays, self.z, R, S, self.d_enc, N, st.grad_table,
-                   self.bwd_ws, self.bwd_ws_bytes, flags, s)
+                   None, None, self.bwd_ws, self.bwd_ws_bytes, flags, s)
 
     def ogm_update(self, rays, depth_gt, scale):
         """Optimizer._step_occupancy_grid (optimizer.py:897-908).  Data-parallel: the grid gradient
@@ -569,14 +569,16 @@ class StepEngine:
         # The build and compaction of step k + 1 run on a side stream while step k runs, so that sync
         # never waits for the main stream: the host stays a step ahead of the GPU (double-buffered).
         main = torch.cuda.current_stream(self.state.device)
-        want = (id(window), global_step, n, self.ray_offset, n_rays_global)
+        want = (global_step, n, self.ray_offset, n_rays_global)
         pf, self._pf = self._pf, None
-        if pf is None or pf["want"] != want:
+        if pf is not None:
+            # a prefetch is consumed or discarded only after the main stream waits for it, so the
+            # window it read (kept alive by pf["window"] until now) is free for reuse afterwards
+            main.wait_event(pf["done"])
+        if pf is None or pf["window"] is not window or pf["want"] != want:
             m(prof, "rays")
             pf = self._build_compact(window, global_step, n, n_rays_global, self._pf_parity, main)
             m(prof, "rays")
-        else:
-            main.wait_event(pf["done"])
         self._pf_parity = pf["parity"]
         self._pf_fork.record(main)  # the other buffer is free once everything enqueued so far is done
         out = self.step(pf["rays"], pf["dgt"], global_step, iteration_idx, scale=window.scale, far_ref=pf["far"],
@@ -593,10 +595,14 @@ class StepEngine:
         k + 1's build + sampling prefetched (``pipeline``)."""
         m = self._mark
         main = torch.cuda.current_stream(self.state.device)
-        want = (id(window), global_step, n, self.ray_offset)
+        want = (global_step, n, self.ray_offset)
         pp, self._pp = self._pp, None
-        if pp is not None and pp["want"] == want:
+        if pp is not None:
+            # consumed or discarded, the prefetch is waited for first: the main stream's later work
+            # (and the caching allocator's reuse of the window it read, which pp["window"] kept alive
+            # until here) is ordered after its side-stream reads
             main.wait_event(pp["done"])
+        if pp is not None and pp["window"] is window and pp["want"] == want:
             parity, presampled = pp["parity"], pp["sampled"]
             b = self._pp_bufs[parity]
         else:
@@ -636,8 +642,17 @@ class StepEngine:
                            bq["z"], s)
             done = torch.cuda.Event()
             done.record(self._pp_stream)
-        self._pp = dict(want=(id(window), global_step + 1, n, self.ray_offset), parity=q, sampled=sample, done=done)
+        self._pp = dict(window=window, want=(global_step + 1, n, self.ray_offset), parity=q, sampled=sample, done=done)
         return out
+
+    def drop_prefetch(self):
+        """Discard a pending prefetch (the main stream waits for its side-stream work, then the window it
+        read is released).  step_window does this itself when the next call does not match."""
+        main = torch.cuda.current_stream(self.state.device)
+        for pend in (self._pp, self._pf):
+            if pend is not None:
+                main.wait_event(pend["done"])
+        self._pp = self._pf = None
 
     def _build_compact(self, window, global_step, n, n_rays_global, parity, stream):
         """Build slots [ray_offset, ray_offset + n) of ``window`` for ``global_step`` into ray buffer
@@ -657,6 +672,6 @@ class StepEngine:
             n_glob = int(cnt.item())
             done = torch.cuda.Event()
             done.record(stream)
-        return dict(want=(id(window), global_step, n, self.ray_offset, n_rays_global), rays=b["rays_c"][:k],
+        return dict(window=window, want=(global_step, n, self.ray_offset, n_rays_global), rays=b["rays_c"][:k],
                     dgt=b["dgt_c"][:k], far=b["far"], n_glob=n_glob, done=done, parity=parity)
 

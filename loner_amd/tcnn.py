@@ -9,15 +9,19 @@ Drop-in for the three tcnn classes LONER constructs (src/models/nerf_tcnn.py:35-
 Same constructor dicts (passed verbatim from cfg/nerf_config/default_nerf_hash.yaml), one flat fp32
 ``params`` Parameter per module (network first, then encoding, as tcnn lays them out), ``dtype`` =
 torch.half, ``n_input_dims`` / ``n_output_dims``, fp16 outputs, and a custom autograd Function
-whose backward returns the parameter gradient.  Unsupported configurations raise
+whose backward returns the parameter gradient and, when the input requires grad, the input gradient
+(tcnn's dL/dx: joint pose + map optimisation differentiates the sample positions through the grid,
+src/models/nerf_tcnn.py:63,68-71, src/mapping/optimizer.py:256-262).  Unsupported configurations raise
 ``RuntimeError`` at construction, like tcnn's CHECK_THROW; CPU inputs raise (there is no CPU path).
 
 Implementation per configuration:
   * HashGrid (n_features_per_level = 2) encode / backward: HIP kernels (lnr_hashgrid_*), the
-    backward is the binned int64-fixed-point scatter (DESIGN.md), so gradients are deterministic;
+    table backward is the binned int64-fixed-point scatter, so gradients are
+    deterministic; the input gradient is lnr_hashgrid_bwd's d_pos (one fixed-order sum per sample);
   * NetworkWithInputEncoding(HashGrid, FullyFusedMLP 64 neurons x 1 hidden layer, 1 output) — the
     LONER sigma field: HIP hash encode + MFMA sigma MLP (lnr_sigma_mlp_fwd/_bwd);
-  * SphericalHarmonics (degree <= 4): HIP kernel, forward only (directions carry no gradient);
+  * SphericalHarmonics (degree <= 4): HIP kernel forward; its input gradient (the polynomials'
+    derivative) as torch ops on the GPU;
   * other FullyFusedMLP shapes (the colour head 48 -> 4x64 -> 3): fp16 GEMMs through hipBLASLt
     (torch.matmul), fp32 accumulate — a plain library GEMM, off the sigma hot path.
 
@@ -92,16 +96,21 @@ class _GridSpec:
         self.n_output_dims = self.n_levels * self.n_features
 
 
-def _grid_backward(spec, pos01, d_enc, n):
-    """d_enc (L, n, 2) fp32 level-major -> d_table (n_params) fp32 (binned HIP backward)."""
+def _grid_backward(spec, pos01, d_enc, n, want_table=True, table16=None):
+    """d_enc (L, n, 2) fp32 level-major -> (d_table (n_params) fp32 or None, d_pos01 (n, 3) fp32 or None).
+    The table gradient is the binned HIP backward; with ``table16`` (the forward's fp16 table) the input
+    gradient dL/dpos01 is computed as well (tcnn returns it when the positions require grad)."""
     dev = pos01.device
-    if n == 0:
-        return torch.zeros(spec.n_params, dtype=torch.float32, device=dev)
-    d_table = torch.empty(spec.n_params, dtype=torch.float32, device=dev)  # overwritten by the backward
-    nbytes = int(L.lib().lnr_hashgrid_bwd_workspace_bytes(ctypes.byref(spec.desc), n))
-    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    L.call("lnr_hashgrid_bwd", ctypes.byref(spec.desc), pos01, n, d_enc, n, d_table, ws, nbytes, 0, L.stream(dev))
-    return d_table
+    want_pos = table16 is not None
+    d_table = torch.empty(spec.n_params, dtype=torch.float32, device=dev) if want_table else None  # overwritten
+    d_pos = torch.empty(n, 3, dtype=torch.float32, device=dev) if want_pos else None
+    if n == 0 or not (want_table or want_pos):
+        return (d_table.zero_() if want_table else None), d_pos
+    nbytes = int(L.lib().lnr_hashgrid_bwd_workspace_bytes(ctypes.byref(spec.desc), n)) if want_table else 0
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev) if want_table else None
+    L.call("lnr_hashgrid_bwd", ctypes.byref(spec.desc), pos01, n, d_enc, n, d_table, table16, d_pos, ws, nbytes, 0,
+           L.stream(dev))
+    return d_table, d_pos
 
 
 def _grid_forward(spec, pos01, table16, n):
@@ -122,14 +131,12 @@ class _EncodingFn(torch.autograd.Function):
         if n:
             L.call("lnr_enc_to_aos", enc, n, n, spec.n_levels, out, L.stream(pos01.device))
         ctx.spec = spec
-        ctx.save_for_backward(pos01)
+        ctx.save_for_backward(pos01, table16)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        if ctx.needs_input_grad[0]:
-            raise RuntimeError("loner_amd.tcnn.Encoding: input gradients are not implemented")
-        (pos01,) = ctx.saved_tensors
+        pos01, table16 = ctx.saved_tensors
         spec = ctx.spec
         n = pos01.shape[0]
         g = g.contiguous()
@@ -138,7 +145,27 @@ class _EncodingFn(torch.autograd.Function):
             g16 = g if g.dtype == torch.half else None
             g32 = g.float().contiguous() if g16 is None else None
             L.call("lnr_aos_grad_to_enc", g16, g32, n, spec.n_levels, d_enc, n, L.stream(pos01.device))
-        return None, _grid_backward(spec, pos01, d_enc, n), None
+        d_table, d_pos = _grid_backward(spec, pos01, d_enc, n, want_table=ctx.needs_input_grad[1],
+                                        table16=table16 if ctx.needs_input_grad[0] else None)
+        return d_pos, d_table, None
+
+
+def _sh_basis(d01, degree):
+    """tcnn SphericalHarmonics basis (degree <= 4) of directions in [0,1]^3 as differentiable torch ops; only
+    its derivative is used (the forward values come from lnr_sh_encode)."""
+    x, y, z = (d01 * 2 - 1).unbind(-1)
+    out = [torch.full_like(x, 0.28209479177387814)]
+    if degree > 1:
+        out += [-0.48860251190291987 * y, 0.48860251190291987 * z, -0.48860251190291987 * x]
+    if degree > 2:
+        out += [1.0925484305920792 * x * y, -1.0925484305920792 * y * z, 0.94617469575755997 * z * z - 0.31539156525251999,
+                -1.0925484305920792 * x * z, 0.54627421529603959 * (x * x - y * y)]
+    if degree > 3:
+        out += [0.59004358992664352 * y * (-3 * x * x + y * y), 2.8906114426405538 * x * y * z,
+                0.45704579946446572 * y * (1 - 5 * z * z), 0.3731763325901154 * z * (5 * z * z - 3),
+                0.45704579946446572 * x * (1 - 5 * z * z), 1.4453057213202769 * z * (x * x - y * y),
+                0.59004358992664352 * x * (-x * x + 3 * y * y)]
+    return torch.stack(out, -1)
 
 
 class _SHFn(torch.autograd.Function):
@@ -147,11 +174,21 @@ class _SHFn(torch.autograd.Function):
         n = dir01.shape[0]
         out = torch.empty(n, degree * degree, dtype=torch.half, device=dir01.device)
         L.call("lnr_sh_encode", dir01, n, degree, out, L.stream(dir01.device))
+        ctx.degree = degree
+        ctx.save_for_backward(dir01)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        raise RuntimeError("loner_amd.tcnn: SphericalHarmonics input gradients are not implemented")
+        # tcnn's SphericalHarmonics input gradient (the polynomials' derivative, fp32); the encoding has no
+        # parameters.  A 16-term polynomial on (n, 3): plain torch ops on the GPU, off the sigma path.
+        (dir01,) = ctx.saved_tensors
+        if not ctx.needs_input_grad[0]:
+            return None, None
+        with torch.enable_grad():
+            d = dir01.detach().float().requires_grad_()
+            (gd,) = torch.autograd.grad(_sh_basis(d, ctx.degree), d, g.float())
+        return gd, None
 
 
 class Encoding(nn.Module):
@@ -287,24 +324,26 @@ class _SigmaFieldFn(torch.autograd.Function):
         if n:
             L.call("lnr_sigma_mlp_fwd", w16, enc, n, n, sigma, L.stream(dev))
         ctx.spec = spec
-        ctx.save_for_backward(pos01, w16, enc)
+        ctx.save_for_backward(pos01, p16, enc)
         return sigma.view(n, 1)
 
     @staticmethod
     def backward(ctx, g):
-        if ctx.needs_input_grad[0]:
-            raise RuntimeError("loner_amd.tcnn.NetworkWithInputEncoding: input gradients are not implemented")
-        pos01, w16, enc = ctx.saved_tensors
+        pos01, p16, enc = ctx.saved_tensors
         spec = ctx.spec
         n = pos01.shape[0]
         dev = pos01.device
+        w16, table16 = p16[:L.SIGMA_MLP_PARAMS], p16[L.SIGMA_MLP_PARAMS:]
         d_w = torch.zeros(L.SIGMA_MLP_PARAMS, dtype=torch.float32, device=dev)
         d_enc = torch.empty(spec.n_levels, max(n, 1), 2, dtype=torch.float32, device=dev)
         if n:
             ds = g.reshape(n).float().contiguous()
             ws = torch.empty(int(L.lib().lnr_dw_workspace_words(n)), dtype=torch.float32, device=dev)
             L.call("lnr_sigma_mlp_bwd", w16, enc, n, n, ds, d_enc, d_w, ws, L.stream(dev))
-        return None, torch.cat([d_w, _grid_backward(spec, pos01, d_enc, n)]), None
+        d_table, d_pos = _grid_backward(spec, pos01, d_enc, n, want_table=ctx.needs_input_grad[1],
+                                        table16=table16 if ctx.needs_input_grad[0] else None)
+        d_params = torch.cat([d_w, d_table]) if ctx.needs_input_grad[1] else None
+        return d_pos, d_params, None
 
 
 class NetworkWithInputEncoding(nn.Module):

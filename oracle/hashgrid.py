@@ -110,6 +110,76 @@ def encode(pos01, table_f16, layout):
     return out.astype(np.float16)
 
 
+def encode_input_grad(pos01, table_f16, d_enc, layout, exact=False):
+    """Input gradient: d_enc (N, L*F) -> dL/dpos01 (N, 3) fp64.  tcnn v1.7 ``grid.h``: ``kernel_grid``
+    with ``dy_dx`` (per level, feature and axis: over the 4 cell edges along the axis, scale_l times
+    the product of the other axes' weights times (upper corner value - lower corner value), the other
+    axes in increasing order; ``pos_derivative`` = 1 for linear interpolation) and
+    ``kernel_grid_backward_input`` (dL/dx = sum over output features of dL/dy * dy/dx).  Table values
+    are the fp16 forward operand, cell fractions fp32 as in the forward (tcnn: fmaf(scale, x, 0.5f)); the
+    sums are fp64 here.  ``exact``: fractions from fp64 positions instead (the derivative of
+    ``encode_f64``, for the central-difference check of the formula itself)."""
+    pos64 = np.asarray(pos01, dtype=np.float64)
+    pos01 = np.asarray(pos01, dtype=np.float32)
+    tab = np.asarray(table_f16).astype(np.float64)
+    d_enc = np.asarray(d_enc, dtype=np.float64)
+    n = pos01.shape[0]
+    out = np.zeros((n, 3), dtype=np.float64)
+    for lvl in range(layout.n_levels):
+        if exact:
+            pf = pos64 * np.float64(layout.scales[lvl]) + 0.5
+            cell = np.floor(pf).astype(np.int64)
+            frac = pf - cell
+        else:
+            cell, frac = _corners(pos01, layout, lvl)
+            frac = frac.astype(np.float64)
+        scale = np.float64(layout.scales[lvl])
+        res, size, off = layout.resolutions[lvl], layout.sizes[lvl], layout.offsets[lvl]
+        dl = d_enc[:, lvl * layout.n_features:(lvl + 1) * layout.n_features]
+        for dim in range(3):
+            others = [d for d in range(3) if d != dim]
+            acc = np.zeros((n, layout.n_features))
+            for e in range(4):
+                w = np.full(n, scale)
+                lo = cell.copy()
+                for j, od in enumerate(others):
+                    bit = (e >> j) & 1
+                    w = w * (frac[:, od] if bit else 1.0 - frac[:, od])
+                    lo[:, od] += bit
+                hi = lo.copy()
+                hi[:, dim] += 1
+                v_lo = tab[off + grid_index(lo, res, size)]
+                v_hi = tab[off + grid_index(hi, res, size)]
+                acc += w[:, None] * (v_hi - v_lo)
+            out[:, dim] += (dl * acc).sum(-1)
+    return out
+
+
+def encode_f64(pos01, table, layout):
+    """The trilinear blend in fp64 throughout (no fp32 fractions, no fp16 output rounding): the smooth
+    function whose central differences check ``encode_input_grad`` (tests/test_oracle_tcnn.py)."""
+    pos01 = np.asarray(pos01, dtype=np.float64)
+    tab = np.asarray(table).astype(np.float64)
+    out = np.zeros((pos01.shape[0], layout.n_output_dims))
+    for lvl in range(layout.n_levels):
+        p = pos01 * np.float64(layout.scales[lvl]) + 0.5
+        cell = np.floor(p).astype(np.int64)
+        frac = p - cell
+        acc = np.zeros((pos01.shape[0], layout.n_features))
+        for c in range(8):
+            w = np.ones(pos01.shape[0])
+            cc = cell.copy()
+            for d in range(3):
+                if (c >> d) & 1:
+                    w = w * frac[:, d]
+                    cc[:, d] += 1
+                else:
+                    w = w * (1.0 - frac[:, d])
+            acc += w[:, None] * tab[layout.offsets[lvl] + grid_index(cc, layout.resolutions[lvl], layout.sizes[lvl])]
+        out[:, lvl * layout.n_features:(lvl + 1) * layout.n_features] = acc
+    return out
+
+
 def encode_backward(pos01, d_enc, layout):
     """Backward: d_enc (N, L*F) -> dtable (n_entries, F) fp64 (scatter-add of w * d_enc)."""
     pos01 = np.asarray(pos01, dtype=np.float32)

@@ -179,10 +179,14 @@ def raw2outputs_adjusted(sigma, z, rays_d, ret_var=True):
     return dict(weights=w, depth=depth, opacity=opacity, variance=var, alphas=alphas, T=T)
 
 
-def composite_backward(sigma, z, rays_d, noise, far, g_w, g_depth, g_opacity):
+def composite_backward(sigma, z, rays_d, noise, far, g_w, g_depth, g_opacity, ray_grads=False):
     """d loss / d sigma (R,S) fp64 for the default strategy, given upstream gradients on the
     weights (R,S), the depth (R,) and the opacity (R,).  Uses the division-free suffix scan
-    S_k = sum_{i>k} G_i a_i prod_{k<j<i} s_j,  dL/da_k = T_k (G_k - S_k)."""
+    S_k = sum_{i>k} G_i a_i prod_{k<j<i} s_j,  dL/da_k = T_k (G_k - S_k).
+    ``ray_grads``: also the render's gradient w.r.t. the ray, (dL/d|d|, dL/dfar) per ray: the deltas
+    are dl * |d| (rendering_tcnn.py:248), so dL/d|d| = sum_k dL/da_k dl_k relu(sigma_k + n_k)
+    exp(-delta_k relu(.)); the depth's far term (1 - sum w) far (:274-278) gives dL/dfar =
+    g_depth (1 - sum w)."""
     f64 = np.float64
     sig = sigma.astype(f64) + (0.0 if noise is None else noise.astype(f64))
     dl = _deltas(z, rays_d).astype(f64)
@@ -199,7 +203,14 @@ def composite_backward(sigma, z, rays_d, noise, far, g_w, g_depth, g_opacity):
     dA = T * (G - Ssuf)
     with np.errstate(over="ignore", invalid="ignore"):
         dadsig = np.where(sig > 0, dl * np.exp(-dl * sr), 0.0)
-    return dA * dadsig
+    if not ray_grads:
+        return dA * dadsig
+    dlr = (z[:, 1:] - z[:, :-1]).astype(F32).astype(f64)
+    dlr = np.concatenate([dlr, np.full((R, 1), 1e10)], -1)
+    d_dnorm = (dA * dlr * sr * np.exp(-dl * sr)).sum(-1)
+    w = a * T
+    d_far = np.asarray(g_depth, f64) * (1.0 - w.sum(-1))
+    return dA * dadsig, d_dnorm, d_far
 
 
 def sh4(dir01):

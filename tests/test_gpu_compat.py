@@ -363,3 +363,11 @@ def test_occupancy_interpolate_golden_and_backward(tc):
     assert np.abs(got_g - ref_g).max() <= 2e-5 * np.abs(ref_g).max(), np.abs(got_g - ref_g).max()
     with pytest.raises(ValueError):
         M.OccupancyGridModel.interpolate(occ.cpu(), torch.from_numpy(P))
+    # a non-finite output gradient propagates (torch: NaN / inf at the touched voxels) instead of becoming
+    # arbitrary fixed-point integers: the grid gradient is NaN
+    for bad in (np.nan, np.inf):
+        d2 = dout.copy()
+        d2[3, 5] = bad
+        gdev = occ.clone().requires_grad_(True)
+        M.OccupancyGridModel.interpolate(gdev, torch.from_numpy(P).cuda()).backward(torch.from_numpy(d2).cuda())
+        assert np.all(np.isnan(host(gdev.grad)))

@@ -23,13 +23,37 @@ def test_empty_batches_are_noops(L):
     d = L.grid_desc()
     assert L.lib().lnr_sample_ogm(None, 0, 512, None, 100, 1.0, None, None, 0, 0, None, s) == 0
     assert L.lib().lnr_hashgrid_fwd_rays(L.ctypes.byref(d), None, None, 0, 512, None, None, 0, None, 0, s) == 0
-    assert L.lib().lnr_hashgrid_bwd_rays(L.ctypes.byref(d), None, None, 0, 512, None, 0, None, None, 0, 0, s) == 0
+    assert L.lib().lnr_hashgrid_bwd_rays(L.ctypes.byref(d), None, None, 0, 512, None, 0, None, None, None, None, 0, 0,
+                                        s) == 0
     assert L.lib().lnr_field_render(None, None, 0, None, None, 0, 512, 0, 1.0, None, 0, 0, None, None, None, None,
                                     s) == 0
     assert L.lib().lnr_rgb_render(None, 4, None, 0, None, None, 0, 512, None, s) == 0
     assert L.lib().lnr_adam_step(None, None, None, None, None, 0, 1, 0.01, 0.9, 0.999, 1e-8, s) == 0
     L.call("lnr_count_opaque", z, 0, 1.0, None, torch.zeros(1, device="cuda"), s)
     torch.cuda.synchronize()
+
+
+def test_zero_ray_step_writes_zero_gradient_and_loss(L):
+    """A step over an empty batch (one rank's share of a tiny global batch, or a compacted batch with no
+    valid ray) stores a zero gradient and finalizes the loss scalars: nothing of the previous step's
+    MLP or table gradient survives into Adam (lnr_field_train with LNR_LP_DW_OVERWRITE, the hash-grid
+    backward's overwrite contract at N = 0)."""
+    from loner_amd import step as S_
+    from loner_amd import synthetic as syn
+    cfg = S_.StepConfig(n_samples=64)
+    st = S_.FieldState(cfg, device="cuda:0", table_init=0.5)
+    win = syn.make_window("quad", 1, seed=2)
+    rays, dgt = syn.build_batch(win, "quad", 64, 0, "RANDOM", seed=4)
+    rays, dgt = rays.cuda(), dgt.cuda()
+    eng = S_.StepEngine(st, rays.shape[0], seed=1)
+    eng.step(rays, dgt, global_step=1, scale=121.426537, far_ref=float(rays[0, 12]))
+    torch.cuda.synchronize()
+    assert float(st.grad.abs().max()) > 0 and float(eng.loss_out[0]) != 0
+    eng.step(rays[:0], dgt[:0], global_step=2, scale=121.426537, far_ref=float(rays[0, 12]),
+             n_rays_global=rays.shape[0])
+    torch.cuda.synchronize()
+    assert int(torch.count_nonzero(st.grad)) == 0
+    assert float(eng.loss_out[0]) == 0.0 and float(eng.loss_out[5]) == 0.0
 
 
 def test_unsupported_sizes_raise(L):

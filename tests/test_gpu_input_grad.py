@@ -1,0 +1,274 @@
+"""K3: the hash grid's input gradient (dL/dpos) through the C ABI, the tcnn-compatible modules and
+render_rays, against the oracle (oracle/hashgrid.encode_input_grad: tcnn v1.7 kernel_grid's dy_dx +
+kernel_grid_backward_input, itself checked against fp64 central differences in
+tests/test_oracle_tcnn.py).  The reference differentiates the sample positions through tcnn when the
+poses are optimised (src/models/nerf_tcnn.py:63,68-71; src/mapping/optimizer.py:256-262;
+cfg/defaults.yaml:86-97).  GPU only.
+
+Tolerances: d_pos is an fp32 sum of fp32 products of fp16 table values and fp32 cell fractions (the
+same fractions the forward uses), against an fp64 sum of the same products: rel L2 <= 1e-3 overall and
+per level (measured ~1e-6).  Through the MLP and compositing (module level): rel L2 <= 1e-2 (the fp16
+dL/dsigma autograd hands tcnn and the hidden-layer ReLU / fp16 rounding flips, test_gpu_compat)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import hashgrid as ohg
+from oracle import mlp as omlp
+from oracle import render as orender
+from oracle import rng as orng
+
+pytestmark = pytest.mark.gpu
+
+SIGMA_ENC = dict(otype="HashGrid", n_levels=16, n_features_per_level=2, log2_hashmap_size=18, base_resolution=16)
+SIGMA_NET = dict(otype="FullyFusedMLP", activation="ReLU", output_activation="None", n_neurons=64, n_hidden_layers=1)
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from loner_amd import _lib
+    _lib.lib()
+    return _lib
+
+
+def cu(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+def rel(a, b):
+    return float(np.linalg.norm(np.asarray(a, np.float64) - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def _ray_positions(rng, R, S):
+    o = rng.uniform(-0.5, 0.5, (R, 3))
+    dr = rng.normal(0, 1, (R, 3))
+    dr /= np.linalg.norm(dr, axis=1, keepdims=True)
+    rays = np.zeros((R, 13), np.float32)
+    rays[:, 0:3], rays[:, 3:6] = o, dr
+    z = np.sort(rng.uniform(0.0, 0.45, (R, S)), 1).astype(np.float32)
+    xyz = (rays[:, None, 0:3] + rays[:, None, 3:6] * z[:, :, None]).astype(np.float32)
+    pos = ((xyz + np.float32(1)) / np.float32(2)).astype(np.float32).reshape(-1, 3)
+    return rays, z, pos
+
+
+@pytest.mark.parametrize("kind", ["random", "rays"])
+def test_hashgrid_dpos_vs_oracle_all_levels(L, kind):
+    """d_pos of lnr_hashgrid_bwd against the oracle, with the gradient at all 16 levels and at each level
+    alone; the table gradient of the same call is bitwise that of a call without d_pos."""
+    rng = np.random.default_rng(5)
+    lay = ohg.GridLayout(16, 2, 18, 16)
+    d = L.grid_desc(16, 2, 18, 16)
+    if kind == "random":
+        n = 4099
+        pos = rng.uniform(0, 1, (n, 3)).astype(np.float32)
+        pos[:4] = [[0, 0, 0], [1, 1, 1], [0.5, 0.5, 0.5], [0.999999, 0.25, 0.0]]
+    else:
+        _, _, pos = _ray_positions(rng, 24, 256)
+        n = pos.shape[0]
+    table = rng.uniform(-1, 1, (lay.n_entries, 2)).astype(np.float16)
+    t16 = cu(table.view(np.int16))
+    denc = rng.normal(0, 1, (n, 32)).astype(np.float32)
+    nb = int(L.lib().lnr_hashgrid_bwd_workspace_bytes(ctypes.byref(d), n))
+    ws = torch.empty(nb, dtype=torch.uint8, device="cuda")
+
+    def run(de, with_table, with_pos):
+        de_lm = cu(np.ascontiguousarray(de.reshape(n, 16, 2).transpose(1, 0, 2)))
+        gt = torch.empty(lay.n_entries * 2, dtype=torch.float32, device="cuda") if with_table else None
+        dp = torch.empty(n, 3, dtype=torch.float32, device="cuda") if with_pos else None
+        L.call("lnr_hashgrid_bwd", ctypes.byref(d), cu(pos), n, de_lm, n, gt, t16 if with_pos else None, dp,
+               ws if with_table else None, nb if with_table else 0, 0, L.stream())
+        torch.cuda.synchronize()
+        return gt, dp
+
+    gt_both, dp = run(denc, True, True)
+    gt_only, _ = run(denc, True, False)
+    _, dp_only = run(denc, False, True)
+    assert torch.equal(gt_both, gt_only)  # the input gradient leaves the table gradient untouched
+    assert torch.equal(dp, dp_only)       # and is deterministic, with or without the table pass
+    ref = ohg.encode_input_grad(pos, table, denc, lay)
+    assert rel(host(dp), ref) <= 1e-3, rel(host(dp), ref)
+    assert np.all(np.isfinite(host(dp)))
+    for lvl in range(16):
+        dl = np.zeros_like(denc)
+        dl[:, 2 * lvl:2 * lvl + 2] = denc[:, 2 * lvl:2 * lvl + 2]
+        _, dpl = run(dl, False, True)
+        r = ohg.encode_input_grad(pos, table, dl, lay)
+        assert rel(host(dpl), r) <= 1e-3, (lvl, rel(host(dpl), r))
+
+
+def test_hashgrid_dpos_rays_and_compact_forms(L):
+    """lnr_hashgrid_bwd_rays (positions from rays and z) and lnr_hashgrid_bwd_rays_jac (d_enc = d_sigma J)
+    give the d_pos of lnr_hashgrid_bwd on the same positions bit for bit; n = 0 zeroes d_table."""
+    rng = np.random.default_rng(6)
+    R, S = 20, 128
+    rays, z, pos = _ray_positions(rng, R, S)
+    n = R * S
+    lay = ohg.GridLayout(16, 2, 18, 16)
+    d = L.grid_desc(16, 2, 18, 16)
+    t16 = cu(rng.uniform(-1, 1, (lay.n_entries, 2)).astype(np.float16).view(np.int16))
+    jac = rng.uniform(-1, 1, (16, n, 2)).astype(np.float16)
+    dsig = rng.normal(0, 1, n).astype(np.float32)
+    denc_lm = (jac.astype(np.float32) * dsig[None, :, None]).astype(np.float32)
+    outs = []
+    dp = torch.empty(n, 3, dtype=torch.float32, device="cuda")
+    L.call("lnr_hashgrid_bwd", ctypes.byref(d), cu(pos), n, cu(denc_lm), n, None, t16, dp, None, 0, 0, L.stream())
+    outs.append(dp)
+    dp = torch.empty(n, 3, dtype=torch.float32, device="cuda")
+    L.call("lnr_hashgrid_bwd_rays", ctypes.byref(d), cu(rays), cu(z), R, S, cu(denc_lm), n, None, t16, dp, None, 0,
+           0, L.stream())
+    outs.append(dp)
+    dp = torch.empty(n, 3, dtype=torch.float32, device="cuda")
+    L.call("lnr_hashgrid_bwd_rays_jac", ctypes.byref(d), cu(rays), cu(z), R, S, cu(jac.view(np.int32)), cu(dsig), n,
+           None, t16, dp, None, 0, 0, L.stream())
+    outs.append(dp)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    # an empty batch overwrites d_table with zeros (the header's contract)
+    gt = torch.full((lay.n_entries * 2,), 7.0, device="cuda")
+    nb = int(L.lib().lnr_hashgrid_bwd_workspace_bytes(ctypes.byref(d), 0))
+    ws = torch.empty(max(nb, 1), dtype=torch.uint8, device="cuda")
+    L.call("lnr_hashgrid_bwd_rays", ctypes.byref(d), cu(rays), cu(z), 0, S, cu(denc_lm), n, gt, None, None, ws, nb, 0,
+           L.stream())
+    assert int(torch.count_nonzero(gt)) == 0
+    gt.fill_(7.0)
+    L.call("lnr_hashgrid_bwd_accum", ctypes.byref(d), 0, ws, nb, 3, 9, gt, L.stream())
+    o = [int(v) for v in d.offset]
+    g = host(gt)
+    assert np.all(g[2 * o[3]:2 * o[9]] == 0) and np.all(g[:2 * o[3]] == 7) and np.all(g[2 * o[9]:] == 7)
+
+
+def _field(tc, seed=0):
+    m = tc.NetworkWithInputEncoding(n_input_dims=3, n_output_dims=1, encoding_config=SIGMA_ENC,
+                                    network_config=SIGMA_NET)
+    torch.manual_seed(seed)
+    with torch.no_grad():  # a non-trivial field (tcnn's U(1e-4) table gives sigma ~ 0)
+        m.params[3072:].uniform_(-0.5, 0.5)
+        m.params[2048:3072].mul_(8.0)
+    p16 = host(m.params).astype(np.float16)
+    return m, p16[:2048].reshape(64, 32), p16[2048:3072].reshape(16, 64), p16[3072:].reshape(-1, 2)
+
+
+def test_tcnn_modules_input_gradient(L):
+    """tcnn.Encoding and tcnn.NetworkWithInputEncoding return dL/dx when x requires grad (instead of
+    raising), matching the oracle chain: MLP backward -> encode_input_grad."""
+    from loner_amd import tcnn as tc
+    rng = np.random.default_rng(8)
+    n = 3000
+    lay = ohg.GridLayout(16, 2, 18, 16)
+    pos = rng.uniform(0.01, 0.99, (n, 3)).astype(np.float32)
+    # Encoding
+    e = tc.Encoding(3, SIGMA_ENC)
+    with torch.no_grad():
+        e.params.uniform_(-1, 1)
+    x = torch.from_numpy(pos).cuda().requires_grad_()
+    out = e(x)
+    gd = rng.normal(0, 1, (n, 32)).astype(np.float32)
+    (out.float() * cu(gd)).sum().backward()
+    table = host(e.params).astype(np.float16).reshape(-1, 2)
+    g16 = gd.astype(np.float16).astype(np.float64)  # autograd hands the fp16 output an fp16 gradient
+    ref = ohg.encode_input_grad(pos, table, g16, lay)
+    assert rel(host(x.grad), ref) <= 1e-3, rel(host(x.grad), ref)
+    assert e.params.grad is not None
+    # NetworkWithInputEncoding (the fused sigma field), params frozen: only the input gradient
+    m, w0, w1, table = _field(tc)
+    m.params.requires_grad_(False)
+    x = torch.from_numpy(pos).cuda().requires_grad_()
+    sig = m(x)
+    gs = rng.normal(0, 1, (n, 1)).astype(np.float32)
+    (sig.float() * cu(gs)).sum().backward()
+    enc = ohg.encode(pos, table, lay)
+    _, hid = omlp.forward(enc, [w0, w1])
+    dout = np.zeros((n, 16))
+    dout[:, 0] = gs[:, 0].astype(np.float16)
+    dx, _ = omlp.backward(enc, [w0, w1], hid, dout)
+    ref = ohg.encode_input_grad(pos, table, dx, lay)
+    assert rel(host(x.grad), ref) <= 1e-2, rel(host(x.grad), ref)
+    # and with the params trainable, both gradients, the params' unchanged by asking for x's
+    m.params.requires_grad_(True)
+    x1 = torch.from_numpy(pos).cuda().requires_grad_()
+    (m(x1).float() * cu(gs)).sum().backward()
+    g_with = m.params.grad.clone()
+    m.params.grad = None
+    (m(torch.from_numpy(pos).cuda()).float() * cu(gs)).sum().backward()
+    assert torch.equal(g_with, m.params.grad)
+    assert torch.equal(x1.grad, x.grad)
+
+
+def test_render_rays_ray_gradient_vs_oracle(L):
+    """render_rays with rays that require grad (the reference's joint pose + map optimisation) returns a
+    finite gradient on rays_o, rays_d and far that matches the oracle: d depth/opacity -> compositing
+    backward (d sigma, and the direction-norm / far terms) -> fp16 d sigma -> MLP backward -> encode input
+    gradient -> d xyz = d pos01 / 2 -> rays_o (sum over samples), rays_d (sum of z d xyz)."""
+    from loner_amd import random as lr
+    from loner_amd import ray_sampling
+    from loner_amd import rendering
+    from loner_amd import tcnn as tc
+    from loner_amd.nerf import DecoupledNeRF
+
+    nerf_cfg = {"enable_view_dependence": True, "pos_encoding_sigma": SIGMA_ENC, "sigma_network": SIGMA_NET,
+                "pos_encoding_intensity": dict(SIGMA_ENC, log2_hashmap_size=19),
+                "dir_encoding_intensity": dict(otype="SphericalHarmonics", degree=4),
+                "intensity_network": dict(SIGMA_NET, n_hidden_layers=4)}
+    nerf = DecoupledNeRF(nerf_cfg)
+    torch.manual_seed(0)
+    with torch.no_grad():
+        p = nerf._model_sigma.params
+        p[3072:].uniform_(-0.5, 0.5)
+        p[2048:3072].mul_(8.0)
+    p16 = host(nerf._model_sigma.params).astype(np.float16)
+    w0, w1, table = p16[:2048].reshape(64, 32), p16[2048:3072].reshape(16, 64), p16[3072:].reshape(-1, 2)
+    rng = np.random.default_rng(9)
+    R, S = 16, 128
+    rays_np = np.zeros((R, 13), np.float32)
+    rays_np[:, 0:3] = rng.uniform(-0.3, 0.3, (R, 3))
+    dr = rng.normal(0, 1, (R, 3))
+    rays_np[:, 3:6] = dr / np.linalg.norm(dr, axis=1, keepdims=True)
+    rays_np[:, 6:9] = -rays_np[:, 3:6]
+    rays_np[:, 11], rays_np[:, 12] = 0.01, 0.4
+    rays = torch.from_numpy(rays_np).cuda().requires_grad_()
+    occ = torch.zeros(1, 1, 100, 100, 100, device="cuda")
+    sampler = ray_sampling.OccGridRaySampler()
+    sampler.update_occ_grid(occ)
+    lr.manual_seed(33)
+    res = rendering.render_rays(rays, sampler, nerf, [1, 75], 100.0, N_samples=S, retraw=True, perturb=1.0,
+                                white_bkgd=True, raw_noise_std=1.0, sigma_only=True, DEBUG=False)
+    ga = rng.normal(0, 1, R).astype(np.float32)
+    gb = rng.normal(0, 1, R).astype(np.float32)
+    loss = (res["depth_fine"] * cu(ga)).sum() + (res["opacity_fine"] * cu(gb)).sum()
+    loss.backward()
+    g = host(rays.grad)
+    assert np.all(np.isfinite(g))
+    # oracle on the GPU's samples and the same noise draws (render key = the second key after the seed)
+    from loner_amd import _lib as Lb
+    z = host(res["samples_fine"])
+    xyz = (rays_np[:, None, 0:3] + rays_np[:, None, 3:6] * z[:, :, None]).astype(np.float32)
+    pos = ((xyz + np.float32(1)) / np.float32(2)).astype(np.float32).reshape(-1, 3)
+    lay = ohg.GridLayout(16, 2, 18, 16)
+    enc = ohg.encode(pos, table, lay)
+    out16, hid = omlp.forward(enc, [w0, w1])
+    sig = out16[:, 0].astype(np.float32).reshape(R, S)
+    a2, b2 = orng.ray_sample_grid(np.arange(R), S)
+    noise = orng.normal(Lb.step_key(33, 1), orng.STREAM_NOISE, a2, b2).astype(np.float32)
+    dsig, d_dn, d_far = orender.composite_backward(sig, z, rays_np[:, 3:6], noise, rays_np[:, -1:],
+                                                   np.zeros((R, S)), ga.astype(np.float64), gb.astype(np.float64),
+                                                   ray_grads=True)
+    dout = np.zeros((R * S, 16))
+    dout[:, 0] = dsig.reshape(-1).astype(np.float16)  # the raw output is fp16: so is its gradient
+    dx, _ = omlp.backward(enc, [w0, w1], hid, dout)
+    dxyz = 0.5 * ohg.encode_input_grad(pos, table, dx, lay).reshape(R, S, 3)
+    d = rays_np[:, 3:6].astype(np.float64)
+    ref_o = dxyz.sum(1)
+    ref_d = (dxyz * z[:, :, None]).sum(1) + d_dn[:, None] * d / np.linalg.norm(d, axis=1, keepdims=True)
+    assert rel(g[:, 0:3], ref_o) <= 1e-2, rel(g[:, 0:3], ref_o)
+    assert rel(g[:, 3:6], ref_d) <= 1e-2, rel(g[:, 3:6], ref_d)
+    assert rel(g[:, 12], d_far) <= 1e-4, rel(g[:, 12], d_far)
+    assert np.all(g[:, 6:12] == 0)

@@ -183,10 +183,10 @@ def test_hashgrid_bwd(L, variant):
         table = torch.zeros(lay.n_entries * 2, dtype=torch.int16, device="cuda")
         enc = torch.empty(16, n, dtype=torch.int32, device="cuda")
         L.call("lnr_hashgrid_fwd", ctypes.byref(d), cu(pos), n, table, enc, n, ws, nb, L.stream())
-        L.call("lnr_hashgrid_bwd", ctypes.byref(d), cu(pos), n, cu(denc_lm), n, gt, ws, nb, L.BWD_COUNTS_READY,
+        L.call("lnr_hashgrid_bwd", ctypes.byref(d), cu(pos), n, cu(denc_lm), n, gt, None, None, ws, nb, L.BWD_COUNTS_READY,
                L.stream())
     elif variant == "bucketed":
-        L.call("lnr_hashgrid_bwd", ctypes.byref(d), cu(pos), n, cu(denc_lm), n, gt, ws, nb, 0, L.stream())
+        L.call("lnr_hashgrid_bwd", ctypes.byref(d), cu(pos), n, cu(denc_lm), n, gt, None, None, ws, nb, 0, L.stream())
     else:
         L.call("lnr_hashgrid_bwd_atomic", ctypes.byref(d), cu(pos), n, cu(denc_lm), n, gt, L.stream())
     got = host(gt).reshape(-1, 2)
@@ -441,7 +441,7 @@ def test_hashgrid_bwd_record_dynamic_range(L, lvl):
     nb = int(L.lib().lnr_hashgrid_bwd_workspace_bytes(ctypes.byref(d), n))
     ws = torch.empty(nb, dtype=torch.uint8, device="cuda")
     gt = torch.zeros(lay.n_entries * 2, dtype=torch.float32, device="cuda")
-    L.call("lnr_hashgrid_bwd", ctypes.byref(d), cu(pos), n, cu(denc_lm), n, gt, ws, nb, 0, L.stream())
+    L.call("lnr_hashgrid_bwd", ctypes.byref(d), cu(pos), n, cu(denc_lm), n, gt, None, None, ws, nb, 0, L.stream())
     got = host(gt).reshape(-1, 2)
     g = denc[:, 2 * lvl:2 * lvl + 2].astype(np.float64)
     E = int(np.frexp(np.float32(np.abs(g).max()))[1])

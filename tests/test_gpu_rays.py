@@ -198,3 +198,47 @@ def test_pipelined_build_and_sampling_equals_plain(L):
             np.testing.assert_array_equal(a, b)
         for a, b in zip(res[0][1:], r[1:]):
             np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("all_valid", [True, False])
+def test_prefetch_across_windows_equals_plain(L, all_valid):
+    """Back-to-back windows (a new RayWindow per window, the old one released, consecutive global steps,
+    as Optimizer._run_config does): a prefetch built from the previous window is never used for the new
+    one (it is matched by the window object, not its id(), which CPython may hand to the next window),
+    so the pipelined (all-valid windows) / prefetched (windows with invalid rays) path equals the plain
+    path bit for bit."""
+    from loner_amd import step as S_
+    from loner_amd.rays import RayWindow
+
+    def make(seed):
+        scans, wc, rr = _window("forest" if all_valid else "quad", 2, seed=seed)
+        if all_valid:
+            return RayWindow(scans, wc, rr, n_lidar=128, n_sky=16, strategy="MASK")
+        scale, shift = float(wc.scale_factor[0]), wc.shift.numpy()
+        s1 = dict(scans[1])
+        pose = s1["pose"].clone()
+        pose[0, 3] = float(0.9995 * scale - shift[0])
+        s1["pose"] = pose
+        return RayWindow([scans[0], s1], wc, rr, n_lidar=128, strategy="RANDOM")
+
+    res = []
+    for fast in (False, True):
+        st = S_.FieldState(S_.StepConfig(n_samples=64, occ_lr=1e-3), device="cuda:0", table_init=0.5)
+        eng = None
+        outs, g = [], 31
+        for seed in (8, 9, 10, 11):
+            win = make(seed)
+            assert win.all_valid == all_valid
+            if eng is None:
+                eng = S_.StepEngine(st, win.n_slots, seed=5)
+                eng.pipeline = eng.prefetch = fast
+            for _ in range(3):
+                outs.append(host(eng.step_window(win, global_step=g)).copy())
+                g += 1
+            del win  # the next window may reuse its address
+        torch.cuda.synchronize()
+        res.append((outs, host(st.params).copy(), host(st.occ).copy()))
+    for a, b in zip(res[0][0], res[1][0]):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(res[0][1], res[1][1])
+    np.testing.assert_array_equal(res[0][2], res[1][2])

@@ -221,7 +221,7 @@ def _assert_accum_paths_equal(L, st, rays, eng, R, Sn, g_ref=None):
                     os.environ[k] = v
                 g = torch.full((2 * st.n_entries,), float("nan"), dtype=torch.float32, device="cuda")  # all written
                 L.call("lnr_hashgrid_bwd_rays_jac", L.ctypes.byref(st.desc), rays, eng.z, R, Sn, eng.d_jac,
-                       eng.d_sigma(), R * Sn, g, eng.bwd_ws, eng.bwd_ws_bytes, 0, s)
+                       eng.d_sigma(), R * Sn, g, None, None, eng.bwd_ws, eng.bwd_ws_bytes, 0, s)
                 out[name].append(g)
         for name, gs in out.items():
             bad = [(groups[name][i], float((g - gs[0]).abs().max())) for i, g in enumerate(gs) if not torch.equal(g, gs[0])]
@@ -292,14 +292,14 @@ def test_full_size_properties_c4(L):
     ga = torch.zeros_like(g1)
     d_enc = eng.denc_f32()  # fp16(J) * d_sigma in fp32: the products the compact backward forms
     for g in (g1, g2):
-        L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(st.desc), rays, eng.z, R, Sn, d_enc, N, g, eng.bwd_ws,
+        L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(st.desc), rays, eng.z, R, Sn, d_enc, N, g, None, None, eng.bwd_ws,
                eng.bwd_ws_bytes, 0, s)
     L.call("lnr_hashgrid_bwd_rays_atomic", L.ctypes.byref(st.desc), rays, eng.z, R, Sn, d_enc, N, ga, s)
     assert torch.equal(g1, g2)
     # the compact source (J fp16 pairs + d_sigma) gives the very same records
     gj = torch.zeros_like(g1)
     L.call("lnr_hashgrid_bwd_rays_jac", L.ctypes.byref(st.desc), rays, eng.z, R, Sn, eng.d_jac, eng.d_sigma(), N, gj,
-           eng.bwd_ws, eng.bwd_ws_bytes, 0, s)
+           None, None, eng.bwd_ws, eng.bwd_ws_bytes, 0, s)
     assert torch.equal(gj, g1)
     # the whole-bucket accumulation (k_bwd_accum_buckets, the small-batch path) gives the bitwise
     # same gradient as the record-balanced one at full size

@@ -55,6 +55,45 @@ def test_backward_is_adjoint():
     assert abs(lhs - rhs) < 5e-3 * (abs(lhs) + 1)
 
 
+def test_input_grad_matches_central_differences():
+    """encode_input_grad (tcnn's dy_dx + backward_input) against fp64 central differences of the blend at
+    all 16 levels, on points whose cells do not change within the step at any level.  ``exact``: the
+    formula with fp64 fractions (the derivative of encode_f64); the default form takes tcnn's fp32
+    fractions (fmaf(scale, x, 0.5f) quantises the finest level's fraction to 2^-5), checked separately
+    against the exact form."""
+    L = hg.GridLayout(16, 2, 18, 16)
+    rng = np.random.default_rng(3)
+    T = rng.uniform(-1, 1, (L.n_entries, 2)).astype(np.float16)
+    pos = rng.uniform(0.02, 0.98, (400, 3))
+    h = 1e-9
+    ok = np.ones(len(pos), bool)  # at least 1e-3 of a cell from every cell boundary at every level
+    for s in L.scales:
+        f = pos * float(s) + 0.5
+        fr = f - np.floor(f)
+        ok &= np.all((fr > 1e-3) & (fr < 1 - 1e-3), axis=1)
+    pos = pos[ok][:128]
+    d = rng.normal(0, 1, (len(pos), 32))
+
+    def fd_grad(dd):
+        out = np.zeros((len(pos), 3))
+        for dim in range(3):
+            e = np.zeros(3); e[dim] = h
+            out[:, dim] = ((hg.encode_f64(pos + e, T, L) - hg.encode_f64(pos - e, T, L)) * dd).sum(-1) / (2 * h)
+        return out
+
+    got = hg.encode_input_grad(pos, T, d, L, exact=True)
+    fd = fd_grad(d)
+    assert np.linalg.norm(got - fd) / np.linalg.norm(fd) < 1e-5
+    for lvl in (0, 7, 15):  # level by level (the finest level's slope dominates the sum)
+        dl = np.zeros_like(d); dl[:, 2 * lvl:2 * lvl + 2] = d[:, 2 * lvl:2 * lvl + 2]
+        g1, f1 = hg.encode_input_grad(pos, T, dl, L, exact=True), fd_grad(dl)
+        assert np.linalg.norm(g1 - f1) / np.linalg.norm(f1) < 1e-5, lvl
+    # tcnn's fp32 fractions: the coarse levels agree closely, the finest to its 2^-5 fraction quantum
+    d0 = np.zeros_like(d); d0[:, :8] = d[:, :8]
+    g32, g64 = hg.encode_input_grad(pos, T, d0, L), hg.encode_input_grad(pos, T, d0, L, exact=True)
+    assert np.linalg.norm(g32 - g64) / np.linalg.norm(g64) < 1e-5
+
+
 def test_mlp_backward_matches_finite_difference():
     rng = np.random.default_rng(2)
     shapes = mlp.layer_shapes(32, 1, 64, 1)
