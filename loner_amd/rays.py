@@ -2,7 +2,8 @@
 
 Mirrors the reference's interface and semantics:
   WorldCube                ``src/common/pose_utils.py:23-57``
-  compute_world_cube       ``src/common/pose_utils.py:222-314`` (lidar-only, trajectory or bbox)
+  compute_world_cube       ``src/common/pose_utils.py:131-149,222-314`` (every branch: camera
+                           frustums or LiDAR cube, ground-truth poses or trajectory bbox, submaps)
   get_far_val              ``src/common/ray_utils.py:31-60``
   LidarRayDirections       ``src/common/ray_utils.py:252-322`` (13-column rays, 1 m validity filter)
   build_keyframe_rays      ``KeyFrame.build_lidar_rays`` ``src/mapping/keyframe.py:75-105`` (+ sky rays)
@@ -27,22 +28,66 @@ class WorldCube:
         return {"scale_factor": float(self.scale_factor.reshape(-1)[0]), "shift": [float(s) for s in self.shift.cpu()]}
 
 
-def compute_world_cube(lidar_poses=None, ray_range=(1.0, 75.0), padding=0.3, traj_bounding_box=None):
-    """Lidar-only ``compute_world_cube``; callers in the reference pass padding=0.3
-    (src/loner.py:104, examples/fdt_optimize_implicit_map.py:232)."""
+def _frustum_corners(K, H, W, near, far):
+    """The 8 homogeneous corners of a camera's view frustum between depths near and far (camera frame:
+    x right, y up, looking down -z), ``_get_view_frustum_corners`` (src/common/pose_utils.py:131-149):
+    per (left/right, up/down, near/far) corner the image-plane extent (cx / fx, cy / fy, (W - cx) / fx,
+    (H - cy) / fy) scaled by the depth, in the reference's order (left before right, up before down,
+    near before far)."""
+    assert 0 < near < far
+    fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
+    xs = (-cx / fx, (W - cx) / fx)
+    ys = (cy / fy, -(H - cy) / fy)
+    rows = [[x * d, y * d, -d, 1.0] for x in xs for y in ys for d in (near, far)]
+    return torch.tensor([[float(v) for v in r] for r in rows], dtype=torch.float32)
+
+
+def compute_world_cube(camera_to_lidar, intrinsic_mats, image_sizes, lidar_poses, ray_range, padding=0.1,
+                       traj_bounding_box=None, submap=None):
+    """``compute_world_cube`` (src/common/pose_utils.py:222-314), every branch, fp32 torch on the host:
+    * poses: the ground-truth lidar poses (N, 4, 4), re-based on the first pose unless ``submap`` is set
+      (:244-248), or, without poses, the 8 corners of ``traj_bounding_box`` as identity-rotation poses
+      (:228-242);
+    * with a camera (``camera_to_lidar`` given, Fusion Portable calibrations): camera poses =
+      lidar poses @ camera_to_lidar^-1, and the points are every camera's view-frustum corners between
+      the ray range's depths (one K and image size (H, W) for all, or one per pose) plus every camera and
+      lidar position (:250-283);
+    * without: the (+-max range)^3 cube corners transformed by every lidar pose plus the lidar positions
+      (:285-302);
+    then origin = the points' box centre, scale = |box diagonal| / (2 sqrt 3) (1 + padding),
+    WorldCube(scale, -origin) (:304-314).  Callers pass padding=0.3 (src/loner.py:104,
+    examples/fdt_optimize_implicit_map.py:232-233)."""
     assert 0 <= padding < 1
+    assert lidar_poses is not None or traj_bounding_box is not None
     if lidar_poses is None:
         xs, ys, zs = traj_bounding_box["x"], traj_bounding_box["y"], traj_bounding_box["z"]
         combos = torch.tensor([[x, y, z] for x in xs for y in ys for z in zs], dtype=torch.float32)
         lidar_poses = torch.eye(4).tile((8, 1, 1))
         lidar_poses[:, :3, 3] = combos
     else:
-        lidar_poses = lidar_poses @ lidar_poses[0].inverse()
-    m = float(ray_range[1])
-    corners = torch.tensor([[-m, -m, -m, 1], [-m, m, -m, 1], [m, -m, -m, 1], [m, m, -m, 1],
-                            [-m, -m, m, 1], [-m, m, m, 1], [m, -m, m, 1], [m, m, m, 1]], dtype=lidar_poses.dtype)
-    all_corners = torch.cat([(p[:3, :] @ corners.T).T for p in lidar_poses], 0)
-    pts = torch.cat([all_corners, lidar_poses[:, :3, 3]])
+        lidar_poses = torch.as_tensor(lidar_poses, dtype=torch.float32)
+        if submap is None:
+            lidar_poses = lidar_poses @ lidar_poses[0].inverse()
+    if camera_to_lidar is not None:
+        cam_poses = lidar_poses @ torch.as_tensor(camera_to_lidar, dtype=torch.float32).inverse()
+        n = cam_poses.shape[0]
+        Ks = torch.as_tensor(intrinsic_mats, dtype=torch.float32)
+        if Ks.dim() == 2:
+            Ks = Ks.expand(n, 3, 3)
+        hw = torch.as_tensor(image_sizes, dtype=torch.float32)
+        if hw.shape == (2,):
+            hw = hw.expand(n, 2)
+        assert hw.shape[0] == n
+        corners = [(c2w[:3, :] @ _frustum_corners(K, h_w[0], h_w[1], ray_range[0], ray_range[1]).T).T
+                   for K, h_w, c2w in zip(Ks, hw, cam_poses)]
+        positions = torch.cat([cam_poses[:, :3, 3], lidar_poses[:, :3, 3]], 0)
+    else:
+        m = float(ray_range[1])
+        box = torch.tensor([[-m, -m, -m, 1], [-m, m, -m, 1], [m, -m, -m, 1], [m, m, -m, 1],
+                            [-m, -m, m, 1], [-m, m, m, 1], [m, -m, m, 1], [m, m, m, 1]], dtype=torch.float32)
+        corners = [(p[:3, :] @ box.T).T for p in lidar_poses]
+        positions = lidar_poses[:, :3, 3]
+    pts = torch.cat([torch.cat(corners, 0), positions])
     mn, mx = pts.min(0)[0], pts.max(0)[0]
     origin = mn + (mx - mn) / 2
     scale = (torch.linalg.norm(mx - mn) / (2 * torch.sqrt(torch.tensor([3.0])))) * (1 + padding)

@@ -66,9 +66,11 @@ def middle_points(positions, parts):
     return np.stack([(p[s] + p[e]) / 2 for s, e in parts])
 
 
-def poses_from_tum(tum):
-    """pose_utils.build_poses_from_df(df, zero_origin=False) (:387-409): rows [t x y z qx qy qz qw] ->
-    (N, 4, 4) float32 (the quaternion normalised, as scipy's Rotation.from_quat does; fp64, then fp32)."""
+def poses_from_tum(tum, zero_origin=False):
+    """pose_utils.build_poses_from_df(df, zero_origin) (:387-409): rows [t x y z qx qy qz qw] ->
+    (N, 4, 4) float32 (the quaternion normalised, as scipy's Rotation.from_quat does; fp64, then fp32).
+    ``zero_origin``: every pose is expressed relative to the first (the inverse of the first pose, formed
+    as [R^T | -R^T t], applied on the left, in fp64), as the driver does for whole runs (:208-213)."""
     tum = np.asarray(tum, np.float64)
     q = tum[:, 4:8] / np.linalg.norm(tum[:, 4:8], axis=1, keepdims=True)
     x, y, z, w = q.T
@@ -79,6 +81,11 @@ def poses_from_tum(tum):
     P[:, :3, :3] = Rm
     P[:, :3, 3] = tum[:, 1:4]
     P[:, 3, 3] = 1.0
+    if zero_origin:
+        inv = np.eye(4)
+        inv[:3, :3] = P[0, :3, :3].T
+        inv[:3, 3] = -P[0, :3, :3].T @ P[0, :3, 3]
+        P = inv[None] @ P
     return P.astype(np.float32)
 
 

@@ -572,11 +572,60 @@ def main_r3():
     print("round-3 golden vectors written to", OUT, names, scales, err_s, files_s, calls_s)
 
 
+# ---------------------------------------------------------------------------------------------
+# Round-4 fixtures (``python tests/golden/make_golden.py r4``): every branch of compute_world_cube
+# (src/common/pose_utils.py:131-149,222-314), in particular the camera-frustum branch the fdt driver
+# takes with a Fusion Portable calibration (examples/fdt_optimize_implicit_map.py:195-233).  The
+# Fusion Portable calibration files are dataset files (not in the reference), so the camera is a
+# synthetic one of the same shape: K of a 1024 x 768 camera at im_scale_factor 0.5, a lidar-to-camera
+# extrinsic rotating the lidar's x axis onto the camera's -z axis, plus a small offset.  Poses: the
+# committed haveri keyframe trajectory through build_poses_from_df (zero_origin True for whole runs,
+# False for submaps, as the driver does at :208-213).
+
+def main_r4():
+    import pandas as pd
+    ref = import_reference()
+    tum = np.load(f"{OUT}/haveri_keyframe_trajectory.npz")["tum"][:240]
+    df = pd.DataFrame(tum, columns=["timestamp", "x", "y", "z", "q_x", "q_y", "q_z", "q_w"])
+    poses_zero, _ = ref.pose_utils.build_poses_from_df(df, True)
+    poses_raw, _ = ref.pose_utils.build_poses_from_df(df, False)
+    K = torch.tensor([[303.3, 0.0, 258.0], [0.0, 303.1, 193.25], [0.0, 0.0, 1.0]])
+    image_size = (384, 512)  # (height, width), as the driver passes it
+    R = torch.tensor([[0.0, -1.0, 0.0], [0.0, 0.0, 1.0], [-1.0, 0.0, 0.0]])  # lidar x -> camera -z
+    l2c = torch.eye(4)
+    l2c[:3, :3] = R
+    l2c[:3, 3] = torch.tensor([0.05, -0.12, 0.08])
+    c2l = l2c.inverse()
+    n = poses_raw.shape[0]
+    Ks = K.expand(n, 3, 3).clone()
+    Ks[:, 0, 0] += torch.linspace(0, 5, n)
+    sizes = torch.tensor(image_size, dtype=torch.float32).expand(n, 2).clone()
+    sizes[n // 2:] = torch.tensor([360.0, 480.0])
+    bbox = dict(x=[-5.0, 50.0], y=[-25.0, 15.0], z=[-3.0, 10.0])
+    cases = {
+        "camera_rebased": (c2l, K, image_size, poses_zero, (1.0, 50.0), 0.3, None, None),
+        "camera_submap_per_pose": (c2l, Ks, sizes, poses_raw, (1.0, 50.0), 0.3, None, "submap_1"),
+        "lidar_rebased": (None, None, None, poses_zero, (2.5, 45.0), 0.3, None, None),
+        "bbox_camera": (c2l, K, image_size, None, (1.0, 50.0), 0.3, bbox, None),
+        "bbox_lidar": (None, None, None, None, (1.0, 75.0), 0.3, bbox, None),
+    }
+    out = dict(tum=tum, K=K.numpy(), Ks=Ks.numpy(), image_size=np.float32(image_size), sizes=sizes.numpy(),
+               camera_to_lidar=c2l.numpy(), bbox=np.float32([bbox["x"], bbox["y"], bbox["z"]]))
+    for name, (c, k, hw, poses, rr, pad, bb, sub) in cases.items():
+        wc = ref.pose_utils.compute_world_cube(c, k, hw, poses, rr, padding=pad, traj_bounding_box=bb, submap=sub)
+        out[f"{name}_scale"] = np.float32(wc.scale_factor.reshape(-1)[0])
+        out[f"{name}_shift"] = wc.shift.numpy().reshape(3).astype(np.float32)
+        print(name, float(wc.scale_factor.reshape(-1)[0]), wc.shift.numpy())
+    np.savez_compressed(f"{OUT}/world_cube_camera.npz", **out)
+    print("round-4 golden vectors written to", OUT)
+
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "r2":
         main_r2()
     elif len(sys.argv) > 1 and sys.argv[1] == "r3":
         main_r3()
+    elif len(sys.argv) > 1 and sys.argv[1] == "r4":
+        main_r4()
     else:
         main()

@@ -82,3 +82,32 @@ def test_submap_window_is_its_segment():
     assert float(cube.scale_factor[0]) == info["cube_scale"]
     np.testing.assert_allclose(info["cube_scale"], SUB["scale"][1], rtol=1e-6)
     np.testing.assert_allclose(cube.shift.numpy(), SUB["shift"][1], rtol=1e-6, atol=1e-5)
+
+
+def test_compute_world_cube_every_branch_golden():
+    """loner_amd.rays.compute_world_cube against the reference's own compute_world_cube
+    (tests/golden/world_cube_camera.npz, make_golden.py r4): the camera-frustum branch (Fusion Portable
+    calibrations, examples/fdt_optimize_implicit_map.py:195-233) with one K / image size and with one per
+    pose, re-based and submap poses; the LiDAR branch; the trajectory bounding box with and without a camera.
+    fp32 matrix products in another order: rtol 1e-5."""
+    import torch
+    from loner_amd.rays import compute_world_cube
+    g = np.load("tests/golden/world_cube_camera.npz")
+    tum = g["tum"]
+    zero = torch.from_numpy(SM.poses_from_tum(tum, zero_origin=True))
+    raw = torch.from_numpy(SM.poses_from_tum(tum))
+    c2l, K, Ks = torch.from_numpy(g["camera_to_lidar"]), torch.from_numpy(g["K"]), torch.from_numpy(g["Ks"])
+    hw = tuple(int(v) for v in g["image_size"])
+    bbox = dict(x=list(g["bbox"][0]), y=list(g["bbox"][1]), z=list(g["bbox"][2]))
+    cases = {
+        "camera_rebased": (c2l, K, hw, zero, (1.0, 50.0), None, None),
+        "camera_submap_per_pose": (c2l, Ks, torch.from_numpy(g["sizes"]), raw, (1.0, 50.0), None, "submap_1"),
+        "lidar_rebased": (None, None, None, zero, (2.5, 45.0), None, None),
+        "bbox_camera": (c2l, K, hw, None, (1.0, 50.0), bbox, None),
+        "bbox_lidar": (None, None, None, None, (1.0, 75.0), bbox, None),
+    }
+    for name, (c, k, s, poses, rr, bb, sub) in cases.items():
+        wc = compute_world_cube(c, k, s, poses, rr, padding=0.3, traj_bounding_box=bb, submap=sub)
+        np.testing.assert_allclose(float(wc.scale_factor[0]), g[f"{name}_scale"], rtol=1e-5, err_msg=name)
+        np.testing.assert_allclose(wc.shift.numpy(), g[f"{name}_shift"], rtol=1e-5, atol=1e-4, err_msg=name)
+    assert float(g["bbox_lidar_scale"]) == pytest.approx(121.426537, rel=1e-6)  # the quad cube (SURVEY §8(c))
