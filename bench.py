@@ -298,7 +298,7 @@ def bench_render(args):
         window.build(key, 0, R, rays, dgt)
         if prof:
             mark("sample")
-        L.call("lnr_sample_ogm", rays, R, S, state.occ, 100, 0.0, None, None, key, 0, rend.z, st)
+        L.call("lnr_sample_ogm", rays, R, S, state.occ, 100, 0.0, None, None, key, 0, rend.z, None, st)
         if prof:
             mark("sample")
             mark("encode")
@@ -487,7 +487,7 @@ def _camera_stages(eng, fr, rays, inten, L):
     mark("rays")
     fr.build(1, rays, inten)
     mark("sample")
-    L.call("lnr_sample_ogm", rays, R, S, fs.occ, fs.cfg.occ_res, 1.0, None, None, key, 0, eng.z, s)
+    L.call("lnr_sample_ogm", rays, R, S, fs.occ, fs.cfg.occ_res, 1.0, None, None, key, 0, eng.z, None, s)
     mark("encode")
     L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(fs.desc), rays, eng.z, R, S, fs.table_f16, eng.enc, N, None, 0, s)
     mark("weights")
@@ -507,7 +507,7 @@ def _camera_stages(eng, fr, rays, inten, L):
     L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(cs.desc), rays, eng.z, R, S, eng.d_enc, N, cs.grad_table,
            None, None, eng.bwd_ws, eng.bwd_ws_bytes, (0 if eng.skip_zero else L.BWD_COUNTS_READY) | L.BWD_LEVEL_MAX_READY, s)
     mark("adam")
-    L.call("lnr_adam_step", cs.params, cs.shadow, cs.grad, cs.m, cs.v, cs.n_padded, 1, 0.0, 0.9, 0.999, 1e-8, s)
+    L.call("lnr_adam_step", cs.params, cs.shadow, cs.grad, cs.m, cs.v, cs.n_padded, 1, 0.0, 0.9, 0.999, 1e-8, None, s)
     mark("end")
     torch.cuda.synchronize()
     return {ev[i][0]: float(ev[i][1].elapsed_time(ev[i + 1][1])) for i in range(len(ev) - 1)}

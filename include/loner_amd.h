@@ -63,6 +63,31 @@ extern "C" {
 const char* lnr_last_error(void);
 int lnr_version(void);
 
+/* ---------------------------------------------------------------- per-step scalars (graph replay) */
+/* The scalars that change from one optimiser step to the next, in DEVICE memory, so that a step
+ * captured once in a hipGraph replays with the current step's values (no kernel argument changes).
+ * Every entry point that takes `dev_step` (or a struct holding it) reads these fields from it when it
+ * is not NULL, in place of the corresponding host argument:
+ *   key             the draw key (lnr_step_key(seed, global_step)): lnr_sample_ogm / _uniform, the
+ *                   ray build (lnr_ray_window.dev_step), the sigma noise (lnr_loss_params.dev_step)
+ *   los_lambda      lnr_loss_params.los_lambda (optimizer.py:712-716, decayed on global_step + 1)
+ *   los_eps         lnr_loss_params.los_eps (optimizer.py:781-785)
+ *   adam_step_size  lr / (1 - beta1^t), adam_bc2_sqrt = sqrt(1 - beta2^t): lnr_adam_step(_ranges)
+ *                   (lnr_adam_coefficients forms both exactly as those calls do from step and lr) */
+typedef struct lnr_step_scalars {
+  uint32_t key;
+  float los_lambda;
+  float los_eps;
+  float adam_step_size;
+  float adam_bc2_sqrt;
+  uint32_t pad[3];
+} lnr_step_scalars;
+/* *dev = *value (value: a HOST struct, carried as the kernel's argument), enqueued on `stream`: the
+ * launch before a captured step's replay sets that step's scalars in stream order. */
+int lnr_step_scalars_set(const lnr_step_scalars* value, lnr_step_scalars* dev, void* stream);
+/* Host: the fp32 Adam coefficients lnr_adam_step forms for 1-based step t and learning rate lr. */
+int lnr_adam_coefficients(int32_t step, double lr, double beta1, double beta2, float* step_size, float* bc2_sqrt);
+
 /* ---------------------------------------------------------------- hash grid */
 typedef struct lnr_grid_desc {
   uint32_t n_levels;          /* tcnn "n_levels" */
@@ -178,9 +203,9 @@ int lnr_sigma_mlp_bwd(const uint16_t* w, const uint32_t* enc, int64_t enc_stride
 uint32_t lnr_step_key(uint32_t seed, uint32_t step);
 int lnr_sample_ogm(const float* rays, int64_t n_rays, int32_t n_samples, const float* occ, int32_t occ_res,
                    float perturb, const float* u_jitter, const float* u_pdf, uint32_t key, int64_t ray_offset,
-                   float* z, void* stream);
+                   float* z, const lnr_step_scalars* dev_step, void* stream);
 int lnr_sample_uniform(const float* rays, int64_t n_rays, int32_t n_samples, float perturb, const float* u_jitter,
-                       uint32_t key, int64_t ray_offset, float* z, void* stream);
+                       uint32_t key, int64_t ray_offset, float* z, const lnr_step_scalars* dev_step, void* stream);
 
 /* ---------------------------------------------------------------- compositing + loss */
 #define LNR_RENDER_DEFAULT 0
@@ -211,6 +236,7 @@ typedef struct lnr_loss_params {
   float* dev_loss_out;       /* optional DEVICE [8]: lnr_field_train also writes lnr_loss_finalize's output
                                 here, in its last launch (one launch less per step) */
   int32_t flags;             /* LNR_LP_* */
+  const lnr_step_scalars* dev_step; /* optional DEVICE: key (the noise), los_lambda and los_eps from here */
 } lnr_loss_params;
 #define LNR_LP_DW_OVERWRITE 1  /* lnr_field_train STORES d_w (the MLP gradient) instead of adding to it */
 
@@ -316,6 +342,7 @@ typedef struct lnr_ray_window {
   const int32_t* ray_off;     /* [K+1] output slots of each keyframe: its LiDAR rays, then its sky rays */
   const int32_t* n_sel;       /* [K] LiDAR slots per keyframe (slots beyond them are sky rays) */
   const int32_t* n_sel_trunk; /* MASK: [K] LiDAR slots drawn from the trunk points */
+  const lnr_step_scalars* dev_step; /* optional DEVICE: the draw key from here instead of `key` */
 } lnr_ray_window;
 
 /* Build output slots [slot0, slot0 + n_slots) of the window's ray batch: rays (n_slots, 13), depth
@@ -370,9 +397,10 @@ int lnr_rgb_train(const uint16_t* w_rgb, int32_t n_hidden_layers, const uint32_t
                   void* workspace, int64_t workspace_bytes, float* d_enc_level_max, void* stream);
 
 /* ---------------------------------------------------------------- optimiser */
-/* torch.optim.Adam (no weight decay); step is 1-based.  shadow (fp16) may be NULL. */
+/* torch.optim.Adam (no weight decay); step is 1-based.  shadow (fp16) may be NULL.  dev_step (optional):
+ * the step size and bias correction from there (step and lr are then ignored). */
 int lnr_adam_step(float* param, uint16_t* shadow, const float* grad, float* m, float* v, int64_t n, int32_t step,
-                  double lr, double beta1, double beta2, double eps, void* stream);
+                  double lr, double beta1, double beta2, double eps, const lnr_step_scalars* dev_step, void* stream);
 /* The same step over up to LNR_ADAM_MAX_RANGES independent ranges in one launch (the sharded
  * optimiser's per-level-range chunks, loner_amd.step.StepEngine(zero=...)). */
 #define LNR_ADAM_MAX_RANGES 8
@@ -385,7 +413,7 @@ typedef struct lnr_adam_range {
   int64_t n;
 } lnr_adam_range;
 int lnr_adam_step_ranges(const lnr_adam_range* ranges, int32_t n_ranges, int32_t step, double lr, double beta1,
-                         double beta2, double eps, void* stream);
+                         double beta2, double eps, const lnr_step_scalars* dev_step, void* stream);
 /* OGM update: occ (res^3) -= lr * grid_sample^T(logits_grad(z*scale - depth_gt*scale)).  grad_ws is
  * workspace of ws_words fp32 (lnr_ogm_workspace_words(occ_res) for full speed; at least 3 res^3):
  * the splat accumulates in int64 fixed point in replicas of the grid that spread same-voxel

@@ -41,6 +41,12 @@ class GridDesc(ctypes.Structure):
                 ("size", ctypes.c_uint32 * MAX_LEVELS), ("offset", ctypes.c_uint32 * (MAX_LEVELS + 1))]
 
 
+class StepScalars(ctypes.Structure):
+    """``lnr_step_scalars``: the per-step scalars a captured step reads from device memory."""
+    _fields_ = [("key", ctypes.c_uint32), ("los_lambda", ctypes.c_float), ("los_eps", ctypes.c_float),
+                ("adam_step_size", ctypes.c_float), ("adam_bc2_sqrt", ctypes.c_float), ("pad", ctypes.c_uint32 * 3)]
+
+
 class AdamRange(ctypes.Structure):
     """lnr_adam_range (include/loner_amd.h)."""
     _fields_ = [("param", ctypes.c_void_p), ("shadow", ctypes.c_void_p), ("grad", ctypes.c_void_p),
@@ -56,7 +62,8 @@ class LossParams(ctypes.Structure):
                 ("min_js", ctypes.c_float), ("max_js", ctypes.c_float), ("js_alpha", ctypes.c_float),
                 ("los_eps", ctypes.c_float), ("far_ref", ctypes.c_float), ("inv_n_opaque", ctypes.c_float),
                 ("inv_rs", ctypes.c_float), ("dev_n_opaque", ctypes.c_void_p), ("dev_far_ref", ctypes.c_void_p),
-                ("dev_status", ctypes.c_void_p), ("dev_loss_out", ctypes.c_void_p), ("flags", ctypes.c_int32)]
+                ("dev_status", ctypes.c_void_p), ("dev_loss_out", ctypes.c_void_p), ("flags", ctypes.c_int32),
+                ("dev_step", ctypes.c_void_p)]
 
 
 LP_DW_OVERWRITE = 1
@@ -73,7 +80,7 @@ class RayWindowDesc(ctypes.Structure):
     _fields_ = [("n_kf", ctypes.c_int32), ("scale", ctypes.c_float), ("shift", ctypes.c_float * 3),
                 ("r_min", ctypes.c_float), ("r_max", ctypes.c_float), ("poses", c_p), ("dirs", c_p), ("dists", c_p),
                 ("scan_off", c_p), ("order", c_p), ("n_trunk", c_p), ("sky_dirs", c_p), ("sky_off", c_p),
-                ("ray_off", c_p), ("n_sel", c_p), ("n_sel_trunk", c_p)]
+                ("ray_off", c_p), ("n_sel", c_p), ("n_sel_trunk", c_p), ("dev_step", c_p)]
 
 
 class MotionComp(ctypes.Structure):
@@ -127,8 +134,8 @@ _SIGNATURES = {
     "lnr_field_train_workspace_words": (c_i64, [c_i64, c_i32]),
     "lnr_sigma_mlp_bwd": (ctypes.c_int, [c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p]),
     "lnr_step_key": (c_u32, [c_u32, c_u32]),
-    "lnr_sample_ogm": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i32, c_f, c_p, c_p, c_u32, c_i64, c_p, c_p]),
-    "lnr_sample_uniform": (ctypes.c_int, [c_p, c_i64, c_i32, c_f, c_p, c_u32, c_i64, c_p, c_p]),
+    "lnr_sample_ogm": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i32, c_f, c_p, c_p, c_u32, c_i64, c_p, c_p, c_p]),
+    "lnr_sample_uniform": (ctypes.c_int, [c_p, c_i64, c_i32, c_f, c_p, c_u32, c_i64, c_p, c_p, c_p]),
     "lnr_composite": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_i32, c_f, c_p, c_u32, c_i64, c_p, c_p, c_p, c_p,
                                      c_p]),
     "lnr_composite_bwd": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_i32, c_f, c_p, c_u32, c_i64, c_p, c_p, c_p,
@@ -157,8 +164,10 @@ _SIGNATURES = {
     "lnr_count_opaque": (ctypes.c_int, [c_p, c_i64, c_f, c_p, c_p, c_p]),
     "lnr_build_lidar_rays": (ctypes.c_int, [ctypes.POINTER(RayWindowDesc), c_i32, c_p, c_u32, c_i64, c_i64, c_p, c_p,
                                             c_p, c_p, c_p, c_p]),
-    "lnr_adam_step": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i32, c_d, c_d, c_d, c_d, c_p]),
-    "lnr_adam_step_ranges": (ctypes.c_int, [c_p, c_i32, c_i32, c_d, c_d, c_d, c_d, c_p]),
+    "lnr_adam_step": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i32, c_d, c_d, c_d, c_d, c_p, c_p]),
+    "lnr_adam_step_ranges": (ctypes.c_int, [c_p, c_i32, c_i32, c_d, c_d, c_d, c_d, c_p, c_p]),
+    "lnr_step_scalars_set": (ctypes.c_int, [ctypes.POINTER(StepScalars), c_p, c_p]),
+    "lnr_adam_coefficients": (ctypes.c_int, [c_i32, c_d, c_d, c_d, ctypes.POINTER(c_f), ctypes.POINTER(c_f)]),
     "lnr_ogm_workspace_words": (c_i64, [c_i32]),
     "lnr_ogm_update": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_f, c_f, c_p, c_p, c_i64, c_i32, c_p]),
     "lnr_ogm_grad": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_i64, c_i32, c_p]),

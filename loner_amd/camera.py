@@ -240,9 +240,9 @@ class CameraStepEngine:
         key = int(L.lib().lnr_step_key(self.seed, gstep))
         if fs.cfg.sampler == "OGM":
             L.call("lnr_sample_ogm", rays, R, S, fs.occ, fs.cfg.occ_res, self.perturb, None, None, key,
-                   self.ray_offset, self.z, s)
+                   self.ray_offset, self.z, None, s)
         else:
-            L.call("lnr_sample_uniform", rays, R, S, self.perturb, None, key, self.ray_offset, self.z, s)
+            L.call("lnr_sample_uniform", rays, R, S, self.perturb, None, key, self.ray_offset, self.z, None, s)
         L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(fs.desc), rays, self.z, R, S, fs.table_f16, self.enc, N,
                None, 0, s)
         L.call("lnr_field_render", fs.mlp_f16, self.enc, N, rays, self.z, R, S, 0, self.noise_std, None, key,
@@ -268,6 +268,6 @@ class CameraStepEngine:
         cs.adam_step += 1
         lr = self.lr * self.gamma ** (cs.adam_step - 1)  # ExponentialLR stepped once per iteration
         L.call("lnr_adam_step", cs.params, cs.shadow, cs.grad, cs.m, cs.v, cs.n_padded, cs.adam_step, lr, 0.9,
-               0.999, 1e-8, s)
+               0.999, 1e-8, None, s)
         self.iteration += 1
         return self.loss

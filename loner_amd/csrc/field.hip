@@ -56,6 +56,17 @@ struct FieldArgs {
 // lnr_loss_params.kind for the plain autograd backward of the render (no loss inside the kernel)
 constexpr int32_t kLossExternal = 100;
 
+// Graph replay: the step's key, los_lambda and los_eps from device memory (lnr_step_scalars).
+__device__ __forceinline__ uint32_t step_key_of(const FieldArgs& a) { return a.lp.dev_step ? a.lp.dev_step->key : a.key; }
+__device__ __forceinline__ lnr_loss_params step_lp(const lnr_loss_params& in) {
+  lnr_loss_params lp = in;
+  if (lp.dev_step) {
+    lp.los_lambda = lp.dev_step->los_lambda;
+    lp.los_eps = lp.dev_step->los_eps;
+  }
+  return lp;
+}
+
 struct RayShared {
   float* sig;        // [S] sigma, then dL/dsigma
   float* red;        // reduction scratch [16 * NW]
@@ -142,7 +153,7 @@ __device__ void composite_ray(const FieldArgs& a, const RayShared& sh, int64_t r
       float nz = 0.f;
       if (!ADJ) {
         if (a.noise) nz = a.noise[r * S + i] * a.noise_std;
-        else if (a.noise_std > 0.f) nz = rand_normal(a.key, kStreamNoise, (uint32_t)gr, (uint32_t)i) * a.noise_std;
+        else if (a.noise_std > 0.f) nz = rand_normal(step_key_of(a), kStreamNoise, (uint32_t)gr, (uint32_t)i) * a.noise_std;
       }
       x[c] = sh.sig[i] + nz;
       const float sr = fmaxf(x[c], 0.f);
@@ -232,7 +243,7 @@ __device__ void composite_ray(const FieldArgs& a, const RayShared& sh, int64_t r
     return;
   }
 
-  const lnr_loss_params& lp = a.lp;
+  const lnr_loss_params lp = step_lp(a.lp);
   if (lp.kind == kLossExternal) {
     // autograd of raw2outputs(_adjusted) w.r.t. sigma given dL/d{weights, depth, opacity, variance}
     // (rendering_tcnn.py:262-293): variance = sum w (depth - z)^2 feeds w directly and via depth;
@@ -585,7 +596,7 @@ __device__ void composite_loss_wave(const FieldArgs& a, float* sig, int64_t r) {
   const float dnorm = sqrtf(dx * dx + dy * dy + dz * dz);
   const float* zr = a.z + r * S;
   const int64_t gr = a.ray_offset + r;
-  const lnr_loss_params& lp = a.lp;
+  const lnr_loss_params lp = step_lp(a.lp);
 
   float z[C], alpha[C], s[C], delta[C], x[C], T[C], w[C];
   double tl[C];
@@ -601,7 +612,7 @@ __device__ void composite_loss_wave(const FieldArgs& a, float* sig, int64_t r) {
     delta[c] = dl * dnorm;
     float nz = 0.f;
     if (a.noise) nz = a.noise[r * S + i] * a.noise_std;
-    else if (a.noise_std > 0.f) nz = rand_normal(a.key, kStreamNoise, (uint32_t)gr, (uint32_t)i) * a.noise_std;
+    else if (a.noise_std > 0.f) nz = rand_normal(step_key_of(a), kStreamNoise, (uint32_t)gr, (uint32_t)i) * a.noise_std;
     x[c] = sig[i] + nz;
     const float sr = fmaxf(x[c], 0.f);
     alpha[c] = 1.0f - expf(-(delta[c] * sr));
@@ -1014,8 +1025,9 @@ static size_t bwd_tiles_smem_bytes() {
 constexpr int kReduceThreads = 1024;  // single-workgroup reductions over rays: latency, not bandwidth
 
 // lnr_loss_finalize's body (one workgroup of kReduceThreads): per-ray partials -> the loss scalars
-__device__ __forceinline__ void loss_finalize_block(const float* __restrict__ st, int64_t n, const lnr_loss_params& lp,
+__device__ __forceinline__ void loss_finalize_block(const float* __restrict__ st, int64_t n, const lnr_loss_params& lp_in,
                                                     float* out) {
+  const lnr_loss_params lp = step_lp(lp_in);
   __shared__ float red[5 * kReduceThreads / 64];
   double a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0;
   for (int64_t r = threadIdx.x; r < n; r += blockDim.x) {

@@ -58,7 +58,12 @@ __device__ __forceinline__ void adam_range(float* __restrict__ p, uint16_t* __re
 __global__ void __launch_bounds__(256) k_adam(float* __restrict__ p, uint16_t* __restrict__ shadow,
                                               const float* __restrict__ g, float* __restrict__ m,
                                               float* __restrict__ v, int64_t n, float one_minus_b1, float b2,
-                                              float one_minus_b2, float step_size, float bc2_sqrt, float eps) {
+                                              float one_minus_b2, float step_size, float bc2_sqrt, float eps,
+                                              const lnr_step_scalars* dev_step) {
+  if (dev_step) {  // graph replay: this step's coefficients from device memory
+    step_size = dev_step->adam_step_size;
+    bc2_sqrt = dev_step->adam_bc2_sqrt;
+  }
   adam_range(p, shadow, g, m, v, n, one_minus_b1, b2, one_minus_b2, step_size, bc2_sqrt, eps, blockIdx.x, gridDim.x);
 }
 
@@ -68,7 +73,12 @@ struct AdamRanges {
   lnr_adam_range r[LNR_ADAM_MAX_RANGES];
 };
 __global__ void __launch_bounds__(256) k_adam_ranges(AdamRanges rs, float one_minus_b1, float b2, float one_minus_b2,
-                                                     float step_size, float bc2_sqrt, float eps) {
+                                                     float step_size, float bc2_sqrt, float eps,
+                                                     const lnr_step_scalars* dev_step) {
+  if (dev_step) {
+    step_size = dev_step->adam_step_size;
+    bc2_sqrt = dev_step->adam_bc2_sqrt;
+  }
   const lnr_adam_range& r = rs.r[blockIdx.y];
   adam_range(r.param, r.shadow, r.grad, r.m, r.v, r.n, one_minus_b1, b2, one_minus_b2, step_size, bc2_sqrt, eps,
              blockIdx.x, gridDim.x);
@@ -272,28 +282,48 @@ static unsigned grid1d(int64_t n, int64_t cap = 1 << 20) {
 
 using namespace lnr;
 
+__global__ void k_step_scalars_set(lnr_step_scalars value, lnr_step_scalars* __restrict__ out) {
+  if (threadIdx.x == 0) *out = value;
+}
+
+extern "C" int lnr_step_scalars_set(const lnr_step_scalars* value, lnr_step_scalars* dev, void* stream) {
+  LNR_REQUIRE(value && dev, "lnr_step_scalars_set: null pointer");
+  hipLaunchKernelGGL(k_step_scalars_set, dim3(1), dim3(64), 0, as_stream(stream), *value, dev);
+  LNR_RETURN_LAUNCH("lnr_step_scalars_set");
+}
+
+// the hyper-parameters arrive as doubles (Python floats) and every derived scalar is formed in double
+// before its single rounding to fp32, as torch.optim.Adam forms them (1 - beta2 from the float 0.999f
+// would be 1.3e-5 off)
+extern "C" int lnr_adam_coefficients(int32_t step, double lr, double beta1, double beta2, float* step_size,
+                                     float* bc2_sqrt) {
+  LNR_REQUIRE(step >= 1 && step_size && bc2_sqrt, "lnr_adam_coefficients: step=%d", step);
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  *step_size = (float)(lr / bc1);
+  *bc2_sqrt = (float)std::sqrt(bc2);
+  return LNR_OK;
+}
+
 extern "C" int lnr_adam_step(float* param, uint16_t* shadow, const float* grad, float* m, float* v, int64_t n,
-                             int32_t step, double lr, double beta1, double beta2, double eps, void* stream) {
+                             int32_t step, double lr, double beta1, double beta2, double eps,
+                             const lnr_step_scalars* dev_step, void* stream) {
   LNR_REQUIRE(n >= 0 && step >= 1, "lnr_adam_step: n=%lld step=%d", (long long)n, step);
   if (n == 0) return LNR_OK;
   LNR_REQUIRE(param && grad && m && v, "lnr_adam_step: null pointer");
   LNR_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) % 16 == 0 &&
                   (shadow == nullptr || (uintptr_t)shadow % 8 == 0),
               "lnr_adam_step: buffers must be 16-byte aligned");
-  // the hyper-parameters arrive as doubles (Python floats) and every derived scalar is formed in double
-  // before its single rounding to fp32, as torch.optim.Adam forms them (1 - beta2 from the float 0.999f
-  // would be 1.3e-5 off)
-  const double bc1 = 1.0 - std::pow(beta1, (double)step);
-  const double bc2 = 1.0 - std::pow(beta2, (double)step);
-  const float step_size = (float)(lr / bc1);
-  const float bc2_sqrt = (float)std::sqrt(bc2);
+  float step_size, bc2_sqrt;
+  if (int e = lnr_adam_coefficients(step, lr, beta1, beta2, &step_size, &bc2_sqrt)) return e;
   hipLaunchKernelGGL(k_adam, dim3(grid1d(n / 4, 8192)), dim3(256), 0, as_stream(stream), param, shadow, grad, m, v, n,
-                     (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), step_size, bc2_sqrt, (float)eps);
+                     (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), step_size, bc2_sqrt, (float)eps, dev_step);
   LNR_RETURN_LAUNCH("lnr_adam_step");
 }
 
 extern "C" int lnr_adam_step_ranges(const lnr_adam_range* ranges, int32_t n_ranges, int32_t step, double lr,
-                                    double beta1, double beta2, double eps, void* stream) {
+                                    double beta1, double beta2, double eps, const lnr_step_scalars* dev_step,
+                                    void* stream) {
   LNR_REQUIRE(n_ranges >= 0 && n_ranges <= LNR_ADAM_MAX_RANGES && step >= 1,
               "lnr_adam_step_ranges: n_ranges=%d (at most %d) step=%d", n_ranges, LNR_ADAM_MAX_RANGES, step);
   if (n_ranges == 0) return LNR_OK;
@@ -311,11 +341,10 @@ extern "C" int lnr_adam_step_ranges(const lnr_adam_range* ranges, int32_t n_rang
     nmax = r.n > nmax ? r.n : nmax;
   }
   if (nmax == 0) return LNR_OK;
-  const double bc1 = 1.0 - std::pow(beta1, (double)step);  // (as lnr_adam_step)
-  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  float step_size, bc2_sqrt;
+  if (int e = lnr_adam_coefficients(step, lr, beta1, beta2, &step_size, &bc2_sqrt)) return e;
   hipLaunchKernelGGL(k_adam_ranges, dim3(grid1d(nmax / 4, 8192), n_ranges), dim3(256), 0, as_stream(stream), rs,
-                     (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)(lr / bc1), (float)std::sqrt(bc2),
-                     (float)eps);
+                     (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), step_size, bc2_sqrt, (float)eps, dev_step);
   LNR_RETURN_LAUNCH("lnr_adam_step_ranges");
 }
 

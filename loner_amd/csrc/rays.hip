@@ -168,6 +168,7 @@ __global__ void __launch_bounds__(256) k_build_rays(lnr_ray_window w, int32_t se
                                                     uint32_t key, int64_t slot0, int64_t n, float* __restrict__ rays,
                                                     float* __restrict__ depth, uint8_t* __restrict__ valid,
                                                     int32_t* __restrict__ point_index, float* __restrict__ far_ref) {
+  if (w.dev_step) key = w.dev_step->key;  // graph replay: this step's key from device memory
   __shared__ KfTables tb;
   if (w.n_kf <= kKfLds) {  // (uniform)
     const int K = w.n_kf;

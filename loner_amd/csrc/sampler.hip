@@ -33,10 +33,12 @@ struct SamplerArgs {
   int64_t ray_offset;
   float* z;
   int32_t P2;      // next power of two >= S (sort width)
+  const lnr_step_scalars* dev_step;  // optional: the key from device memory (graph replay)
 };
 
 template <bool OGM>
 __global__ void __launch_bounds__(SNT) k_sampler(SamplerArgs a) {
+  if (a.dev_step) a.key = a.dev_step->key;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* zs = reinterpret_cast<float*>(smem);  // [H] stratified (jittered)
   float* cdf = zs + a.H;                       // [H-1]
@@ -222,6 +224,7 @@ constexpr int kSamplerWaves = 4;
 
 template <int E>
 __global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_wave(SamplerArgs a) {
+  if (a.dev_step) a.key = a.dev_step->key;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int QMAX = E / 2;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -346,7 +349,7 @@ extern "C" uint32_t lnr_step_key(uint32_t seed, uint32_t step) { return mix32(mi
 
 extern "C" int lnr_sample_ogm(const float* rays, int64_t n_rays, int32_t n_samples, const float* occ, int32_t occ_res,
                               float perturb, const float* u_jitter, const float* u_pdf, uint32_t key, int64_t ray_offset,
-                              float* z, void* stream) {
+                              float* z, const lnr_step_scalars* dev_step, void* stream) {
   LNR_REQUIRE(n_rays >= 0, "lnr_sample_ogm: n_rays < 0");
   LNR_REQUIRE(n_samples >= 8 && n_samples % 2 == 0 && n_samples <= 4096,
               "lnr_sample_ogm: n_samples=%d must be even in [8,4096]", n_samples);
@@ -356,6 +359,7 @@ extern "C" int lnr_sample_ogm(const float* rays, int64_t n_rays, int32_t n_sampl
   SamplerArgs a{};
   a.rays = rays; a.n_rays = n_rays; a.S = n_samples; a.H = n_samples / 2; a.occ = occ; a.occ_res = occ_res;
   a.perturb = perturb; a.u_jitter = u_jitter; a.u_pdf = u_pdf; a.key = key; a.ray_offset = ray_offset; a.z = z;
+  a.dev_step = dev_step;
   int p2 = 1;
   while (p2 < n_samples) p2 <<= 1;
   a.P2 = p2;
@@ -380,14 +384,15 @@ extern "C" int lnr_sample_ogm(const float* rays, int64_t n_rays, int32_t n_sampl
 }
 
 extern "C" int lnr_sample_uniform(const float* rays, int64_t n_rays, int32_t n_samples, float perturb,
-                                  const float* u_jitter, uint32_t key, int64_t ray_offset, float* z, void* stream) {
+                                  const float* u_jitter, uint32_t key, int64_t ray_offset, float* z,
+                                  const lnr_step_scalars* dev_step, void* stream) {
   LNR_REQUIRE(n_rays >= 0, "lnr_sample_uniform: n_rays < 0");
   LNR_REQUIRE(n_samples >= 2 && n_samples <= 2048, "lnr_sample_uniform: n_samples=%d not in [2,2048]", n_samples);
   if (n_rays == 0) return LNR_OK;
   LNR_REQUIRE(rays && z, "lnr_sample_uniform: null pointer");
   SamplerArgs a{};
   a.rays = rays; a.n_rays = n_rays; a.S = n_samples; a.H = n_samples; a.perturb = perturb; a.u_jitter = u_jitter;
-  a.key = key; a.ray_offset = ray_offset; a.z = z; a.P2 = 0;
+  a.key = key; a.ray_offset = ray_offset; a.z = z; a.P2 = 0; a.dev_step = dev_step;
   const int nb = (int)(n_rays < 4096 ? n_rays : 4096);
   hipLaunchKernelGGL(k_sampler<false>, dim3(nb), dim3(SNT), sampler_smem(a.H, 0), as_stream(stream), a);
   LNR_RETURN_LAUNCH("lnr_sample_uniform");

@@ -107,9 +107,9 @@ class DepthRenderer:
             rc = rays[r0:r0 + n]
             off = ray_offset + r0
             if self.sampler == "OGM":
-                L.call("lnr_sample_ogm", rc, n, self.S, st.occ, st.cfg.occ_res, 0.0, None, None, key, off, self.z, s)
+                L.call("lnr_sample_ogm", rc, n, self.S, st.occ, st.cfg.occ_res, 0.0, None, None, key, off, self.z, None, s)
             else:
-                L.call("lnr_sample_uniform", rc, n, self.S, 0.0, None, key, off, self.z, s)
+                L.call("lnr_sample_uniform", rc, n, self.S, 0.0, None, key, off, self.z, None, s)
             L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(st.desc), rc, self.z, n, self.S, st.table_f16, self.enc,
                    stride, None, 0, s)
             cw = self.color is not None and rgb is not None

@@ -28,7 +28,7 @@ class UniformRaySampler():
         n = rays.shape[0]
         z = torch.empty(n, N_samples, dtype=torch.float32, device=rays.device)
         key = R.next_key() if perturb > 0 else 0
-        L.call("lnr_sample_uniform", rays, n, N_samples, float(perturb), None, key, 0, z, L.stream(rays.device))
+        L.call("lnr_sample_uniform", rays, n, N_samples, float(perturb), None, key, 0, z, None, L.stream(rays.device))
         return z
 
 
@@ -52,5 +52,5 @@ class OccGridRaySampler():
         z = torch.empty(n, N_samples, dtype=torch.float32, device=rays.device)
         key = R.next_key()
         L.call("lnr_sample_ogm", rays, n, N_samples, occ, res, float(perturb), None, None, key, 0, z,
-               L.stream(rays.device))
+               None, L.stream(rays.device))
         return z

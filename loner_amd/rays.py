@@ -264,10 +264,11 @@ class RayWindow:
         return d
 
     def build(self, key, slot0=0, n=None, rays=None, depth=None, valid=None, point_index=None, far_ref=None,
-              given=None):
+              given=None, dev_step=None):
         """Enqueue the build of slots [slot0, slot0 + n) for the step keyed by ``key``
         (``lnr_step_key``).  Returns (rays, depth, valid, point_index, far_ref) device tensors; outputs
-        may be passed in (preallocated).  ``given``: int32 scan-local indices per slot (parity tests)."""
+        may be passed in (preallocated).  ``given``: int32 scan-local indices per slot (parity tests).
+        ``dev_step``: a device ``lnr_step_scalars`` whose key is used instead of ``key`` (graph replay)."""
         L = self._L
         n = self.n_slots - slot0 if n is None else n
         dev = self.device
@@ -276,6 +277,10 @@ class RayWindow:
         valid = torch.empty(n, dtype=torch.uint8, device=dev) if valid is None else valid
         far_ref = torch.empty(1, dtype=torch.float32, device=dev) if far_ref is None else far_ref
         sel = L.SELECT["GIVEN"] if given is not None else L.SELECT[self.strategy]
-        L.call("lnr_build_lidar_rays", L.ctypes.byref(self.desc), sel, given, int(key) & 0xFFFFFFFF, slot0, n, rays,
+        desc = self.desc
+        if dev_step is not None:
+            desc = L.RayWindowDesc.from_buffer_copy(self.desc)
+            desc.dev_step = dev_step.data_ptr()
+        L.call("lnr_build_lidar_rays", L.ctypes.byref(desc), sel, given, int(key) & 0xFFFFFFFF, slot0, n, rays,
                depth, valid, point_index, far_ref, L.stream(dev))
         return rays, depth, valid, point_index, far_ref

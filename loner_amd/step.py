@@ -222,6 +222,7 @@ class StepEngine:
             if len(self.zero_chunks) > L.ADAM_MAX_RANGES:
                 raise ValueError(f"{len(self.zero_chunks)} level ranges: at most {L.ADAM_MAX_RANGES} (one Adam launch)")
             self.zero_grad = [torch.empty(c, dtype=torch.float32, device=dev) for _, _, c in self.zero_chunks]
+        self._pending_shadow = []  # async all-gather works of the last sharded step (finish())
         self.z = torch.empty(n_rays, self.S, dtype=torch.float32, device=dev)
         self.enc = torch.empty(self.cfg.n_levels, self.N, dtype=torch.int32, device=dev)
         self.ws = torch.empty(L.lib().lnr_field_train_workspace_words(n_rays, self.S), dtype=torch.float32, device=dev)
@@ -277,6 +278,16 @@ class StepEngine:
         if self.pipe_at not in ("start", "encode", "field"):
             raise ValueError(f"LONER_PIPE_AT={self.pipe_at!r}: expected start, encode or field")
         self._pp_mid = torch.cuda.Event()
+        # step_window on all-valid windows, single process: the whole step (ray build, sampling, encode,
+        # field, backward, Adam, and the OGM update on its steps) captured once per (window, OGM or not)
+        # in a HIP graph and replayed, its per-step scalars (key, loss scalars, Adam coefficients) set in
+        # device memory by one small launch before each replay (``lnr_step_scalars``): one graph launch
+        # in place of ~18 kernel launches (LONER_GRAPH=0 turns it off; the pipelined path then runs)
+        self.use_graph = os.environ.get("LONER_GRAPH", "1") != "0"
+        self.dev_step = torch.zeros(8, dtype=torch.int32, device=dev)  # lnr_step_scalars (32 B)
+        self._dev_step = None
+        self._graphs, self._graph_window = {}, None
+        self._graph_pool = None
         self._pp_bufs = [dict(rays=self.rays if i == 0 else torch.empty_like(self.rays),
                               dgt=self.depth_gt if i == 0 else torch.empty_like(self.depth_gt),
                               valid=self.ray_valid if i == 0 else torch.empty_like(self.ray_valid),
@@ -332,6 +343,7 @@ class StepEngine:
     def sync_master(self):
         """Sharded optimiser: all-gather the fp32 master (and the Adam moments) chunks so every rank holds
         the whole current state (e.g. before a checkpoint).  A no-op otherwise."""
+        self.finish()
         if self.zero is None or self.zero[1] == 1 or self.all_gather is None:
             return
         st, (zr, zw) = self.state, self.zero
@@ -358,11 +370,13 @@ class StepEngine:
             prof.setdefault(stage, []).append(ev)
 
     def step(self, rays, depth_gt, global_step, iteration_idx=0, scale=1.0, far_ref=None, n_rays_global=None,
-             u_jitter=None, u_pdf=None, noise=None, update_ogm=None, prof=None, presampled=False):
+             u_jitter=None, u_pdf=None, noise=None, update_ogm=None, prof=None, presampled=False, dev_step=None):
         """rays (R,13) fp32, depth_gt (R,) fp32 normalised, both on this GPU, R <= the engine's
         capacity.  Returns the device loss buffer [loss, mean_eps, depth_term, los_term, opacity_term,
         n_opaque] (no host sync).  ``far_ref``: the far bound of global ray 0, a float or a 1-element
-        device tensor.  ``prof``: optional dict collecting (begin, end) HIP event pairs per stage."""
+        device tensor.  ``prof``: optional dict collecting (begin, end) HIP event pairs per stage.
+        ``dev_step``: a device ``lnr_step_scalars`` holding this step's key, loss scalars and Adam
+        coefficients, read by the kernels instead of their host arguments (the graph-captured step)."""
         st = self.state
         cfg = self.cfg
         R, S, N = rays.shape[0], self.S, self.N  # N: the level stride of enc / d_enc (capacity)
@@ -386,17 +400,22 @@ class StepEngine:
             pending = self._allreduce_async(self.n_opaque) if self.allreduce is not None else None
             self._join.record(self._side)
         lp = self.loss_params(global_step, iteration_idx, scale, far_h, n_glob, dev_far)
+        dsp = None if dev_step is None else dev_step.data_ptr()
+        lp.dev_step = dsp
+        self._dev_step = dsp
         # 2. sampling (``presampled``: step_window's pipeline already drew self.z for these rays)
         m(prof, "sample")
         if presampled:
             pass
         elif cfg.sampler == "OGM":
             L.call("lnr_sample_ogm", rays, R, S, st.occ, cfg.occ_res, cfg.perturb, u_jitter, u_pdf, key,
-                   self.ray_offset, self.z, s)
+                   self.ray_offset, self.z, dsp, s)
         else:
-            L.call("lnr_sample_uniform", rays, R, S, cfg.perturb, u_jitter, key, self.ray_offset, self.z, s)
+            L.call("lnr_sample_uniform", rays, R, S, cfg.perturb, u_jitter, key, self.ray_offset, self.z, dsp, s)
         m(prof, "sample")
-        # 3. encode (+ backward record histogram)
+        # 3. encode (+ backward record histogram); it reads the fp16 shadow, which the previous step's
+        # sharded-optimiser all-gathers may still be writing
+        self.finish()
         m(prof, "encode")
         if self.count_in_forward:  # the backward's record histogram, counted from the forward's corners
             L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(st.desc), rays, self.z, R, S, st.table_f16, self.enc, N,
@@ -449,7 +468,7 @@ class StepEngine:
         st.adam_step += 1
         m(prof, "adam")
         L.call("lnr_adam_step", st.params, st.shadow, st.grad, st.m, st.v, st.n_padded, st.adam_step,
-               cfg.lr * self.lr_factor, 0.9, 0.999, 1e-8, s)
+               cfg.lr * self.lr_factor, 0.9, 0.999, 1e-8, dsp, s)
         m(prof, "adam")
         # 8. OGM every N_iters_acc global steps (optimizer.py:466-469)
         if update_ogm is None:
@@ -461,48 +480,52 @@ class StepEngine:
         return self.loss_out
 
     def _step_zero(self, rays, depth_gt, R, S, N, flags, s, scale, update_ogm, global_step, prof):
-        """The step's tail with the sharded optimiser (see __init__): per level range, accumulate, then
-        reduce-scatter the range's gradient (asynchronous: the next range accumulates meanwhile); Adam on
-        this rank's chunk of every range; all-gather the fp16 shadow chunks."""
+        """The step's tail with the sharded optimiser (see __init__), pipelined per level range: each range
+        is accumulated and its gradient slice reduce-scattered (asynchronous: the next range accumulates
+        meanwhile); then, range by range as its reduce-scatter lands, Adam on this rank's chunk of it and
+        the all-gather of that chunk's fp16 shadow (asynchronous).  Nothing waits for the all-gathers here:
+        the next reader of the shadow (the next step's encode, after its ray build and sampling, or
+        finish()) does, so the gather overlaps the next step's head.  Exposed per step: the last range's
+        reduce-scatter and its Adam."""
         st, cfg, m = self.state, self.cfg, self._mark
         zr, zw = self.zero
         comm = self.allreduce is not None and zw > 1
+        rs = [None] * len(self.zero_chunks)
         if comm:
             self._grid_bwd(rays, R, S, N, flags | L.BWD_NO_ACCUM, s)
-            pending = []
-            for (l0, l1), (a0, a1, c), out in zip(self.ar_groups, self.zero_chunks, self.zero_grad):
+            for i, ((l0, l1), (a0, a1, c), out) in enumerate(zip(self.ar_groups, self.zero_chunks, self.zero_grad)):
                 L.call("lnr_hashgrid_bwd_accum", L.ctypes.byref(st.desc), R * S, self.bwd_ws, self.bwd_ws_bytes, l0,
                        l1, st.grad_table, s)
-                pending.append(self.reduce_scatter(out, st.grad[a0:a1], async_op=True))
+                rs[i] = self.reduce_scatter(out, st.grad[a0:a1], async_op=True)
             m(prof, "grid_bwd")
-            m(prof, "allreduce")
-            for w in pending:
-                if w is not None:
-                    w.wait()
-            m(prof, "allreduce")
         else:  # one process: this rank's share of the work only (no exchange)
             self._grid_bwd(rays, R, S, N, flags, s)
             m(prof, "grid_bwd")
         st.adam_step += 1
         m(prof, "adam")
-        # this rank's chunk of every level range, one launch (lnr_adam_step_ranges)
-        rng = (L.AdamRange * len(self.zero_chunks))()
-        for i, ((a0, a1, c), g) in enumerate(zip(self.zero_chunks, self.zero_grad)):
-            o = a0 + zr * c
-            grad = g if comm else st.grad[o:o + c]
-            rng[i] = L.AdamRange(L.ptr(st.params[o:o + c]), L.ptr(st.shadow[o:o + c]), L.ptr(grad),
-                                 L.ptr(st.m[o:o + c]), L.ptr(st.v[o:o + c]), c)
-        L.call("lnr_adam_step_ranges", rng, len(self.zero_chunks), st.adam_step, cfg.lr * self.lr_factor, 0.9, 0.999,
-               1e-8, s)
+        lr = cfg.lr * self.lr_factor
+        if not comm:
+            # this rank's chunk of every level range, one launch (lnr_adam_step_ranges)
+            rng = (L.AdamRange * len(self.zero_chunks))()
+            for i, (a0, a1, c) in enumerate(self.zero_chunks):
+                o = a0 + zr * c
+                rng[i] = L.AdamRange(L.ptr(st.params[o:o + c]), L.ptr(st.shadow[o:o + c]), L.ptr(st.grad[o:o + c]),
+                                     L.ptr(st.m[o:o + c]), L.ptr(st.v[o:o + c]), c)
+            L.call("lnr_adam_step_ranges", rng, len(self.zero_chunks), st.adam_step, lr, 0.9, 0.999, 1e-8,
+                   self._dev_step, s)
+        else:
+            pend = []
+            for i, ((a0, a1, c), g) in enumerate(zip(self.zero_chunks, self.zero_grad)):
+                if rs[i] is not None:
+                    rs[i].wait()  # orders the current stream after this range's reduce-scatter
+                o = a0 + zr * c
+                L.call("lnr_adam_step", st.params[o:o + c], st.shadow[o:o + c], g, st.m[o:o + c], st.v[o:o + c], c,
+                       st.adam_step, lr, 0.9, 0.999, 1e-8, self._dev_step, s)
+                pend.append(self.all_gather(st.shadow[a0:a1], st.shadow[o:o + c], async_op=True))
+            self._pending_shadow = [w for w in pend if w is not None]
+            if prof is not None:
+                self.finish()  # a profiled step keeps its stages apart
         m(prof, "adam")
-        if comm:
-            m(prof, "allgather")
-            pending = [self.all_gather(st.shadow[a0:a1], st.shadow[a0 + zr * c:a0 + (zr + 1) * c], async_op=True)
-                       for a0, a1, c in self.zero_chunks]
-            for w in pending:
-                if w is not None:
-                    w.wait()
-            m(prof, "allgather")
         if update_ogm is None:
             update_ogm = (global_step % cfg.n_iters_acc == 0)
         if update_ogm:
@@ -510,6 +533,14 @@ class StepEngine:
             self.ogm_update(rays, depth_gt, scale)
             m(prof, "ogm")
         return self.loss_out
+
+    def finish(self):
+        """Order the current stream after the sharded optimiser's pending shadow all-gathers (the shadow is
+        then whole again).  step() calls it before its encode; call it before reading the fp16 parameters
+        elsewhere (checkpoints, evaluation on the same FieldState).  A no-op without pending gathers."""
+        pend, self._pending_shadow = self._pending_shadow, []
+        for w in pend:
+            w.wait()
 
     def d_sigma(self, n_rays=None):
         """dL/dsigma (n_rays * S) of the last step: lnr_field_train leaves it in its workspace after the dW
@@ -593,6 +624,9 @@ class StepEngine:
     def _step_window_pipelined(self, window, global_step, iteration_idx, n, n_rays_global, prof, kw):
         """step_window for windows with no invalid rays (fixed batch size, no host sync), with step
         k + 1's build + sampling prefetched (``pipeline``)."""
+        if (self.use_graph and prof is None and self.allreduce is None and not
+                any(k in kw for k in ("u_jitter", "u_pdf", "noise", "presampled"))):
+            return self._step_window_graph(window, global_step, iteration_idx, n, n_rays_global, kw)
         m = self._mark
         main = torch.cuda.current_stream(self.state.device)
         want = (global_step, n, self.ray_offset)
@@ -636,10 +670,10 @@ class StepEngine:
                 s = L.stream(self.state.device)
                 if cfg.sampler == "OGM":
                     L.call("lnr_sample_ogm", bq["rays"][:n], n, self.S, self.state.occ, cfg.occ_res, cfg.perturb, None,
-                           None, key, self.ray_offset, bq["z"], s)
+                           None, key, self.ray_offset, bq["z"], None, s)
                 else:
                     L.call("lnr_sample_uniform", bq["rays"][:n], n, self.S, cfg.perturb, None, key, self.ray_offset,
-                           bq["z"], s)
+                           bq["z"], None, s)
             done = torch.cuda.Event()
             done.record(self._pp_stream)
         self._pp = dict(window=window, want=(global_step + 1, n, self.ray_offset), parity=q, sampled=sample, done=done)
@@ -653,6 +687,67 @@ class StepEngine:
             if pend is not None:
                 main.wait_event(pend["done"])
         self._pp = self._pf = None
+        self.finish()
+
+    def step_scalars(self, global_step, iteration_idx=0, adam_step=None):
+        """The host ``lnr_step_scalars`` of a step: the values the eager step passes as kernel arguments
+        (the same host arithmetic), for a captured step to read from device memory."""
+        st, cfg = self.state, self.cfg
+        sc = L.StepScalars()
+        sc.key = L.step_key(self.seed, global_step)
+        sc.los_lambda = float(cfg.loss.los_lambda_at(global_step))
+        sc.los_eps = float(cfg.loss.los_eps_at(iteration_idx))
+        t = st.adam_step + 1 if adam_step is None else adam_step
+        a, b = L.ctypes.c_float(), L.ctypes.c_float()
+        L.check(L.lib().lnr_adam_coefficients(t, cfg.lr * self.lr_factor, 0.9, 0.999, L.ctypes.byref(a),
+                                              L.ctypes.byref(b)), "lnr_adam_coefficients")
+        sc.adam_step_size, sc.adam_bc2_sqrt = a.value, b.value
+        return sc
+
+    def _step_window_graph(self, window, global_step, iteration_idx, n, n_rays_global, kw):
+        """step_window as a replayed HIP graph (see __init__).  The first step of each (window, batch, OGM
+        or not) runs eagerly with the device scalars (so every kernel is loaded and the result is the
+        step's own), and is then captured without executing; later steps set their scalars and replay.
+        Bitwise the eager step (tests/test_gpu_step.py::test_graph_replay_equals_eager)."""
+        st, cfg = self.state, self.cfg
+        self.drop_prefetch()
+        ogm = kw.get("update_ogm")
+        if ogm is None:
+            ogm = global_step % cfg.n_iters_acc == 0
+        n_glob = window.n_slots if n_rays_global is None else n_rays_global
+        if self._graph_window is not window:  # a new window: its tensors back the captured pointers
+            self._graphs.clear()
+            self._graph_window = window
+        gkey = (n, self.ray_offset, n_glob, bool(ogm), self.zero)
+        s = L.stream(st.device)
+        sc = self.step_scalars(global_step, iteration_idx)
+        L.call("lnr_step_scalars_set", L.ctypes.byref(sc), self.dev_step, s)
+        b = self._pp_bufs[0]
+        self._pp_parity = 0
+        self.z, self.rays, self.depth_gt, self.ray_valid, self.far_ref = b["z"], b["rays"], b["dgt"], b["valid"], b["far"]
+
+        def body():
+            window.build(sc.key, self.ray_offset, n, b["rays"][:n], b["dgt"][:n], b["valid"][:n], None, b["far"],
+                         dev_step=self.dev_step)
+            return self.step(b["rays"][:n], b["dgt"][:n], global_step, iteration_idx, scale=window.scale,
+                             far_ref=b["far"], n_rays_global=n_glob, update_ogm=ogm, dev_step=self.dev_step)
+
+        g = self._graphs.get(gkey)
+        if g is not None:
+            g.replay()
+            st.adam_step += 1
+            self._r_last = n
+            return self.loss_out
+        out = body()  # this step, eagerly
+        saved = st.adam_step
+        g = torch.cuda.CUDAGraph()
+        if self._graph_pool is None:
+            self._graph_pool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(g, pool=self._graph_pool):
+            body()  # recorded, not executed
+        st.adam_step = saved
+        self._graphs[gkey] = g
+        return out
 
     def _build_compact(self, window, global_step, n, n_rays_global, parity, stream):
         """Build slots [ray_offset, ray_offset + n) of ``window`` for ``global_step`` into ray buffer

@@ -21,14 +21,14 @@ def test_empty_batches_are_noops(L):
     s = L.stream()
     z = torch.empty(0, dtype=torch.float32, device="cuda")
     d = L.grid_desc()
-    assert L.lib().lnr_sample_ogm(None, 0, 512, None, 100, 1.0, None, None, 0, 0, None, s) == 0
+    assert L.lib().lnr_sample_ogm(None, 0, 512, None, 100, 1.0, None, None, 0, 0, None, None, s) == 0
     assert L.lib().lnr_hashgrid_fwd_rays(L.ctypes.byref(d), None, None, 0, 512, None, None, 0, None, 0, s) == 0
     assert L.lib().lnr_hashgrid_bwd_rays(L.ctypes.byref(d), None, None, 0, 512, None, 0, None, None, None, None, 0, 0,
                                         s) == 0
     assert L.lib().lnr_field_render(None, None, 0, None, None, 0, 512, 0, 1.0, None, 0, 0, None, None, None, None,
                                     s) == 0
     assert L.lib().lnr_rgb_render(None, 4, None, 0, None, None, 0, 512, None, s) == 0
-    assert L.lib().lnr_adam_step(None, None, None, None, None, 0, 1, 0.01, 0.9, 0.999, 1e-8, s) == 0
+    assert L.lib().lnr_adam_step(None, None, None, None, None, 0, 1, 0.01, 0.9, 0.999, 1e-8, None, s) == 0
     L.call("lnr_count_opaque", z, 0, 1.0, None, torch.zeros(1, device="cuda"), s)
     torch.cuda.synchronize()
 
@@ -72,7 +72,7 @@ def test_unsupported_sizes_raise(L):
     with pytest.raises(RuntimeError, match="n_hidden_layers"):
         L.call("lnr_rgb_render", None, 6, None, 0, rays, None, 4, 128, None, s)
     with pytest.raises(RuntimeError, match="n_samples"):
-        L.call("lnr_sample_ogm", rays, 4, 7, torch.zeros(8, device="cuda"), 2, 1.0, None, None, 0, 0, zz, s)
+        L.call("lnr_sample_ogm", rays, 4, 7, torch.zeros(8, device="cuda"), 2, 1.0, None, None, 0, 0, zz, None, s)
     from loner_amd import rendering
     with pytest.raises(ValueError, match="render strategy"):
         from loner_amd import evaluate as E

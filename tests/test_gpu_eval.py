@@ -77,7 +77,7 @@ def test_depth_renderer_vs_oracle(L, strategy):
     for r0 in range(0, rn.shape[0], 64):  # re-render chunk by chunk to read each chunk's z
         n = min(64, rn.shape[0] - r0)
         L.call("lnr_sample_ogm", rays[r0:r0 + n], n, 2048, st.occ, 100, 0.0, None, None, key, r0, rend.z,
-               L.stream(st.device))
+               None, L.stream(st.device))
         zs.append(host(rend.z[:n]).copy())
     z = np.concatenate(zs)
     dz = np.abs(z - z_ref)

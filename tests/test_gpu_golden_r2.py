@@ -124,7 +124,7 @@ def test_adam_with_tcnn_fp16_gradients_golden(L):
     sh = torch.empty(n, dtype=torch.float16, device="cuda")
     for k in range(g["grad_f16"].shape[0]):
         L.call("lnr_adam_step", tp, sh, cu(g["grad_f16"][k]), tm, tv, n, k + 1, float(g["lr"]), 0.9, 0.999, 1e-8,
-               L.stream())
+               None, L.stream())
         np.testing.assert_allclose(host(tp), g["params_fp32"][k], rtol=2e-6, atol=1e-8)
     np.testing.assert_allclose(host(tv), g["exp_avg_sq_fp32"], rtol=1e-6, atol=1e-30)
 
@@ -155,12 +155,12 @@ def test_adam_ranges_match_single_launches(L):
     for step in (1, 2):
         for k, (o, e) in enumerate(cuts):
             L.call("lnr_adam_step", a[0][o:e], sh[0][o:e] if k else None, gd[o:e], m[0][o:e], v[0][o:e], e - o, step,
-                   1e-3, 0.9, 0.999, 1e-8, L.stream())
+                   1e-3, 0.9, 0.999, 1e-8, None, L.stream())
         rng = (L.AdamRange * len(cuts))()
         for k, (o, e) in enumerate(cuts):
             rng[k] = L.AdamRange(L.ptr(a[1][o:e]), L.ptr(sh[1][o:e]) if k else None, L.ptr(gd[o:e]), L.ptr(m[1][o:e]),
                                  L.ptr(v[1][o:e]), e - o)
-        L.call("lnr_adam_step_ranges", rng, len(cuts), step, 1e-3, 0.9, 0.999, 1e-8, L.stream())
+        L.call("lnr_adam_step_ranges", rng, len(cuts), step, 1e-3, 0.9, 0.999, 1e-8, None, L.stream())
     torch.cuda.synchronize()
     for x, y in ((a[0], a[1]), (m[0], m[1]), (v[0], v[1]), (sh[0], sh[1])):
         assert torch.equal(x, y)

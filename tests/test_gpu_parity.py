@@ -263,7 +263,7 @@ def test_ogm_sampler_golden(L):
     R = rays.shape[0]
     z = torch.empty(R, 512, dtype=torch.float32, device="cuda")
     L.call("lnr_sample_ogm", (cu(rays)), R, 512, (cu(occ)), 100, 1.0, (cu(g["u_jitter"])),
-           (cu(g["u_pdf"])), 0, 0, (z), L.stream())
+           (cu(g["u_pdf"])), 0, 0, (z), None, L.stream())
     got = host(z)
     assert np.all(np.diff(got, axis=1) >= 0)
     np.testing.assert_allclose(got, g["z_ogm"], rtol=1e-5, atol=5e-6)
@@ -275,7 +275,7 @@ def test_uniform_sampler_golden(L):
     R = rays.shape[0]
     z = torch.empty(R, 64, dtype=torch.float32, device="cuda")
     L.call("lnr_sample_uniform", (cu(rays)), R, 64, 1.0, (cu(g["u_jitter_uniform"])), 0, 0, (z),
-           L.stream())
+           None, L.stream())
     np.testing.assert_allclose(host(z), g["z_uniform"], rtol=1e-6, atol=1e-7)
 
 
@@ -286,7 +286,7 @@ def test_ogm_sampler_inkernel_rng_matches_oracle(L):
     key, off = orng.step_key(7, 3), 1000
     z = torch.empty(R, 512, dtype=torch.float32, device="cuda")
     L.call("lnr_sample_ogm", (cu(rays)), R, 512, (cu(occ)), 100, 1.0, None, None, key, off, (z),
-           L.stream())
+           None, L.stream())
     a, b = orng.ray_sample_grid(np.arange(off, off + R), 256)
     uj = orng.uniform(key, orng.STREAM_JITTER, a, b)
     up = orng.uniform(key, orng.STREAM_PDF, a, b)
@@ -400,7 +400,7 @@ def test_adam_matches_torch_semantics(L):
         grad = rng.normal(0, 1e-3, n).astype(np.float32)
         ooptim.adam_step(p, grad, m, v, step, 0.01)
         L.call("lnr_adam_step", (tp), (sh), (cu(np.pad(grad, (0, 1)))), (tm), (tv), n, step,
-               0.01, 0.9, 0.999, 1e-8, L.stream())
+               0.01, 0.9, 0.999, 1e-8, None, L.stream())
     np.testing.assert_allclose(host(tp)[:n], p, rtol=1e-6, atol=1e-7)
     np.testing.assert_array_equal(host(sh)[:n], host(tp)[:n].astype(np.float16))
     # torch.optim.Adam itself on the same data (CPU reference semantics)
@@ -414,7 +414,7 @@ def test_adam_matches_torch_semantics(L):
         q.grad = torch.from_numpy(gr)
         opt.step()
         L.call("lnr_adam_step", (tq), None, (cu(gr)), (tm2), (tv2), 64, step, 0.01, 0.9, 0.999,
-               1e-8, L.stream())
+               1e-8, None, L.stream())
     np.testing.assert_allclose(host(tq), q.detach().numpy(), rtol=1e-6, atol=1e-7)
 
 

@@ -242,3 +242,40 @@ def test_prefetch_across_windows_equals_plain(L, all_valid):
         np.testing.assert_array_equal(a, b)
     np.testing.assert_array_equal(res[0][1], res[1][1])
     np.testing.assert_array_equal(res[0][2], res[1][2])
+
+
+@pytest.mark.parametrize("zero", [None, (1, 4)])
+def test_graph_replay_equals_eager(L, zero):
+    """step_window as a replayed HIP graph (per-step key, decaying los_lambda, los_eps, Adam coefficients
+    and the ExponentialLR factor read from device memory, set by one launch per step) gives bitwise the
+    eager path's losses, parameters, moments, occupancy grid and samples, across OGM steps (their own
+    graph), a skipped global step, a changed iteration index / learning-rate factor and a second window
+    (the graphs are re-captured); also with the sharded optimiser's one-rank share (bench --shard-of)."""
+    from loner_amd import step as S_
+    from loner_amd.rays import RayWindow
+    loss = S_.LossConfig.from_dict(dict(loss_selection="L1_LOS", decay_los_lambda=True, los_lambda=1000.0,
+                                        los_lambda_decay_rate=1e-4, los_lambda_decay_steps=30))
+    res = []
+    for graph in (False, True):
+        st = S_.FieldState(S_.StepConfig(n_samples=64, occ_lr=1e-3, loss=loss), device="cuda:0", table_init=0.5)
+        eng = None
+        outs = []
+        for seed, steps in ((8, (8, 9, 10, 11, 12, 14, 15, 20, 21)), (9, (22, 23, 30, 31))):
+            scans, wc, rr = _window("forest", 2, seed=seed)
+            win = RayWindow(scans, wc, rr, n_lidar=128, n_sky=16, strategy="MASK")
+            if eng is None:
+                eng = S_.StepEngine(st, win.n_slots, seed=4, zero=zero)
+                eng.use_graph = graph
+            st.reset_optimizer()
+            for it, g in enumerate(steps):
+                eng.lr_factor = 0.97 ** it
+                outs.append(host(eng.step_window(win, global_step=g, iteration_idx=it)).copy())
+            if graph:
+                assert len(eng._graphs) == 2  # the OGM and the plain step of this window
+        torch.cuda.synchronize()
+        res.append((outs, host(st.params).copy(), host(st.m).copy(), host(st.v).copy(), host(st.occ).copy(),
+                    host(eng.z).copy(), st.adam_step))
+    for a, b in zip(res[0][0], res[1][0]):
+        np.testing.assert_array_equal(a, b)
+    for a, b in zip(res[0][1:], res[1][1:]):
+        np.testing.assert_array_equal(a, b)

@@ -75,7 +75,7 @@ def main():
 
         def sample():
             L.call("lnr_sample_ogm", e.rays, R, S, st.occ, cfg.occ_res, cfg.perturb, None, None, L.step_key(e.seed, 5),
-                   e.ray_offset, e.z, L.stream(dev))
+                   e.ray_offset, e.z, None, L.stream(dev))
 
         def restore():
             hist.copy_(snap)
