@@ -82,9 +82,10 @@ typedef struct lnr_step_scalars {
   float adam_bc2_sqrt;
   uint32_t pad[3];
 } lnr_step_scalars;
-/* *dev = *value (value: a HOST struct, carried as the kernel's argument), enqueued on `stream`: the
- * launch before a captured step's replay sets that step's scalars in stream order. */
-int lnr_step_scalars_set(const lnr_step_scalars* value, lnr_step_scalars* dev, void* stream);
+/* dev[0..n) = values[0..n) (n <= 4 HOST structs, carried as the kernel's argument), enqueued on `stream`:
+ * the launch before a captured step's replay sets that step's scalars (and the next step's, for its
+ * prefetched ray build and sampling) in stream order. */
+int lnr_step_scalars_set(const lnr_step_scalars* values, int32_t n, lnr_step_scalars* dev, void* stream);
 /* Host: the fp32 Adam coefficients lnr_adam_step forms for 1-based step t and learning rate lr. */
 int lnr_adam_coefficients(int32_t step, double lr, double beta1, double beta2, float* step_size, float* bc2_sqrt);
 

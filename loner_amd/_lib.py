@@ -166,7 +166,7 @@ _SIGNATURES = {
                                             c_p, c_p, c_p, c_p]),
     "lnr_adam_step": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i32, c_d, c_d, c_d, c_d, c_p, c_p]),
     "lnr_adam_step_ranges": (ctypes.c_int, [c_p, c_i32, c_i32, c_d, c_d, c_d, c_d, c_p, c_p]),
-    "lnr_step_scalars_set": (ctypes.c_int, [ctypes.POINTER(StepScalars), c_p, c_p]),
+    "lnr_step_scalars_set": (ctypes.c_int, [c_p, c_i32, c_p, c_p]),
     "lnr_adam_coefficients": (ctypes.c_int, [c_i32, c_d, c_d, c_d, ctypes.POINTER(c_f), ctypes.POINTER(c_f)]),
     "lnr_ogm_workspace_words": (c_i64, [c_i32]),
     "lnr_ogm_update": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i32, c_f, c_f, c_p, c_p, c_i64, c_i32, c_p]),

@@ -282,13 +282,18 @@ static unsigned grid1d(int64_t n, int64_t cap = 1 << 20) {
 
 using namespace lnr;
 
-__global__ void k_step_scalars_set(lnr_step_scalars value, lnr_step_scalars* __restrict__ out) {
-  if (threadIdx.x == 0) *out = value;
+struct StepScalarsArg {
+  lnr_step_scalars v[4];
+};
+__global__ void k_step_scalars_set(StepScalarsArg values, int32_t n, lnr_step_scalars* __restrict__ out) {
+  if (threadIdx.x < (uint32_t)n) out[threadIdx.x] = values.v[threadIdx.x];
 }
 
-extern "C" int lnr_step_scalars_set(const lnr_step_scalars* value, lnr_step_scalars* dev, void* stream) {
-  LNR_REQUIRE(value && dev, "lnr_step_scalars_set: null pointer");
-  hipLaunchKernelGGL(k_step_scalars_set, dim3(1), dim3(64), 0, as_stream(stream), *value, dev);
+extern "C" int lnr_step_scalars_set(const lnr_step_scalars* values, int32_t n, lnr_step_scalars* dev, void* stream) {
+  LNR_REQUIRE(values && dev && n >= 1 && n <= 4, "lnr_step_scalars_set: bad arguments (n=%d, at most 4)", n);
+  StepScalarsArg arg{};
+  for (int i = 0; i < n; ++i) arg.v[i] = values[i];
+  hipLaunchKernelGGL(k_step_scalars_set, dim3(1), dim3(64), 0, as_stream(stream), arg, n, dev);
   LNR_RETURN_LAUNCH("lnr_step_scalars_set");
 }
 

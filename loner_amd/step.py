@@ -284,10 +284,15 @@ class StepEngine:
         # device memory by one small launch before each replay (``lnr_step_scalars``): one graph launch
         # in place of ~18 kernel launches (LONER_GRAPH=0 turns it off; the pipelined path then runs)
         self.use_graph = os.environ.get("LONER_GRAPH", "1") != "0"
-        self.dev_step = torch.zeros(8, dtype=torch.int32, device=dev)  # lnr_step_scalars (32 B)
+        # two lnr_step_scalars (32 B each): this step's, and the next step's (its prefetched build + sampling)
+        self._dev_steps = torch.zeros(16, dtype=torch.int32, device=dev)
+        self.dev_step, self.dev_step_next = self._dev_steps[:8], self._dev_steps[8:]
         self._dev_step = None
         self._graphs, self._graph_window = {}, None
         self._graph_pool = None
+        self._gpp = None  # what the last graph step prefetched for the next: window, want, parity, have
+        self._capture_stream = torch.cuda.Stream(device=dev)
+        self._gfork, self._gjoin = torch.cuda.Event(), torch.cuda.Event()
         self._pp_bufs = [dict(rays=self.rays if i == 0 else torch.empty_like(self.rays),
                               dgt=self.depth_gt if i == 0 else torch.empty_like(self.depth_gt),
                               valid=self.ray_valid if i == 0 else torch.empty_like(self.ray_valid),
@@ -599,6 +604,7 @@ class StepEngine:
         # Windows with rays the 1 m filter drops: the batch size must reach the host (one sync per step).
         # The build and compaction of step k + 1 run on a side stream while step k runs, so that sync
         # never waits for the main stream: the host stays a step ahead of the GPU (double-buffered).
+        self._gpp = None
         main = torch.cuda.current_stream(self.state.device)
         want = (global_step, n, self.ray_offset, n_rays_global)
         pf, self._pf = self._pf, None
@@ -628,6 +634,7 @@ class StepEngine:
                 any(k in kw for k in ("u_jitter", "u_pdf", "noise", "presampled"))):
             return self._step_window_graph(window, global_step, iteration_idx, n, n_rays_global, kw)
         m = self._mark
+        self._gpp = None  # (the eager path neither uses nor keeps the graph path's prefetched buffers)
         main = torch.cuda.current_stream(self.state.device)
         want = (global_step, n, self.ray_offset)
         pp, self._pp = self._pp, None
@@ -686,7 +693,7 @@ class StepEngine:
         for pend in (self._pp, self._pf):
             if pend is not None:
                 main.wait_event(pend["done"])
-        self._pp = self._pf = None
+        self._pp = self._pf = self._gpp = None
         self.finish()
 
     def step_scalars(self, global_step, iteration_idx=0, adam_step=None):
@@ -705,32 +712,71 @@ class StepEngine:
         return sc
 
     def _step_window_graph(self, window, global_step, iteration_idx, n, n_rays_global, kw):
-        """step_window as a replayed HIP graph (see __init__).  The first step of each (window, batch, OGM
-        or not) runs eagerly with the device scalars (so every kernel is loaded and the result is the
-        step's own), and is then captured without executing; later steps set their scalars and replay.
-        Bitwise the eager step (tests/test_gpu_step.py::test_graph_replay_equals_eager)."""
+        """step_window as a replayed HIP graph (see __init__), with the pipelined path's prefetch inside it:
+        a second branch, forked at the graph's start and joined at its end, builds step k + 1's rays (and
+        samples them, unless step k updates the OGM the sampler reads) into the other buffers, keyed by
+        the next step's scalars.  Graphs are captured per (buffer parity, what the previous step
+        prefetched, OGM step or not, batch) and per window: the first step of each runs eagerly with the
+        device scalars (every kernel loaded; the step's own result) and is then captured without
+        executing; later steps set their scalars (one small launch) and replay.  Bitwise the eager path
+        (tests/test_gpu_rays.py::test_graph_replay_equals_eager)."""
         st, cfg = self.state, self.cfg
-        self.drop_prefetch()
+        if self._pp is not None or self._pf is not None:
+            self.drop_prefetch()
+        self.finish()
         ogm = kw.get("update_ogm")
         if ogm is None:
             ogm = global_step % cfg.n_iters_acc == 0
+        ogm = bool(ogm)
         n_glob = window.n_slots if n_rays_global is None else n_rays_global
         if self._graph_window is not window:  # a new window: its tensors back the captured pointers
             self._graphs.clear()
             self._graph_window = window
-        gkey = (n, self.ray_offset, n_glob, bool(ogm), self.zero)
+        gp = self._gpp
+        if gp is not None and gp["window"] is window and gp["want"] == (global_step, n, self.ray_offset):
+            p, have = gp["parity"], gp["have"]
+        else:
+            p, have = self._pp_parity, 0
+        prefetch = self.pipeline
+        sample_next = prefetch and (cfg.sampler != "OGM" or not ogm)  # the OGM sampler reads the grid step k updates
+        gkey = (p, have, ogm, prefetch, n, self.ray_offset, n_glob, self.zero)
         s = L.stream(st.device)
-        sc = self.step_scalars(global_step, iteration_idx)
-        L.call("lnr_step_scalars_set", L.ctypes.byref(sc), self.dev_step, s)
-        b = self._pp_bufs[0]
-        self._pp_parity = 0
+        sc = (L.StepScalars * 2)()
+        sc[0] = self.step_scalars(global_step, iteration_idx)
+        sc[1].key = L.step_key(self.seed, global_step + 1)
+        L.call("lnr_step_scalars_set", sc, 2, self._dev_steps, s)
+        b, bq = self._pp_bufs[p], self._pp_bufs[1 - p]
+        self._pp_parity = p
         self.z, self.rays, self.depth_gt, self.ray_valid, self.far_ref = b["z"], b["rays"], b["dgt"], b["valid"], b["far"]
+        self._gpp = (dict(window=window, want=(global_step + 1, n, self.ray_offset), parity=1 - p,
+                          have=2 if sample_next else 1) if prefetch else None)
 
         def body():
-            window.build(sc.key, self.ray_offset, n, b["rays"][:n], b["dgt"][:n], b["valid"][:n], None, b["far"],
-                         dev_step=self.dev_step)
-            return self.step(b["rays"][:n], b["dgt"][:n], global_step, iteration_idx, scale=window.scale,
-                             far_ref=b["far"], n_rays_global=n_glob, update_ogm=ogm, dev_step=self.dev_step)
+            main = torch.cuda.current_stream(st.device)
+            if prefetch:
+                self._gfork.record(main)
+                with torch.cuda.stream(self._pp_stream):
+                    self._pp_stream.wait_event(self._gfork)
+                    window.build(sc[1].key, self.ray_offset, n, bq["rays"][:n], bq["dgt"][:n], bq["valid"][:n], None,
+                                 bq["far"], dev_step=self.dev_step_next)
+                    if sample_next:
+                        ss = L.stream(st.device)
+                        if cfg.sampler == "OGM":
+                            L.call("lnr_sample_ogm", bq["rays"][:n], n, self.S, st.occ, cfg.occ_res, cfg.perturb, None,
+                                   None, sc[1].key, self.ray_offset, bq["z"], self.dev_step_next, ss)
+                        else:
+                            L.call("lnr_sample_uniform", bq["rays"][:n], n, self.S, cfg.perturb, None, sc[1].key,
+                                   self.ray_offset, bq["z"], self.dev_step_next, ss)
+                    self._gjoin.record(self._pp_stream)
+            if have < 1:
+                window.build(sc[0].key, self.ray_offset, n, b["rays"][:n], b["dgt"][:n], b["valid"][:n], None, b["far"],
+                             dev_step=self.dev_step)
+            out = self.step(b["rays"][:n], b["dgt"][:n], global_step, iteration_idx, scale=window.scale,
+                            far_ref=b["far"], n_rays_global=n_glob, update_ogm=ogm, presampled=have >= 2,
+                            dev_step=self.dev_step)
+            if prefetch:
+                main.wait_event(self._gjoin)
+            return out
 
         g = self._graphs.get(gkey)
         if g is not None:
@@ -743,8 +789,15 @@ class StepEngine:
         g = torch.cuda.CUDAGraph()
         if self._graph_pool is None:
             self._graph_pool = torch.cuda.graph_pool_handle()
-        with torch.cuda.graph(g, pool=self._graph_pool):
-            body()  # recorded, not executed
+        cs = self._capture_stream
+        cs.wait_stream(torch.cuda.current_stream(st.device))
+        with torch.cuda.stream(cs):  # capture_begin / _end directly: no device sync, gc or cache flush
+            g.capture_begin(pool=self._graph_pool)
+            try:
+                body()  # recorded, not executed
+            finally:
+                g.capture_end()
+        torch.cuda.current_stream(st.device).wait_stream(cs)
         st.adam_step = saved
         self._graphs[gkey] = g
         return out

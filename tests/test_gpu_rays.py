@@ -250,32 +250,34 @@ def test_graph_replay_equals_eager(L, zero):
     and the ExponentialLR factor read from device memory, set by one launch per step) gives bitwise the
     eager path's losses, parameters, moments, occupancy grid and samples, across OGM steps (their own
     graph), a skipped global step, a changed iteration index / learning-rate factor and a second window
-    (the graphs are re-captured); also with the sharded optimiser's one-rank share (bench --shard-of)."""
+    (the graphs are re-captured), with and without the in-graph prefetch of the next step's rays and
+    samples; also with the sharded optimiser's one-rank share (bench --shard-of)."""
     from loner_amd import step as S_
     from loner_amd.rays import RayWindow
     loss = S_.LossConfig.from_dict(dict(loss_selection="L1_LOS", decay_los_lambda=True, los_lambda=1000.0,
                                         los_lambda_decay_rate=1e-4, los_lambda_decay_steps=30))
     res = []
-    for graph in (False, True):
+    for graph, pipe in ((False, True), (True, True), (True, False)):
         st = S_.FieldState(S_.StepConfig(n_samples=64, occ_lr=1e-3, loss=loss), device="cuda:0", table_init=0.5)
         eng = None
         outs = []
-        for seed, steps in ((8, (8, 9, 10, 11, 12, 14, 15, 20, 21)), (9, (22, 23, 30, 31))):
+        for seed, steps in ((8, (8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 19, 20, 21, 22, 23)), (9, (24, 25, 30, 31, 32))):
             scans, wc, rr = _window("forest", 2, seed=seed)
             win = RayWindow(scans, wc, rr, n_lidar=128, n_sky=16, strategy="MASK")
             if eng is None:
                 eng = S_.StepEngine(st, win.n_slots, seed=4, zero=zero)
-                eng.use_graph = graph
+                eng.use_graph, eng.pipeline = graph, pipe
             st.reset_optimizer()
             for it, g in enumerate(steps):
                 eng.lr_factor = 0.97 ** it
                 outs.append(host(eng.step_window(win, global_step=g, iteration_idx=it)).copy())
-            if graph:
-                assert len(eng._graphs) == 2  # the OGM and the plain step of this window
+            if graph:  # at least the OGM and the plain step of this window (times parities and prefetch states)
+                assert len(eng._graphs) >= 2
         torch.cuda.synchronize()
         res.append((outs, host(st.params).copy(), host(st.m).copy(), host(st.v).copy(), host(st.occ).copy(),
                     host(eng.z).copy(), st.adam_step))
-    for a, b in zip(res[0][0], res[1][0]):
-        np.testing.assert_array_equal(a, b)
-    for a, b in zip(res[0][1:], res[1][1:]):
-        np.testing.assert_array_equal(a, b)
+    for r in res[1:]:
+        for a, b in zip(res[0][0], r[0]):
+            np.testing.assert_array_equal(a, b)
+        for a, b in zip(res[0][1:], r[1:]):
+            np.testing.assert_array_equal(a, b)
