@@ -3,9 +3,11 @@
 // Replaces tcnn's kernel_grid behind tcnn.NetworkWithInputEncoding (src/models/nerf_tcnn.py:35-38,
 // 68, 71) and tcnn.Encoding (:40, 64).  The backward lives in hashgrid_bwd.hip.
 //
-// Launch shape: grid (ceil(N / 256), n_levels) with the LEVEL as the slow grid dimension, so the
-// dispatcher walks level by level and the live gather footprint is one level's table slice
-// (<= 1 MB fp16) — L2-resident on every XCD — instead of the whole 14.8 MB table.
+// Launch shape: grid (ceil(N / kSB), n_levels) of kSB-thread workgroups (kSB = 512 samples, one
+// histogram row each; the live-masked eval launch: kSB / 2 threads of two samples), with the LEVEL
+// as the slow grid dimension, so the dispatcher walks level by level and the live gather footprint
+// is one level's table slice (<= 1 MB fp16) — L2-resident on every XCD — instead of the whole
+// 14.8 MB table.
 // Output layout is level-major half2 (enc[l * stride + n]) so every store is a coalesced 4 B/lane.
 // In training mode the forward also emits the backward's per-block record histogram (same
 // corners), which removes a full corner-recompute pass from the backward.

@@ -1,6 +1,7 @@
 """The data-parallel StepEngine through a real torch.distributed backend: two processes (gloo, both
 on GPU 0) each step their shard with the bucketed, asynchronous gradient all-reduce
-(``allreduce(t, async_op=True)``, three level-range buckets overlapping the accumulation) and must
+(``allreduce(t, async_op=True)``, two level-range buckets by default (LONER_AR_BUCKETS: levels 8-15,
+then 0-7 with the MLP), each exchanged while the next accumulates) and must
 reproduce the single-engine gradient, with bit-identical parameters on both replicas (SURVEY.md
 §8(e)).  The driver's multi-GPU runs use the same code path over RCCL."""
 import os
