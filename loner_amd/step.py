@@ -289,7 +289,6 @@ class StepEngine:
         self.dev_step, self.dev_step_next = self._dev_steps[:8], self._dev_steps[8:]
         self._dev_step = None
         self._graphs, self._graph_window = {}, None
-        self._graph_pool = None
         self._gpp = None  # what the last graph step prefetched for the next: window, want, parity, have
         self._capture_stream = torch.cuda.Stream(device=dev)
         self._gfork, self._gjoin = torch.cuda.Event(), torch.cuda.Event()
@@ -787,12 +786,10 @@ class StepEngine:
         out = body()  # this step, eagerly
         saved = st.adam_step
         g = torch.cuda.CUDAGraph()
-        if self._graph_pool is None:
-            self._graph_pool = torch.cuda.graph_pool_handle()
         cs = self._capture_stream
         cs.wait_stream(torch.cuda.current_stream(st.device))
         with torch.cuda.stream(cs):  # capture_begin / _end directly: no device sync, gc or cache flush
-            g.capture_begin(pool=self._graph_pool)
+            g.capture_begin()  # (its own memory pool, which stays empty: the captured step allocates nothing)
             try:
                 body()  # recorded, not executed
             finally:
