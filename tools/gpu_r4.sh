@@ -6,7 +6,7 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r4
 mkdir -p $O
-PARTS=${1:-"tests bench calib pmc slack"}
+PARTS=${1:-"tests bench graphcost calib pmc slack"}
 cd $R
 if [[ " $PARTS " == *" tests "* ]]; then
   timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_rays.py \
@@ -23,6 +23,9 @@ if [[ " $PARTS " == *" bench "* ]]; then
       python3 -c "import json,sys; d=json.loads(open('$O/bench_${TAG}_g$g.json').read().strip().splitlines()[-1]); print('$TAG graph=$g', d['ms_per_step'], d['value'])"
     done
   done
+fi
+if [[ " $PARTS " == *" graphcost "* ]]; then
+  for c in C1 C2; do timeout -k 10 120 python tools/graph_cost.py $c | tee $O/graph_cost_$c.json || exit 1; done
 fi
 if [[ " $PARTS " == *" calib "* ]]; then
   hipcc -O3 --offload-arch=gfx950 tools/ubench/ubench_fetch.hip -o /tmp/ubf || exit 1
