@@ -113,7 +113,7 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
     // and issue no gathers
     use[h] = in[h] && (live == nullptr || live[i] != 0.f);
     x[h] = y[h] = z[h] = 0.f;
-    if (in[h]) pos(i, x[h], y[h], z[h]);
+    pos.wave(i, n, in[h], x[h], y[h], z[h]);
   }
   const LevelParams& lv = a.lv[l];
   if (lv.fine) {  // block-uniform

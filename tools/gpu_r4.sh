@@ -9,7 +9,7 @@ mkdir -p $O
 PARTS=${1:-"tests bench graphcost calib pmc slack"}
 cd $R
 if [[ " $PARTS " == *" tests "* ]]; then
-  timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_rays.py \
+  timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_rays.py tests/test_gpu_parity.py \
     tests/test_gpu_dist.py tests/test_gpu_step.py > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
   tail -2 $O/tests.txt
 fi
