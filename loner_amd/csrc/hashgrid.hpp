@@ -2,6 +2,7 @@
 // level layout, corner indexing, sample positions, and the backward's bucket geometry.
 #pragma once
 #include "common.hpp"
+#include <cstdlib>
 
 namespace lnr {
 
@@ -46,7 +47,18 @@ struct GridArgs {
   uint32_t n_levels;
   uint32_t n_buckets;
   uint32_t merge_levels;  // levels [0, merge_levels) merge equal corner indices across lanes
+  uint32_t accum_direct_level;  // the accumulation reads levels from this one on without its tile stage
 };
+
+// Levels from which the accumulation adds each thread's own records (no dealing through an LDS tile
+// stage: hashgrid_bwd.hip accum_records); LONER_ACCUM_DIRECT_LEVEL overrides (read per launch).
+#ifndef LNR_ACCUM_DIRECT_LEVEL
+#define LNR_ACCUM_DIRECT_LEVEL 9
+#endif
+inline uint32_t accum_direct_level() {
+  const char* e = getenv("LONER_ACCUM_DIRECT_LEVEL");
+  return e ? (uint32_t)atoi(e) : (uint32_t)LNR_ACCUM_DIRECT_LEVEL;
+}
 
 // Levels whose cell edge spans several consecutive samples of a ray produce runs of equal corner
 // indices.  At the reference's 512 samples per ray (after the OGM has concentrated them) that holds
@@ -86,6 +98,7 @@ inline GridArgs make_args(const lnr_grid_desc* d, int32_t samples_per_ray = 0) {
   a.bucket_base[d->n_levels] = b;
   a.n_buckets = b;
   a.merge_levels = merge_levels_for(d, samples_per_ray);
+  a.accum_direct_level = accum_direct_level();
   for (uint32_t l = 0; l < d->n_levels; ++l)
     a.lv[l].fine = (a.lv[l].hashed && a.lv[l].size_mask && l >= a.merge_levels) ? 1u : 0u;
   return a;

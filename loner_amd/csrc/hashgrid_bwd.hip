@@ -800,8 +800,13 @@ __device__ __forceinline__ uint32_t level_of_bucket(const GridArgs& a, uint32_t 
 // A pair record (p > 0) adds (1 - tx) v to corner e0 and tx v to e1 = e0 ^ (2^p - 1), a single
 // record (p = 0, tx = 0) adds v to e0.  int64 sums: the result does not depend on the order.
 // fs = 2^k2, the bucket's fixed-point scale (the records carry 2^k_l already).
+// DIRECT (levels >= GridArgs.accum_direct_level, block-uniform per bucket): no tile stage.  At the fine levels
+// consecutive records of a bucket come from consecutive samples of a row, whose cells are unrelated
+// (mean run of one cell ~1 sample from level 9 on), so a wave's atomic
+// instruction over 64 records 2 apart meets equal entries only by hash collision: each thread adds
+// the 2 records of its own 16-B load, with no stage write, no barriers and no stage reads.
 __device__ __forceinline__ void accum_records(unsigned long long* acc, uint2* stage, const BwdWorkspace& ws,
-                                              uint64_t beg, uint64_t end, float fs) {
+                                              uint64_t beg, uint64_t end, float fs, bool direct = false) {
   const int lane = threadIdx.x & 63;
   const uint64_t beg2 = beg & ~1ull;
   const float ftx = fs * kInvU16;
@@ -846,6 +851,41 @@ __device__ __forceinline__ void accum_records(unsigned long long* acc, uint2* st
       }
     }
   };
+  auto add_rec = [&](uint32_t w, uint32_t h) {
+    const float v0 = rec_v0(h), v1 = rec_v1(h);
+    const uint32_t e0 = w & (kChunk - 1);
+    const uint32_t p = (w >> kChunkLog2) & 15u;
+    const float tx = (float)(w >> 16) * ftx;
+    const float s0 = fs - tx;
+    atomicAdd(&acc[e0], fixed_i64(s0 * v0));
+    atomicAdd(&acc[kChunk + e0], fixed_i64(s0 * v1));
+    if (p) {
+#ifdef LNR_BWD_CHECK
+      if (p > kChunkLog2) __builtin_trap();
+#endif
+      const uint32_t e1 = e0 ^ ((1u << p) - 1u);
+      atomicAdd(&acc[e1], fixed_i64(tx * v0));
+      atomicAdd(&acc[kChunk + e1], fixed_i64(tx * v1));
+    }
+  };
+  if (direct) {
+    u32x4 buf[kAccumTrip];
+#pragma unroll
+    for (int d = 0; d < kAccumTrip; ++d) buf[d] = load_tile(d);
+    for (uint64_t tile = 0; tile < n_tiles; tile += kAccumTrip) {
+#pragma unroll
+      for (int d = 0; d < kAccumTrip; ++d) {
+        if (tile + d < n_tiles) {  // block-uniform
+          const u32x4 c = buf[d];
+          buf[d] = load_tile(tile + d + kAccumTrip);
+          const uint64_t rr = beg2 + (tile + d) * kTile + 2 * threadIdx.x;
+          if (rr >= beg && rr < end) add_rec(c.x, c.y);
+          if (rr + 1 >= beg && rr + 1 < end) add_rec(c.z, c.w);
+        }
+      }
+    }
+    return;
+  }
   // kAccumTrip tiles per trip, each in a register set of its own (the unrolled loop indexes them
   // statically), its next load issued as soon as it is staged: the loads of the following
   // kAccumTrip tiles are in flight while these accumulate
@@ -930,7 +970,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
     lds_barrier();
     // one scale per bucket (the pieces' partials add exactly)
     const int k2 = bucket_k2(ws, b);
-    accum_records(acc, stage, ws, beg, end, ldexpf(1.f, k2));
+    accum_records(acc, stage, ws, beg, end, ldexpf(1.f, k2), l >= a.accum_direct_level);
     lds_barrier();
     if (beg == s0 && end == s1) {  // the whole bucket: the final values
       store_bucket(acc, a, ws, d_table, l, ent0, nent, k2);
@@ -1003,7 +1043,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
   for (int t = threadIdx.x; t < 2 * kChunk; t += blockDim.x) acc[t] = 0ull;
   lds_barrier();
   const int k2 = bucket_k2(ws, b);
-  accum_records(acc, stage, ws, s0, s1, ldexpf(1.f, k2));
+  accum_records(acc, stage, ws, s0, s1, ldexpf(1.f, k2), l >= a.accum_direct_level);
   lds_barrier();
   store_bucket(acc, a, ws, d_table, l, ent0, nent, k2);
 }
@@ -1037,7 +1077,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
   for (int t = threadIdx.x; t < 2 * kChunk; t += blockDim.x) acc[t] = 0ull;
   lds_barrier();
   const int k2 = bucket_k2(ws, b);
-  accum_records(acc, stage, ws, beg, end, ldexpf(1.f, k2));
+  accum_records(acc, stage, ws, beg, end, ldexpf(1.f, k2), l >= a.accum_direct_level);
   lds_barrier();
   if (P == 1) {
     store_bucket(acc, a, ws, d_table, l, ent0, nent, k2);
