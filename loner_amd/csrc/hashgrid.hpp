@@ -53,7 +53,7 @@ struct GridArgs {
 // Levels from which the accumulation adds each thread's own records (no dealing through an LDS tile
 // stage: hashgrid_bwd.hip accum_records); LONER_ACCUM_DIRECT_LEVEL overrides (read per launch).
 #ifndef LNR_ACCUM_DIRECT_LEVEL
-#define LNR_ACCUM_DIRECT_LEVEL 9
+#define LNR_ACCUM_DIRECT_LEVEL 99  // measured: 9 equal to off (C2 grid_bwd 0.969 vs 0.964 ms), 6 or 0 +0.21 ms (same-entry conflicts)
 #endif
 inline uint32_t accum_direct_level() {
   const char* e = getenv("LONER_ACCUM_DIRECT_LEVEL");
