@@ -284,6 +284,7 @@ class StepEngine:
         # device memory by one small launch before each replay (``lnr_step_scalars``): one graph launch
         # in place of ~18 kernel launches (LONER_GRAPH=0 turns it off; the pipelined path then runs)
         self.use_graph = os.environ.get("LONER_GRAPH", "1") != "0"
+        self.graph_prefetch = os.environ.get("LONER_GRAPH_PREFETCH", "0") == "1"
         # two lnr_step_scalars (32 B each): this step's, and the next step's (its prefetched build + sampling)
         self._dev_steps = torch.zeros(16, dtype=torch.int32, device=dev)
         self.dev_step, self.dev_step_next = self._dev_steps[:8], self._dev_steps[8:]
@@ -374,7 +375,8 @@ class StepEngine:
             prof.setdefault(stage, []).append(ev)
 
     def step(self, rays, depth_gt, global_step, iteration_idx=0, scale=1.0, far_ref=None, n_rays_global=None,
-             u_jitter=None, u_pdf=None, noise=None, update_ogm=None, prof=None, presampled=False, dev_step=None):
+             u_jitter=None, u_pdf=None, noise=None, update_ogm=None, prof=None, presampled=False, dev_step=None,
+             fork_count=True):
         """rays (R,13) fp32, depth_gt (R,) fp32 normalised, both on this GPU, R <= the engine's
         capacity.  Returns the device loss buffer [loss, mean_eps, depth_term, los_term, opacity_term,
         n_opaque] (no host sync).  ``far_ref``: the far bound of global ray 0, a float or a 1-element
@@ -396,13 +398,17 @@ class StepEngine:
         # 1. opaque count (global): local count + all-reduce, on the side stream; the count is first
         # needed by the field kernel, so both overlap sampling + encode
         main = torch.cuda.current_stream(st.device)
-        self._fork.record(main)
-        with torch.cuda.stream(self._side):
-            self._side.wait_event(self._fork)
-            L.call("lnr_count_opaque", depth_gt, R, 0.0 if far_h is None else far_h, dev_far, self.n_opaque,
-                   L.stream(st.device))
-            pending = self._allreduce_async(self.n_opaque) if self.allreduce is not None else None
-            self._join.record(self._side)
+        pending = None
+        if fork_count or self.allreduce is not None:
+            self._fork.record(main)
+            with torch.cuda.stream(self._side):
+                self._side.wait_event(self._fork)
+                L.call("lnr_count_opaque", depth_gt, R, 0.0 if far_h is None else far_h, dev_far, self.n_opaque,
+                       L.stream(st.device))
+                pending = self._allreduce_async(self.n_opaque) if self.allreduce is not None else None
+                self._join.record(self._side)
+        else:  # (a captured single-stream step: the count inline, one stream in the graph)
+            L.call("lnr_count_opaque", depth_gt, R, 0.0 if far_h is None else far_h, dev_far, self.n_opaque, s)
         lp = self.loss_params(global_step, iteration_idx, scale, far_h, n_glob, dev_far)
         dsp = None if dev_step is None else dev_step.data_ptr()
         lp.dev_step = dsp
@@ -432,7 +438,8 @@ class StepEngine:
             self._pp_mid.record(main)
         # 4. fused field + loss + backward through compositing and MLP (stores the MLP gradient, and the
         # loss scalars into loss_out)
-        main.wait_event(self._join)
+        if fork_count or self.allreduce is not None:
+            main.wait_event(self._join)
         if pending is not None:
             pending.wait()  # orders the current stream after the collective (no host sync)
         m(prof, "field")
@@ -736,7 +743,9 @@ class StepEngine:
             p, have = gp["parity"], gp["have"]
         else:
             p, have = self._pp_parity, 0
-        prefetch = self.pipeline
+        # the next step's build + sampling as a forked branch of the graph (LONER_GRAPH_PREFETCH=1) measured
+        # slower than a single-stream graph (C1 0.284 against 0.170 ms eager on one box): off by default
+        prefetch = self.pipeline and self.graph_prefetch
         sample_next = prefetch and (cfg.sampler != "OGM" or not ogm)  # the OGM sampler reads the grid step k updates
         gkey = (p, have, ogm, prefetch, n, self.ray_offset, n_glob, self.zero)
         s = L.stream(st.device)
@@ -772,7 +781,7 @@ class StepEngine:
                              dev_step=self.dev_step)
             out = self.step(b["rays"][:n], b["dgt"][:n], global_step, iteration_idx, scale=window.scale,
                             far_ref=b["far"], n_rays_global=n_glob, update_ogm=ogm, presampled=have >= 2,
-                            dev_step=self.dev_step)
+                            dev_step=self.dev_step, fork_count=prefetch)
             if prefetch:
                 main.wait_event(self._gjoin)
             return out

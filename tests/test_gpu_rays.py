@@ -266,7 +266,7 @@ def test_graph_replay_equals_eager(L, zero):
             win = RayWindow(scans, wc, rr, n_lidar=128, n_sky=16, strategy="MASK")
             if eng is None:
                 eng = S_.StepEngine(st, win.n_slots, seed=4, zero=zero)
-                eng.use_graph, eng.pipeline = graph, pipe
+                eng.use_graph, eng.pipeline, eng.graph_prefetch = graph, pipe, pipe
             st.reset_optimizer()
             for it, g in enumerate(steps):
                 eng.lr_factor = 0.97 ** it
