@@ -740,6 +740,9 @@ def main():
                    (f"shard 0 of {args.shard_of} (one rank's strong-scaling step: its rays, its 1/{args.shard_of} "
                     f"of the sharded Adam; no collective)" if args.shard_of else "single"),
                    "optimizer": "sharded (ZeRO-1)" if zero is not None else "replicated",
+                   "launch": ("HIP graph replay (one graph per window and OGM-or-not step)"
+                              if eng.use_graph and args.rays == "device" and eng.allreduce is None else
+                              "eager, next step's ray build + sampling prefetched on a side stream"),
                    **({"submap_rank0": submap} if submap is not None else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,

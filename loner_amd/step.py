@@ -283,7 +283,12 @@ class StepEngine:
         # in a HIP graph and replayed, its per-step scalars (key, loss scalars, Adam coefficients) set in
         # device memory by one small launch before each replay (``lnr_step_scalars``): one graph launch
         # in place of ~18 kernel launches (LONER_GRAPH=0 turns it off; the pipelined path then runs)
-        self.use_graph = os.environ.get("LONER_GRAPH", "1") != "0"
+        # LONER_GRAPH: auto (default: batches of at most 2^18 samples, where the host's launch cost is a
+        # visible share of the step; measured C1 0.161 against 0.163 ms eager on a fast host, 0.188 against
+        # 0.236 on a slow one; C2 2.040 against 2.016 and C4 shard 1/8 0.396 against 0.392, where the eager
+        # path's next-step prefetch overlaps more than the launches cost), 1 always, 0 never
+        g = os.environ.get("LONER_GRAPH", "auto")
+        self.use_graph = (g == "1") or (g == "auto" and self.N <= (1 << 18))
         self.graph_prefetch = os.environ.get("LONER_GRAPH_PREFETCH", "0") == "1"
         # two lnr_step_scalars (32 B each): this step's, and the next step's (its prefetched build + sampling)
         self._dev_steps = torch.zeros(16, dtype=torch.int32, device=dev)
