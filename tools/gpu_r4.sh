@@ -43,7 +43,7 @@ if [[ " $PARTS " == *" pmc "* ]]; then
   tail -20 $O/pmc_split.txt
 fi
 if [[ " $PARTS " == *" slack "* ]]; then
-  for g in 1 0; do
+  for g in 0; do
     ( cd /tmp && export TMPDIR=/tmp && LONER_GRAPH=$g timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv \
         -d $O/trace_C4s8_g$g -o run -- python3 $R/bench.py --config C4 --shard-of 8 --no-cpu-baseline \
         > $O/trace_C4s8_g$g.json 2> $O/trace_C4s8_g$g.err ) || { tail -20 $O/trace_C4s8_g$g.err; exit 1; }
