@@ -1361,16 +1361,28 @@ static int check_desc_bwd(const lnr_grid_desc* d, const char* who) {
 // Only launched when the caller asks for d_pos: the training step (which holds the poses fixed)
 // never pays for it.
 constexpr int kDposThreads = 256;
+#ifndef LNR_DPOS_LEVELS_PER_PASS
+#define LNR_DPOS_LEVELS_PER_PASS 16
+#endif
+// Levels [l0, l1) per launch, added to the running sums d_pos holds (l0 > 0) in level order: the same
+// fp32 additions in the same order as one pass over every level, so the result does not depend on the
+// split, while each launch's gathers stay within a few levels' table slices (L2-resident: the whole
+// 14.8 MB table is not).
 template <class PosFn, class GradFn>
 __global__ void __launch_bounds__(kDposThreads) k_hashgrid_dpos(GridArgs a, PosFn pos, int64_t n,
                                                                 const uint32_t* __restrict__ table, GradFn grad,
-                                                                float* __restrict__ d_pos) {
+                                                                float* __restrict__ d_pos, uint32_t l0, uint32_t l1) {
   const int64_t i = (int64_t)blockIdx.x * kDposThreads + threadIdx.x;
   if (i >= n) return;
   float x, y, z;
   pos(i, x, y, z);
   float r0 = 0.f, r1 = 0.f, r2 = 0.f;
-  for (uint32_t l = 0; l < a.n_levels; ++l) {
+  if (l0 > 0) {
+    r0 = d_pos[3 * i + 0];
+    r1 = d_pos[3 * i + 1];
+    r2 = d_pos[3 * i + 2];
+  }
+  for (uint32_t l = l0; l < l1; ++l) {
     const LevelParams& p = a.lv[l];
     Corners c;
     level_corners(p, x, y, z, c);
@@ -1425,8 +1437,11 @@ static int launch_dpos(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint1
   const GridArgs a = make_args(d, pos.samples_per_ray());
   const int64_t nb = (n + kDposThreads - 1) / kDposThreads;
   LNR_REQUIRE(nb < (int64_t(1) << 31), "%s: n=%lld too large", who, (long long)n);
-  hipLaunchKernelGGL((k_hashgrid_dpos<PosFn, GradFn>), dim3((unsigned)nb), dim3(kDposThreads), 0, st, a, pos, n,
-                     reinterpret_cast<const uint32_t*>(table), grad, d_pos);
+  const char* e = getenv("LONER_DPOS_LEVELS_PER_PASS");
+  const uint32_t per = e ? (uint32_t)std::max(1, atoi(e)) : (uint32_t)LNR_DPOS_LEVELS_PER_PASS;
+  for (uint32_t l0 = 0; l0 < d->n_levels; l0 += per)
+    hipLaunchKernelGGL((k_hashgrid_dpos<PosFn, GradFn>), dim3((unsigned)nb), dim3(kDposThreads), 0, st, a, pos, n,
+                       reinterpret_cast<const uint32_t*>(table), grad, d_pos, l0, std::min(l0 + per, d->n_levels));
   LNR_RETURN_LAUNCH(who);
 }
 

@@ -55,19 +55,29 @@ def main():
     de = torch.randn(16, N, 2, device="cuda")
     out = torch.empty(N, 3, device="cuda")
     s = L.stream()
-    times = []
-    for it in range(13):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        L.call("lnr_hashgrid_bwd_rays", ctypes.byref(d), rays, z, R, S, de, N, None, t16, out, None, 0, 0, s)
-        b.record()
-        torch.cuda.synchronize()
-        if it >= 3:
-            times.append(a.elapsed_time(b))
-    ms = float(np.median(times))
+    per_pass = {}
+    ref_out = None
+    for per in (16, 8, 4, 2, 1):  # levels per launch (LONER_DPOS_LEVELS_PER_PASS, read per call)
+        os.environ["LONER_DPOS_LEVELS_PER_PASS"] = str(per)
+        times = []
+        for it in range(13):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            L.call("lnr_hashgrid_bwd_rays", ctypes.byref(d), rays, z, R, S, de, N, None, t16, out, None, 0, 0, s)
+            b.record()
+            torch.cuda.synchronize()
+            if it >= 3:
+                times.append(a.elapsed_time(b))
+        per_pass[per] = float(np.median(times))
+        if ref_out is None:
+            ref_out = out.clone()
+        assert torch.equal(out, ref_out), per  # the split does not change a bit
+    os.environ.pop("LONER_DPOS_LEVELS_PER_PASS")
+    ms = min(per_pass.values())
     # bytes per sample: 512 B of fp16 corner gathers (16 levels x 8 corners x 4 B), 128 B of d_enc, 12 B out
     print(json.dumps(dict(dpos_rel_l2=overall, dpos_rel_l2_worst_level=max(per_level),
                           dpos_rel_l2_per_level=[float(f"{v:.3g}") for v in per_level], c2_dpos_ms=ms,
+                          c2_dpos_ms_by_levels_per_pass=per_pass,
                           c2_samples=N, gathered_gb_per_s=N * 512 / ms / 1e6)))
 
 
