@@ -35,6 +35,18 @@ def main():
     enc = torch.empty(16, N, dtype=torch.int32, device="cuda")
     s = L.stream()
     out = {}
+    ref = None
+    for rl in (0, 3, 6):  # LONER_ENC_RUN_LEVELS: coherent levels gathering once per run of lanes in a cell
+        os.environ["LONER_ENC_RUN_LEVELS"] = str(rl)
+        out[f"run_levels_{rl}"] = one(rays, z, table, enc, R, S, N, s)
+        if ref is None:
+            ref = enc.clone()
+        out[f"run_levels_{rl}"]["bitwise_equal"] = bool(torch.equal(ref, enc))
+    print(json.dumps(out))
+
+
+def one(rays, z, table, enc, R, S, N, s):
+    out = {}
     for train in (False, True):
         per = []
         for k in range(1, 17):
@@ -57,7 +69,7 @@ def main():
             del ws
         levels = [per[0]] + [per[k] - per[k - 1] for k in range(1, 16)]
         out["train" if train else "eval"] = dict(total_ms=per[-1], per_level_ms=[round(v, 4) for v in levels])
-    print(json.dumps(out))
+    return out
 
 
 if __name__ == "__main__":
