@@ -840,6 +840,9 @@ __device__ __forceinline__ uint32_t pack_h2(float x, float y) {
 #ifndef LNR_MLP_W_LDS
 #define LNR_MLP_W_LDS 0  // the layer-0 weight operands in LDS instead of registers (k_mlp_bwd_tiles)
 #endif
+#ifndef LNR_MLP_SPLIT_PAIR
+#define LNR_MLP_SPLIT_PAIR 0  // k_mlp_bwd_tiles: one tile of the pair live at a time (pair_split)
+#endif
 #ifndef LNR_MLP_BWD_WAVES
 #define LNR_MLP_BWD_WAVES 2  // waves per SIMD (3 spills 113 registers with the weights in registers)
 #endif
@@ -947,6 +950,61 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(LNR_MLP
     }
     dw0_pair_mfma(lds, h0, h1, e0, e1, ds0, ds1, pair_max, acc);
   };
+  // the same pair with one tile live at a time: the pair's operand scale first (from the inputs), then
+  // per tile the forward, dW1, its dW0 operands staged in LDS, its d_enc; the dW0 MFMAs last
+  auto pair_split = [&](int64_t n0, const Pre& p) {
+    float mx = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float a0 = (float)__builtin_bit_cast(_Float16, (uint16_t)(p.x0[q] & 0xFFFFu));
+      const float b0 = (float)__builtin_bit_cast(_Float16, (uint16_t)(p.x0[q] >> 16));
+      const float a1 = (float)__builtin_bit_cast(_Float16, (uint16_t)(p.x1[q] & 0xFFFFu));
+      const float b1 = (float)__builtin_bit_cast(_Float16, (uint16_t)(p.x1[q] >> 16));
+      mx = fmaxf(mx, fmaxf(fabsf(a0 * p.d0), fabsf(a1 * p.d1)));
+      mx = fmaxf(mx, fmaxf(fabsf(b0 * p.d0), fabsf(b1 * p.d1)));
+    }
+    float scale = 1.f;
+    const bool dw0 = dw0_scale(wave_max(mx), acc, scale);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      half8_t e;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t x = t ? p.x1[q] : p.x0[q];
+        e[2 * q + 0] = __builtin_bit_cast(_Float16, (uint16_t)(x & 0xFFFFu));
+        e[2 * q + 1] = __builtin_bit_cast(_Float16, (uint16_t)(x >> 16));
+      }
+      const float ds = t ? p.d1 : p.d0;
+      SigmaHidden h;
+      (void)sigma_tile_fwd(sw, e, h);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) dw1[k] = fmaf(ds, h[k], dw1[k]);
+      if (dw0) dw0_stage(lds, t, h, e, ds * scale);
+      float d[2][4];
+      sigma_tile_bwd_denc(sw, h, d);
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int lvl = 8 * m + 2 * g;
+        const float2 q0 = make_float2(d[m][0] * ds, d[m][1] * ds), q1 = make_float2(d[m][2] * ds, d[m][3] * ds);
+        if (JAC) {
+          const uint32_t o = row_j + 8u * (uint32_t)m * st4 + (uint32_t)(n0 + 16 * t + c) * 4u;
+          st_off(a.d_jac, o, pack_h2(d[m][0], d[m][1]));
+          st_off(a.d_jac, o + st4, pack_h2(d[m][2], d[m][3]));
+        } else {
+          denc[(int64_t)lvl * a.enc_stride + n0 + 16 * t + c] = q0;
+          denc[(int64_t)(lvl + 1) * a.enc_stride + n0 + 16 * t + c] = q1;
+        }
+        lmax[2 * m] = fmaxf(lmax[2 * m], fmaxf(fabsf(q0.x), fabsf(q0.y)));
+        lmax[2 * m + 1] = fmaxf(lmax[2 * m + 1], fmaxf(fabsf(q1.x), fabsf(q1.y)));
+      }
+    }
+    if (dw0) dw0_mfma(lds, acc);
+  };
+#if LNR_MLP_SPLIT_PAIR
+#define LNR_MLP_PAIR pair_split
+#else
+#define LNR_MLP_PAIR pair
+#endif
 #if LNR_MLP_PREFETCH == 2
   Pre pa, pb;
   prefetch(n0, pa);
@@ -955,12 +1013,12 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(LNR_MLP
     {
       const Pre cur = pa;
       prefetch(n0 + 2 * step, pa);
-      pair(n0, cur);
+      LNR_MLP_PAIR(n0, cur);
     }
     if (n0 + step < N) {  // (wave-uniform)
       const Pre cur = pb;
       prefetch(n0 + 3 * step, pb);
-      pair(n0 + step, cur);
+      LNR_MLP_PAIR(n0 + step, cur);
     }
   }
 #else
@@ -969,9 +1027,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(LNR_MLP
   for (; n0 < N; n0 += step) {
     const Pre cur = pa;
     prefetch(n0 + step, pa);
-    pair(n0, cur);
+    LNR_MLP_PAIR(n0, cur);
   }
 #endif
+#undef LNR_MLP_PAIR
   __syncthreads();
   {
     DW0Acc out;

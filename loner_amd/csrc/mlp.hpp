@@ -287,6 +287,64 @@ __device__ __forceinline__ void dw0_pair_mfma(_Float16* __restrict__ lds, const 
   __builtin_amdgcn_wave_barrier();
 }
 
+// dw0_pair_mfma in three parts, so a tile's hidden layer and encoding can be handed to the LDS right
+// after its own use and the two tiles are never live together (same operands, same MFMAs: bitwise
+// the same sums).  dw0_scale: the pair's operand scale from max |ds * Enc| over both tiles (an input
+// property, known before the forward), false when the pair adds nothing; dw0_stage: tile half's mask
+// and scaled ds * Enc into the wave's LDS; dw0_mfma: the 8 MFMAs once both halves are staged.
+__device__ __forceinline__ bool dw0_scale(float maxabs, DW0Mfma& acc, float& scale) {
+  if (!(maxabs > 0.f) || !isfinite(maxabs)) return false;  // (wave-uniform) nothing to add
+  int e;
+  frexpf(maxabs, &e);
+  int k = 13 - e;
+  k = k > 100 ? 100 : (k < -100 ? -100 : k);
+  if (k < acc.kc) {
+    if (acc.kc != DW0Mfma::kUnset) {
+      const float f = ldexpf(1.f, k - acc.kc);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) acc.v[t][m] *= f;
+    }
+    acc.kc = k;
+  }
+  scale = ldexpf(1.f, acc.kc);
+  return true;
+}
+__device__ __forceinline__ void dw0_stage(_Float16* __restrict__ lds, int half, const SigmaHidden& h, const half8_t& e,
+                                          float ds_scaled) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  _Float16* mk = lds + 16 * half;
+  _Float16* ens = lds + 64 * 32 + 16 * half;
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kk = 8 * q + j, hid = 16 * (kk >> 2) + 4 * g + (kk & 3);
+      mk[hid * 32 + c] = h.q[q][j] > (_Float16)0.f ? (_Float16)1.f : (_Float16)0.f;
+    }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ens[(8 * g + j) * 32 + c] = (_Float16)((float)e[j] * ds_scaled);
+}
+__device__ __forceinline__ void dw0_mfma(const _Float16* __restrict__ lds, DW0Mfma& acc) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const _Float16* mk = lds;
+  const _Float16* ens = lds + 64 * 32;
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-local hand-off through LDS
+  __builtin_amdgcn_wave_barrier();
+  half8_t a[4], b[2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) a[t] = *reinterpret_cast<const half8_t*>(mk + (16 * t + c) * 32 + 8 * g);
+#pragma unroll
+  for (int m = 0; m < 2; ++m) b[m] = *reinterpret_cast<const half8_t*>(ens + (16 * m + c) * 32 + 8 * g);
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int m = 0; m < 2; ++m) acc.v[t][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[t], b[m], acc.v[t][m], 0, 0, 0);
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+}
+
 // Block-level write of the per-block dW slab (3072 fp32, layout W0 (64,32) then W1 (16,64)).
 // red: LDS scratch of 3072 floats.  dw1 is per-lane (hid 16t+4g+r) summed over the lane's samples.
 template <int NT>
