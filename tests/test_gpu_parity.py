@@ -134,6 +134,46 @@ def test_hashgrid_fwd_live_mask_matches_full_encode(L, R):
     assert torch.equal(part, torch.where(mask, full, torch.zeros_like(full)))
 
 
+@pytest.mark.parametrize("S", [512, 64, 40])
+def test_hashgrid_fwd_run_head_gathers_bitwise(L, S, monkeypatch):
+    """The coherent levels' run-head gathers (LONER_ENC_RUN_LEVELS: one lane per run of lanes in one cell
+    gathers, the run's other lanes take its values through ds_bpermute) give the same encodings and
+    record histograms as every lane gathering, for the training, plain eval and live-masked launches;
+    40 samples per ray puts rays and ragged rows across waves."""
+    rng = np.random.default_rng(5)
+    R = 37
+    d = L.grid_desc(16, 2, 18, 16)
+    lay = ohg.GridLayout(16, 2, 18, 16)
+    o = rng.uniform(-0.5, 0.5, (R, 3))
+    dr = rng.normal(0, 1, (R, 3))
+    dr /= np.linalg.norm(dr, axis=1, keepdims=True)
+    rays = np.zeros((R, 13), np.float32)
+    rays[:, 0:3], rays[:, 3:6] = o, dr
+    z = np.sort(rng.uniform(0.0, 0.45, (R, S)), 1).astype(np.float32)
+    z[:, S // 2:] = np.sort(0.2 + rng.uniform(-0.01, 0.01, (R, S - S // 2)), 1)  # long runs near a surface
+    z = np.sort(z, 1)
+    live = cu((rng.uniform(0, 1, (R, S)) < 0.5).astype(np.float32))
+    table = cu(rng.uniform(-1, 1, (lay.n_entries, 2)).astype(np.float16).view(np.int16))
+    n = R * S
+    nb = int(L.lib().lnr_hashgrid_bwd_workspace_bytes(ctypes.byref(d), n))
+    outs = {}
+    for rl in ("0", "16"):
+        monkeypatch.setenv("LONER_ENC_RUN_LEVELS", rl)
+        ws = torch.zeros(nb // 4 + 1, dtype=torch.int32, device="cuda")
+        e_train = torch.full((16, n), -1, dtype=torch.int32, device="cuda")
+        e_eval = torch.full((16, n), -1, dtype=torch.int32, device="cuda")
+        e_live = torch.full((16, n), -1, dtype=torch.int32, device="cuda")
+        L.call("lnr_hashgrid_fwd_rays", ctypes.byref(d), cu(rays), cu(z), R, S, table, e_train, n, ws, nb, L.stream())
+        L.call("lnr_hashgrid_fwd_rays", ctypes.byref(d), cu(rays), cu(z), R, S, table, e_eval, n, None, 0, L.stream())
+        L.call("lnr_hashgrid_fwd_rays_live", ctypes.byref(d), cu(rays), cu(z), R, S, table, live, e_live, n,
+               L.stream())
+        torch.cuda.synchronize()
+        outs[rl] = (e_train, ws, e_eval, e_live)
+    for a, b in zip(outs["0"], outs["16"]):
+        assert torch.equal(a, b)
+    assert torch.equal(outs["0"][0], outs["0"][2])
+
+
 def test_hashgrid_fwd_rays_matches_positions(L):
     g = np.load("tests/golden/samplers.npz")
     rays, z = g["rays"], g["z_ogm"]
