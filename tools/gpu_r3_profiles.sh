@@ -2,6 +2,7 @@
 # rocprofv3 --kernel-trace --stats summary of the same command; PMC passes (HBM bytes of the backward
 # stage and of the whole step, MFMA busy) for the configs named in PMC.
 #   bash tools/gpu_r3_profiles.sh "C2 C1 C4:--shard-of 8 C3 CAM C4"   (tools/refresh_profiles.py per config)
+# Output under gpurun_out/${PROF_DIR:-r3p}/<config tag>/.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
@@ -9,7 +10,7 @@ for spec in $1; do
   CFG=${spec%%:*}; ARGS=""; [ "$spec" != "$CFG" ] && ARGS="${spec#*:}"
   ARGS=${ARGS//_/ }
   TAG=$CFG$(echo "$ARGS" | tr -d ' -' | sed 's/shardof/s/')
-  export OUT=$R/gpurun_out/r3p/$TAG ARGS
+  export OUT=$R/gpurun_out/${PROF_DIR:-r3p}/$TAG ARGS
   mkdir -p $OUT
   timeout -k 10 300 python bench.py --config $CFG $ARGS > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
   echo "== $TAG"; cat $OUT/bench.json
