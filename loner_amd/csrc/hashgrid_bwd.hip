@@ -1362,7 +1362,7 @@ static int check_desc_bwd(const lnr_grid_desc* d, const char* who) {
 // never pays for it.
 constexpr int kDposThreads = 256;
 #ifndef LNR_DPOS_LEVELS_PER_PASS
-#define LNR_DPOS_LEVELS_PER_PASS 16
+#define LNR_DPOS_LEVELS_PER_PASS 2  // C2 (tools/k3_metrics.py): 1.47 ms at 16, 1.35 at 8, 1.23 at 4, 1.13 at 2, 1.25 at 1
 #endif
 // Levels [l0, l1) per launch, added to the running sums d_pos holds (l0 > 0) in level order: the same
 // fp32 additions in the same order as one pass over every level, so the result does not depend on the
