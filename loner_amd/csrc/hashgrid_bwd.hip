@@ -1364,26 +1364,19 @@ constexpr int kDposThreads = 256;
 #ifndef LNR_DPOS_LEVELS_PER_PASS
 #define LNR_DPOS_LEVELS_PER_PASS 2  // C2 (tools/k3_metrics.py): 1.47 ms at 16, 1.35 at 8, 1.23 at 4, 1.13 at 2, 1.25 at 1
 #endif
+#ifndef LNR_DPOS_SPT
+#define LNR_DPOS_SPT 0  // samples per thread of the one-launch, level-outer kernel (k_hashgrid_dpos_k: 2, 4, 8); 0: passes
+#endif
 // Levels [l0, l1) per launch, added to the running sums d_pos holds (l0 > 0) in level order: the same
 // fp32 additions in the same order as one pass over every level, so the result does not depend on the
 // split, while each launch's gathers stay within a few levels' table slices (L2-resident: the whole
 // 14.8 MB table is not).
-template <class PosFn, class GradFn>
-__global__ void __launch_bounds__(kDposThreads) k_hashgrid_dpos(GridArgs a, PosFn pos, int64_t n,
-                                                                const uint32_t* __restrict__ table, GradFn grad,
-                                                                float* __restrict__ d_pos, uint32_t l0, uint32_t l1) {
-  const int64_t i = (int64_t)blockIdx.x * kDposThreads + threadIdx.x;
-  if (i >= n) return;
-  float x, y, z;
-  pos(i, x, y, z);
-  float r0 = 0.f, r1 = 0.f, r2 = 0.f;
-  if (l0 > 0) {
-    r0 = d_pos[3 * i + 0];
-    r1 = d_pos[3 * i + 1];
-    r2 = d_pos[3 * i + 2];
-  }
-  for (uint32_t l = l0; l < l1; ++l) {
-    const LevelParams& p = a.lv[l];
+// One level's term of sample i, added to its running sums (r0, r1, r2).
+template <class GradFn>
+__device__ __forceinline__ void dpos_level(const LevelParams& p, uint32_t l, int64_t i, float x, float y, float z,
+                                           const uint32_t* __restrict__ table, const GradFn& grad, float& r0,
+                                           float& r1, float& r2) {
+  {
     Corners c;
     level_corners(p, x, y, z, c);
     uint32_t raw[8];
@@ -1424,9 +1417,61 @@ __global__ void __launch_bounds__(kDposThreads) k_hashgrid_dpos(GridArgs a, PosF
     r1 += g.y * dy[1][1];
     r2 += g.y * dy[1][2];
   }
+}
+
+template <class PosFn, class GradFn>
+__global__ void __launch_bounds__(kDposThreads) k_hashgrid_dpos(GridArgs a, PosFn pos, int64_t n,
+                                                                const uint32_t* __restrict__ table, GradFn grad,
+                                                                float* __restrict__ d_pos, uint32_t l0, uint32_t l1) {
+  const int64_t i = (int64_t)blockIdx.x * kDposThreads + threadIdx.x;
+  if (i >= n) return;
+  float x, y, z;
+  pos(i, x, y, z);
+  float r0 = 0.f, r1 = 0.f, r2 = 0.f;
+  if (l0 > 0) {
+    r0 = d_pos[3 * i + 0];
+    r1 = d_pos[3 * i + 1];
+    r2 = d_pos[3 * i + 2];
+  }
+  for (uint32_t l = l0; l < l1; ++l) dpos_level(a.lv[l], l, i, x, y, z, table, grad, r0, r1, r2);
   d_pos[3 * i + 0] = r0;
   d_pos[3 * i + 1] = r1;
   d_pos[3 * i + 2] = r2;
+}
+
+// The same sums with K samples per thread (samples blockIdx.x K kDposThreads + k kDposThreads + t) and
+// the levels as the OUTER loop, running sums in registers: the whole grid walks the levels roughly
+// together (every workgroup starts at level 0), so the live table slices stay few without the passes'
+// re-reads and re-writes of the running sums.  Same additions per sample in the same order: bitwise
+// the result of k_hashgrid_dpos.
+template <class PosFn, class GradFn, int K>
+__global__ void __launch_bounds__(kDposThreads) k_hashgrid_dpos_k(GridArgs a, PosFn pos, int64_t n,
+                                                                  const uint32_t* __restrict__ table, GradFn grad,
+                                                                  float* __restrict__ d_pos) {
+  const int64_t base = (int64_t)blockIdx.x * K * kDposThreads + threadIdx.x;
+  float r[K][3];
+#pragma unroll
+  for (int k = 0; k < K; ++k) r[k][0] = r[k][1] = r[k][2] = 0.f;
+  for (uint32_t l = 0; l < a.n_levels; ++l) {
+    const LevelParams& p = a.lv[l];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int64_t i = base + (int64_t)k * kDposThreads;
+      const bool in = i < n;
+      float x = 0.f, y = 0.f, z = 0.f;
+      pos.wave(i, n, in, x, y, z);
+      if (in) dpos_level(p, l, i, x, y, z, table, grad, r[k][0], r[k][1], r[k][2]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int64_t i = base + (int64_t)k * kDposThreads;
+    if (i < n) {
+      d_pos[3 * i + 0] = r[k][0];
+      d_pos[3 * i + 1] = r[k][1];
+      d_pos[3 * i + 2] = r[k][2];
+    }
+  }
 }
 
 template <class PosFn, class GradFn>
@@ -1437,6 +1482,19 @@ static int launch_dpos(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint1
   const GridArgs a = make_args(d, pos.samples_per_ray());
   const int64_t nb = (n + kDposThreads - 1) / kDposThreads;
   LNR_REQUIRE(nb < (int64_t(1) << 31), "%s: n=%lld too large", who, (long long)n);
+  const char* ek = getenv("LONER_DPOS_SPT");
+  const int spt = ek ? atoi(ek) : LNR_DPOS_SPT;
+  if (spt == 2 || spt == 4 || spt == 8) {
+    const unsigned g = (unsigned)((n + (int64_t)spt * kDposThreads - 1) / ((int64_t)spt * kDposThreads));
+    const uint32_t* tb = reinterpret_cast<const uint32_t*>(table);
+    if (spt == 2)
+      hipLaunchKernelGGL((k_hashgrid_dpos_k<PosFn, GradFn, 2>), dim3(g), dim3(kDposThreads), 0, st, a, pos, n, tb, grad, d_pos);
+    else if (spt == 4)
+      hipLaunchKernelGGL((k_hashgrid_dpos_k<PosFn, GradFn, 4>), dim3(g), dim3(kDposThreads), 0, st, a, pos, n, tb, grad, d_pos);
+    else
+      hipLaunchKernelGGL((k_hashgrid_dpos_k<PosFn, GradFn, 8>), dim3(g), dim3(kDposThreads), 0, st, a, pos, n, tb, grad, d_pos);
+    LNR_RETURN_LAUNCH(who);
+  }
   const char* e = getenv("LONER_DPOS_LEVELS_PER_PASS");
   const uint32_t per = e ? (uint32_t)std::max(1, atoi(e)) : (uint32_t)LNR_DPOS_LEVELS_PER_PASS;
   for (uint32_t l0 = 0; l0 < d->n_levels; l0 += per)

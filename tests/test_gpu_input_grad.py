@@ -146,6 +146,32 @@ def test_hashgrid_dpos_rays_and_compact_forms(L):
     assert np.all(g[2 * o[3]:2 * o[9]] == 0) and np.all(g[:2 * o[3]] == 7) and np.all(g[2 * o[9]:] == 7)
 
 
+@pytest.mark.parametrize("spt", ["2", "4", "8"])
+def test_hashgrid_dpos_launch_shapes_bitwise(L, spt, monkeypatch):
+    """The one-launch level-outer d_pos kernel (LONER_DPOS_SPT samples per thread) and the level-pass
+    launches (LONER_DPOS_LEVELS_PER_PASS) give the same bits: the same additions per sample in the same
+    order.  A ragged sample count (not a multiple of spt x 256)."""
+    rng = np.random.default_rng(8)
+    R, S = 37, 128
+    rays, z, pos = _ray_positions(rng, R, S)
+    n = R * S
+    lay = ohg.GridLayout(16, 2, 18, 16)
+    d = L.grid_desc(16, 2, 18, 16)
+    t16 = cu(rng.uniform(-1, 1, (lay.n_entries, 2)).astype(np.float16).view(np.int16))
+    denc = cu(rng.normal(0, 1, (16, n, 2)).astype(np.float32))
+    outs = []
+    for env in ({"LONER_DPOS_SPT": "0", "LONER_DPOS_LEVELS_PER_PASS": "16"},
+                {"LONER_DPOS_SPT": "0", "LONER_DPOS_LEVELS_PER_PASS": "3"}, {"LONER_DPOS_SPT": spt}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        dp = torch.full((n, 3), 7.0, dtype=torch.float32, device="cuda")
+        L.call("lnr_hashgrid_bwd_rays", ctypes.byref(d), cu(rays), cu(z), R, S, denc, n, None, t16, dp, None, 0, 0,
+               L.stream())
+        torch.cuda.synchronize()
+        outs.append(dp)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
 def _field(tc, seed=0):
     m = tc.NetworkWithInputEncoding(n_input_dims=3, n_output_dims=1, encoding_config=SIGMA_ENC,
                                     network_config=SIGMA_NET)

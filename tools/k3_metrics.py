@@ -57,8 +57,14 @@ def main():
     s = L.stream()
     per_pass = {}
     ref_out = None
-    for per in (16, 8, 4, 2, 1):  # levels per launch (LONER_DPOS_LEVELS_PER_PASS, read per call)
-        os.environ["LONER_DPOS_LEVELS_PER_PASS"] = str(per)
+    # levels per launch (LONER_DPOS_LEVELS_PER_PASS, read per call), then the one-launch level-outer
+    # kernel at K samples per thread (LONER_DPOS_SPT = K)
+    for per in (16, 8, 4, 2, 1, "spt2", "spt4", "spt8"):
+        if isinstance(per, int):
+            os.environ["LONER_DPOS_SPT"] = "0"
+            os.environ["LONER_DPOS_LEVELS_PER_PASS"] = str(per)
+        else:
+            os.environ["LONER_DPOS_SPT"] = per[3:]
         times = []
         for it in range(13):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -73,6 +79,7 @@ def main():
             ref_out = out.clone()
         assert torch.equal(out, ref_out), per  # the split does not change a bit
     os.environ.pop("LONER_DPOS_LEVELS_PER_PASS")
+    os.environ.pop("LONER_DPOS_SPT")
     ms = min(per_pass.values())
     # bytes per sample: 512 B of fp16 corner gathers (16 levels x 8 corners x 4 B), 128 B of d_enc, 12 B out
     print(json.dumps(dict(dpos_rel_l2=overall, dpos_rel_l2_worst_level=max(per_level),
