@@ -470,7 +470,22 @@ constexpr int rows_stages() {
   return LNR_SCATTER_STAGES ? LNR_SCATTER_STAGES : (sizeof(typename GradFn::Raw) <= 4 || NB > 64 ? 1 : 2);
 }
 template <class GradFn, int NB>
-constexpr int rows_waves() { return rows_stages<GradFn, NB>() == 1 ? 6 : 4; }
+#ifndef LNR_ROWS_STAGE12
+#define LNR_ROWS_STAGE12 0  // (experiment) the stage as {word, values} + slot arrays, 12 B a record
+#endif
+#ifndef LNR_ROWS_G_AHEAD
+#define LNR_ROWS_G_AHEAD 0  // (experiment) levels of gradient loaded ahead (0: all in the prologue)
+#endif
+#ifndef LNR_ROWS_COH_HALF
+#define LNR_ROWS_COH_HALF 0  // (experiment) coherent levels' run sums 8 values at a time
+#endif
+#ifndef LNR_ROWS_PLACE_SEQ
+#define LNR_ROWS_PLACE_SEQ 0  // (experiment) records ranked and placed this many at a time (0: all 4)
+#endif
+#ifndef LNR_ROWS_WAVES1
+#define LNR_ROWS_WAVES1 6  // waves per SIMD of the one-stage scatter (8 needs <= 64 VGPRs and <= 40 KB LDS)
+#endif
+constexpr int rows_waves() { return rows_stages<GradFn, NB>() == 1 ? LNR_ROWS_WAVES1 : 4; }
 #ifndef LNR_PRESCALE
 #define LNR_PRESCALE 1
 #endif
@@ -483,7 +498,12 @@ struct RowsLds {  // the small tables first: their addresses fit the 16-bit LDS 
   uint32_t total[NL];         // records of the row at each level
   uint32_t ctr[2][NB];        // rank counters
   LevelParams lv[NL];         // the level table (kernel arguments indexed per level would be loads)
+#if LNR_ROWS_STAGE12
+  uint2 stage[STG][kRowsCap];      // staged records {word, fp16 value pair}, bucket order
+  uint32_t stage_slot[STG][kRowsCap];  // and their global slots (12 B a record: 26 KB for one stage)
+#else
   uint4 stage[STG][kRowsCap];  // staged records {word, global slot, fp16 value pair, -}, bucket order
+#endif
 };
 
 // NL levels, the first NM coherent (run-merging) and the rest fine, at most NB buckets per level:
@@ -511,10 +531,11 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
   if (threadIdx.x < 2 * NB) (&sm.ctr[0][0])[threadIdx.x] = 0u;
   // prologue 2: every global load of the kernel
   const typename PosFn::Raw raw = pos.load(ic);
-  typename GradFn::Raw g[NL];  // (GradJac: the fp16 pair, scaled by d sigma at use: half the registers)
+  constexpr int kGA = LNR_ROWS_G_AHEAD > 0 && LNR_ROWS_G_AHEAD < NL ? LNR_ROWS_G_AHEAD : NL;
+  typename GradFn::Raw g[kGA];  // (GradJac: the fp16 pair, scaled by d sigma at use: half the registers)
 #pragma unroll
-  for (int l = 0; l < NL; ++l) g[l] = grad.load_raw_nt(LB + l, ic);  // read once: nontemporal, so they do not
-                                                                // displace the runs' L2 lines
+  for (int l = 0; l < kGA; ++l) g[l] = grad.load_raw_nt(LB + l, ic);  // read once: nontemporal, so they do not
+                                                                 // displace the runs' L2 lines
   const float gsc = grad.scale(ic);
   uint32_t h0[2][2], h1[2][2];
   uint64_t seg[2][2];
@@ -576,9 +597,15 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
       if ((uint32_t)(u * kSB) < lim) {
         const uint32_t t = threadIdx.x + u * kSB;
         if (t < lim) {
+#if LNR_ROWS_STAGE12
+          const uint2 q = sm.stage[sbuf][t];
+          const uint32_t sl = sm.stage_slot[sbuf][t];
+          ws.rec[sl < spare ? sl : spare] = q;
+#else
           const uint4 q = sm.stage[sbuf][t];
           const uint32_t d = q.y < spare ? q.y : spare;  // (the bound: never a store outside the records)
           ws.rec[d] = make_uint2(q.x, q.z);
+#endif
         }
       }
     }
@@ -593,7 +620,8 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
     const bool staged = sm.total[l] <= (uint32_t)kRowsCap;  // block-uniform
     uint32_t* ctr = sm.ctr[sbuf];
     const uint2* sgl = sm.sg[l];
-    const float2 gl = GradFn::finish(g[l], gsc);
+    const float2 gl = GradFn::finish(g[l % kGA], gsc);
+    if (kGA < NL && l + kGA < NL) g[l % kGA] = grad.load_raw_nt(LB + l + kGA, ic);  // (experiment) kGA levels ahead
 #if LNR_PRESCALE
     // the level's record scale applied to the gradient once, not to every record value: a power of
     // two, so w (g 2^k) rounds exactly as (w g) 2^k
@@ -609,19 +637,35 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
       if (valid) {
         uint2 s4[4];
         uint32_t rank[4];
+#if LNR_ROWS_PLACE_SEQ
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // (experiment) two records at a time: fewer live registers
+          if (k % LNR_ROWS_PLACE_SEQ == 0) {
+#pragma unroll
+            for (int m = k; m < k + LNR_ROWS_PLACE_SEQ; ++m) s4[m] = sgl[bk[m]];
+#pragma unroll
+            for (int m = k; m < k + LNR_ROWS_PLACE_SEQ; ++m) rank[m] = atomicAdd(&ctr[bk[m]], 1u);
+          }
+#else
 #pragma unroll
         for (int k = 0; k < 4; ++k) s4[k] = sgl[bk[k]];
 #pragma unroll
         for (int k = 0; k < 4; ++k) rank[k] = atomicAdd(&ctr[bk[k]], 1u);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
+#endif
           const uint32_t slot = s4[k].y + rank[k];
           const uint32_t h = rec_half2(val[k].x, val[k].y, rs);
           if (staged) {  // three 32-bit fields (ds_write2_b32 + ds_write_b32: no register moves for a b128 quad)
+#if LNR_ROWS_STAGE12
+            sm.stage[stg][s4[k].x + rank[k]] = make_uint2(word[k], h);
+            sm.stage_slot[stg][s4[k].x + rank[k]] = slot;
+#else
             uint32_t* q = reinterpret_cast<uint32_t*>(&sm.stage[stg][s4[k].x + rank[k]]);
             q[0] = word[k];
             q[1] = slot;
             q[2] = h;
+#endif
           } else {  // (block-uniform) more records than the stage holds: each straight to its global slot
             ws.rec[slot < spare ? slot : spare] = make_uint2(word[k], h);
           }
@@ -660,6 +704,29 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
       Corners c;
       level_corners<true>(lv, x, y, z, c);
       const uint32_t off = lv.offset;
+#if LNR_ROWS_COH_HALF
+      // (experiment) corners 0-3, then 4-7: half the run-summed values live at a time
+      const RunInfo ri = cell_runs_dpp(in, c.cx, c.cy, c.cz);
+      const bool valid = in && ri.tail;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float v[8];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          v[2 * kk] = c.w[4 * h + kk] * gv.x;
+          v[2 * kk + 1] = c.w[4 * h + kk] * gv.y;
+        }
+        run_sum_dpp_n<8>(ri, v);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const uint32_t e = c.idx[4 * h + kk] - off;
+          bk4[kk] = e >> kChunkLog2;
+          w4[kk] = e & (kChunk - 1);
+          val4[kk] = make_float2(v[2 * kk], v[2 * kk + 1]);
+        }
+        place(valid, bk4, w4, val4);
+      }
+#else
       RunInfo ri;
       float v[16];
       coherent_run_values(c, in, gv.x, gv.y, ri, v);
@@ -676,6 +743,7 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
         }
         place(valid, bk4, w4, val4);
       }
+#endif
     }
     if (threadIdx.x < NB) sm.ctr[sbuf ^ 1][threadIdx.x] = 0u;  // level l + 1's counters (last used by l - 1)
     if (kRowsStages == 2) {
@@ -765,6 +833,9 @@ __device__ __forceinline__ unsigned long long fixed_i64(float x) {
 #ifndef LNR_ACCUM_TRIP
 #define LNR_ACCUM_TRIP 2
 #endif
+#ifndef LNR_ACCUM_BANKSORT
+#define LNR_ACCUM_BANKSORT 0  // (experiment) bits of the bank-pair index sorted on inside each wave, 0..5
+#endif
 constexpr int kAccumTrip = LNR_ACCUM_TRIP;        // tiles per trip of the accumulate loop (loads ahead)
 constexpr int kTile = 2 * kAccumThreads;         // records per tile: 2 per thread
 static_assert(kTile == 2048, "the stage's swizzle and the strided reads assume 64-lane waves x 16 x 2");
@@ -822,6 +893,45 @@ __device__ __forceinline__ void accum_records(unsigned long long* acc, uint2* st
     *reinterpret_cast<u32x4*>(&stage[stage_pos(2 * threadIdx.x)]) = cur;
     lds_barrier();
     const uint64_t base = beg2 + tile * kTile;
+#if LNR_ACCUM_BANKSORT
+    // (experiment) each atomic instruction's 64 records radix-sorted inside the wave on the low
+    // LNR_ACCUM_BANKSORT bits of their bank pair (e0 mod 32: acc[e0] and acc[kChunk + e0] share it),
+    // ballot + mbcnt + ds_permute per bit, then dealt alternately to the two 32-lane halves, so a
+    // bank's records split over the halves.  Records outside [beg, end) become zero adds to entry 0.
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      uint2 rec = stage[stage_pos(q0 + r)];
+      const uint64_t rr = base + q0 + r;
+      if (!(rr >= beg && rr < end)) rec = make_uint2(0u, 0u);
+#pragma unroll
+      for (int bit = 0; bit < LNR_ACCUM_BANKSORT; ++bit) {
+        const bool one = (rec.x >> bit) & 1u;
+        const uint64_t m = __ballot(one);
+        const uint32_t below = one ? __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))
+                                   : __builtin_amdgcn_mbcnt_hi(~(uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo(~(uint32_t)m, 0u));
+        uint32_t dst = one ? (uint32_t)(64 - __popcll(m)) + below : below;
+        if (bit == LNR_ACCUM_BANKSORT - 1) dst = (dst >> 1) + ((dst & 1u) << 5);
+        rec.x = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)rec.x);
+        rec.y = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)rec.y);
+      }
+      {
+        const uint32_t w = rec.x;
+        const float v0 = rec_v0(rec.y), v1 = rec_v1(rec.y);
+        const uint32_t e0 = w & (kChunk - 1);
+        const uint32_t p = (w >> kChunkLog2) & 15u;
+        const float tx = (float)(w >> 16) * ftx;
+        const float s0 = fs - tx;
+        atomicAdd(&acc[e0], fixed_i64(s0 * v0));
+        atomicAdd(&acc[kChunk + e0], fixed_i64(s0 * v1));
+        if (p) {
+          const uint32_t e1 = e0 ^ ((1u << p) - 1u);
+          atomicAdd(&acc[e1], fixed_i64(tx * v0));
+          atomicAdd(&acc[kChunk + e1], fixed_i64(tx * v1));
+        }
+      }
+    }
+    return;
+#endif
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const uint2 rec = stage[stage_pos(q0 + r)];
