@@ -86,6 +86,9 @@ __device__ __forceinline__ void fine_gather_paired(const uint32_t* __restrict__ 
 // takes samples t and t + kSB / 2 of the row, so each wave still covers 64-sample groups (the
 // coherent levels' run merging sees the lanes the scatter sees), and a fine level's gathers of both
 // samples are in flight together.
+#ifndef LNR_ENC_LPB
+#define LNR_ENC_LPB 1  // levels per workgroup (experiment: 2 decodes each position once for two levels)
+#endif
 #ifndef LNR_ENC_WAVES
 #define LNR_ENC_WAVES 8  // waves per SIMD asked of the encode (68 registers would allow 7)
 #endif
@@ -96,13 +99,9 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
                                                                BwdWorkspace ws, const float* __restrict__ live) {
   constexpr int H = kSB / kEncSpt;
   const int64_t i0 = (int64_t)blockIdx.x * kSB + threadIdx.x;
-  const uint32_t l = blockIdx.y;
   const bool count = ws.hist != nullptr;
   if (!count && (i0 & ~(int64_t)1) >= n) return;  // (lane pairs leave together: fine_gather_paired)
   __shared__ uint32_t hist[kMaxChunksPerLevel];
-  if (count) {
-    for (int b = threadIdx.x; b < kMaxChunksPerLevel; b += blockDim.x) hist[b] = 0;
-  }
   bool in[kEncSpt], use[kEncSpt];
   float x[kEncSpt], y[kEncSpt], z[kEncSpt];
 #pragma unroll
@@ -114,6 +113,13 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
     use[h] = in[h] && (live == nullptr || live[i] != 0.f);
     x[h] = y[h] = z[h] = 0.f;
     pos.wave(i, n, in[h], x[h], y[h], z[h]);
+  }
+  // LNR_ENC_LPB levels per workgroup (grid.y = L / LNR_ENC_LPB): the position is decoded once for them
+  for (int li = 0; li < LNR_ENC_LPB; ++li) {
+  const uint32_t l = blockIdx.y * LNR_ENC_LPB + li;
+  if (count) {
+    if (li > 0) lds_barrier();  // the previous level's histogram is published
+    for (int b = threadIdx.x; b < kMaxChunksPerLevel; b += blockDim.x) hist[b] = 0;
   }
   const LevelParams& lv = a.lv[l];
   if (lv.fine) {  // block-uniform
@@ -154,7 +160,7 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
       lds_barrier();
       publish_block_counts(a, l, hist, ws);
     }
-    return;
+    continue;
   }
   // coherent levels below a.enc_run_levels: only the head lane of each run of lanes in one cell
   // gathers the 8 corners, and the run's other lanes take them from it (ds_bpermute, the LDS
@@ -209,6 +215,7 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
   if (count) {
     lds_barrier();
     publish_block_counts(a, l, hist, ws);
+  }
   }
 }
 
@@ -335,6 +342,8 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
   // with a ``live`` mask (C3's colour encode, most samples dead): plain gathers, so dead lanes issue
   // none, two samples per thread from LNR_ENC_SPT2_MIN_N samples
   const bool spt2 = n >= (int64_t)LNR_ENC_SPT2_MIN_N;
+  LNR_REQUIRE(d->n_levels % LNR_ENC_LPB == 0, "%s: %u levels, not a multiple of %d per workgroup", who, d->n_levels,
+              LNR_ENC_LPB);
   if (bwd_ws) {
     LNR_REQUIRE(bwd_ws_bytes >= bwd_workspace_bytes(d, n), "%s: backward workspace too small", who);
     LNR_REQUIRE(a.n_buckets <= (uint32_t)kMaxBuckets, "%s: too many table chunks (%u)", who, a.n_buckets);
@@ -343,12 +352,12 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
                   "%s: level %u has more than %d table chunks", who, l, kMaxChunksPerLevel);
     BwdWorkspace w = carve_workspace(bwd_ws, a, d, n);
     // one workgroup per histogram row (kSB samples) so the row is written whole
-    dim3 gridc((unsigned)w.n_sb, d->n_levels);
+    dim3 gridc((unsigned)w.n_sb, d->n_levels / LNR_ENC_LPB);
     hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED>), gridc, dim3(kSB), 0, st, a, pos, n,
                        reinterpret_cast<const uint32_t*>(table), enc, enc_stride, w, nullptr);
   } else {
     // kSB-sample workgroups as in training (C2-size eval launch: 1011 us at 256 one-sample threads, 836 at 512)
-    dim3 grid((unsigned)((n + kSB - 1) / kSB), d->n_levels);
+    dim3 grid((unsigned)((n + kSB - 1) / kSB), d->n_levels / LNR_ENC_LPB);
     const uint32_t* tb = reinterpret_cast<const uint32_t*>(table);
     if (live == nullptr)
       hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED>), grid, dim3(kSB), 0, st, a, pos, n, tb, enc,
