@@ -3,11 +3,12 @@
 // Replaces tcnn's kernel_grid behind tcnn.NetworkWithInputEncoding (src/models/nerf_tcnn.py:35-38,
 // 68, 71) and tcnn.Encoding (:40, 64).  The backward lives in hashgrid_bwd.hip.
 //
-// Launch shape: grid (ceil(N / kSB), n_levels) of kSB-thread workgroups (kSB = 512 samples, one
-// histogram row each; the live-masked eval launch: kSB / 2 threads of two samples), with the LEVEL
-// as the slow grid dimension, so the dispatcher walks level by level and the live gather footprint
-// is one level's table slice (<= 1 MB fp16) — L2-resident on every XCD — instead of the whole
-// 14.8 MB table.
+// Launch shape: grid (ceil(N / kSB), n_levels / 2) of kSB-thread workgroups (kSB = 512 samples, one
+// histogram row each), each taking two consecutive levels (LNR_ENC_LPB; one level when n_levels is
+// odd, and for the live-masked eval launch: grid (ceil(N / kSB), n_levels) of kSB / 2 threads of two
+// samples), with the LEVEL as the slow grid dimension, so the dispatcher walks level pair by level
+// pair and the live gather footprint is two levels' table slices (<= 2 MB fp16) — L2-resident on
+// every XCD — instead of the whole 14.8 MB table.
 // Output layout is level-major half2 (enc[l * stride + n]) so every store is a coalesced 4 B/lane.
 // In training mode the forward also emits the backward's per-block record histogram (same
 // corners), which removes a full corner-recompute pass from the backward.
@@ -87,12 +88,12 @@ __device__ __forceinline__ void fine_gather_paired(const uint32_t* __restrict__ 
 // coherent levels' run merging sees the lanes the scatter sees), and a fine level's gathers of both
 // samples are in flight together.
 #ifndef LNR_ENC_LPB
-#define LNR_ENC_LPB 1  // levels per workgroup (experiment: 2 decodes each position once for two levels)
+#define LNR_ENC_LPB 2  // levels per workgroup of the training / plain eval encode (C2: 0.681 -> 0.669 ms)
 #endif
 #ifndef LNR_ENC_WAVES
 #define LNR_ENC_WAVES 8  // waves per SIMD asked of the encode (68 registers would allow 7)
 #endif
-template <class PosFn, int kEncSpt, bool PAIRED>
+template <class PosFn, int kEncSpt, bool PAIRED, int LPB = 1>
 __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per_eu(LNR_ENC_WAVES, LNR_ENC_WAVES))) k_hashgrid_fwd(GridArgs a, PosFn pos, int64_t n,
                                                                const uint32_t* __restrict__ table,
                                                                uint32_t* __restrict__ enc, int64_t stride,
@@ -114,9 +115,11 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
     x[h] = y[h] = z[h] = 0.f;
     pos.wave(i, n, in[h], x[h], y[h], z[h]);
   }
-  // LNR_ENC_LPB levels per workgroup (grid.y = L / LNR_ENC_LPB): the position is decoded once for them
-  for (int li = 0; li < LNR_ENC_LPB; ++li) {
-  const uint32_t l = blockIdx.y * LNR_ENC_LPB + li;
+  // LPB consecutive levels per workgroup (grid.y = L / LPB), in level order: the sample's position is
+  // decoded and its depth loaded once for them.  Two levels' table slices (<= 2 MB) still fit an
+  // XCD's L2; four (lpb 4: 0.720 ms) do not.
+  for (int li = 0; li < LPB; ++li) {
+  const uint32_t l = blockIdx.y * LPB + li;
   if (count) {
     if (li > 0) lds_barrier();  // the previous level's histogram is published
     for (int b = threadIdx.x; b < kMaxChunksPerLevel; b += blockDim.x) hist[b] = 0;
@@ -342,8 +345,7 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
   // with a ``live`` mask (C3's colour encode, most samples dead): plain gathers, so dead lanes issue
   // none, two samples per thread from LNR_ENC_SPT2_MIN_N samples
   const bool spt2 = n >= (int64_t)LNR_ENC_SPT2_MIN_N;
-  LNR_REQUIRE(d->n_levels % LNR_ENC_LPB == 0, "%s: %u levels, not a multiple of %d per workgroup", who, d->n_levels,
-              LNR_ENC_LPB);
+  const bool lpb = LNR_ENC_LPB == 2 && d->n_levels % 2 == 0;  // two levels per workgroup when they pair up
   if (bwd_ws) {
     LNR_REQUIRE(bwd_ws_bytes >= bwd_workspace_bytes(d, n), "%s: backward workspace too small", who);
     LNR_REQUIRE(a.n_buckets <= (uint32_t)kMaxBuckets, "%s: too many table chunks (%u)", who, a.n_buckets);
@@ -352,14 +354,21 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
                   "%s: level %u has more than %d table chunks", who, l, kMaxChunksPerLevel);
     BwdWorkspace w = carve_workspace(bwd_ws, a, d, n);
     // one workgroup per histogram row (kSB samples) so the row is written whole
-    dim3 gridc((unsigned)w.n_sb, d->n_levels / LNR_ENC_LPB);
-    hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED>), gridc, dim3(kSB), 0, st, a, pos, n,
-                       reinterpret_cast<const uint32_t*>(table), enc, enc_stride, w, nullptr);
+    dim3 gridc((unsigned)w.n_sb, lpb ? d->n_levels / 2 : d->n_levels);
+    if (lpb)
+      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 2>), gridc, dim3(kSB), 0, st, a, pos, n,
+                         reinterpret_cast<const uint32_t*>(table), enc, enc_stride, w, nullptr);
+    else
+      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED>), gridc, dim3(kSB), 0, st, a, pos, n,
+                         reinterpret_cast<const uint32_t*>(table), enc, enc_stride, w, nullptr);
   } else {
     // kSB-sample workgroups as in training (C2-size eval launch: 1011 us at 256 one-sample threads, 836 at 512)
-    dim3 grid((unsigned)((n + kSB - 1) / kSB), d->n_levels / LNR_ENC_LPB);
+    dim3 grid((unsigned)((n + kSB - 1) / kSB), d->n_levels);
     const uint32_t* tb = reinterpret_cast<const uint32_t*>(table);
-    if (live == nullptr)
+    if (live == nullptr && lpb)
+      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 2>), dim3(grid.x, d->n_levels / 2), dim3(kSB), 0, st, a,
+                         pos, n, tb, enc, enc_stride, BwdWorkspace{}, live);
+    else if (live == nullptr)
       hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED>), grid, dim3(kSB), 0, st, a, pos, n, tb, enc,
                          enc_stride, BwdWorkspace{}, live);
     else if (spt2)

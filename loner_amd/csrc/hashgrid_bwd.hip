@@ -455,7 +455,16 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
 //  * A (row, level) with more than kRowsCap records (coherent rows whose runs did not merge) writes
 //    every record straight to its global slot instead (same slots, unstaged).
 // Same records, counts and blockmax as k_bwd_scatter.
-constexpr int kRowsCap = 2176;  // 4.25 records per sample: fine rows hold 4 + the rare split pairs
+#ifndef LNR_ROWS_CAP
+#define LNR_ROWS_CAP 2176
+#endif
+#ifndef LNR_ROWS_SG_SPLIT
+#define LNR_ROWS_SG_SPLIT 0  // (experiment) bucket starts as u16 + global slots as u32 (6 B per bucket, not 8)
+#endif
+#ifndef LNR_ROWS_LV_ARGS
+#define LNR_ROWS_LV_ARGS 0  // (experiment) level parameters read from the kernel arguments, not staged in LDS
+#endif
+constexpr int kRowsCap = LNR_ROWS_CAP;  // 4.25 records per sample: fine rows hold 4 + the rare split pairs
 // Stages: 1, one stage with the copy-out after each level's placement: 44 KB of LDS and 80 VGPRs
 // (GradJac: the Jacobian held as fp16 pairs), so 3 workgroups (6 waves per SIMD) share a CU; 2, a
 // double-buffered stage with the copy-out of level l - 1 overlapping level l, 79 KB, 2 workgroups
@@ -494,10 +503,17 @@ constexpr int rows_waves() { return rows_stages<GradFn, NB>() == 1 ? LNR_ROWS_WA
 #endif
 template <int NL, int NB, int STG>
 struct RowsLds {  // the small tables first: their addresses fit the 16-bit LDS instruction offset
+#if LNR_ROWS_SG_SPLIT
+  uint32_t sg_slot[NL][NB];   // per level and bucket: global slot of the run
+  uint16_t sg_start[NL][NB];  // and its start in the stage
+#else
   uint2 sg[NL][NB];           // per level and bucket: {start in the stage, global slot of the run}
+#endif
   uint32_t total[NL];         // records of the row at each level
   uint32_t ctr[2][NB];        // rank counters
+#if !LNR_ROWS_LV_ARGS
   LevelParams lv[NL];         // the level table (kernel arguments indexed per level would be loads)
+#endif
 #if LNR_ROWS_STAGE12
   uint2 stage[STG][kRowsCap];      // staged records {word, fp16 value pair}, bucket order
   uint32_t stage_slot[STG][kRowsCap];  // and their global slots (12 B a record: 26 KB for one stage)
@@ -526,8 +542,10 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
   const uint32_t spare = (uint32_t)(8 * n * (int64_t)a.n_levels);  // one of the 2 slack records past the last slot
 
   // prologue 1: the level table and zero rank counters
+#if !LNR_ROWS_LV_ARGS
   if (threadIdx.x < NL * (sizeof(LevelParams) / 4))
     reinterpret_cast<uint32_t*>(sm.lv)[threadIdx.x] = reinterpret_cast<const uint32_t*>(a.lv + LB)[threadIdx.x];
+#endif
   if (threadIdx.x < 2 * NB) (&sm.ctr[0][0])[threadIdx.x] = 0u;
   // prologue 2: every global load of the kernel
   const typename PosFn::Raw raw = pos.load(ic);
@@ -569,8 +587,19 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
       const uint32_t c1 = 2 * lane + 1 < nb ? h1[p][1] - h0[p][1] : 0u;
       const uint32_t inc = wave_incl_scan_u32(c0 + c1);
       const uint32_t ex = inc - c0 - c1;
+#if LNR_ROWS_SG_SPLIT
+      if (2 * lane < nb) {
+        sm.sg_start[l][2 * lane] = (uint16_t)ex;
+        sm.sg_slot[l][2 * lane] = (uint32_t)(seg[p][0] + h0[p][0]);
+      }
+      if (2 * lane + 1 < nb) {
+        sm.sg_start[l][2 * lane + 1] = (uint16_t)(ex + c0);
+        sm.sg_slot[l][2 * lane + 1] = (uint32_t)(seg[p][1] + h0[p][1]);
+      }
+#else
       if (2 * lane < nb) sm.sg[l][2 * lane] = make_uint2(ex, (uint32_t)(seg[p][0] + h0[p][0]));
       if (2 * lane + 1 < nb) sm.sg[l][2 * lane + 1] = make_uint2(ex + c0, (uint32_t)(seg[p][1] + h0[p][1]));
+#endif
       if (lane == 63) sm.total[l] = inc;
     }
   }
@@ -616,10 +645,19 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
   for (int l = 0; l < NL; ++l) {
     const int sbuf = l & 1;  // rank counters (and, with two stages, the stage)
     const int stg = kRowsStages == 2 ? sbuf : 0;
+#if LNR_ROWS_LV_ARGS
+    const LevelParams lv = a.lv[LB + l];
+#else
     const LevelParams lv = sm.lv[l];
+#endif
     const bool staged = sm.total[l] <= (uint32_t)kRowsCap;  // block-uniform
     uint32_t* ctr = sm.ctr[sbuf];
+#if LNR_ROWS_SG_SPLIT
+    auto sgl_at = [&](uint32_t b) { return make_uint2(sm.sg_start[l][b], sm.sg_slot[l][b]); };
+#else
     const uint2* sgl = sm.sg[l];
+    auto sgl_at = [&](uint32_t b) { return sgl[b]; };
+#endif
     const float2 gl = GradFn::finish(g[l % kGA], gsc);
     if (kGA < NL && l + kGA < NL) g[l % kGA] = grad.load_raw_nt(LB + l + kGA, ic);  // (experiment) kGA levels ahead
 #if LNR_PRESCALE
@@ -642,13 +680,13 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
         for (int k = 0; k < 4; ++k) {  // (experiment) two records at a time: fewer live registers
           if (k % LNR_ROWS_PLACE_SEQ == 0) {
 #pragma unroll
-            for (int m = k; m < k + LNR_ROWS_PLACE_SEQ; ++m) s4[m] = sgl[bk[m]];
+            for (int m = k; m < k + LNR_ROWS_PLACE_SEQ; ++m) s4[m] = sgl_at(bk[m]);
 #pragma unroll
             for (int m = k; m < k + LNR_ROWS_PLACE_SEQ; ++m) rank[m] = atomicAdd(&ctr[bk[m]], 1u);
           }
 #else
 #pragma unroll
-        for (int k = 0; k < 4; ++k) s4[k] = sgl[bk[k]];
+        for (int k = 0; k < 4; ++k) s4[k] = sgl_at(bk[k]);
 #pragma unroll
         for (int k = 0; k < 4; ++k) rank[k] = atomicAdd(&ctr[bk[k]], 1u);
 #pragma unroll

@@ -108,7 +108,7 @@ def main(tag, cfg, src=None):
         bench = json.load(open(os.path.join(out, "bench.json")))
         rec = {"stage": "hash-grid backward (one launch of the stage per step)", "config": cfg,
                "hbm_bytes_per_launch": total, "algorithmic_bytes_per_launch": bench["roofline"]["algorithmic_bytes_per_launch"],
-               "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving)",
+               "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving, validated per access pattern in profiles/r04_fetch_calibration.json)",
                "kernels": kern}
         json.dump(rec, open(os.path.join(prof, f"{tag}_traffic_{cfg}.json"), "w"), indent=1)
         print(f"traffic {total / 1e9:.3f} GB per launch vs algorithmic {rec['algorithmic_bytes_per_launch'] / 1e9:.3f} GB")
@@ -123,7 +123,7 @@ def main(tag, cfg, src=None):
                        "WRITE_SIZE passes over the bench command)", "config": cfg, "steps_profiled": n_steps,
                "hbm_bytes_per_step": total, "step_algorithmic_bytes": alg,
                "ratio_to_algorithmic": total / alg if alg else None,
-               "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving)",
+               "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving, validated per access pattern in profiles/r04_fetch_calibration.json)",
                "kernels": dict(sorted(kern.items(), key=lambda kv: -kv[1]["bytes_per_step"]))}
         json.dump(rec, open(os.path.join(prof, f"{tag}_traffic_{cfg}_step.json"), "w"), indent=1)
         print(f"step traffic {total / 1e9:.3f} GB per step vs algorithmic {(alg or 0) / 1e9:.3f} GB")
