@@ -3,12 +3,13 @@
 // Replaces tcnn's kernel_grid behind tcnn.NetworkWithInputEncoding (src/models/nerf_tcnn.py:35-38,
 // 68, 71) and tcnn.Encoding (:40, 64).  The backward lives in hashgrid_bwd.hip.
 //
-// Launch shape: grid (ceil(N / kSB), n_levels / 2) of kSB-thread workgroups (kSB = 512 samples, one
-// histogram row each), each taking two consecutive levels (LNR_ENC_LPB; one level when n_levels is
-// odd, and for the live-masked eval launch: grid (ceil(N / kSB), n_levels) of kSB / 2 threads of two
-// samples), with the LEVEL as the slow grid dimension, so the dispatcher walks level pair by level
-// pair and the live gather footprint is two levels' table slices (<= 2 MB fp16) — L2-resident on
-// every XCD — instead of the whole 14.8 MB table.
+// Launch shape: grid (ceil(N / kSB), n_levels / G) of kSB-thread workgroups (kSB = 512 samples, one
+// histogram row each), each taking G levels y, y + L/G, y + 2 L/G, ... (G = 4 from 512 rows, see
+// enc_levels_per_group; the live-masked eval launch: G = 1, kSB / 2 threads of two samples).  The
+// level group is the slow grid dimension, so the dispatcher walks group by group and the live gather
+// footprint is one group's table slices (<= 4 MB fp16, about an XCD's L2) instead of the whole
+// 14.8 MB table; and every group mixes coherent levels (position decoding, run detection: VALU) with
+// fine ones (hashed gathers: the texture addresser), so the two bottlenecks overlap.
 // Output layout is level-major half2 (enc[l * stride + n]) so every store is a coalesced 4 B/lane.
 // In training mode the forward also emits the backward's per-block record histogram (same
 // corners), which removes a full corner-recompute pass from the backward.
@@ -88,8 +89,22 @@ __device__ __forceinline__ void fine_gather_paired(const uint32_t* __restrict__ 
 // coherent levels' run merging sees the lanes the scatter sees), and a fine level's gathers of both
 // samples are in flight together.
 #ifndef LNR_ENC_LPB
-#define LNR_ENC_LPB 2  // levels per workgroup of the training / plain eval encode (C2: 0.681 -> 0.669 ms)
+#define LNR_ENC_LPB 4  // most levels per workgroup of the training / plain eval encode (1, 2 or 4)
 #endif
+#ifndef LNR_ENC_GROUP_MIN_ROWS
+#define LNR_ENC_GROUP_MIN_ROWS 512  // fewer rows: one level per workgroup (C1's 64 rows need the workgroups)
+#endif
+// Levels per workgroup for n levels and n_sb rows: G levels y, y + n/G, ... share a workgroup.
+// Measured at C2 (encode ms, tools/gpu_ab_libs.sh): one level 0.677; two consecutive levels 0.662;
+// two levels y, y + 8 0.618; four consecutive 0.720 (a 4 MB working set of fine levels); four levels
+// y, y + 4, y + 8, y + 12 0.605-0.612; eight 0.767, sixteen 0.890.  C3's sigma encode 1.188 / 1.135 /
+// 0.965 / 0.960 for one / two consecutive / two strided / four strided.
+inline int enc_levels_per_group(uint32_t n_levels, int64_t n_sb) {
+  if (n_sb < LNR_ENC_GROUP_MIN_ROWS) return 1;
+  for (int g = LNR_ENC_LPB; g > 1; g /= 2)
+    if (n_levels % g == 0) return g;
+  return 1;
+}
 #ifndef LNR_ENC_WAVES
 #define LNR_ENC_WAVES 8  // waves per SIMD asked of the encode (68 registers would allow 7)
 #endif
@@ -115,11 +130,11 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
     x[h] = y[h] = z[h] = 0.f;
     pos.wave(i, n, in[h], x[h], y[h], z[h]);
   }
-  // LPB consecutive levels per workgroup (grid.y = L / LPB), in level order: the sample's position is
-  // decoded and its depth loaded once for them.  Two levels' table slices (<= 2 MB) still fit an
-  // XCD's L2; four (lpb 4: 0.720 ms) do not.
+  // LPB levels per workgroup, y, y + L/LPB, y + 2 L/LPB, ... (grid.y = L / LPB), in level order: the
+  // sample's position is decoded and its depth loaded once for them, and a coherent level's VALU-heavy
+  // work runs beside a fine level's gathers (head comment)
   for (int li = 0; li < LPB; ++li) {
-  const uint32_t l = blockIdx.y * LPB + li;
+  const uint32_t l = blockIdx.y + li * gridDim.y;
   if (count) {
     if (li > 0) lds_barrier();  // the previous level's histogram is published
     for (int b = threadIdx.x; b < kMaxChunksPerLevel; b += blockDim.x) hist[b] = 0;
@@ -345,7 +360,12 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
   // with a ``live`` mask (C3's colour encode, most samples dead): plain gathers, so dead lanes issue
   // none, two samples per thread from LNR_ENC_SPT2_MIN_N samples
   const bool spt2 = n >= (int64_t)LNR_ENC_SPT2_MIN_N;
-  const bool lpb = LNR_ENC_LPB == 2 && d->n_levels % 2 == 0;  // two levels per workgroup when they pair up
+  const int lpb = enc_levels_per_group(d->n_levels, (n + kSB - 1) / kSB);
+  auto enc_kernel = [&]() {
+    return lpb == 4 ? k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 4>
+         : lpb == 2 ? k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 2>
+                    : k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 1>;
+  };
   if (bwd_ws) {
     LNR_REQUIRE(bwd_ws_bytes >= bwd_workspace_bytes(d, n), "%s: backward workspace too small", who);
     LNR_REQUIRE(a.n_buckets <= (uint32_t)kMaxBuckets, "%s: too many table chunks (%u)", who, a.n_buckets);
@@ -354,23 +374,16 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
                   "%s: level %u has more than %d table chunks", who, l, kMaxChunksPerLevel);
     BwdWorkspace w = carve_workspace(bwd_ws, a, d, n);
     // one workgroup per histogram row (kSB samples) so the row is written whole
-    dim3 gridc((unsigned)w.n_sb, lpb ? d->n_levels / 2 : d->n_levels);
-    if (lpb)
-      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 2>), gridc, dim3(kSB), 0, st, a, pos, n,
-                         reinterpret_cast<const uint32_t*>(table), enc, enc_stride, w, nullptr);
-    else
-      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED>), gridc, dim3(kSB), 0, st, a, pos, n,
-                         reinterpret_cast<const uint32_t*>(table), enc, enc_stride, w, nullptr);
+    dim3 gridc((unsigned)w.n_sb, d->n_levels / lpb);
+    hipLaunchKernelGGL(enc_kernel(), gridc, dim3(kSB), 0, st, a, pos, n, reinterpret_cast<const uint32_t*>(table), enc,
+                       enc_stride, w, nullptr);
   } else {
     // kSB-sample workgroups as in training (C2-size eval launch: 1011 us at 256 one-sample threads, 836 at 512)
     dim3 grid((unsigned)((n + kSB - 1) / kSB), d->n_levels);
     const uint32_t* tb = reinterpret_cast<const uint32_t*>(table);
-    if (live == nullptr && lpb)
-      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 2>), dim3(grid.x, d->n_levels / 2), dim3(kSB), 0, st, a,
-                         pos, n, tb, enc, enc_stride, BwdWorkspace{}, live);
-    else if (live == nullptr)
-      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED>), grid, dim3(kSB), 0, st, a, pos, n, tb, enc,
-                         enc_stride, BwdWorkspace{}, live);
+    if (live == nullptr)
+      hipLaunchKernelGGL(enc_kernel(), dim3(grid.x, d->n_levels / lpb), dim3(kSB), 0, st, a, pos, n, tb, enc, enc_stride,
+                         BwdWorkspace{}, live);
     else if (spt2)
       hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 2, false>), grid, dim3(kSB / 2), 0, st, a, pos, n, tb, enc,
                          enc_stride, BwdWorkspace{}, live);

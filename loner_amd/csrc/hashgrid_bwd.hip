@@ -491,6 +491,9 @@ template <class GradFn, int NB>
 #ifndef LNR_ROWS_PLACE_SEQ
 #define LNR_ROWS_PLACE_SEQ 0  // (experiment) records ranked and placed this many at a time (0: all 4)
 #endif
+#ifndef LNR_ROWS_ROT
+#define LNR_ROWS_ROT 0
+#endif
 #ifndef LNR_ROWS_WAVES1
 #define LNR_ROWS_WAVES1 6  // waves per SIMD of the one-stage scatter (8 needs <= 64 VGPRs and <= 40 KB LDS)
 #endif
@@ -526,7 +529,7 @@ struct RowsLds {  // the small tables first: their addresses fit the 16-bit LDS 
 // compile-time, so the level loop unrolls into straight-line code.  Record slots are 32-bit (the
 // launcher checks 8 N L < 2^32).
 // The body walks levels [LB, LB + NL) of histogram row sb (local level l is level LB + l).
-template <class PosFn, class GradFn, int LB, int NL, int NM, int NB, int kRowsStages>
+template <class PosFn, class GradFn, int LB, int NL, int NM, int NB, int kRowsStages, bool ROT = false>
 __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& sm, const GridArgs& a, const PosFn& pos,
                                                   int64_t n, const GradFn& grad, const BwdWorkspace& ws, bool skip_zero,
                                                   int64_t sb) {
@@ -641,8 +644,11 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
 #endif
   };
 
+  static_assert(!ROT || (kRowsStages == 1 && NL % 4 == 0), "rotated level order: one stage, an even half");
 #pragma unroll
-  for (int l = 0; l < NL; ++l) {
+  for (int ll = 0; ll < NL; ++ll) {
+    // ROT: this row walks levels NL/2 .. NL-1 first, then 0 .. NL/2-1 (the counters' parity is kept)
+    const int l = ROT ? (ll + NL / 2) % NL : ll;
     const int sbuf = l & 1;  // rank counters (and, with two stages, the stage)
     const int stg = kRowsStages == 2 ? sbuf : 0;
 #if LNR_ROWS_LV_ARGS
@@ -790,7 +796,7 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
     } else {
       lds_barrier();  // level l placed
       copy_out(l);
-      if (l + 1 < NL) lds_barrier();  // the stage is free for level l + 1
+      if (ll + 1 < NL) lds_barrier();  // the stage is free for the next level
     }
   }
   if (kRowsStages == 2) copy_out(NL - 1);
@@ -801,7 +807,18 @@ __global__ void __launch_bounds__(kSB)
 __attribute__((amdgpu_waves_per_eu(rows_waves<GradFn, NB>(), rows_waves<GradFn, NB>())))
 k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace ws, bool skip_zero) {
   __shared__ RowsLds<NL, NB, rows_stages<GradFn, NB>()> sm;
+#if LNR_ROWS_ROT
+  // (experiment) odd rows walk the fine levels first: workgroups that start together then run
+  // VALU-heavy coherent levels beside LDS-heavy fine ones
+  constexpr int kStg = rows_stages<GradFn, NB>();
+  const int64_t sb = xcd_row(blockIdx.x, gridDim.x);
+  if (kStg == 1 && (sb & 1))
+    scatter_rows_body<PosFn, GradFn, 0, NL, NM, NB, kStg, kStg == 1>(sm, a, pos, n, grad, ws, skip_zero, sb);
+  else
+    scatter_rows_body<PosFn, GradFn, 0, NL, NM, NB, kStg>(sm, a, pos, n, grad, ws, skip_zero, sb);
+#else
   scatter_rows_body<PosFn, GradFn, 0, NL, NM, NB>(sm, a, pos, n, grad, ws, skip_zero, xcd_row(blockIdx.x, gridDim.x));
+#endif
 }
 
 constexpr size_t kScatterLds = (size_t)kCap * 4 + kMaxChunksPerLevel * 8 + (size_t)kCap * 4 + kMaxChunksPerLevel * 4 +

@@ -174,6 +174,42 @@ def test_hashgrid_fwd_run_head_gathers_bitwise(L, S, monkeypatch):
     assert torch.equal(outs["0"][0], outs["0"][2])
 
 
+@pytest.mark.parametrize("nl", [15, 14])
+def test_hashgrid_fwd_level_groups_bitwise(L, nl):
+    """From 512 histogram rows a 16-level grid encodes four levels per workgroup (y, y + 4, y + 8,
+    y + 12), a 14-level grid two (y, y + 7) and a 15-level grid one: the levels the grids share have
+    bit for bit the same encodings and training-launch record histograms."""
+    rng = np.random.default_rng(17)
+    R, S = 520, 512
+    o = rng.uniform(-0.5, 0.5, (R, 3))
+    dr = rng.normal(0, 1, (R, 3))
+    dr /= np.linalg.norm(dr, axis=1, keepdims=True)
+    rays = np.zeros((R, 13), np.float32)
+    rays[:, 0:3], rays[:, 3:6] = o, dr
+    z = np.sort(rng.uniform(0.0, 0.45, (R, S)), 1).astype(np.float32)
+    n = R * S
+    lay = ohg.GridLayout(16, 2, 18, 16)
+    table = cu(rng.uniform(-1, 1, (lay.n_entries, 2)).astype(np.float16).view(np.int16))
+    outs = {}
+    for g in (16, nl):
+        d = L.grid_desc(g, 2, 18, 16)
+        nb = int(L.lib().lnr_hashgrid_bwd_workspace_bytes(ctypes.byref(d), n))
+        ws = torch.zeros(nb // 4 + 1, dtype=torch.int32, device="cuda")
+        e_train = torch.full((g, n), -1, dtype=torch.int32, device="cuda")
+        e_eval = torch.full((g, n), -1, dtype=torch.int32, device="cuda")
+        L.call("lnr_hashgrid_fwd_rays", ctypes.byref(d), cu(rays), cu(z), R, S, table, e_train, n, ws, nb, L.stream())
+        L.call("lnr_hashgrid_fwd_rays", ctypes.byref(d), cu(rays), cu(z), R, S, table, e_eval, n, None, 0, L.stream())
+        torch.cuda.synchronize()
+        outs[g] = (e_train, e_eval, ws)
+    assert torch.equal(outs[16][0][:nl], outs[nl][0])
+    assert torch.equal(outs[16][1][:nl], outs[nl][1])
+    assert torch.equal(outs[16][0], outs[16][1])
+    # histogram rows of the shared levels: the workspace's level maxima (256 B) come first, then the rows
+    n_sb = (n + 511) // 512
+    words = sum((s + 4095) // 4096 for s in lay.sizes[:nl]) * n_sb
+    assert torch.equal(outs[16][2][64:64 + words], outs[nl][2][64:64 + words])
+
+
 def test_hashgrid_fwd_rays_matches_positions(L):
     g = np.load("tests/golden/samplers.npz")
     rays, z = g["rays"], g["z_ogm"]
