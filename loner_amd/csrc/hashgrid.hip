@@ -102,10 +102,14 @@ __device__ __forceinline__ void fine_gather_paired(const uint32_t* __restrict__ 
 // two levels y, y + 8 0.618; four consecutive 0.720 (a 4 MB working set of fine levels); four levels
 // y, y + 4, y + 8, y + 12 0.605-0.612; eight 0.767, sixteen 0.890.  C3's sigma encode 1.188 / 1.135 /
 // 0.965 / 0.960 for one / two consecutive / two strided / four strided.
-inline int enc_levels_per_group(uint32_t n_levels, int64_t n_sb) {
+// A group's fine levels must fit an XCD's 4 MB L2 together: four 1 MB levels of the sigma grid (2^18
+// entries), two 2 MB levels of the colour grid (2^19: CAM's colour encode 0.33 ms at one level per
+// workgroup, 0.37 at four).
+inline int enc_levels_per_group(const lnr_grid_desc* d, int64_t n_sb) {
   if (n_sb < LNR_ENC_GROUP_MIN_ROWS) return 1;
+  const int64_t level_bytes = (int64_t)4 << d->log2_hashmap_size;
   for (int g = LNR_ENC_LPB; g > 1; g /= 2)
-    if (n_levels % g == 0) return g;
+    if (d->n_levels % g == 0 && g * level_bytes <= ((int64_t)4 << 20)) return g;
   return 1;
 }
 #ifndef LNR_ENC_WAVES
@@ -363,7 +367,7 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
   // with a ``live`` mask (C3's colour encode, most samples dead): plain gathers, so dead lanes issue
   // none, two samples per thread from LNR_ENC_SPT2_MIN_N samples
   const bool spt2 = n >= (int64_t)LNR_ENC_SPT2_MIN_N;
-  const int lpb = enc_levels_per_group(d->n_levels, (n + kSB - 1) / kSB);
+  const int lpb = enc_levels_per_group(d, (n + kSB - 1) / kSB);
   auto enc_kernel = [&]() {
     return lpb == 4 ? k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 4>
          : lpb == 2 ? k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 2>

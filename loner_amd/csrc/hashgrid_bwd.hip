@@ -812,7 +812,10 @@ k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace w
   // VALU-heavy coherent levels beside LDS-heavy fine ones
   constexpr int kStg = rows_stages<GradFn, NB>();
   const int64_t sb = xcd_row(blockIdx.x, gridDim.x);
-  if (kStg == 1 && (sb & 1))
+  // 1: odd rows; 2: every row; 3: rows whose index / 32 is odd (a CU's co-resident rows are 32 apart,
+  // adjacent rows keep one order)
+  const bool rot = LNR_ROWS_ROT == 1 ? (sb & 1) != 0 : LNR_ROWS_ROT == 2 ? true : ((sb >> 5) & 1) != 0;
+  if (kStg == 1 && rot)
     scatter_rows_body<PosFn, GradFn, 0, NL, NM, NB, kStg, kStg == 1>(sm, a, pos, n, grad, ws, skip_zero, sb);
   else
     scatter_rows_body<PosFn, GradFn, 0, NL, NM, NB, kStg>(sm, a, pos, n, grad, ws, skip_zero, sb);
