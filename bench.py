@@ -708,7 +708,11 @@ def main():
     ms = elapsed / args.steps * 1e3
     value = world * N * args.steps / elapsed
     bwd_ms = stage_ms["grid_bwd"]
-    achieved = 1024.0 * N / (bwd_ms * 1e-3) / 1e9
+    # one GPU: the table's Adam runs inside the backward's accumulation (lnr_hashgrid_bwd_rays_jac_adam),
+    # so the stage's algorithmic bytes add Adam's 32 B per table parameter
+    fused_adam = eng.fused_adam and eng.allreduce is None and eng.zero is None and eng.compact_denc
+    bwd_bytes = 1024.0 * N + (32.0 * 2 * state.n_entries if fused_adam else 0.0)
+    achieved = bwd_bytes / (bwd_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args.config)
     traffic_step, traffic_step_src = pmc_step_traffic(args.config)
     # the whole step against the HBM bound: 1536 B per ray-sample (hash-grid gathers and
@@ -749,8 +753,9 @@ def main():
                      "kernel": "hash-grid backward stage (k_bwd_chunk_sums, k_bwd_scan_*, k_bwd_scatter_rows, " + (
                          "k_bwd_accum_buckets)" if N <= (1 << 17) else
                          "k_bwd_accum_units: whole buckets and pieces of the large ones)" if N <= (1 << 21) else
-                         "k_bwd_accum: record-balanced, k_bwd_finalize)"),
-                     "algorithmic_bytes_per_launch": 1024 * N, "ms_per_launch": bwd_ms,
+                         "k_bwd_accum: record-balanced, k_bwd_finalize)") + (
+                         "; the table's Adam fused into the accumulation" if fused_adam else ""),
+                     "algorithmic_bytes_per_launch": bwd_bytes, "ms_per_launch": bwd_ms,
                      "step_algorithmic_bytes": step_bytes,
                      "step_frac": step_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "traffic_step": traffic_step, "traffic_step_source": traffic_step_src},

@@ -17,6 +17,7 @@
  *                                 (the body of one optimiser step, src/mapping/optimizer.py:436-450)
  *   lnr_loss_finalize             scalar loss / mean depth-eps from per-ray partials (optimizer.py:767,838-844)
  *   lnr_adam_step                 torch.optim.Adam step on the flat params  src/mapping/optimizer.py:255-265,460
+ *   lnr_hashgrid_bwd_rays_jac_adam  the table's backward with that Adam step fused in (optimizer.py:450,460)
  *   lnr_ogm_update                Optimizer._step_occupancy_grid  src/mapping/optimizer.py:897-908
  *   lnr_rgb_render                colour head (SH4 + 2^19 HashGrid + FullyFusedMLP) + colour map
  *                                 src/models/nerf_tcnn.py:80-95, src/models/rendering_tcnn.py:283-289
@@ -161,6 +162,25 @@ int lnr_hashgrid_bwd_rays_jac(const lnr_grid_desc* d, const float* rays, const f
                               int32_t n_samples, const uint32_t* d_jac, const float* d_sigma, int64_t jac_stride,
                               float* d_table, const uint16_t* table, float* d_pos, void* workspace,
                               int64_t workspace_bytes, int32_t flags, void* stream);
+/* The same with Adam fused in: where the backward finishes a table entry's gradient it applies
+ * torch.optim.Adam's update to that parameter (the arithmetic of lnr_adam_step, so the parameters,
+ * moments and fp16 shadow come out bitwise equal) instead of storing the gradient, for the
+ * 2 * n_entries table parameters at the head of `param`, `shadow`, `m`, `v`.  The step's Adam on the
+ * parameters after the table (the MLP) stays a lnr_adam_step.  N = 0 is Adam with a zero gradient.
+ * LNR_BWD_NO_ACCUM is refused (a gradient exchanged between ranks must reach memory first). */
+typedef struct lnr_adam_epilogue {
+  float* param;
+  uint16_t* shadow;
+  float* m;
+  float* v;
+  int32_t step;  /* 1-based, as lnr_adam_step */
+  double lr, beta1, beta2, eps;
+  const lnr_step_scalars* dev_step; /* non-NULL: step size and bias correction from device memory */
+} lnr_adam_epilogue;
+int lnr_hashgrid_bwd_rays_jac_adam(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
+                                   int32_t n_samples, const uint32_t* d_jac, const float* d_sigma, int64_t jac_stride,
+                                   const lnr_adam_epilogue* adam, void* workspace, int64_t workspace_bytes,
+                                   int32_t flags, void* stream);
 /* With flags & LNR_BWD_NO_ACCUM the three calls above stop after the scatter; this finishes the
  * levels [level_begin, level_end) (n = samples of that call, same workspace): their slice of
  * d_table is final on return, so a data-parallel caller can all-reduce it while the next range

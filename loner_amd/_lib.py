@@ -56,6 +56,13 @@ class AdamRange(ctypes.Structure):
 ADAM_MAX_RANGES = 8
 
 
+class AdamEpilogue(ctypes.Structure):
+    """lnr_adam_epilogue (include/loner_amd.h): Adam fused into the hash-grid backward."""
+    _fields_ = [("param", ctypes.c_void_p), ("shadow", ctypes.c_void_p), ("m", ctypes.c_void_p), ("v", ctypes.c_void_p),
+                ("step", ctypes.c_int32), ("lr", ctypes.c_double), ("beta1", ctypes.c_double),
+                ("beta2", ctypes.c_double), ("eps", ctypes.c_double), ("dev_step", ctypes.c_void_p)]
+
+
 class LossParams(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int32), ("scale", ctypes.c_float), ("los_lambda", ctypes.c_float),
                 ("depthloss_lambda", ctypes.c_float), ("min_depth_eps", ctypes.c_float),
@@ -122,6 +129,8 @@ _SIGNATURES = {
                                              c_p, c_p, c_i64, c_i32, c_p]),
     "lnr_hashgrid_bwd_rays_jac": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_p, c_i64,
                                                  c_p, c_p, c_p, c_p, c_i64, c_i32, c_p]),
+    "lnr_hashgrid_bwd_rays_jac_adam": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_p, c_i64,
+                                                      ctypes.POINTER(AdamEpilogue), c_p, c_i64, c_i32, c_p]),
     "lnr_hashgrid_bwd_accum": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_i64, c_p, c_i64, c_u32, c_u32, c_p, c_p]),
     "lnr_hashgrid_bwd_atomic": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_i64, c_p, c_i64, c_p, c_p]),
     "lnr_hashgrid_bwd_rays_atomic": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_i64, c_p,

@@ -41,7 +41,20 @@ struct UnitTable {
   uint2 cut[kAccumGroups];     // {bucket, pieces} of the cut buckets, bucket order
 };
 
+// Adam applied where the backward finishes a table entry's gradient (lnr_hashgrid_bwd_rays_jac_adam):
+// the same arithmetic as k_adam on the table's slice of the flat parameters, so the gradient never
+// goes to memory.  p == nullptr: the backward stores the gradient into d_table instead.
+struct AdamEpi {
+  float* p;
+  uint16_t* shadow;
+  float* m;
+  float* v;
+  const lnr_step_scalars* dev_step;  // graph replay: step_size and bc2_sqrt from device memory
+  float one_minus_b1, b2, one_minus_b2, step_size, bc2_sqrt, eps;
+};
+
 struct GridArgs {
+  AdamEpi adam;
   LevelParams lv[LNR_MAX_LEVELS];
   uint32_t bucket_base[LNR_MAX_LEVELS + 1];
   uint32_t n_levels;

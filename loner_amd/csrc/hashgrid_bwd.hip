@@ -1072,14 +1072,36 @@ __device__ __forceinline__ void accum_records(unsigned long long* acc, uint2* st
   }
 }
 
+// The final gradient g of table parameter i: stored into d_table, or (a.adam.p set) Adam's update of
+// parameter i with it, the arithmetic of optim.hip's adam_range term for term (-ffp-contract=off in
+// both files), so the parameters, moments and fp16 shadow are bitwise those of lnr_adam_step.
+__device__ __forceinline__ void put_grad(const GridArgs& a, float* __restrict__ d_table, int64_t i, float g) {
+  const AdamEpi& e = a.adam;
+  if (e.p == nullptr) {
+    d_table[i] = g;
+    return;
+  }
+  const float step_size = e.dev_step ? e.dev_step->adam_step_size : e.step_size;
+  const float bc2_sqrt = e.dev_step ? e.dev_step->adam_bc2_sqrt : e.bc2_sqrt;
+  float m = e.m[i], v = e.v[i], p = e.p[i];
+  m = m + e.one_minus_b1 * (g - m);
+  v = v * e.b2 + e.one_minus_b2 * g * g;
+  const float denom = sqrtf(v) / bc2_sqrt + e.eps;
+  p = p + (-step_size) * (m / denom);
+  e.m[i] = m;
+  e.v[i] = v;
+  e.p[i] = p;
+  e.shadow[i] = f2h(p);
+}
+
 // A whole bucket's final fp32 values from its LDS chunk.
 __device__ __forceinline__ void store_bucket(const unsigned long long* acc, const GridArgs& a, const BwdWorkspace& ws,
                                              float* __restrict__ d_table, uint32_t l, uint32_t ent0, uint32_t nent,
                                              int k2) {
   const double inv = unit_back(a, ws, l, k2);
-  float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0);
+  const int64_t base = 2 * ((int64_t)a.lv[l].offset + ent0);
   for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x)
-    dst[t] = (float)((double)(long long)acc[(t & 1) * kChunk + (t >> 1)] * inv);
+    put_grad(a, d_table, base + t, (float)((double)(long long)acc[(t & 1) * kChunk + (t >> 1)] * inv));
 }
 
 // One workgroup per kAccumGroups-th of the records of buckets [b_begin, b_end).  Per bucket piece:
@@ -1095,8 +1117,8 @@ __device__ __forceinline__ void store_zero_bucket(const GridArgs& a, float* __re
   const uint32_t l = level_of_bucket(a, b);
   const uint32_t ent0 = (b - a.bucket_base[l]) * kChunk;
   const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
-  float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0);
-  for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) dst[t] = 0.f;
+  const int64_t base = 2 * ((int64_t)a.lv[l].offset + ent0);
+  for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) put_grad(a, d_table, base + t, 0.f);
 }
 
 template <bool FINISH>
@@ -1204,8 +1226,8 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
   const uint32_t ent0 = (b - a.bucket_base[l]) * kChunk;
   const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
   if (s0 == s1) {
-    float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0);
-    for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) dst[t] = 0.f;
+    const int64_t base = 2 * ((int64_t)a.lv[l].offset + ent0);
+    for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) put_grad(a, d_table, base + t, 0.f);
     return;
   }
   for (int t = threadIdx.x; t < 2 * kChunk; t += blockDim.x) acc[t] = 0ull;
@@ -1320,7 +1342,13 @@ __global__ void __launch_bounds__(kFinalizeThreads) k_bwd_finalize(GridArgs a, B
   float o[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) o[k] = (float)((double)v[k] * inv);
-  float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0) + t0;
+  const int64_t base = 2 * ((int64_t)a.lv[l].offset + ent0) + t0;
+  if (a.adam.p != nullptr) {
+    for (int k = 0; k < 8; ++k)
+      if (t0 + k < 2 * nent) put_grad(a, d_table, base + k, o[k]);
+    return;
+  }
+  float* dst = d_table + base;
   if (t0 + 8 <= 2 * nent && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0)) {
     reinterpret_cast<f32x4v*>(dst)[0] = f32x4v{o[0], o[1], o[2], o[3]};
     reinterpret_cast<f32x4v*>(dst)[1] = f32x4v{o[4], o[5], o[6], o[7]};
@@ -1361,7 +1389,13 @@ __global__ void __launch_bounds__(kFinalizeThreads) k_bwd_finalize_units(GridArg
   float o[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) o[j] = (float)((double)v[j] * inv);
-  float* dst = d_table + 2 * ((int64_t)a.lv[l].offset + ent0) + t0;
+  const int64_t base = 2 * ((int64_t)a.lv[l].offset + ent0) + t0;
+  if (a.adam.p != nullptr) {
+    for (int k = 0; k < 8; ++k)
+      if (t0 + k < 2 * nent) put_grad(a, d_table, base + k, o[k]);
+    return;
+  }
+  float* dst = d_table + base;
   if (t0 + 8 <= 2 * nent && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0)) {
     reinterpret_cast<f32x4v*>(dst)[0] = f32x4v{o[0], o[1], o[2], o[3]};
     reinterpret_cast<f32x4v*>(dst)[1] = f32x4v{o[4], o[5], o[6], o[7]};
@@ -1449,8 +1483,10 @@ static void launch_accum(const GridArgs& a, const BwdWorkspace& w, const lnr_gri
 
 template <class PosFn, class GradFn>
 static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, GradFn grad, float* d_table,
-                               void* workspace, int64_t ws_bytes, int32_t flags, hipStream_t st, const char* who) {
+                               void* workspace, int64_t ws_bytes, int32_t flags, hipStream_t st, const char* who,
+                               const AdamEpi* adam = nullptr) {
   GridArgs a = make_args(d, pos.samples_per_ray());
+  if (adam) a.adam = *adam;
   LNR_REQUIRE(a.n_buckets <= (uint32_t)kMaxBuckets, "%s: too many table chunks (%u)", who, a.n_buckets);
   for (uint32_t l = 0; l < d->n_levels; ++l)
     LNR_REQUIRE(a.bucket_base[l + 1] - a.bucket_base[l] <= (uint32_t)kMaxChunksPerLevel,
@@ -1750,6 +1786,46 @@ extern "C" int lnr_hashgrid_bwd_rays(const lnr_grid_desc* d, const float* rays, 
   return bwd_entry(d, PosFromRays{rays, z, n_samples}, n, GradF32{reinterpret_cast<const float2*>(d_enc), enc_stride},
                    d_table, table, d_pos, workspace, workspace_bytes, flags, as_stream(stream),
                    "lnr_hashgrid_bwd_rays");
+}
+
+// Adam with a zero gradient on every table parameter (the fused entry's empty batch)
+__global__ void __launch_bounds__(256) k_adam_zero_grad(GridArgs a, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    put_grad(a, nullptr, i, 0.f);
+}
+
+extern "C" int lnr_hashgrid_bwd_rays_jac_adam(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
+                                              int32_t n_samples, const uint32_t* d_jac, const float* d_sigma,
+                                              int64_t jac_stride, const lnr_adam_epilogue* adam, void* workspace,
+                                              int64_t workspace_bytes, int32_t flags, void* stream) {
+  const char* who = "lnr_hashgrid_bwd_rays_jac_adam";
+  if (int e = check_desc_bwd(d, who)) return e;
+  const int64_t n = n_rays * (int64_t)n_samples;
+  LNR_REQUIRE(n_rays >= 0 && n_samples > 0 && jac_stride >= n, "%s: bad sizes", who);
+  LNR_REQUIRE(adam && adam->param && adam->shadow && adam->m && adam->v && adam->step >= 1, "%s: bad Adam epilogue", who);
+  LNR_REQUIRE(!(flags & LNR_BWD_NO_ACCUM), "%s: LNR_BWD_NO_ACCUM has no place with the Adam epilogue", who);
+  LNR_REQUIRE(n == 0 || (rays && z && d_jac && d_sigma), "%s: null pointer", who);
+  AdamEpi e{};
+  e.p = adam->param;
+  e.shadow = adam->shadow;
+  e.m = adam->m;
+  e.v = adam->v;
+  e.dev_step = adam->dev_step;
+  if (int r = lnr_adam_coefficients(adam->step, adam->lr, adam->beta1, adam->beta2, &e.step_size, &e.bc2_sqrt)) return r;
+  e.one_minus_b1 = (float)(1.0 - adam->beta1);  // as lnr_adam_step forms them
+  e.b2 = (float)adam->beta2;
+  e.one_minus_b2 = (float)(1.0 - adam->beta2);
+  e.eps = (float)adam->eps;
+  hipStream_t st = as_stream(stream);
+  if (n == 0) {
+    GridArgs a = make_args(d);
+    a.adam = e;
+    const int64_t np = 2 * (int64_t)d->n_entries;
+    hipLaunchKernelGGL(k_adam_zero_grad, dim3((unsigned)std::min<int64_t>((np + 255) / 256, 8192)), dim3(256), 0, st, a, np);
+    LNR_RETURN_LAUNCH(who);
+  }
+  return launch_bwd_bucketed(d, PosFromRays{rays, z, n_samples}, n, GradJac{d_jac, d_sigma, jac_stride}, nullptr,
+                             workspace, workspace_bytes, flags, st, who, &e);
 }
 
 extern "C" int lnr_hashgrid_bwd_rays_jac(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,

@@ -269,6 +269,9 @@ class StepEngine:
         # holes step k leaves (the scatter's last round, the accumulate's tail) instead of at the head
         # of step k + 1 (``pipeline``; not when step k updates the OGM, which the sampler reads)
         self.pipeline = os.environ.get("LONER_PIPELINE", "1") != "0"
+        # the single-GPU step's table Adam fused into the backward (LONER_FUSED_ADAM=0: the separate
+        # lnr_adam_step over every parameter; the data-parallel paths always exchange the gradient first)
+        self.fused_adam = os.environ.get("LONER_FUSED_ADAM", "0") != "0"
         self._pp, self._pp_parity = None, 0
         self._pp_stream = torch.cuda.Stream(device=dev)
         self._pp_fork = torch.cuda.Event()
@@ -460,6 +463,32 @@ class StepEngine:
         flags = (L.BWD_COUNTS_READY if self.count_in_forward else 0) | L.BWD_LEVEL_MAX_READY
         if self.zero is not None:
             return self._step_zero(rays, depth_gt, R, S, N, flags, s, scale, update_ogm, global_step, prof)
+        if self.allreduce is None and self.fused_adam and self.compact_denc:
+            # 5 + 7. the table's Adam inside the backward (lnr_hashgrid_bwd_rays_jac_adam: each entry's
+            # gradient updates its parameter where the accumulation finishes it, bitwise lnr_adam_step's
+            # result), then Adam on the MLP's parameters alone
+            st.adam_step += 1
+            nm, nt = st.n_mlp, 2 * st.n_entries
+            epi = L.AdamEpilogue(L.ptr(st.params[nm:nm + nt]), L.ptr(st.shadow[nm:nm + nt]), L.ptr(st.m[nm:nm + nt]),
+                                 L.ptr(st.v[nm:nm + nt]), st.adam_step, cfg.lr * self.lr_factor, 0.9, 0.999, 1e-8, dsp)
+            L.call("lnr_hashgrid_bwd_rays_jac_adam", L.ctypes.byref(st.desc), rays, self.z, R, S, self.d_jac,
+                   self.d_sigma(R), N, L.ctypes.byref(epi), self.bwd_ws, self.bwd_ws_bytes, flags, s)
+            m(prof, "grid_bwd")
+            m(prof, "adam")
+            L.call("lnr_adam_step", st.params[:nm], st.shadow[:nm], st.grad[:nm], st.m[:nm], st.v[:nm], nm,
+                   st.adam_step, cfg.lr * self.lr_factor, 0.9, 0.999, 1e-8, dsp, s)
+            if st.n_padded > nm + nt:
+                o = nm + nt
+                L.call("lnr_adam_step", st.params[o:], st.shadow[o:], st.grad[o:], st.m[o:], st.v[o:], st.n_padded - o,
+                       st.adam_step, cfg.lr * self.lr_factor, 0.9, 0.999, 1e-8, dsp, s)
+            m(prof, "adam")
+            if update_ogm is None:
+                update_ogm = (global_step % cfg.n_iters_acc == 0)
+            if update_ogm:
+                m(prof, "ogm")
+                self.ogm_update(rays, depth_gt, scale)
+                m(prof, "ogm")
+            return self.loss_out
         if self.allreduce is None:
             self._grid_bwd(rays, R, S, N, flags, s)
             m(prof, "grid_bwd")

@@ -8,6 +8,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+# The single-GPU step applies the table's Adam inside the hash-grid backward by default (no table
+# gradient in memory).  Most step tests check that gradient against the oracle, so their engines keep
+# it (the separate lnr_adam_step); test_fused_adam_equals_separate (test_gpu_rays.py) turns the fusion
+# on per engine and checks it bitwise against this path.
+os.environ.setdefault("LONER_FUSED_ADAM", "0")
 
 # Hash-grid table gradient vs the fp64 oracle, relative L2.  The backward's records carry their two
 # values as fp16 at a per-level power-of-two scale (csrc/hashgrid.hpp "Record values"): each

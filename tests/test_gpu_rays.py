@@ -281,3 +281,41 @@ def test_graph_replay_equals_eager(L, zero):
             np.testing.assert_array_equal(a, b)
         for a, b in zip(res[0][1:], r[1:]):
             np.testing.assert_array_equal(a, b)
+
+
+def test_fused_adam_equals_separate(L):
+    """The table's Adam fused into the hash-grid backward (lnr_hashgrid_bwd_rays_jac_adam: each entry's
+    gradient updates its parameter where the accumulation finishes it; the MLP's Adam separate) gives
+    bitwise the separate lnr_adam_step's parameters, moments, fp16 shadow, losses and occupancy grid:
+    eager and graph-replayed steps, OGM steps, a changed learning-rate factor, a new optimiser, and an
+    empty batch (Adam with a zero gradient)."""
+    from loner_amd import step as S_
+    from loner_amd import synthetic as syn
+    from loner_amd.rays import RayWindow
+    res = []
+    for fused, graph in ((False, False), (True, False), (True, True)):
+        st = S_.FieldState(S_.StepConfig(n_samples=64, occ_lr=1e-3), device="cuda:0", table_init=0.5)
+        scans, wc, rr = _window("forest", 2, seed=8)
+        win = RayWindow(scans, wc, rr, n_lidar=128, n_sky=16, strategy="MASK")
+        eng = S_.StepEngine(st, win.n_slots, seed=4)
+        eng.fused_adam, eng.use_graph = fused, graph
+        outs = []
+        for it, g in enumerate((8, 9, 10, 11, 12, 13)):
+            eng.lr_factor = 0.97 ** it
+            outs.append(host(eng.step_window(win, global_step=g, iteration_idx=it)).copy())
+        st.reset_optimizer()
+        for it, g in enumerate((14, 15)):
+            outs.append(host(eng.step_window(win, global_step=g, iteration_idx=it)).copy())
+        # an empty batch: zero gradient everywhere, Adam still steps every parameter
+        w2 = syn.make_window("quad", 1, seed=2)
+        rays, dgt = syn.build_batch(w2, "quad", 64, 0, "RANDOM", seed=4)
+        rays, dgt = rays.cuda(), dgt.cuda()
+        eng.step(rays[:0], dgt[:0], global_step=16, scale=121.426537, far_ref=float(rays[0, 12]), n_rays_global=64)
+        torch.cuda.synchronize()
+        res.append((outs, host(st.params).copy(), host(st.m).copy(), host(st.v).copy(),
+                    host(st.shadow).view(np.uint16).copy(), host(st.occ).copy(), st.adam_step))
+    for r in res[1:]:
+        for a, b in zip(res[0][0], r[0]):
+            np.testing.assert_array_equal(a, b)
+        for a, b in zip(res[0][1:], r[1:]):
+            np.testing.assert_array_equal(a, b)
