@@ -766,8 +766,8 @@ def main():
                             "ms_per_launch": stage_ms["encode"], "algorithmic_bytes_per_launch": 512 * N,
                             "achieved": 512.0 * N / (stage_ms["encode"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                             "unit": "GB/s", "frac": 512.0 * N / (stage_ms["encode"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                            "bound": "texture addresser: TA busy 0.85 of the launch at C2 "
-                                     "(rocprofv3 TA_BUSY_avr, profiles/r03_l2req_C2.txt)"},
+                            "bound": "texture addresser + the coherent levels' VALU: TA busy 0.78 of the launch at C2 "
+                                     "(rocprofv3 TA_BUSY_avr, profiles/r04_l2req_C2.txt)"},
         # the sigma MLP (fwd 4224 + bwd 8448 FLOP/sample) over the field stage
         # (k_sigma_fwd_tiles + k_composite_wave + k_mlp_bwd_tiles), against the dense fp16 MFMA peak
         "mfma": {"achieved": mlp_tflops, "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": mlp_tflops / MFMA_PEAK_TFLOPS,

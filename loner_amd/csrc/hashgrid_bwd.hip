@@ -1094,12 +1094,74 @@ __device__ __forceinline__ void put_grad(const GridArgs& a, float* __restrict__ 
   e.shadow[i] = f2h(p);
 }
 
+// Eight consecutive final gradients g[0..7] of table parameters i0 .. i0 + 7 (i0 a multiple of 8, the
+// table's slice 16-B aligned), the first `cnt` of them valid: with the Adam epilogue every load of the
+// eight is issued before any arithmetic (16-B loads of p, m, v, one 16-B shadow store), so a thread
+// waits for memory once per eight parameters, not once per parameter.
+__device__ __forceinline__ void put_grad8(const GridArgs& a, float* __restrict__ d_table, int64_t i0, const float (&g)[8],
+                                          uint32_t cnt) {
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  const AdamEpi& e = a.adam;
+  if (cnt < 8) {
+    for (uint32_t k = 0; k < cnt; ++k) put_grad(a, d_table, i0 + k, g[k]);
+    return;
+  }
+  if (e.p == nullptr) {
+    f32x4v* d = reinterpret_cast<f32x4v*>(d_table + i0);
+    d[0] = f32x4v{g[0], g[1], g[2], g[3]};
+    d[1] = f32x4v{g[4], g[5], g[6], g[7]};
+    return;
+  }
+  const float step_size = e.dev_step ? e.dev_step->adam_step_size : e.step_size;
+  const float bc2_sqrt = e.dev_step ? e.dev_step->adam_bc2_sqrt : e.bc2_sqrt;
+  f32x4v* pp = reinterpret_cast<f32x4v*>(e.p + i0);
+  f32x4v* mp = reinterpret_cast<f32x4v*>(e.m + i0);
+  f32x4v* vp = reinterpret_cast<f32x4v*>(e.v + i0);
+  const f32x4v p4[2] = {pp[0], pp[1]}, m4[2] = {mp[0], mp[1]}, v4[2] = {vp[0], vp[1]};
+  float po[8], mo[8], vo[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float m = m4[k >> 2][k & 3], v = v4[k >> 2][k & 3], p = p4[k >> 2][k & 3];
+    m = m + e.one_minus_b1 * (g[k] - m);
+    v = v * e.b2 + e.one_minus_b2 * g[k] * g[k];
+    const float denom = sqrtf(v) / bc2_sqrt + e.eps;
+    p = p + (-step_size) * (m / denom);
+    po[k] = p;
+    mo[k] = m;
+    vo[k] = v;
+  }
+  pp[0] = f32x4v{po[0], po[1], po[2], po[3]};
+  pp[1] = f32x4v{po[4], po[5], po[6], po[7]};
+  mp[0] = f32x4v{mo[0], mo[1], mo[2], mo[3]};
+  mp[1] = f32x4v{mo[4], mo[5], mo[6], mo[7]};
+  vp[0] = f32x4v{vo[0], vo[1], vo[2], vo[3]};
+  vp[1] = f32x4v{vo[4], vo[5], vo[6], vo[7]};
+  uint4 h;
+  h.x = (uint32_t)f2h(po[0]) | ((uint32_t)f2h(po[1]) << 16);
+  h.y = (uint32_t)f2h(po[2]) | ((uint32_t)f2h(po[3]) << 16);
+  h.z = (uint32_t)f2h(po[4]) | ((uint32_t)f2h(po[5]) << 16);
+  h.w = (uint32_t)f2h(po[6]) | ((uint32_t)f2h(po[7]) << 16);
+  *reinterpret_cast<uint4*>(e.shadow + i0) = h;
+}
+
 // A whole bucket's final fp32 values from its LDS chunk.
 __device__ __forceinline__ void store_bucket(const unsigned long long* acc, const GridArgs& a, const BwdWorkspace& ws,
                                              float* __restrict__ d_table, uint32_t l, uint32_t ent0, uint32_t nent,
                                              int k2) {
   const double inv = unit_back(a, ws, l, k2);
   const int64_t base = 2 * ((int64_t)a.lv[l].offset + ent0);
+  if (a.adam.p != nullptr) {  // eight consecutive parameters per thread per pass (put_grad8)
+    for (uint32_t t0 = 8 * threadIdx.x; t0 < 2 * nent; t0 += 8 * blockDim.x) {
+      float g[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t t = t0 + k;
+        g[k] = (float)((double)(long long)acc[(t & 1) * kChunk + (t >> 1)] * inv);
+      }
+      put_grad8(a, d_table, base + t0, g, 2 * nent - t0 < 8 ? 2 * nent - t0 : 8);
+    }
+    return;
+  }
   for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x)
     put_grad(a, d_table, base + t, (float)((double)(long long)acc[(t & 1) * kChunk + (t >> 1)] * inv));
 }
@@ -1118,6 +1180,12 @@ __device__ __forceinline__ void store_zero_bucket(const GridArgs& a, float* __re
   const uint32_t ent0 = (b - a.bucket_base[l]) * kChunk;
   const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
   const int64_t base = 2 * ((int64_t)a.lv[l].offset + ent0);
+  if (a.adam.p != nullptr) {
+    const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (uint32_t t0 = 8 * threadIdx.x; t0 < 2 * nent; t0 += 8 * blockDim.x)
+      put_grad8(a, d_table, base + t0, z, 2 * nent - t0 < 8 ? 2 * nent - t0 : 8);
+    return;
+  }
   for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) put_grad(a, d_table, base + t, 0.f);
 }
 
@@ -1226,8 +1294,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
   const uint32_t ent0 = (b - a.bucket_base[l]) * kChunk;
   const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
   if (s0 == s1) {
-    const int64_t base = 2 * ((int64_t)a.lv[l].offset + ent0);
-    for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) put_grad(a, d_table, base + t, 0.f);
+    store_zero_bucket(a, d_table, b);
     return;
   }
   for (int t = threadIdx.x; t < 2 * kChunk; t += blockDim.x) acc[t] = 0ull;
@@ -1344,8 +1411,7 @@ __global__ void __launch_bounds__(kFinalizeThreads) k_bwd_finalize(GridArgs a, B
   for (int k = 0; k < 8; ++k) o[k] = (float)((double)v[k] * inv);
   const int64_t base = 2 * ((int64_t)a.lv[l].offset + ent0) + t0;
   if (a.adam.p != nullptr) {
-    for (int k = 0; k < 8; ++k)
-      if (t0 + k < 2 * nent) put_grad(a, d_table, base + k, o[k]);
+    put_grad8(a, d_table, base, o, 2 * nent - t0 < 8 ? 2 * nent - t0 : 8);
     return;
   }
   float* dst = d_table + base;
@@ -1391,8 +1457,7 @@ __global__ void __launch_bounds__(kFinalizeThreads) k_bwd_finalize_units(GridArg
   for (int j = 0; j < 8; ++j) o[j] = (float)((double)v[j] * inv);
   const int64_t base = 2 * ((int64_t)a.lv[l].offset + ent0) + t0;
   if (a.adam.p != nullptr) {
-    for (int k = 0; k < 8; ++k)
-      if (t0 + k < 2 * nent) put_grad(a, d_table, base + k, o[k]);
+    put_grad8(a, d_table, base, o, 2 * nent - t0 < 8 ? 2 * nent - t0 : 8);
     return;
   }
   float* dst = d_table + base;
@@ -1790,8 +1855,9 @@ extern "C" int lnr_hashgrid_bwd_rays(const lnr_grid_desc* d, const float* rays, 
 
 // Adam with a zero gradient on every table parameter (the fused entry's empty batch)
 __global__ void __launch_bounds__(256) k_adam_zero_grad(GridArgs a, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    put_grad(a, nullptr, i, 0.f);
+  const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int64_t i = 8 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x); i < n; i += 8 * (int64_t)gridDim.x * blockDim.x)
+    put_grad8(a, nullptr, i, z, n - i < 8 ? (uint32_t)(n - i) : 8u);
 }
 
 extern "C" int lnr_hashgrid_bwd_rays_jac_adam(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
@@ -1803,6 +1869,8 @@ extern "C" int lnr_hashgrid_bwd_rays_jac_adam(const lnr_grid_desc* d, const floa
   const int64_t n = n_rays * (int64_t)n_samples;
   LNR_REQUIRE(n_rays >= 0 && n_samples > 0 && jac_stride >= n, "%s: bad sizes", who);
   LNR_REQUIRE(adam && adam->param && adam->shadow && adam->m && adam->v && adam->step >= 1, "%s: bad Adam epilogue", who);
+  LNR_REQUIRE(((uintptr_t)adam->param | (uintptr_t)adam->shadow | (uintptr_t)adam->m | (uintptr_t)adam->v) % 16 == 0,
+              "%s: the Adam epilogue's buffers must be 16-byte aligned", who);
   LNR_REQUIRE(!(flags & LNR_BWD_NO_ACCUM), "%s: LNR_BWD_NO_ACCUM has no place with the Adam epilogue", who);
   LNR_REQUIRE(n == 0 || (rays && z && d_jac && d_sigma), "%s: null pointer", who);
   AdamEpi e{};
