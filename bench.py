@@ -710,7 +710,8 @@ def main():
     bwd_ms = stage_ms["grid_bwd"]
     # one GPU: the table's Adam runs inside the backward's accumulation (lnr_hashgrid_bwd_rays_jac_adam),
     # so the stage's algorithmic bytes add Adam's 32 B per table parameter
-    fused_adam = eng.fused_adam and eng.allreduce is None and eng.zero is None and eng.compact_denc
+    fused_adam = eng.allreduce is None and eng.zero is None and eng.compact_denc and (
+        eng.fused_adam is True or (eng.fused_adam == "auto" and N <= S_.FUSED_ADAM_MAX_N))
     bwd_bytes = 1024.0 * N + (32.0 * 2 * state.n_entries if fused_adam else 0.0)
     achieved = bwd_bytes / (bwd_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args.config)

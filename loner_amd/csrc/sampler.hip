@@ -220,9 +220,46 @@ __device__ __forceinline__ void wave_bitonic_sort(float (&v)[E]) {
   }
 }
 
+// The last stage of the bitonic sort alone: a bitonic sequence of 64 E values (ascending, then
+// descending) merged into ascending order, the same compare-exchanges as wave_bitonic_sort's stage
+// k = 64 E.
+template <int E>
+__device__ __forceinline__ void wave_bitonic_merge(float (&v)[E]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 32 * E; j > 0; j >>= 1) {
+    if (j >= E) {
+      const int dl = j / E;
+      const bool lower = (lane & dl) == 0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const float o = __shfl_xor(v[e], dl, 64);
+        v[e] = lower ? fminf(v[e], o) : fmaxf(v[e], o);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if ((e & j) == 0) {
+          const float x = v[e], y = v[e + j];
+          v[e] = fminf(x, y);
+          v[e + j] = fmaxf(x, y);
+        }
+      }
+    }
+  }
+}
+
+#ifndef LNR_SAMPLER_MERGE
+#define LNR_SAMPLER_MERGE 0  // sort the importance draws alone, then merge with the strata (LONER_SAMPLER_MERGE)
+#endif
+static bool sampler_merge() {  // read at every launch
+  const char* e = getenv("LONER_SAMPLER_MERGE");
+  return e ? atoi(e) != 0 : LNR_SAMPLER_MERGE != 0;
+}
+
 constexpr int kSamplerWaves = 4;
 
-template <int E>
+template <int E, bool MERGE>
 __global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_wave(SamplerArgs a) {
   if (a.dev_step) a.key = a.dev_step->key;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -325,9 +362,47 @@ __global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_wave(SamplerArgs
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");
     // 5. sort (torch.sort, ray_sampling.py:90) and store
     float v[E];
+    if constexpr (MERGE) {
+    // the jittered strata are ascending unless rounding crossed two of them (checked, wave-uniform):
+    // then only the H importance draws need sorting, and one bitonic merge stage finishes the sort.
+    // Same values in the same places as the full sort (depths are positive: no -0 / NaN ties)
+    bool strat_sorted = 2 * H == 64 * E;  // no padding
+    {
+      float prev = -INFINITY;
+#pragma unroll
+      for (int q = 0; q < QMAX; ++q) {
+        if (q >= Q) break;
+        strat_sorted = strat_sorted && !(zq[q] < prev);
+        prev = zq[q];
+      }
+      const float next_first = __shfl_down(zq[0], 1, 64);
+      if (lane < 63) strat_sorted = strat_sorted && !(next_first < prev);
+    }
+    if (__all(strat_sorted)) {
+      constexpr int E2 = E / 2;
+      float vi[E2];
+#pragma unroll
+      for (int e = 0; e < E2; ++e) vi[e] = buf[H + lane * E2 + e];
+      wave_bitonic_sort<E2>(vi);
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");
+#pragma unroll
+      for (int e = 0; e < E2; ++e) buf[2 * H - 1 - (lane * E2 + e)] = vi[e];  // descending after the strata
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");
+#pragma unroll
+      for (int e = 0; e < E; ++e) v[e] = buf[lane * E + e];
+      wave_bitonic_merge<E>(v);
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) v[e] = buf[lane * E + e];
+      wave_bitonic_sort<E>(v);
+    }
+    } else {
 #pragma unroll
     for (int e = 0; e < E; ++e) v[e] = buf[lane * E + e];
     wave_bitonic_sort<E>(v);
+    }
     float* zr = a.z + r * S;
 #pragma unroll
     for (int e = 0; e < E; ++e)
@@ -366,15 +441,16 @@ extern "C" int lnr_sample_ogm(const float* rays, int64_t n_rays, int32_t n_sampl
   LNR_REQUIRE(a.H <= 8 * SNT, "lnr_sample_ogm: too many samples");
   if (a.H % 64 == 0 && p2 >= 128 && p2 <= 2048) {  // one wave per ray
     const int E = p2 / 64;
+    const bool merge = sampler_merge();
     const int64_t nbw = (n_rays + kSamplerWaves - 1) / kSamplerWaves;
     const dim3 g((unsigned)(nbw < 8192 ? nbw : 8192)), b(64 * kSamplerWaves);
     const size_t sm = sampler_wave_smem(E, a.H);
     switch (E) {
-      case 2: hipLaunchKernelGGL(k_sampler_wave<2>, g, b, sm, as_stream(stream), a); break;
-      case 4: hipLaunchKernelGGL(k_sampler_wave<4>, g, b, sm, as_stream(stream), a); break;
-      case 8: hipLaunchKernelGGL(k_sampler_wave<8>, g, b, sm, as_stream(stream), a); break;
-      case 16: hipLaunchKernelGGL(k_sampler_wave<16>, g, b, sm, as_stream(stream), a); break;
-      default: hipLaunchKernelGGL(k_sampler_wave<32>, g, b, sm, as_stream(stream), a); break;
+      case 2: hipLaunchKernelGGL((merge ? k_sampler_wave<2, true> : k_sampler_wave<2, false>), g, b, sm, as_stream(stream), a); break;
+      case 4: hipLaunchKernelGGL((merge ? k_sampler_wave<4, true> : k_sampler_wave<4, false>), g, b, sm, as_stream(stream), a); break;
+      case 8: hipLaunchKernelGGL((merge ? k_sampler_wave<8, true> : k_sampler_wave<8, false>), g, b, sm, as_stream(stream), a); break;
+      case 16: hipLaunchKernelGGL((merge ? k_sampler_wave<16, true> : k_sampler_wave<16, false>), g, b, sm, as_stream(stream), a); break;
+      default: hipLaunchKernelGGL((merge ? k_sampler_wave<32, true> : k_sampler_wave<32, false>), g, b, sm, as_stream(stream), a); break;
     }
     LNR_RETURN_LAUNCH("lnr_sample_ogm");
   }

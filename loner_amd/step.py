@@ -155,6 +155,9 @@ class FieldState:
         self.refresh_shadow()
 
 
+FUSED_ADAM_MAX_N = 1 << 17  # samples up to which the step fuses the table's Adam into the backward ("auto")
+
+
 class StepEngine:
     """Preallocated workspaces for a fixed ray-batch size; ``step`` runs one optimiser step."""
 
@@ -269,9 +272,13 @@ class StepEngine:
         # holes step k leaves (the scatter's last round, the accumulate's tail) instead of at the head
         # of step k + 1 (``pipeline``; not when step k updates the OGM, which the sampler reads)
         self.pipeline = os.environ.get("LONER_PIPELINE", "1") != "0"
-        # the single-GPU step's table Adam fused into the backward (LONER_FUSED_ADAM=0: the separate
-        # lnr_adam_step over every parameter; the data-parallel paths always exchange the gradient first)
-        self.fused_adam = os.environ.get("LONER_FUSED_ADAM", "0") != "0"
+        # the single-GPU step's table Adam fused into the backward (lnr_hashgrid_bwd_rays_jac_adam, bitwise
+        # the separate lnr_adam_step).  "auto" (default): for batches of at most 2^17 samples, whose
+        # whole-bucket accumulation spreads the Adam work over a workgroup per bucket (C1 0.161 -> 0.152
+        # ms); at C2 the record-balanced accumulation's bucket ends carry it less well (1.950 -> 1.958-
+        # 1.989 ms), so there it stays a separate pass.  LONER_FUSED_ADAM=1 / 0 forces it on / off; the
+        # data-parallel paths always exchange the gradient first.
+        self.fused_adam = {"0": False, "1": True}.get(os.environ.get("LONER_FUSED_ADAM", "auto"), "auto")
         self._pp, self._pp_parity = None, 0
         self._pp_stream = torch.cuda.Stream(device=dev)
         self._pp_fork = torch.cuda.Event()
@@ -463,7 +470,8 @@ class StepEngine:
         flags = (L.BWD_COUNTS_READY if self.count_in_forward else 0) | L.BWD_LEVEL_MAX_READY
         if self.zero is not None:
             return self._step_zero(rays, depth_gt, R, S, N, flags, s, scale, update_ogm, global_step, prof)
-        if self.allreduce is None and self.fused_adam and self.compact_denc:
+        if self.allreduce is None and self.compact_denc and (
+                self.fused_adam is True or (self.fused_adam == "auto" and N <= FUSED_ADAM_MAX_N)):
             # 5 + 7. the table's Adam inside the backward (lnr_hashgrid_bwd_rays_jac_adam: each entry's
             # gradient updates its parameter where the accumulation finishes it, bitwise lnr_adam_step's
             # result), then Adam on the MLP's parameters alone

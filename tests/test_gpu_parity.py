@@ -370,6 +370,30 @@ def test_ogm_sampler_inkernel_rng_matches_oracle(L):
     np.testing.assert_allclose(host(z), ref, rtol=1e-5, atol=5e-6)
 
 
+@pytest.mark.parametrize("S", [128, 512, 2048])
+@pytest.mark.parametrize("perturb", [1.0, 0.0])
+def test_ogm_sampler_merge_equals_full_sort(L, S, perturb, monkeypatch):
+    """The one-wave sampler's sort of the importance draws alone + one bitonic merge with the (checked
+    ascending) strata (LONER_SAMPLER_MERGE=1) gives the full bitonic sort's depths bit for bit, for
+    training (jittered strata) and eval (perturb 0) draws, 2 to 32 values per lane; rays whose strata
+    rounding would cross fall back to the full sort."""
+    g = np.load("tests/golden/samplers.npz")
+    rays, occ = g["rays"], g["occ"]
+    rng = np.random.default_rng(3)
+    rays = np.concatenate([rays] * 4)
+    R = rays.shape[0]
+    rays[:, 11] = rng.uniform(0.0, 0.05, R)  # a spread of near / far bounds
+    outs = []
+    for m in ("0", "1"):
+        monkeypatch.setenv("LONER_SAMPLER_MERGE", m)
+        z = torch.empty(R, S, dtype=torch.float32, device="cuda")
+        L.call("lnr_sample_ogm", cu(rays), R, S, cu(occ), 100, perturb, None, None, orng.step_key(5, 2), 0, z, None,
+               L.stream())
+        outs.append(host(z).copy())
+    np.testing.assert_array_equal(outs[0], outs[1])
+    assert np.all(np.diff(outs[1], axis=1) >= 0)
+
+
 # ------------------------------------------------------------------ compositing + loss
 def test_composite_default_and_adjusted_golden(L):
     g = np.load("tests/golden/composite.npz")
