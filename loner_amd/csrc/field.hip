@@ -797,15 +797,8 @@ __global__ void __launch_bounds__(NT) k_sigma_fwd_tiles(FieldArgs a) {
 
 // Phase 1b, one wave per ray: compositing -> loss -> compositing backward on the sigma of phase 1a,
 // dL/dsigma written over it (a.d_sigma, (R, S) fp32).
-#ifndef LNR_COMPOSITE_WAVES
-#define LNR_COMPOSITE_WAVES 0  // (experiment) waves per SIMD asked of k_composite_wave (0: the compiler's choice)
-#endif
 template <int C>
-__global__ void __launch_bounds__(NT)
-#if LNR_COMPOSITE_WAVES
-__attribute__((amdgpu_waves_per_eu(LNR_COMPOSITE_WAVES, LNR_COMPOSITE_WAVES)))
-#endif
-k_composite_wave(FieldArgs a) {
+__global__ void __launch_bounds__(NT) k_composite_wave(FieldArgs a) {
   if (a.denc_max && blockIdx.x == 0 && threadIdx.x < kSigmaLevels) a.denc_max[threadIdx.x] = 0.f;  // before k_mlp_bwd_tiles
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;

@@ -91,9 +91,6 @@ __device__ __forceinline__ void fine_gather_paired(const uint32_t* __restrict__ 
 #ifndef LNR_ENC_LPB
 #define LNR_ENC_LPB 4  // most levels per workgroup of the training / plain eval encode (1, 2 or 4)
 #endif
-#ifndef LNR_ENC_LIVE_LPB
-#define LNR_ENC_LIVE_LPB 0
-#endif
 #ifndef LNR_ENC_GROUP_MIN_ROWS
 #define LNR_ENC_GROUP_MIN_ROWS 512  // fewer rows: one level per workgroup (C1's 64 rows need the workgroups)
 #endif
@@ -391,11 +388,6 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
     if (live == nullptr)
       hipLaunchKernelGGL(enc_kernel(), dim3(grid.x, d->n_levels / lpb), dim3(kSB), 0, st, a, pos, n, tb, enc, enc_stride,
                          BwdWorkspace{}, live);
-#if LNR_ENC_LIVE_LPB
-    else if (spt2 && lpb == 4)  // (experiment) the live-masked encode in strided groups of four levels too
-      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 2, false, 4>), dim3(grid.x, d->n_levels / 4), dim3(kSB / 2), 0, st, a, pos,
-                         n, tb, enc, enc_stride, BwdWorkspace{}, live);
-#endif
     else if (spt2)
       hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 2, false>), grid, dim3(kSB / 2), 0, st, a, pos, n, tb, enc,
                          enc_stride, BwdWorkspace{}, live);

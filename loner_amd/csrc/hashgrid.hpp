@@ -428,15 +428,6 @@ __device__ __forceinline__ RunInfo cell_runs_dpp(bool in, uint32_t cx, uint32_t 
         "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]),        \
         "+v"(v[15])                                                                                      \
       : "v"(f))
-#define LNR_FMAC_DPP_8(DPP, v, f)                                                                         \
-  asm volatile(                                                                                          \
-      "s_nop 1\n\t"                                                                                      \
-      "v_fmac_f32_dpp %0, %0, %8 " DPP "\n\tv_fmac_f32_dpp %1, %1, %8 " DPP "\n\t"                      \
-      "v_fmac_f32_dpp %2, %2, %8 " DPP "\n\tv_fmac_f32_dpp %3, %3, %8 " DPP "\n\t"                      \
-      "v_fmac_f32_dpp %4, %4, %8 " DPP "\n\tv_fmac_f32_dpp %5, %5, %8 " DPP "\n\t"                      \
-      "v_fmac_f32_dpp %6, %6, %8 " DPP "\n\tv_fmac_f32_dpp %7, %7, %8 " DPP                             \
-      : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])   \
-      : "v"(f))
 #ifndef LNR_SEG_FMAC
 #define LNR_SEG_FMAC 1  // the segmented sums as v_fmac_f32_dpp (1) or DPP move + masked add (0)
 #endif
@@ -452,15 +443,6 @@ __device__ __forceinline__ void run_sum_dpp_n(const RunInfo& ri, float (&v)[N]) 
   const int lane = threadIdx.x & 63;
   const int h = ri.head_lane;
   const int rs = lane & ~15;
-  if constexpr (LNR_SEG_FMAC && N == 8) {  // (half the values at a time: fewer live registers)
-    LNR_FMAC_DPP_8("row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1", v, (lane - 1 >= h) ? 1.f : 0.f);
-    LNR_FMAC_DPP_8("row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1", v, (lane - 2 >= h) ? 1.f : 0.f);
-    LNR_FMAC_DPP_8("row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1", v, (lane - 4 >= h) ? 1.f : 0.f);
-    LNR_FMAC_DPP_8("row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1", v, (lane - 8 >= h) ? 1.f : 0.f);
-    LNR_FMAC_DPP_8("row_bcast:15 row_mask:0xf bank_mask:0xf bound_ctrl:1", v, ((lane & 16) && h < rs) ? 1.f : 0.f);
-    LNR_FMAC_DPP_8("row_bcast:31 row_mask:0xf bank_mask:0xf bound_ctrl:1", v, (lane >= 32 && h < 32) ? 1.f : 0.f);
-    return;
-  }
   if constexpr (LNR_SEG_FMAC && N == 16) {
     // (branching around a step would cost the register copies the compiler places at the joins; a
     // step no run needs multiplies by 0 everywhere)

@@ -455,16 +455,7 @@ __global__ void __launch_bounds__(kSB, LNR_SCATTER_WAVES_PER_EU) k_bwd_scatter(G
 //  * A (row, level) with more than kRowsCap records (coherent rows whose runs did not merge) writes
 //    every record straight to its global slot instead (same slots, unstaged).
 // Same records, counts and blockmax as k_bwd_scatter.
-#ifndef LNR_ROWS_CAP
-#define LNR_ROWS_CAP 2176
-#endif
-#ifndef LNR_ROWS_SG_SPLIT
-#define LNR_ROWS_SG_SPLIT 0  // (experiment) bucket starts as u16 + global slots as u32 (6 B per bucket, not 8)
-#endif
-#ifndef LNR_ROWS_LV_ARGS
-#define LNR_ROWS_LV_ARGS 0  // (experiment) level parameters read from the kernel arguments, not staged in LDS
-#endif
-constexpr int kRowsCap = LNR_ROWS_CAP;  // 4.25 records per sample: fine rows hold 4 + the rare split pairs
+constexpr int kRowsCap = 2176;  // 4.25 records per sample: fine rows hold 4 + the rare split pairs
 // Stages: 1, one stage with the copy-out after each level's placement: 44 KB of LDS and 80 VGPRs
 // (GradJac: the Jacobian held as fp16 pairs), so 3 workgroups (6 waves per SIMD) share a CU; 2, a
 // double-buffered stage with the copy-out of level l - 1 overlapping level l, 79 KB, 2 workgroups
@@ -479,25 +470,7 @@ constexpr int rows_stages() {
   return LNR_SCATTER_STAGES ? LNR_SCATTER_STAGES : (sizeof(typename GradFn::Raw) <= 4 || NB > 64 ? 1 : 2);
 }
 template <class GradFn, int NB>
-#ifndef LNR_ROWS_STAGE12
-#define LNR_ROWS_STAGE12 0  // (experiment) the stage as {word, values} + slot arrays, 12 B a record
-#endif
-#ifndef LNR_ROWS_G_AHEAD
-#define LNR_ROWS_G_AHEAD 0  // (experiment) levels of gradient loaded ahead (0: all in the prologue)
-#endif
-#ifndef LNR_ROWS_COH_HALF
-#define LNR_ROWS_COH_HALF 0  // (experiment) coherent levels' run sums 8 values at a time
-#endif
-#ifndef LNR_ROWS_PLACE_SEQ
-#define LNR_ROWS_PLACE_SEQ 0  // (experiment) records ranked and placed this many at a time (0: all 4)
-#endif
-#ifndef LNR_ROWS_ROT
-#define LNR_ROWS_ROT 0
-#endif
-#ifndef LNR_ROWS_WAVES1
-#define LNR_ROWS_WAVES1 6  // waves per SIMD of the one-stage scatter (8 needs <= 64 VGPRs and <= 40 KB LDS)
-#endif
-constexpr int rows_waves() { return rows_stages<GradFn, NB>() == 1 ? LNR_ROWS_WAVES1 : 4; }
+constexpr int rows_waves() { return rows_stages<GradFn, NB>() == 1 ? 6 : 4; }
 #ifndef LNR_PRESCALE
 #define LNR_PRESCALE 1
 #endif
@@ -506,30 +479,18 @@ constexpr int rows_waves() { return rows_stages<GradFn, NB>() == 1 ? LNR_ROWS_WA
 #endif
 template <int NL, int NB, int STG>
 struct RowsLds {  // the small tables first: their addresses fit the 16-bit LDS instruction offset
-#if LNR_ROWS_SG_SPLIT
-  uint32_t sg_slot[NL][NB];   // per level and bucket: global slot of the run
-  uint16_t sg_start[NL][NB];  // and its start in the stage
-#else
   uint2 sg[NL][NB];           // per level and bucket: {start in the stage, global slot of the run}
-#endif
   uint32_t total[NL];         // records of the row at each level
   uint32_t ctr[2][NB];        // rank counters
-#if !LNR_ROWS_LV_ARGS
   LevelParams lv[NL];         // the level table (kernel arguments indexed per level would be loads)
-#endif
-#if LNR_ROWS_STAGE12
-  uint2 stage[STG][kRowsCap];      // staged records {word, fp16 value pair}, bucket order
-  uint32_t stage_slot[STG][kRowsCap];  // and their global slots (12 B a record: 26 KB for one stage)
-#else
   uint4 stage[STG][kRowsCap];  // staged records {word, global slot, fp16 value pair, -}, bucket order
-#endif
 };
 
 // NL levels, the first NM coherent (run-merging) and the rest fine, at most NB buckets per level:
 // compile-time, so the level loop unrolls into straight-line code.  Record slots are 32-bit (the
 // launcher checks 8 N L < 2^32).
 // The body walks levels [LB, LB + NL) of histogram row sb (local level l is level LB + l).
-template <class PosFn, class GradFn, int LB, int NL, int NM, int NB, int kRowsStages, bool ROT = false>
+template <class PosFn, class GradFn, int LB, int NL, int NM, int NB, int kRowsStages>
 __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& sm, const GridArgs& a, const PosFn& pos,
                                                   int64_t n, const GradFn& grad, const BwdWorkspace& ws, bool skip_zero,
                                                   int64_t sb) {
@@ -545,18 +506,15 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
   const uint32_t spare = (uint32_t)(8 * n * (int64_t)a.n_levels);  // one of the 2 slack records past the last slot
 
   // prologue 1: the level table and zero rank counters
-#if !LNR_ROWS_LV_ARGS
   if (threadIdx.x < NL * (sizeof(LevelParams) / 4))
     reinterpret_cast<uint32_t*>(sm.lv)[threadIdx.x] = reinterpret_cast<const uint32_t*>(a.lv + LB)[threadIdx.x];
-#endif
   if (threadIdx.x < 2 * NB) (&sm.ctr[0][0])[threadIdx.x] = 0u;
   // prologue 2: every global load of the kernel
   const typename PosFn::Raw raw = pos.load(ic);
-  constexpr int kGA = LNR_ROWS_G_AHEAD > 0 && LNR_ROWS_G_AHEAD < NL ? LNR_ROWS_G_AHEAD : NL;
-  typename GradFn::Raw g[kGA];  // (GradJac: the fp16 pair, scaled by d sigma at use: half the registers)
+  typename GradFn::Raw g[NL];  // (GradJac: the fp16 pair, scaled by d sigma at use: half the registers)
 #pragma unroll
-  for (int l = 0; l < kGA; ++l) g[l] = grad.load_raw_nt(LB + l, ic);  // read once: nontemporal, so they do not
-                                                                 // displace the runs' L2 lines
+  for (int l = 0; l < NL; ++l) g[l] = grad.load_raw_nt(LB + l, ic);  // read once: nontemporal, so they do not
+                                                                // displace the runs' L2 lines
   const float gsc = grad.scale(ic);
   uint32_t h0[2][2], h1[2][2];
   uint64_t seg[2][2];
@@ -590,19 +548,8 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
       const uint32_t c1 = 2 * lane + 1 < nb ? h1[p][1] - h0[p][1] : 0u;
       const uint32_t inc = wave_incl_scan_u32(c0 + c1);
       const uint32_t ex = inc - c0 - c1;
-#if LNR_ROWS_SG_SPLIT
-      if (2 * lane < nb) {
-        sm.sg_start[l][2 * lane] = (uint16_t)ex;
-        sm.sg_slot[l][2 * lane] = (uint32_t)(seg[p][0] + h0[p][0]);
-      }
-      if (2 * lane + 1 < nb) {
-        sm.sg_start[l][2 * lane + 1] = (uint16_t)(ex + c0);
-        sm.sg_slot[l][2 * lane + 1] = (uint32_t)(seg[p][1] + h0[p][1]);
-      }
-#else
       if (2 * lane < nb) sm.sg[l][2 * lane] = make_uint2(ex, (uint32_t)(seg[p][0] + h0[p][0]));
       if (2 * lane + 1 < nb) sm.sg[l][2 * lane + 1] = make_uint2(ex + c0, (uint32_t)(seg[p][1] + h0[p][1]));
-#endif
       if (lane == 63) sm.total[l] = inc;
     }
   }
@@ -629,43 +576,24 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
       if ((uint32_t)(u * kSB) < lim) {
         const uint32_t t = threadIdx.x + u * kSB;
         if (t < lim) {
-#if LNR_ROWS_STAGE12
-          const uint2 q = sm.stage[sbuf][t];
-          const uint32_t sl = sm.stage_slot[sbuf][t];
-          ws.rec[sl < spare ? sl : spare] = q;
-#else
           const uint4 q = sm.stage[sbuf][t];
           const uint32_t d = q.y < spare ? q.y : spare;  // (the bound: never a store outside the records)
           ws.rec[d] = make_uint2(q.x, q.z);
-#endif
         }
       }
     }
 #endif
   };
 
-  static_assert(!ROT || (kRowsStages == 1 && NL % 4 == 0), "rotated level order: one stage, an even half");
 #pragma unroll
-  for (int ll = 0; ll < NL; ++ll) {
-    // ROT: this row walks levels NL/2 .. NL-1 first, then 0 .. NL/2-1 (the counters' parity is kept)
-    const int l = ROT ? (ll + NL / 2) % NL : ll;
+  for (int l = 0; l < NL; ++l) {
     const int sbuf = l & 1;  // rank counters (and, with two stages, the stage)
     const int stg = kRowsStages == 2 ? sbuf : 0;
-#if LNR_ROWS_LV_ARGS
-    const LevelParams lv = a.lv[LB + l];
-#else
     const LevelParams lv = sm.lv[l];
-#endif
     const bool staged = sm.total[l] <= (uint32_t)kRowsCap;  // block-uniform
     uint32_t* ctr = sm.ctr[sbuf];
-#if LNR_ROWS_SG_SPLIT
-    auto sgl_at = [&](uint32_t b) { return make_uint2(sm.sg_start[l][b], sm.sg_slot[l][b]); };
-#else
     const uint2* sgl = sm.sg[l];
-    auto sgl_at = [&](uint32_t b) { return sgl[b]; };
-#endif
-    const float2 gl = GradFn::finish(g[l % kGA], gsc);
-    if (kGA < NL && l + kGA < NL) g[l % kGA] = grad.load_raw_nt(LB + l + kGA, ic);  // (experiment) kGA levels ahead
+    const float2 gl = GradFn::finish(g[l], gsc);
 #if LNR_PRESCALE
     // the level's record scale applied to the gradient once, not to every record value: a power of
     // two, so w (g 2^k) rounds exactly as (w g) 2^k
@@ -681,35 +609,19 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
       if (valid) {
         uint2 s4[4];
         uint32_t rank[4];
-#if LNR_ROWS_PLACE_SEQ
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {  // (experiment) two records at a time: fewer live registers
-          if (k % LNR_ROWS_PLACE_SEQ == 0) {
-#pragma unroll
-            for (int m = k; m < k + LNR_ROWS_PLACE_SEQ; ++m) s4[m] = sgl_at(bk[m]);
-#pragma unroll
-            for (int m = k; m < k + LNR_ROWS_PLACE_SEQ; ++m) rank[m] = atomicAdd(&ctr[bk[m]], 1u);
-          }
-#else
-#pragma unroll
-        for (int k = 0; k < 4; ++k) s4[k] = sgl_at(bk[k]);
+        for (int k = 0; k < 4; ++k) s4[k] = sgl[bk[k]];
 #pragma unroll
         for (int k = 0; k < 4; ++k) rank[k] = atomicAdd(&ctr[bk[k]], 1u);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-#endif
           const uint32_t slot = s4[k].y + rank[k];
           const uint32_t h = rec_half2(val[k].x, val[k].y, rs);
           if (staged) {  // three 32-bit fields (ds_write2_b32 + ds_write_b32: no register moves for a b128 quad)
-#if LNR_ROWS_STAGE12
-            sm.stage[stg][s4[k].x + rank[k]] = make_uint2(word[k], h);
-            sm.stage_slot[stg][s4[k].x + rank[k]] = slot;
-#else
             uint32_t* q = reinterpret_cast<uint32_t*>(&sm.stage[stg][s4[k].x + rank[k]]);
             q[0] = word[k];
             q[1] = slot;
             q[2] = h;
-#endif
           } else {  // (block-uniform) more records than the stage holds: each straight to its global slot
             ws.rec[slot < spare ? slot : spare] = make_uint2(word[k], h);
           }
@@ -748,29 +660,6 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
       Corners c;
       level_corners<true>(lv, x, y, z, c);
       const uint32_t off = lv.offset;
-#if LNR_ROWS_COH_HALF
-      // (experiment) corners 0-3, then 4-7: half the run-summed values live at a time
-      const RunInfo ri = cell_runs_dpp(in, c.cx, c.cy, c.cz);
-      const bool valid = in && ri.tail;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        float v[8];
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          v[2 * kk] = c.w[4 * h + kk] * gv.x;
-          v[2 * kk + 1] = c.w[4 * h + kk] * gv.y;
-        }
-        run_sum_dpp_n<8>(ri, v);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const uint32_t e = c.idx[4 * h + kk] - off;
-          bk4[kk] = e >> kChunkLog2;
-          w4[kk] = e & (kChunk - 1);
-          val4[kk] = make_float2(v[2 * kk], v[2 * kk + 1]);
-        }
-        place(valid, bk4, w4, val4);
-      }
-#else
       RunInfo ri;
       float v[16];
       coherent_run_values(c, in, gv.x, gv.y, ri, v);
@@ -787,7 +676,6 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
         }
         place(valid, bk4, w4, val4);
       }
-#endif
     }
     if (threadIdx.x < NB) sm.ctr[sbuf ^ 1][threadIdx.x] = 0u;  // level l + 1's counters (last used by l - 1)
     if (kRowsStages == 2) {
@@ -796,7 +684,7 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
     } else {
       lds_barrier();  // level l placed
       copy_out(l);
-      if (ll + 1 < NL) lds_barrier();  // the stage is free for the next level
+      if (l + 1 < NL) lds_barrier();  // the stage is free for level l + 1
     }
   }
   if (kRowsStages == 2) copy_out(NL - 1);
@@ -807,21 +695,7 @@ __global__ void __launch_bounds__(kSB)
 __attribute__((amdgpu_waves_per_eu(rows_waves<GradFn, NB>(), rows_waves<GradFn, NB>())))
 k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace ws, bool skip_zero) {
   __shared__ RowsLds<NL, NB, rows_stages<GradFn, NB>()> sm;
-#if LNR_ROWS_ROT
-  // (experiment) odd rows walk the fine levels first: workgroups that start together then run
-  // VALU-heavy coherent levels beside LDS-heavy fine ones
-  constexpr int kStg = rows_stages<GradFn, NB>();
-  const int64_t sb = xcd_row(blockIdx.x, gridDim.x);
-  // 1: odd rows; 2: every row; 3: rows whose index / 32 is odd (a CU's co-resident rows are 32 apart,
-  // adjacent rows keep one order)
-  const bool rot = LNR_ROWS_ROT == 1 ? (sb & 1) != 0 : LNR_ROWS_ROT == 2 ? true : ((sb >> 5) & 1) != 0;
-  if (kStg == 1 && rot)
-    scatter_rows_body<PosFn, GradFn, 0, NL, NM, NB, kStg, kStg == 1>(sm, a, pos, n, grad, ws, skip_zero, sb);
-  else
-    scatter_rows_body<PosFn, GradFn, 0, NL, NM, NB, kStg>(sm, a, pos, n, grad, ws, skip_zero, sb);
-#else
   scatter_rows_body<PosFn, GradFn, 0, NL, NM, NB>(sm, a, pos, n, grad, ws, skip_zero, xcd_row(blockIdx.x, gridDim.x));
-#endif
 }
 
 constexpr size_t kScatterLds = (size_t)kCap * 4 + kMaxChunksPerLevel * 8 + (size_t)kCap * 4 + kMaxChunksPerLevel * 4 +
@@ -891,9 +765,6 @@ __device__ __forceinline__ unsigned long long fixed_i64(float x) {
 #ifndef LNR_ACCUM_TRIP
 #define LNR_ACCUM_TRIP 2
 #endif
-#ifndef LNR_ACCUM_BANKSORT
-#define LNR_ACCUM_BANKSORT 0  // (experiment) bits of the bank-pair index sorted on inside each wave, 0..5
-#endif
 constexpr int kAccumTrip = LNR_ACCUM_TRIP;        // tiles per trip of the accumulate loop (loads ahead)
 constexpr int kTile = 2 * kAccumThreads;         // records per tile: 2 per thread
 static_assert(kTile == 2048, "the stage's swizzle and the strided reads assume 64-lane waves x 16 x 2");
@@ -951,45 +822,6 @@ __device__ __forceinline__ void accum_records(unsigned long long* acc, uint2* st
     *reinterpret_cast<u32x4*>(&stage[stage_pos(2 * threadIdx.x)]) = cur;
     lds_barrier();
     const uint64_t base = beg2 + tile * kTile;
-#if LNR_ACCUM_BANKSORT
-    // (experiment) each atomic instruction's 64 records radix-sorted inside the wave on the low
-    // LNR_ACCUM_BANKSORT bits of their bank pair (e0 mod 32: acc[e0] and acc[kChunk + e0] share it),
-    // ballot + mbcnt + ds_permute per bit, then dealt alternately to the two 32-lane halves, so a
-    // bank's records split over the halves.  Records outside [beg, end) become zero adds to entry 0.
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      uint2 rec = stage[stage_pos(q0 + r)];
-      const uint64_t rr = base + q0 + r;
-      if (!(rr >= beg && rr < end)) rec = make_uint2(0u, 0u);
-#pragma unroll
-      for (int bit = 0; bit < LNR_ACCUM_BANKSORT; ++bit) {
-        const bool one = (rec.x >> bit) & 1u;
-        const uint64_t m = __ballot(one);
-        const uint32_t below = one ? __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))
-                                   : __builtin_amdgcn_mbcnt_hi(~(uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo(~(uint32_t)m, 0u));
-        uint32_t dst = one ? (uint32_t)(64 - __popcll(m)) + below : below;
-        if (bit == LNR_ACCUM_BANKSORT - 1) dst = (dst >> 1) + ((dst & 1u) << 5);
-        rec.x = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)rec.x);
-        rec.y = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)rec.y);
-      }
-      {
-        const uint32_t w = rec.x;
-        const float v0 = rec_v0(rec.y), v1 = rec_v1(rec.y);
-        const uint32_t e0 = w & (kChunk - 1);
-        const uint32_t p = (w >> kChunkLog2) & 15u;
-        const float tx = (float)(w >> 16) * ftx;
-        const float s0 = fs - tx;
-        atomicAdd(&acc[e0], fixed_i64(s0 * v0));
-        atomicAdd(&acc[kChunk + e0], fixed_i64(s0 * v1));
-        if (p) {
-          const uint32_t e1 = e0 ^ ((1u << p) - 1u);
-          atomicAdd(&acc[e1], fixed_i64(tx * v0));
-          atomicAdd(&acc[kChunk + e1], fixed_i64(tx * v1));
-        }
-      }
-    }
-    return;
-#endif
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const uint2 rec = stage[stage_pos(q0 + r)];
