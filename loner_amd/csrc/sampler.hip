@@ -250,7 +250,7 @@ __device__ __forceinline__ void wave_bitonic_merge(float (&v)[E]) {
 }
 
 #ifndef LNR_SAMPLER_MERGE
-#define LNR_SAMPLER_MERGE 0  // sort the importance draws alone, then merge with the strata (LONER_SAMPLER_MERGE)
+#define LNR_SAMPLER_MERGE 1  // sort the importance draws alone, then merge with the strata (LONER_SAMPLER_MERGE)
 #endif
 static bool sampler_merge() {  // read at every launch
   const char* e = getenv("LONER_SAMPLER_MERGE");
