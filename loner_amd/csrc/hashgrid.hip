@@ -91,9 +91,6 @@ __device__ __forceinline__ void fine_gather_paired(const uint32_t* __restrict__ 
 #ifndef LNR_ENC_LPB
 #define LNR_ENC_LPB 4  // most levels per workgroup of the training / plain eval encode (1, 2 or 4)
 #endif
-#ifndef LNR_ENC_SPT
-#define LNR_ENC_SPT 1  // samples per thread of the training / plain eval encode (experiment: 2)
-#endif
 #ifndef LNR_ENC_GROUP_MIN_ROWS
 #define LNR_ENC_GROUP_MIN_ROWS 512  // fewer rows: one level per workgroup (C1's 64 rows need the workgroups)
 #endif
@@ -369,9 +366,9 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
   const bool spt2 = n >= (int64_t)LNR_ENC_SPT2_MIN_N;
   const int lpb = enc_levels_per_group(d, (n + kSB - 1) / kSB);
   auto enc_kernel = [&]() {
-    return lpb == 4 ? k_hashgrid_fwd<PosFn, LNR_ENC_SPT, LNR_ENC_PAIRED, 4>
-         : lpb == 2 ? k_hashgrid_fwd<PosFn, LNR_ENC_SPT, LNR_ENC_PAIRED, 2>
-                    : k_hashgrid_fwd<PosFn, LNR_ENC_SPT, LNR_ENC_PAIRED, 1>;
+    return lpb == 4 ? k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 4>
+         : lpb == 2 ? k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 2>
+                    : k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 1>;
   };
   if (bwd_ws) {
     LNR_REQUIRE(bwd_ws_bytes >= bwd_workspace_bytes(d, n), "%s: backward workspace too small", who);
@@ -382,14 +379,14 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
     BwdWorkspace w = carve_workspace(bwd_ws, a, d, n);
     // one workgroup per histogram row (kSB samples) so the row is written whole
     dim3 gridc((unsigned)w.n_sb, d->n_levels / lpb);
-    hipLaunchKernelGGL(enc_kernel(), gridc, dim3(kSB / LNR_ENC_SPT), 0, st, a, pos, n, reinterpret_cast<const uint32_t*>(table), enc,
+    hipLaunchKernelGGL(enc_kernel(), gridc, dim3(kSB), 0, st, a, pos, n, reinterpret_cast<const uint32_t*>(table), enc,
                        enc_stride, w, nullptr);
   } else {
     // kSB-sample workgroups as in training (C2-size eval launch: 1011 us at 256 one-sample threads, 836 at 512)
     dim3 grid((unsigned)((n + kSB - 1) / kSB), d->n_levels);
     const uint32_t* tb = reinterpret_cast<const uint32_t*>(table);
     if (live == nullptr)
-      hipLaunchKernelGGL(enc_kernel(), dim3(grid.x, d->n_levels / lpb), dim3(kSB / LNR_ENC_SPT), 0, st, a, pos, n, tb, enc, enc_stride,
+      hipLaunchKernelGGL(enc_kernel(), dim3(grid.x, d->n_levels / lpb), dim3(kSB), 0, st, a, pos, n, tb, enc, enc_stride,
                          BwdWorkspace{}, live);
     else if (spt2)
       hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 2, false>), grid, dim3(kSB / 2), 0, st, a, pos, n, tb, enc,
