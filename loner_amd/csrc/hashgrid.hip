@@ -102,11 +102,15 @@ __device__ __forceinline__ void fine_gather_paired(const uint32_t* __restrict__ 
 // A group's fine levels must fit an XCD's 4 MB L2 together: four 1 MB levels of the sigma grid (2^18
 // entries), two 2 MB levels of the colour grid (2^19: CAM's colour encode 0.33 ms at one level per
 // workgroup, 0.37 at four).
+#ifndef LNR_ENC_GROUP4_MIN_ROWS
+#define LNR_ENC_GROUP4_MIN_ROWS 512  // rows from which groups of four are allowed (fewer: at most two)
+#endif
 inline int enc_levels_per_group(const lnr_grid_desc* d, int64_t n_sb) {
   if (n_sb < LNR_ENC_GROUP_MIN_ROWS) return 1;
   const int64_t level_bytes = (int64_t)4 << d->log2_hashmap_size;
   for (int g = LNR_ENC_LPB; g > 1; g /= 2)
-    if (d->n_levels % g == 0 && g * level_bytes <= ((int64_t)4 << 20)) return g;
+    if (d->n_levels % g == 0 && g * level_bytes <= ((int64_t)4 << 20) && (g < 4 || n_sb >= LNR_ENC_GROUP4_MIN_ROWS))
+      return g;
   return 1;
 }
 #ifndef LNR_ENC_WAVES
