@@ -19,7 +19,8 @@ first pose, :245-248).  The hpk (haveri) dataset family has no calibration objec
 corners (+-max range)^3 are transformed by every pose (rotation AND translation, :296-298), and the
 points are those corners plus every pose's position; origin = the points' box centre, scale = |box
 diagonal| / (2 sqrt 3) * (1 + padding), shift = -origin.  The camera-frustum branch (:262-283, taken
-only with a Fusion Portable calibration) is not restated: no C5 workload reaches it."""
+only with a Fusion Portable calibration) is restated with the other branches in
+``loner_amd.rays.compute_world_cube`` and pinned by tests/golden/world_cube_camera.npz."""
 import numpy as np
 
 MAX_LENGTH = 50.0  # metres (:24)
