@@ -4,8 +4,8 @@
 // 68, 71) and tcnn.Encoding (:40, 64).  The backward lives in hashgrid_bwd.hip.
 //
 // Launch shape: grid (ceil(N / kSB), n_levels / G) of kSB-thread workgroups (kSB = 512 samples, one
-// histogram row each), each taking G levels y, y + L/G, y + 2 L/G, ... (G = 4 from 512 rows, see
-// enc_levels_per_group; the live-masked eval launch: G = 1, kSB / 2 threads of two samples).  The
+// histogram row each), each taking G levels y, y + L/G, y + 2 L/G, ... (G = 2 from 512 rows, 4 from
+// 2048, see enc_levels_per_group; the live-masked eval launch: G = 1, kSB / 2 threads of two samples).  The
 // level group is the slow grid dimension, so the dispatcher walks group by group and the live gather
 // footprint is one group's table slices (<= 4 MB fp16, about an XCD's L2) instead of the whole
 // 14.8 MB table; and every group mixes coherent levels (position decoding, run detection: VALU) with
@@ -103,7 +103,9 @@ __device__ __forceinline__ void fine_gather_paired(const uint32_t* __restrict__ 
 // entries), two 2 MB levels of the colour grid (2^19: CAM's colour encode 0.33 ms at one level per
 // workgroup, 0.37 at four).
 #ifndef LNR_ENC_GROUP4_MIN_ROWS
-#define LNR_ENC_GROUP4_MIN_ROWS 512  // rows from which groups of four are allowed (fewer: at most two)
+// Groups of four from 2048 rows: at 1152 (C4, one rank of eight) pairs encode 0.0975 ms against 0.0993
+// with fours, bitwise the same (tools/gpu_ab_libs.sh, three interleaved runs each).
+#define LNR_ENC_GROUP4_MIN_ROWS 2048  // rows from which groups of four are allowed (fewer: at most two)
 #endif
 inline int enc_levels_per_group(const lnr_grid_desc* d, int64_t n_sb) {
   if (n_sb < LNR_ENC_GROUP_MIN_ROWS) return 1;

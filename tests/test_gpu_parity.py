@@ -174,13 +174,14 @@ def test_hashgrid_fwd_run_head_gathers_bitwise(L, S, monkeypatch):
     assert torch.equal(outs["0"][0], outs["0"][2])
 
 
+@pytest.mark.parametrize("R", [520, 2060])
 @pytest.mark.parametrize("nl", [15, 14])
-def test_hashgrid_fwd_level_groups_bitwise(L, nl):
-    """From 512 histogram rows a 16-level grid encodes four levels per workgroup (y, y + 4, y + 8,
-    y + 12), a 14-level grid two (y, y + 7) and a 15-level grid one: the levels the grids share have
-    bit for bit the same encodings and training-launch record histograms."""
+def test_hashgrid_fwd_level_groups_bitwise(L, nl, R):
+    """From 512 histogram rows a 16-level grid encodes two levels per workgroup (y, y + 8), from 2048
+    rows four (y, y + 4, y + 8, y + 12); a 14-level grid two (y, y + 7) and a 15-level grid one: the
+    levels the grids share have bit for bit the same encodings and training-launch record histograms."""
     rng = np.random.default_rng(17)
-    R, S = 520, 512
+    S = 512
     o = rng.uniform(-0.5, 0.5, (R, 3))
     dr = rng.normal(0, 1, (R, 3))
     dr /= np.linalg.norm(dr, axis=1, keepdims=True)
