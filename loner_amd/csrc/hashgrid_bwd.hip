@@ -907,9 +907,12 @@ __device__ __forceinline__ void accum_records(unsigned long long* acc, uint2* st
 // The final gradient g of table parameter i: stored into d_table, or (a.adam.p set) Adam's update of
 // parameter i with it, the arithmetic of optim.hip's adam_range term for term (-ffp-contract=off in
 // both files), so the parameters, moments and fp16 shadow are bitwise those of lnr_adam_step.
+// ADAM is a template flag (the kernels are instantiated twice) so the plain kernels carry none of the
+// epilogue's registers: with a runtime branch the accumulate spilled 20 VGPRs at its 64-VGPR cap.
+template <bool ADAM>
 __device__ __forceinline__ void put_grad(const GridArgs& a, float* __restrict__ d_table, int64_t i, float g) {
   const AdamEpi& e = a.adam;
-  if (e.p == nullptr) {
+  if (!ADAM) {
     d_table[i] = g;
     return;
   }
@@ -930,15 +933,16 @@ __device__ __forceinline__ void put_grad(const GridArgs& a, float* __restrict__ 
 // table's slice 16-B aligned), the first `cnt` of them valid: with the Adam epilogue every load of the
 // eight is issued before any arithmetic (16-B loads of p, m, v, one 16-B shadow store), so a thread
 // waits for memory once per eight parameters, not once per parameter.
+template <bool ADAM>
 __device__ __forceinline__ void put_grad8(const GridArgs& a, float* __restrict__ d_table, int64_t i0, const float (&g)[8],
                                           uint32_t cnt) {
   typedef float f32x4v __attribute__((ext_vector_type(4)));
   const AdamEpi& e = a.adam;
   if (cnt < 8) {
-    for (uint32_t k = 0; k < cnt; ++k) put_grad(a, d_table, i0 + k, g[k]);
+    for (uint32_t k = 0; k < cnt; ++k) put_grad<ADAM>(a, d_table, i0 + k, g[k]);
     return;
   }
-  if (e.p == nullptr) {
+  if (!ADAM) {
     f32x4v* d = reinterpret_cast<f32x4v*>(d_table + i0);
     d[0] = f32x4v{g[0], g[1], g[2], g[3]};
     d[1] = f32x4v{g[4], g[5], g[6], g[7]};
@@ -977,12 +981,13 @@ __device__ __forceinline__ void put_grad8(const GridArgs& a, float* __restrict__
 }
 
 // A whole bucket's final fp32 values from its LDS chunk.
+template <bool ADAM>
 __device__ __forceinline__ void store_bucket(const unsigned long long* acc, const GridArgs& a, const BwdWorkspace& ws,
                                              float* __restrict__ d_table, uint32_t l, uint32_t ent0, uint32_t nent,
                                              int k2) {
   const double inv = unit_back(a, ws, l, k2);
   const int64_t base = 2 * ((int64_t)a.lv[l].offset + ent0);
-  if (a.adam.p != nullptr) {  // eight consecutive parameters per thread per pass (put_grad8)
+  if (ADAM) {  // eight consecutive parameters per thread per pass (put_grad8)
     for (uint32_t t0 = 8 * threadIdx.x; t0 < 2 * nent; t0 += 8 * blockDim.x) {
       float g[8];
 #pragma unroll
@@ -990,12 +995,12 @@ __device__ __forceinline__ void store_bucket(const unsigned long long* acc, cons
         const uint32_t t = t0 + k;
         g[k] = (float)((double)(long long)acc[(t & 1) * kChunk + (t >> 1)] * inv);
       }
-      put_grad8(a, d_table, base + t0, g, 2 * nent - t0 < 8 ? 2 * nent - t0 : 8);
+      put_grad8<true>(a, d_table, base + t0, g, 2 * nent - t0 < 8 ? 2 * nent - t0 : 8);
     }
     return;
   }
   for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x)
-    put_grad(a, d_table, base + t, (float)((double)(long long)acc[(t & 1) * kChunk + (t >> 1)] * inv));
+    put_grad<false>(a, d_table, base + t, (float)((double)(long long)acc[(t & 1) * kChunk + (t >> 1)] * inv));
 }
 
 // One workgroup per kAccumGroups-th of the records of buckets [b_begin, b_end).  Per bucket piece:
@@ -1007,21 +1012,22 @@ __device__ __forceinline__ void store_bucket(const unsigned long long* acc, cons
 // its own LDS sums (int64: exact, so the arrival order does not matter) and stores the fp32 values;
 // the workgroup whose range holds an empty bucket's position stores its zeros.  Without FINISH,
 // k_bwd_finalize does both in a second launch.
+template <bool ADAM>
 __device__ __forceinline__ void store_zero_bucket(const GridArgs& a, float* __restrict__ d_table, uint32_t b) {
   const uint32_t l = level_of_bucket(a, b);
   const uint32_t ent0 = (b - a.bucket_base[l]) * kChunk;
   const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
   const int64_t base = 2 * ((int64_t)a.lv[l].offset + ent0);
-  if (a.adam.p != nullptr) {
+  if (ADAM) {
     const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (uint32_t t0 = 8 * threadIdx.x; t0 < 2 * nent; t0 += 8 * blockDim.x)
-      put_grad8(a, d_table, base + t0, z, 2 * nent - t0 < 8 ? 2 * nent - t0 : 8);
+      put_grad8<true>(a, d_table, base + t0, z, 2 * nent - t0 < 8 ? 2 * nent - t0 : 8);
     return;
   }
-  for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) put_grad(a, d_table, base + t, 0.f);
+  for (uint32_t t = threadIdx.x; t < 2 * nent; t += blockDim.x) put_grad<false>(a, d_table, base + t, 0.f);
 }
 
-template <bool FINISH>
+template <bool FINISH, bool ADAM>
 __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_accum(GridArgs a, BwdWorkspace ws, float* __restrict__ d_table,
                                                                                         uint32_t b_begin, uint32_t b_end) {
   __shared__ unsigned long long acc[2 * kChunk];  // int64 fixed point, one array per feature (8-B atomics
@@ -1031,7 +1037,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
   const uint32_t gi = blockIdx.x;
   if (FINISH && R == 0) {  // no records at all: workgroup 0 stores every bucket's zeros
     if (gi == 0)
-      for (uint32_t b = b_begin; b < b_end; ++b) store_zero_bucket(a, d_table, b);
+      for (uint32_t b = b_begin; b < b_end; ++b) store_zero_bucket<ADAM>(a, d_table, b);
     return;
   }
   const uint64_t rbeg = range_at(r0, R, gi), rend = range_at(r0, R, gi + 1);
@@ -1048,7 +1054,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
     const uint64_t s0 = ws.seg_start[b], s1 = ws.seg_start[b + 1];
     if (s0 >= rend && !(FINISH && s0 == rend && rend == rtot)) break;  // (the last range owns trailing empties)
     if (s0 == s1) {  // empty bucket
-      if (FINISH) store_zero_bucket(a, d_table, b);  // owned: rbeg <= s0 < rend, or trailing
+      if (FINISH) store_zero_bucket<ADAM>(a, d_table, b);  // owned: rbeg <= s0 < rend, or trailing
       continue;
     }
     const uint64_t beg = s0 > rbeg ? s0 : rbeg, end = s1 < rend ? s1 : rend;
@@ -1063,7 +1069,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
     accum_records(acc, stage, ws, beg, end, ldexpf(1.f, k2), l >= a.accum_direct_level);
     lds_barrier();
     if (beg == s0 && end == s1) {  // the whole bucket: the final values
-      store_bucket(acc, a, ws, d_table, l, ent0, nent, k2);
+      store_bucket<ADAM>(acc, a, ws, d_table, l, ent0, nent, k2);
       lds_barrier();
       continue;
     }
@@ -1101,7 +1107,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
             acc[(t & 1) * kChunk + (t >> 1)] += (unsigned long long)src[t];
         }
         lds_barrier();
-        store_bucket(acc, a, ws, d_table, l, ent0, nent, k2);
+        store_bucket<ADAM>(acc, a, ws, d_table, l, ent0, nent, k2);
       }
     }
     lds_barrier();
@@ -1115,6 +1121,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
 // fixed-point unit as k_bwd_accum: bitwise the same gradient.  The record-balanced k_bwd_accum
 // instead pays two 64 KB partial chunks per workgroup and a finalize pass over every cut bucket,
 // which dominates when a bucket holds a tile or two of records.
+template <bool ADAM>
 __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_accum_buckets(GridArgs a, BwdWorkspace ws,
                                                                                                 float* __restrict__ d_table,
                                                                                                 uint32_t b_begin, uint32_t b_end) {
@@ -1126,7 +1133,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
   const uint32_t ent0 = (b - a.bucket_base[l]) * kChunk;
   const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
   if (s0 == s1) {
-    store_zero_bucket(a, d_table, b);
+    store_zero_bucket<ADAM>(a, d_table, b);
     return;
   }
   for (int t = threadIdx.x; t < 2 * kChunk; t += blockDim.x) acc[t] = 0ull;
@@ -1134,7 +1141,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
   const int k2 = bucket_k2(ws, b);
   accum_records(acc, stage, ws, s0, s1, ldexpf(1.f, k2), l >= a.accum_direct_level);
   lds_barrier();
-  store_bucket(acc, a, ws, d_table, l, ent0, nent, k2);
+  store_bucket<ADAM>(acc, a, ws, d_table, l, ent0, nent, k2);
 }
 
 // One workgroup per unit of the work list (UnitTable): a whole bucket (its fp32 values, or its zeros
@@ -1145,7 +1152,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
 // k_bwd_finalize_units launch.  The cut buckets are the coarse levels', first in the list, so their
 // finishing overlaps the fine levels' units.
 static_assert(kUnitMinRecords == (uint64_t)kTile, "pieces of at least one tile");
-template <bool FINISH>
+template <bool FINISH, bool ADAM>
 __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_accum_units(GridArgs a, BwdWorkspace ws,
                                                                                               float* __restrict__ d_table) {
   __shared__ unsigned long long acc[2 * kChunk];
@@ -1159,7 +1166,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
   const uint32_t ent0 = (b - a.bucket_base[l]) * kChunk;
   const uint32_t nent = (a.lv[l].size - ent0) < (uint32_t)kChunk ? (a.lv[l].size - ent0) : (uint32_t)kChunk;
   if (s0 == s1) {
-    store_zero_bucket(a, d_table, b);
+    store_zero_bucket<ADAM>(a, d_table, b);
     return;
   }
   const uint64_t n = s1 - s0, beg = s0 + n * k / P, end = s0 + n * (k + 1) / P;
@@ -1169,7 +1176,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
   accum_records(acc, stage, ws, beg, end, ldexpf(1.f, k2), l >= a.accum_direct_level);
   lds_barrier();
   if (P == 1) {
-    store_bucket(acc, a, ws, d_table, l, ent0, nent, k2);
+    store_bucket<ADAM>(acc, a, ws, d_table, l, ent0, nent, k2);
     return;
   }
   const uint32_t slot0 = ut->slot[b];
@@ -1198,12 +1205,13 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
       acc[(t & 1) * kChunk + (t >> 1)] += (unsigned long long)src[t];
   }
   lds_barrier();
-  store_bucket(acc, a, ws, d_table, l, ent0, nent, k2);
+  store_bucket<ADAM>(acc, a, ws, d_table, l, ent0, nent, k2);
 }
 
 // Buckets the accumulation did not finish: cut buckets = the sum of their pieces' partial chunks in
 // workgroup order (deterministic), empty buckets = 0.  One workgroup per bucket of [b_begin, b_end).
 constexpr int kFinalizeThreads = 1024;  // 8 consecutive values per thread: 2 kChunk in one pass
+template <bool ADAM>
 __global__ void __launch_bounds__(kFinalizeThreads) k_bwd_finalize(GridArgs a, BwdWorkspace ws, float* __restrict__ d_table,
                                                                    uint32_t b_begin, uint32_t b_end) {
   static_assert(2 * kChunk == 8 * kFinalizeThreads, "one pass");
@@ -1242,8 +1250,8 @@ __global__ void __launch_bounds__(kFinalizeThreads) k_bwd_finalize(GridArgs a, B
 #pragma unroll
   for (int k = 0; k < 8; ++k) o[k] = (float)((double)v[k] * inv);
   const int64_t base = 2 * ((int64_t)a.lv[l].offset + ent0) + t0;
-  if (a.adam.p != nullptr) {
-    put_grad8(a, d_table, base, o, 2 * nent - t0 < 8 ? 2 * nent - t0 : 8);
+  if (ADAM) {
+    put_grad8<true>(a, d_table, base, o, 2 * nent - t0 < 8 ? 2 * nent - t0 : 8);
     return;
   }
   float* dst = d_table + base;
@@ -1258,6 +1266,7 @@ __global__ void __launch_bounds__(kFinalizeThreads) k_bwd_finalize(GridArgs a, B
 
 // The cut buckets of the unit accumulation: the sum of their pieces' partial chunks in piece order.
 // One workgroup per cut bucket (the grid is the bound kAccumGroups; the rest return at once).
+template <bool ADAM>
 __global__ void __launch_bounds__(kFinalizeThreads) k_bwd_finalize_units(GridArgs a, BwdWorkspace ws,
                                                                          float* __restrict__ d_table) {
   typedef long long i64x2 __attribute__((ext_vector_type(2)));
@@ -1288,8 +1297,8 @@ __global__ void __launch_bounds__(kFinalizeThreads) k_bwd_finalize_units(GridArg
 #pragma unroll
   for (int j = 0; j < 8; ++j) o[j] = (float)((double)v[j] * inv);
   const int64_t base = 2 * ((int64_t)a.lv[l].offset + ent0) + t0;
-  if (a.adam.p != nullptr) {
-    put_grad8(a, d_table, base, o, 2 * nent - t0 < 8 ? 2 * nent - t0 : 8);
+  if (ADAM) {
+    put_grad8<true>(a, d_table, base, o, 2 * nent - t0 < 8 ? 2 * nent - t0 : 8);
     return;
   }
   float* dst = d_table + base;
@@ -1352,30 +1361,31 @@ static void launch_accum(const GridArgs& a, const BwdWorkspace& w, const lnr_gri
                          uint32_t l1, float* d_table, hipStream_t st) {
   const uint32_t b0 = a.bucket_base[l0], b1 = a.bucket_base[l1];
   if (b1 <= b0) return;
+  const bool adam = a.adam.p != nullptr;
   if (accum_units(n)) {  // the work list: whole buckets and equal pieces of the large ones
     if (b0 != 0 || b1 != a.n_buckets)  // (a level range: its own list; the whole range's is the scan's)
       hipLaunchKernelGGL(k_bwd_units, dim3(1), dim3(1024), 0, st, w, b0, b1);
     if (units_finish()) {
-      hipLaunchKernelGGL(k_bwd_accum_units<true>, dim3(b1 - b0 + kAccumGroups), dim3(kAccumThreads), 0, st, a, w,
+      hipLaunchKernelGGL((adam ? k_bwd_accum_units<true, true> : k_bwd_accum_units<true, false>), dim3(b1 - b0 + kAccumGroups), dim3(kAccumThreads), 0, st, a, w,
                          d_table);
       return;
     }
-    hipLaunchKernelGGL(k_bwd_accum_units<false>, dim3(b1 - b0 + kAccumGroups), dim3(kAccumThreads), 0, st, a, w,
+    hipLaunchKernelGGL((adam ? k_bwd_accum_units<false, true> : k_bwd_accum_units<false, false>), dim3(b1 - b0 + kAccumGroups), dim3(kAccumThreads), 0, st, a, w,
                        d_table);
-    hipLaunchKernelGGL(k_bwd_finalize_units, dim3(std::min<uint32_t>(b1 - b0, kAccumGroups)), dim3(kFinalizeThreads), 0,
+    hipLaunchKernelGGL((adam ? k_bwd_finalize_units<true> : k_bwd_finalize_units<false>), dim3(std::min<uint32_t>(b1 - b0, kAccumGroups)), dim3(kFinalizeThreads), 0,
                        st, a, w, d_table);
     return;
   }
   if (n <= accum_buckets_max_n()) {  // small batches: whole buckets, no partials, no finalize
-    hipLaunchKernelGGL(k_bwd_accum_buckets, dim3(b1 - b0), dim3(kAccumThreads), 0, st, a, w, d_table, b0, b1);
+    hipLaunchKernelGGL((adam ? k_bwd_accum_buckets<true> : k_bwd_accum_buckets<false>), dim3(b1 - b0), dim3(kAccumThreads), 0, st, a, w, d_table, b0, b1);
     return;
   }
   if (accum_finish()) {  // cut buckets finished by their last piece's workgroup: no finalize launch
-    hipLaunchKernelGGL(k_bwd_accum<true>, dim3(kAccumGroups), dim3(kAccumThreads), 0, st, a, w, d_table, b0, b1);
+    hipLaunchKernelGGL((adam ? k_bwd_accum<true, true> : k_bwd_accum<true, false>), dim3(kAccumGroups), dim3(kAccumThreads), 0, st, a, w, d_table, b0, b1);
     return;
   }
-  hipLaunchKernelGGL(k_bwd_accum<false>, dim3(kAccumGroups), dim3(kAccumThreads), 0, st, a, w, d_table, b0, b1);
-  hipLaunchKernelGGL(k_bwd_finalize, dim3(b1 - b0), dim3(kFinalizeThreads), 0, st, a, w, d_table, b0, b1);
+  hipLaunchKernelGGL((adam ? k_bwd_accum<false, true> : k_bwd_accum<false, false>), dim3(kAccumGroups), dim3(kAccumThreads), 0, st, a, w, d_table, b0, b1);
+  hipLaunchKernelGGL((adam ? k_bwd_finalize<true> : k_bwd_finalize<false>), dim3(b1 - b0), dim3(kFinalizeThreads), 0, st, a, w, d_table, b0, b1);
 }
 
 template <class PosFn, class GradFn>
@@ -1689,7 +1699,7 @@ extern "C" int lnr_hashgrid_bwd_rays(const lnr_grid_desc* d, const float* rays, 
 __global__ void __launch_bounds__(256) k_adam_zero_grad(GridArgs a, int64_t n) {
   const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int64_t i = 8 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x); i < n; i += 8 * (int64_t)gridDim.x * blockDim.x)
-    put_grad8(a, nullptr, i, z, n - i < 8 ? (uint32_t)(n - i) : 8u);
+    put_grad8<true>(a, nullptr, i, z, n - i < 8 ? (uint32_t)(n - i) : 8u);
 }
 
 extern "C" int lnr_hashgrid_bwd_rays_jac_adam(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
