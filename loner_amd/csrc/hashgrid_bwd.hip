@@ -469,8 +469,13 @@ template <class GradFn, int NB>
 constexpr int rows_stages() {
   return LNR_SCATTER_STAGES ? LNR_SCATTER_STAGES : (sizeof(typename GradFn::Raw) <= 4 || NB > 64 ? 1 : 2);
 }
+#ifndef LNR_ROWS_WIDE_WAVES
+#define LNR_ROWS_WIDE_WAVES 6  // one stage with float2 gradients (GradF32: the colour grid's backward)
+#endif
 template <class GradFn, int NB>
-constexpr int rows_waves() { return rows_stages<GradFn, NB>() == 1 ? 6 : 4; }
+constexpr int rows_waves() {
+  return rows_stages<GradFn, NB>() == 2 ? 4 : (sizeof(typename GradFn::Raw) > 4 ? LNR_ROWS_WIDE_WAVES : 6);
+}
 #ifndef LNR_PRESCALE
 #define LNR_PRESCALE 1
 #endif
