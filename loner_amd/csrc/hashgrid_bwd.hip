@@ -470,7 +470,9 @@ constexpr int rows_stages() {
   return LNR_SCATTER_STAGES ? LNR_SCATTER_STAGES : (sizeof(typename GradFn::Raw) <= 4 || NB > 64 ? 1 : 2);
 }
 #ifndef LNR_ROWS_WIDE_WAVES
-#define LNR_ROWS_WIDE_WAVES 6  // one stage with float2 gradients (GradF32: the colour grid's backward)
+// One stage with float2 gradients (GradF32: the colour grid's backward): 6 waves cap it at 80 VGPRs
+// and it spilled 12; at 5 it does not (CAM backward stage 0.455-0.459 -> 0.449-0.454 ms, bitwise).
+#define LNR_ROWS_WIDE_WAVES 5
 #endif
 template <class GradFn, int NB>
 constexpr int rows_waves() {

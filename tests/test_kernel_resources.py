@@ -6,8 +6,6 @@ code object's AMDGPU metadata note carries every kernel's .vgpr_spill_count.  No
 benched step may spill; the allowlist names the few that do, off that path:
   * k_bwd_accum with the fused Adam epilogue (<*, true>): the record-balanced accumulate only takes
     the epilogue above 2^17 samples, where the step keeps Adam separate (step.FUSED_ADAM_MAX_N);
-  * k_bwd_scatter_rows for fp32 encoding gradients (GradF32): the tcnn-layer backward, not the step,
-    which scatters through GradJac;
   * the two-samples-per-thread encode of plain positions (k_hashgrid_fwd<PosFromArray, 2, false, 1>).
 A spill the allowlist does not name fails here: 20 spilled VGPRs went unnoticed in the C2
 accumulate for a while (the epilogue used to be a runtime branch of the same kernel)."""
@@ -22,7 +20,6 @@ LIB = os.path.join(ROOT, "loner_amd", "_lib", "libloner_amd.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 ALLOWED = [
     r"^_ZN3lnr11k_bwd_accumILb[01]ELb1E",
-    r"^_ZN3lnr18k_bwd_scatter_rowsINS_\d+Pos\w+ENS_7GradF32E",
     r"^_ZN3lnr14k_hashgrid_fwdINS_12PosFromArrayELi2ELb0ELi1EE",
 ]
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
