@@ -29,7 +29,9 @@ FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-ffp-contract=
 # Per-file flags.  The hash-grid kernels keep global loads in flight across LDS-only barriers;
 # SLP-packed f32 math (v_pk_*) needs its loaded operands copied into register pairs, and those
 # copies wait for the loads before the barrier.
-FILE_FLAGS = {"hashgrid_bwd.hip": ["-fno-slp-vectorize"]}
+# rgb_train.hip: MFMA results in VGPRs (the colour-head backward's VALU reads every one of them; the default
+# heuristic put them in AGPRs and paid a v_accvgpr_read per value).
+FILE_FLAGS = {"hashgrid_bwd.hip": ["-fno-slp-vectorize"], "rgb_train.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
 def _sources():

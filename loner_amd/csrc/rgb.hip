@@ -22,22 +22,7 @@
 
 namespace lnr {
 
-struct RgbArgs {
-  const uint16_t* w;      // tcnn flat params of the colour network
-  const uint32_t* enc;    // colour hash-grid encodings, level-major half2
-  int64_t enc_stride;
-  const float* rays;
-  const float* weights;   // (R, S) compositing weights of the sigma pass
-  int64_t n_rays;
-  int32_t S;
-  float* rgb;             // (R, 3)
-  // training (lnr_rgb_train): L1 loss against the pixel intensities, mean over 3 x n_rays_global
-  const float* gt;        // (R, 3)
-  float* g;               // (R, 3) dL/drgb = sign(rgb - gt) * inv_count
-  float* ray_loss;        // (R) sum_k |rgb_k - gt_k|
-  float inv_count;
-  float* denc_max;        // optional [16]: max |d_enc| per level (float bits, atomicMax; zeroed by the render)
-};
+
 
 template <int NH, bool TRAIN>
 __global__ void __launch_bounds__(64 * kRgbWaves) k_rgb_render(RgbArgs a) {
@@ -135,7 +120,6 @@ __global__ void __launch_bounds__(64 * kRgbWaves) k_rgb_render(RgbArgs a) {
 //      slabs in a fixed order (bitwise reproducible).
 // Hidden-layer operands (forward, and transposed with the hid_perm k order) are pre-arranged in LDS
 // so each is one conflict-free 16-B read per lane.
-typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
 constexpr int kRgbBwdWaves = 4;
 constexpr int kRgbXRows = 48;                       // colour-grid features (32) + SH (16)
 constexpr int kRgbCols = 16 * kRgbBwdWaves;         // samples per workgroup iteration
@@ -153,13 +137,6 @@ struct RgbBwdLds {
   int valid[kRgbBwdWaves];
 };
 
-template <int NH>
-constexpr int rgb_mlp_params() { return 64 * kRgbIn + NH * 64 * 64 + kRgbOutPad * 64; }
-
-template <int NH>
-__device__ __forceinline__ int rgb_layer_offset(int l) {  // tcnn flat offset of matrix l (l = NH + 1: output)
-  return l == 0 ? 0 : 64 * kRgbIn + (l - 1) * 64 * 64;
-}
 
 __device__ __forceinline__ void scale_chain(float (&v)[16], float& scale) {
   float mx = 0.f;
@@ -568,6 +545,13 @@ extern "C" int64_t lnr_rgb_train_workspace_bytes(int32_t n_hidden_layers, int64_
   return (int64_t)kRgbBwdMaxBlocks * P * 4 + ((3 * n_rays + 63) / 64) * 64 * 4 + ((n_rays + 63) / 64) * 64 * 4;
 }
 
+// The colour-head backward kernel: 2 (default) k_rgb_bwd2, 1 round 4's k_rgb_bwd_tiles (LONER_RGB_BWD, read
+// at every launch)
+static int rgb_bwd_version() {
+  const char* e = getenv("LONER_RGB_BWD");
+  return e ? atoi(e) : 2;
+}
+
 template <int NH>
 static int rgb_train_launch(RgbArgs a, float* d_enc, float* d_w, float* slab, float* loss, hipStream_t st) {
   const int64_t nb_r = (a.n_rays + kRgbWaves - 1) / kRgbWaves;
@@ -576,7 +560,10 @@ static int rgb_train_launch(RgbArgs a, float* d_enc, float* d_w, float* slab, fl
   const int64_t tiles = a.n_rays * (int64_t)(a.S / 16);
   const int64_t want = (tiles + kRgbBwdWaves - 1) / kRgbBwdWaves;
   const int nb = (int)(want < kRgbBwdMaxBlocks ? want : kRgbBwdMaxBlocks);
-  hipLaunchKernelGGL(k_rgb_bwd_tiles<NH>, dim3(nb), dim3(64 * kRgbBwdWaves), 0, st, a, d_enc, slab);
+  if (rgb_bwd_version() == 1)
+    hipLaunchKernelGGL(k_rgb_bwd_tiles<NH>, dim3(nb), dim3(64 * kRgbBwdWaves), 0, st, a, d_enc, slab);
+  else
+    launch_rgb_bwd2(NH, a, d_enc, slab, nb, st);
   const int P = rgb_mlp_params<NH>();
   hipLaunchKernelGGL(k_rgb_reduce_slabs, dim3((P + 63) / 64), dim3(64 * kSlabWaves), 0, st, slab, nb, P, d_w);
   if (loss) hipLaunchKernelGGL(k_rgb_loss_sum, dim3(1), dim3(1024), 0, st, a.ray_loss, a.n_rays, a.inv_count, loss);

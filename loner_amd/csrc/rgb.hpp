@@ -8,7 +8,38 @@ namespace lnr {
 
 
 constexpr int kRgbWaves = 4;
+
 constexpr int kRgbIn = 48, kRgbWidth = 64, kRgbOutPad = 16;
+typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
+
+struct RgbArgs {
+  const uint16_t* w;      // tcnn flat params of the colour network
+  const uint32_t* enc;    // colour hash-grid encodings, level-major half2
+  int64_t enc_stride;
+  const float* rays;
+  const float* weights;   // (R, S) compositing weights of the sigma pass
+  int64_t n_rays;
+  int32_t S;
+  float* rgb;             // (R, 3)
+  // training (lnr_rgb_train): L1 loss against the pixel intensities, mean over 3 x n_rays_global
+  const float* gt;        // (R, 3)
+  float* g;               // (R, 3) dL/drgb = sign(rgb - gt) * inv_count
+  float* ray_loss;        // (R) sum_k |rgb_k - gt_k|
+  float inv_count;
+  float* denc_max;        // optional [16]: max |d_enc| per level (float bits, atomicMax; zeroed by the render)
+};
+
+template <int NH>
+constexpr int rgb_mlp_params() { return 64 * kRgbIn + NH * 64 * 64 + kRgbOutPad * 64; }
+
+template <int NH>
+__device__ __forceinline__ int rgb_layer_offset(int l) {  // tcnn flat offset of matrix l (l = NH + 1: output)
+  return l == 0 ? 0 : 64 * kRgbIn + (l - 1) * 64 * 64;
+}
+
+// The colour-head training backward, k_rgb_bwd2 (rgb_train.hip: compiled with MFMA results in VGPRs), for
+// NH hidden-to-hidden layers on nb workgroups
+void launch_rgb_bwd2(int NH, const RgbArgs& a, float* d_enc, float* slab, int nb, hipStream_t st);
 
 template <int NH>
 struct RgbWeights {

@@ -17,8 +17,13 @@ iteration is ``StepEngine.step``: no host synchronisation until the window's fin
 
 Scope: the map, i.e. the sigma head.
 * Pose optimisation (tracking, joint refinement) is out of scope. An iteration config that asks
-  for it with a frozen sigma head (tracking only) raises ``NotImplementedError``; a joint config
-  runs the map part with the poses fixed, and warns once.
+  for it with a frozen sigma head (tracking only) raises ``NotImplementedError``.  A joint config
+  (``freeze_poses: False`` with the sigma head trained, the reference's default mapper schedule,
+  cfg/defaults.yaml:93-97) also raises, unless the caller opts in with ``fixed_poses=True``: then the
+  map part runs with the poses held fixed, a different optimisation problem from the reference's
+  joint one (optimizer.py:258-262 puts the pose tensors in the same Adam), so it is never silent.
+  ``use_gt_poses=True`` (the north-star driver, fdt_optimize_implicit_map.py:355) freezes the poses as
+  the reference does and needs no opt-in.
 * The colour head trains in the camera phase: ``iterate_optimizer_camera(frames)`` over a
   ``loner_amd.camera.CameraFrames`` window (``loner_amd.camera``).
 
@@ -76,11 +81,14 @@ def _scan_dict(kf):
 
 class Optimizer:
     def __init__(self, settings, calibration=None, world_cube=None, device="cuda", use_gt_poses=False,
-                 lidar_only=True, enable_sky_segmentation=True, seed=0, allreduce=None, rank=0, world=1):
+                 lidar_only=True, enable_sky_segmentation=True, seed=0, allreduce=None, rank=0, world=1,
+                 fixed_poses=False):
         """``allreduce`` / ``rank`` / ``world``: data-parallel over ranks (one process per GPU):
         rank r optimises the contiguous slice ``shard_range(window slots, r, world)`` of every
         window's rays; the opaque count and the gradients are summed with ``allreduce(t,
-        async_op=...)`` (e.g. ``torch.distributed.all_reduce``), so every rank holds the same map."""
+        async_op=...)`` (e.g. ``torch.distributed.all_reduce``), so every rank holds the same map.
+        ``fixed_poses``: run joint pose + map iteration configs as map-only ones with the poses held
+        fixed (otherwise they raise NotImplementedError; see the module docstring)."""
         if world_cube is None:
             raise ValueError("Optimizer needs the world cube")
         self._settings = settings
@@ -125,6 +133,7 @@ class Optimizer:
         self._optimization_settings = OptimizationSettings()
         self._keyframe_count = 0
         self._global_step = 0
+        self._fixed_poses = bool(fixed_poses)
         self._warned_poses = False
         self._fixed_gen = torch.Generator(device="cpu").manual_seed(seed)
 
@@ -174,10 +183,16 @@ class Optimizer:
                 if os_.freeze_sigma_mlp:
                     raise NotImplementedError("pose tracking (frozen sigma head, free poses) is outside this build's "
                                               "scope (SURVEY.md §8)")
+                if not self._fixed_poses:
+                    raise NotImplementedError(
+                        "joint pose + map optimisation (freeze_poses: False) is outside this build's scope: the "
+                        "reference optimises the poses in the same Adam (optimizer.py:258-262). Pass "
+                        "Optimizer(..., fixed_poses=True) to optimise the map with the poses held fixed, or "
+                        "use_gt_poses=True / freeze_poses: True as the north-star driver does")
                 if not self._warned_poses:
                     self._warned_poses = True
-                    warnings.warn("pose optimisation is outside this build's scope: the poses stay fixed and "
-                                  "only the map is optimised")
+                    warnings.warn("fixed_poses=True: the joint config's poses stay fixed and only the map is "
+                                  "optimised")
             if os_.freeze_sigma_mlp:
                 continue  # nothing of the map to optimise in this config
             window_scans = scans
@@ -205,7 +220,7 @@ class Optimizer:
                                       n_rays_global=window.n_slots, n_slots=n_local)
             self._global_step += 1
         eng.lr_factor = 1.0
-        eng.drop_prefetch()  # the next window is a new object: this one's prefetched step never runs
+        eng.release()  # the next window is a new object: this one's prefetched step and graphs are dropped
         return out
 
     # ------------------------------------------------------------------ camera phase

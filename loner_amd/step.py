@@ -100,6 +100,9 @@ class FieldState:
         self.occ = torch.zeros(cfg.occ_res ** 3, dtype=torch.float32, device=dev)
         self.occ_ws = torch.zeros(int(L.lib().lnr_ogm_workspace_words(cfg.occ_res)), dtype=torch.float32, device=dev)
         self.adam_step = 0
+        # whether grad_table holds the last step's table gradient: a step with the table's Adam fused into
+        # the backward (StepEngine.fused_adam) applies it where it is accumulated and never stores it
+        self.grad_table_current = True
         self.init_params(seed, table_init)
 
     # tcnn init: FullyFusedMLP xavier-uniform per matrix, HashGrid U(-1e-4, 1e-4) (restated with a
@@ -135,7 +138,18 @@ class FieldState:
 
     @property
     def grad_table(self):
+        """The table's slice of the flat gradient (the backward's output buffer).  NOT written by a step whose
+        table Adam is fused into the backward (``grad_table_current`` is then False and the slice keeps an
+        older gradient); use ``table_gradient()`` to read it safely."""
         return self.grad[self.n_mlp:self.n_mlp + 2 * self.n_entries]
+
+    def table_gradient(self):
+        """The last step's table gradient; raises when that step fused the table's Adam into the backward
+        (the gradient never went to memory: run with StepEngine.fused_adam = False to keep it)."""
+        if not self.grad_table_current:
+            raise RuntimeError("the last step fused the table's Adam into the backward: its table gradient was "
+                               "never stored (StepEngine.fused_adam = False keeps it)")
+        return self.grad_table
 
     @property
     def grad_mlp(self):
@@ -156,6 +170,7 @@ class FieldState:
 
 
 FUSED_ADAM_MAX_N = 1 << 17  # samples up to which the step fuses the table's Adam into the backward ("auto")
+AR_CUT_DEFAULT = 8  # the level at which the two gradient-exchange ranges split: [cut, L) first, then [0, cut) + MLP
 
 
 class StepEngine:
@@ -185,12 +200,15 @@ class StepEngine:
         # costs 2.18-2.25 ms with one range, 2.23-2.30 with two (levels 8-15, then 0-7 + the MLP)
         # and 2.41-2.44 with four, against 2.12 without the hook; two ranges hide about half of the
         # 29.7 MB exchange for a fraction of the four ranges' cost.  LONER_AR_BUCKETS = 1, 2 or 4.
+        # With two ranges the cut level is LONER_AR_CUT (default AR_CUT_DEFAULT; the modelled exposure of
+        # the sharded optimiser's tail per cut: DESIGN.md section 7, tools/zero_tail_model.py).
         nl = self.cfg.n_levels
         nbk = int(os.environ.get("LONER_AR_BUCKETS", "2"))
         if nbk <= 1:
             cuts = [nl, 0]
         elif nbk == 2:
-            cuts = sorted({nl, max(nl - 8, 1), 0}, reverse=True)
+            cut = int(os.environ.get("LONER_AR_CUT", str(AR_CUT_DEFAULT)))
+            cuts = sorted({nl, min(max(cut, 1), max(nl - 1, 1)), 0}, reverse=True)
         else:
             cuts = sorted({nl, max(nl - 5, 1), max(nl - 10, 1), min(3, nl), 0}, reverse=True)
         self.ar_groups = [(cuts[i + 1], cuts[i]) for i in range(len(cuts) - 1)]
@@ -226,6 +244,9 @@ class StepEngine:
                 raise ValueError(f"{len(self.zero_chunks)} level ranges: at most {L.ADAM_MAX_RANGES} (one Adam launch)")
             self.zero_grad = [torch.empty(c, dtype=torch.float32, device=dev) for _, _, c in self.zero_chunks]
         self._pending_shadow = []  # async all-gather works of the last sharded step (finish())
+        # data-parallel OGM step: the grid gradient's all-reduce runs asynchronously and the SGD step that
+        # consumes it is enqueued before the grid's next reader (the next step's sampler, or finish())
+        self._pending_ogm = None
         self.z = torch.empty(n_rays, self.S, dtype=torch.float32, device=dev)
         self.enc = torch.empty(self.cfg.n_levels, self.N, dtype=torch.int32, device=dev)
         self.ws = torch.empty(L.lib().lnr_field_train_workspace_words(n_rays, self.S), dtype=torch.float32, device=dev)
@@ -428,7 +449,9 @@ class StepEngine:
         dsp = None if dev_step is None else dev_step.data_ptr()
         lp.dev_step = dsp
         self._dev_step = dsp
-        # 2. sampling (``presampled``: step_window's pipeline already drew self.z for these rays)
+        # 2. sampling (``presampled``: step_window's pipeline already drew self.z for these rays); the previous
+        # step's data-parallel OGM update lands first (the sampler reads the grid)
+        self._apply_pending_ogm()
         m(prof, "sample")
         if presampled:
             pass
@@ -476,6 +499,7 @@ class StepEngine:
             # gradient updates its parameter where the accumulation finishes it, bitwise lnr_adam_step's
             # result), then Adam on the MLP's parameters alone
             st.adam_step += 1
+            st.grad_table_current = False
             nm, nt = st.n_mlp, 2 * st.n_entries
             epi = L.AdamEpilogue(L.ptr(st.params[nm:nm + nt]), L.ptr(st.shadow[nm:nm + nt]), L.ptr(st.m[nm:nm + nt]),
                                  L.ptr(st.v[nm:nm + nt]), st.adam_step, cfg.lr * self.lr_factor, 0.9, 0.999, 1e-8, dsp)
@@ -591,6 +615,7 @@ class StepEngine:
         """Order the current stream after the sharded optimiser's pending shadow all-gathers (the shadow is
         then whole again).  step() calls it before its encode; call it before reading the fp16 parameters
         elsewhere (checkpoints, evaluation on the same FieldState).  A no-op without pending gathers."""
+        self._apply_pending_ogm()
         pend, self._pending_shadow = self._pending_shadow, []
         for w in pend:
             w.wait()
@@ -613,6 +638,7 @@ class StepEngine:
 
     def _grid_bwd(self, rays, R, S, N, flags, s):
         st = self.state
+        st.grad_table_current = True
         if self.compact_denc:
             L.call("lnr_hashgrid_bwd_rays_jac", L.ctypes.byref(st.desc), rays, self.z, R, S, self.d_jac,
                    self.d_sigma(R), N, st.grad_table, None, None, self.bwd_ws, self.bwd_ws_bytes, flags, s)
@@ -622,7 +648,8 @@ class StepEngine:
 
     def ogm_update(self, rays, depth_gt, scale):
         """Optimizer._step_occupancy_grid (optimizer.py:897-908).  Data-parallel: the grid gradient
-        is all-reduced before the SGD step so every replica applies the global-batch update."""
+        is all-reduced before the SGD step so every replica applies the global-batch update; the all-reduce
+        is asynchronous and the SGD step waits for it at the grid's next reader (``_apply_pending_ogm``)."""
         st = self.state
         s = L.stream(st.device)
         if self.allreduce is None:
@@ -632,8 +659,20 @@ class StepEngine:
         L.call("lnr_ogm_grad", (rays), (self.z), (depth_gt), rays.shape[0], self.S, float(scale),
                (st.occ_ws), st.occ_ws.numel(), self.cfg.occ_res, s)
         g = st.occ_ws[:st.occ.numel()]
-        self.allreduce(g)
-        L.call("lnr_sgd_step", (st.occ), g, st.occ.numel(), self.cfg.occ_lr, s)
+        # asynchronous: nothing on this step's stream waits for it; the SGD step is enqueued (after a wait on
+        # the collective) right before the grid's next reader (_apply_pending_ogm)
+        self._pending_ogm = (self._allreduce_async(g), g)
+
+    def _apply_pending_ogm(self):
+        """Enqueue the data-parallel OGM step's SGD update once its gradient all-reduce is waited for (a
+        no-op without one pending)."""
+        p, self._pending_ogm = self._pending_ogm, None
+        if p is None:
+            return
+        w, g = p
+        if w is not None:
+            w.wait()  # orders the current stream after the collective (no host sync)
+        L.call("lnr_sgd_step", self.state.occ, g, self.state.occ.numel(), self.cfg.occ_lr, L.stream(self.state.device))
 
     def step_window(self, window, global_step, iteration_idx=0, n_rays_global=None, prof=None, n_slots=None, **kw):
         """One optimiser step whose rays are selected and built on the device from a resident
@@ -743,6 +782,14 @@ class StepEngine:
                 main.wait_event(pend["done"])
         self._pp = self._pf = self._gpp = None
         self.finish()
+
+    def release(self):
+        """End of a window: drop_prefetch(), and the HIP graphs captured for this window with the window
+        itself (their captured pointers keep its device tensors alive), so two windows' resident data never
+        coexist.  Optimizer calls it when a window's iterations are done."""
+        self.drop_prefetch()
+        self._graphs.clear()
+        self._graph_window = None
 
     def step_scalars(self, global_step, iteration_idx=0, adam_step=None):
         """The host ``lnr_step_scalars`` of a step: the values the eager step passes as kernel arguments

@@ -76,6 +76,33 @@ def test_schedule_selection_and_skips(L):
         opt.iterate_optimizer(scans)       # pose tracking is out of scope
 
 
+def test_joint_pose_config_raises_unless_fixed_poses(L):
+    """The reference's default mapper schedule optimises poses and map jointly (cfg/defaults.yaml:93-97,
+    optimizer.py:258-262).  The fused Optimizer keeps the poses fixed, so such a config raises through
+    iterate_optimizer unless the caller opts in with fixed_poses=True (then it warns and optimises the map
+    exactly as with freeze_poses: True); use_gt_poses freezes them as the reference does."""
+    import warnings
+    from loner_amd.optimizer import Optimizer
+    scans, cube = _window()
+    joint = [dict(num_keyframes=-1, iteration_schedule=[dict(num_iterations=3, freeze_poses=False,
+                                                             freeze_sigma_mlp=False, freeze_rgb_mlp=True)])]
+    opt = Optimizer(_settings(schedule=joint), None, cube, "cuda:0", seed=2)
+    with pytest.raises(NotImplementedError, match="fixed_poses=True"):
+        opt.iterate_optimizer(scans)
+    assert opt._global_step == 0
+    with pytest.warns(UserWarning, match="fixed_poses=True"):
+        loss_fixed = Optimizer(_settings(schedule=joint), None, cube, "cuda:0", seed=2,
+                               fixed_poses=True).iterate_optimizer(scans)
+    frozen = [dict(num_keyframes=-1, iteration_schedule=[dict(num_iterations=3, freeze_poses=True,
+                                                              freeze_sigma_mlp=False, freeze_rgb_mlp=True)])]
+    loss_frozen = Optimizer(_settings(schedule=frozen), None, cube, "cuda:0", seed=2).iterate_optimizer(scans)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        loss_gt = Optimizer(_settings(schedule=joint), None, cube, "cuda:0", seed=2,
+                            use_gt_poses=True).iterate_optimizer(scans)
+    assert loss_fixed == loss_frozen == loss_gt
+
+
 @pytest.mark.parametrize("strategy,sky", [("MASK", 8), ("FIXED", 0), ("FIXED", 8)])
 def test_strategies_run(L, strategy, sky):
     from loner_amd.optimizer import Optimizer

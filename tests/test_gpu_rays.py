@@ -283,39 +283,67 @@ def test_graph_replay_equals_eager(L, zero):
             np.testing.assert_array_equal(a, b)
 
 
-def test_fused_adam_equals_separate(L):
+# Every accumulate version the fused Adam epilogue runs in (the switches are read at every launch): the
+# whole-bucket kernel (the default at this size), the unit work list with its cut buckets finished by the
+# last piece or by k_bwd_finalize_units, and the record-balanced split with k_bwd_finalize or in-kernel
+# finishing.  A bucket finished twice would apply Adam twice: bitwise equality with the separate Adam
+# pins each of them.
+_FUSED_PATHS = {
+    "buckets": {},
+    "units_finish": {"LONER_ACCUM_UNITS": "1", "LONER_UNITS_FINISH": "1"},
+    "units_finalize": {"LONER_ACCUM_UNITS": "1", "LONER_UNITS_FINISH": "0"},
+    "balanced_finalize": {"LONER_ACCUM_UNITS": "0", "LONER_ACCUM_BUCKETS_MAX_N": "0", "LONER_ACCUM_FINISH": "0"},
+    "balanced_finish": {"LONER_ACCUM_UNITS": "0", "LONER_ACCUM_BUCKETS_MAX_N": "0", "LONER_ACCUM_FINISH": "1"},
+}
+
+
+def _fused_adam_run(fused, graph):
+    from loner_amd import step as S_
+    from loner_amd import synthetic as syn
+    from loner_amd.rays import RayWindow
+    st = S_.FieldState(S_.StepConfig(n_samples=64, occ_lr=1e-3), device="cuda:0", table_init=0.5)
+    scans, wc, rr = _window("forest", 2, seed=8)
+    win = RayWindow(scans, wc, rr, n_lidar=128, n_sky=16, strategy="MASK")
+    eng = S_.StepEngine(st, win.n_slots, seed=4)
+    eng.fused_adam, eng.use_graph = fused, graph
+    outs = []
+    for it, g in enumerate((8, 9, 10, 11, 12, 13)):
+        eng.lr_factor = 0.97 ** it
+        outs.append(host(eng.step_window(win, global_step=g, iteration_idx=it)).copy())
+    st.reset_optimizer()
+    for it, g in enumerate((14, 15)):
+        outs.append(host(eng.step_window(win, global_step=g, iteration_idx=it)).copy())
+    # an empty batch: zero gradient everywhere, Adam still steps every parameter
+    w2 = syn.make_window("quad", 1, seed=2)
+    rays, dgt = syn.build_batch(w2, "quad", 64, 0, "RANDOM", seed=4)
+    rays, dgt = rays.cuda(), dgt.cuda()
+    eng.step(rays[:0], dgt[:0], global_step=16, scale=121.426537, far_ref=float(rays[0, 12]), n_rays_global=64)
+    torch.cuda.synchronize()
+    # a fused step never stores the table gradient, and says so (FieldState.table_gradient)
+    assert st.grad_table_current is (not fused)
+    if fused:
+        with pytest.raises(RuntimeError, match="fused"):
+            st.table_gradient()
+    return (outs, host(st.params).copy(), host(st.m).copy(), host(st.v).copy(),
+            host(st.shadow).view(np.uint16).copy(), host(st.occ).copy(), st.adam_step)
+
+
+@pytest.mark.parametrize("path", sorted(_FUSED_PATHS))
+def test_fused_adam_equals_separate(L, path, monkeypatch):
     """The table's Adam fused into the hash-grid backward (lnr_hashgrid_bwd_rays_jac_adam: each entry's
     gradient updates its parameter where the accumulation finishes it; the MLP's Adam separate) gives
     bitwise the separate lnr_adam_step's parameters, moments, fp16 shadow, losses and occupancy grid:
     eager and graph-replayed steps, OGM steps, a changed learning-rate factor, a new optimiser, and an
-    empty batch (Adam with a zero gradient)."""
-    from loner_amd import step as S_
-    from loner_amd import synthetic as syn
-    from loner_amd.rays import RayWindow
-    res = []
-    for fused, graph in ((False, False), (True, False), (True, True)):
-        st = S_.FieldState(S_.StepConfig(n_samples=64, occ_lr=1e-3), device="cuda:0", table_init=0.5)
-        scans, wc, rr = _window("forest", 2, seed=8)
-        win = RayWindow(scans, wc, rr, n_lidar=128, n_sky=16, strategy="MASK")
-        eng = S_.StepEngine(st, win.n_slots, seed=4)
-        eng.fused_adam, eng.use_graph = fused, graph
-        outs = []
-        for it, g in enumerate((8, 9, 10, 11, 12, 13)):
-            eng.lr_factor = 0.97 ** it
-            outs.append(host(eng.step_window(win, global_step=g, iteration_idx=it)).copy())
-        st.reset_optimizer()
-        for it, g in enumerate((14, 15)):
-            outs.append(host(eng.step_window(win, global_step=g, iteration_idx=it)).copy())
-        # an empty batch: zero gradient everywhere, Adam still steps every parameter
-        w2 = syn.make_window("quad", 1, seed=2)
-        rays, dgt = syn.build_batch(w2, "quad", 64, 0, "RANDOM", seed=4)
-        rays, dgt = rays.cuda(), dgt.cuda()
-        eng.step(rays[:0], dgt[:0], global_step=16, scale=121.426537, far_ref=float(rays[0, 12]), n_rays_global=64)
-        torch.cuda.synchronize()
-        res.append((outs, host(st.params).copy(), host(st.m).copy(), host(st.v).copy(),
-                    host(st.shadow).view(np.uint16).copy(), host(st.occ).copy(), st.adam_step))
-    for r in res[1:]:
-        for a, b in zip(res[0][0], r[0]):
+    empty batch (Adam with a zero gradient), in every accumulate version the epilogue runs in
+    (``_FUSED_PATHS``; the batch of 288 rays x 64 samples has cut buckets in the split versions)."""
+    ref = _fused_adam_run(False, False)
+    for k, v in _FUSED_PATHS[path].items():
+        monkeypatch.setenv(k, v)
+    res = [_fused_adam_run(True, False)]
+    if path == "buckets":
+        res.append(_fused_adam_run(True, True))
+    for r in res:
+        for a, b in zip(ref[0], r[0]):
             np.testing.assert_array_equal(a, b)
-        for a, b in zip(res[0][1:], r[1:]):
+        for a, b in zip(ref[1:], r[1:]):
             np.testing.assert_array_equal(a, b)

@@ -1,7 +1,9 @@
 """Per-level cost of the hash-grid backward's accumulation (GPU box): the bench's C2 loop (60 steps), then the
 backward with LNR_BWD_NO_ACCUM and lnr_hashgrid_bwd_accum one level at a time (then any extra
-level ranges "l0-l1" in one launch each), HIP events around each.
-Usage: python tools/bwd_levels.py [C2|C4] [0-5 5-16 ...]"""
+level ranges "l0-l1" in one launch each), HIP events around each.  "s<K>" as an extra argument runs one
+rank's share of a K-way ray split (bench.py --shard-of K); "--json" prints one JSON line at the end.
+Usage: python tools/bwd_levels.py [C2|C4] [s8] [0-5 5-16 ...] [--json]"""
+import json
 import os
 import sys
 
@@ -12,6 +14,9 @@ sys.path.insert(0, ROOT)
 
 
 def main(cfg_name="C2", *extra):
+    shard = next((int(x[1:]) for x in extra if x.startswith("s") and x[1:].isdigit()), 1)
+    as_json = "--json" in extra
+    extra = [x for x in extra if "-" in x and not x.startswith("-") and not x.startswith("s")]
     import bench
     from loner_amd import _lib as L
     from loner_amd import step as S_
@@ -24,11 +29,12 @@ def main(cfg_name="C2", *extra):
     cfg = S_.StepConfig(n_samples=S, occ_lr=1e-3 if preset == "haveri" else 1e-4,
                         loss=S_.LossConfig.from_dict(bench.LOSS_PRESETS[preset]))
     st = S_.FieldState(cfg, device=dev)
-    eng = S_.StepEngine(st, window.n_slots, seed=12345)
+    R = window.n_slots // shard
+    eng = S_.StepEngine(st, R, seed=12345)
     for i in range(60):  # the bench's loop: OGM updates concentrate the samples
-        eng.step_window(window, global_step=i)
+        eng.step_window(window, global_step=i, n_slots=R, n_rays_global=window.n_slots)
     torch.cuda.synchronize()
-    rays, R = eng.rays, window.n_slots
+    rays = eng.rays
     s = L.stream(dev)
     N = eng.N
     nl = st.desc.n_levels
@@ -56,15 +62,20 @@ def main(cfg_name="C2", *extra):
         for k, r in enumerate(ranges):
             times.setdefault(r, []).append(evs[k].elapsed_time(evs[k + 1]))
     d = st.desc
-    print(f"{cfg_name}: N={N} scatter+scans {sum(times['scatter']) / len(times['scatter']):.3f} ms")
+    avg = {k: sum(v) / len(v) for k, v in times.items()}
+    print(f"{cfg_name} shard 1/{shard}: N={N} scatter+scans {avg['scatter']:.3f} ms")
     tot = 0.0
     for l in range(nl):
-        t = sum(times[(l, l + 1)]) / len(times[(l, l + 1)])
+        t = avg[(l, l + 1)]
         tot += t
         print(f"  level {l:2d} res {d.resolution[l]:7d} size {d.size[l]:7d}: accum {t * 1e3:7.1f} us")
     print(f"  accum total {tot:.3f} ms")
     for r in ranges[nl:]:
-        print(f"  levels [{r[0]}, {r[1]}) in one launch: {sum(times[r]) / len(times[r]) * 1e3:7.1f} us")
+        print(f"  levels [{r[0]}, {r[1]}) in one launch: {avg[r] * 1e3:7.1f} us")
+    if as_json:
+        print(json.dumps(dict(config=cfg_name, shard=shard, N=N, scatter_ms=avg["scatter"],
+                              level_accum_ms=[avg[(l, l + 1)] for l in range(nl)],
+                              ranges_ms={f"{a}-{b}": avg[(a, b)] for a, b in ranges[nl:]})))
 
 
 if __name__ == "__main__":
