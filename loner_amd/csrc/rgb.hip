@@ -551,6 +551,7 @@ static int rgb_bwd_version() {
   const char* e = getenv("LONER_RGB_BWD");
   return e ? atoi(e) : 2;
 }
+static int kRgbBwdTileWaves(int v) { return v == 1 ? kRgbBwdWaves : kRgbBwd2Waves; }
 
 template <int NH>
 static int rgb_train_launch(RgbArgs a, float* d_enc, float* d_w, float* slab, float* loss, hipStream_t st) {
@@ -558,9 +559,10 @@ static int rgb_train_launch(RgbArgs a, float* d_enc, float* d_w, float* slab, fl
   hipLaunchKernelGGL((k_rgb_render<NH, true>), dim3((unsigned)(nb_r < 4096 ? nb_r : 4096)), dim3(64 * kRgbWaves), 0,
                      st, a);
   const int64_t tiles = a.n_rays * (int64_t)(a.S / 16);
-  const int64_t want = (tiles + kRgbBwdWaves - 1) / kRgbBwdWaves;
+  const int v = rgb_bwd_version();
+  const int64_t want = (tiles + kRgbBwdTileWaves(v) - 1) / kRgbBwdTileWaves(v);  // a tile per wave per iteration
   const int nb = (int)(want < kRgbBwdMaxBlocks ? want : kRgbBwdMaxBlocks);
-  if (rgb_bwd_version() == 1)
+  if (v == 1)
     hipLaunchKernelGGL(k_rgb_bwd_tiles<NH>, dim3(nb), dim3(64 * kRgbBwdWaves), 0, st, a, d_enc, slab);
   else
     launch_rgb_bwd2(NH, a, d_enc, slab, nb, st);

@@ -38,7 +38,8 @@ __device__ __forceinline__ int rgb_layer_offset(int l) {  // tcnn flat offset of
 }
 
 // The colour-head training backward, k_rgb_bwd2 (rgb_train.hip: compiled with MFMA results in VGPRs), for
-// NH hidden-to-hidden layers on nb workgroups
+// NH hidden-to-hidden layers on nb workgroups of kRgbBwd2Waves waves
+constexpr int kRgbBwd2Waves = 8;
 void launch_rgb_bwd2(int NH, const RgbArgs& a, float* d_enc, float* slab, int nb, hipStream_t st);
 
 template <int NH>

@@ -17,8 +17,9 @@ namespace lnr {
 //    (one ds_write_b64 per 4 neurons of a sample, XOR-swizzled by row pair), and the weight-gradient MFMAs
 //    read them back transposed with ds_read_b64_tr_b16 (neuron on the lane, 4 samples per lane: the
 //    16x16x16 operand), conflict-free;
-//  * wave w owns rows 16w .. 16w+15 of every weight matrix (the same work per wave), each at its own running
-//    power-of-two scale; the images are double-buffered, so one barrier per 64 samples;
+//  * 8 waves (two per SIMD: the serial per-tile chain of one wave hides behind the other's) take a 16-sample
+//    tile each per iteration; wave w owns rows 16 (w/2) .. +15 of every weight matrix, half of its column tiles,
+//    each at its own running power-of-two scale; two barriers per 128 samples (images complete, images read);
 //  * W_l lives in one LDS image, read by rows for the forward and transposed for the backward (W_l^T);
 //  * the output layer's gradient (3 x 64) is each wave's own: its tile's H_NH and scaled dO go through the
 //    wave's own rows of the dY images (before its backward writes them) into 16x16x16 MFMAs at a running scale.
@@ -28,7 +29,7 @@ typedef short v4i16_t __attribute__((__vector_size__(8)));
 typedef _Float16 half2v_t __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4v_t __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2v_t __attribute__((ext_vector_type(2)));
-constexpr int kBw2Waves = 4;
+constexpr int kBw2Waves = kRgbBwd2Waves;
 constexpr int kBw2Cols = 16 * kBw2Waves;  // samples per workgroup iteration
 
 // [sample][64 halves] rows of 16 8-byte chunks: chunk ch of row r at this dword (conflict-free transposed
@@ -53,9 +54,12 @@ template <int NH>
 struct Bw2Lds {
   uint32_t w0[64 * 32];                       // W_0 [hid][48 in + 16 zeros], rows by 16 B for the forward, transposed for d_enc
   uint32_t wt[NH > 0 ? NH : 1][64 * 32];      // W_1 .. W_NH [out][in]: rows (in hid_perm order) and transposed
-  Bw2Buf<NH> buf[2];
-  float red[kBw2Waves][3][64];                // the output layer's gradient, per wave
+  half8_t ao[2][64];                          // the output layer's A operands per lane: W_out (rows by channel)
+  half8_t aot[4][64];                         //   and W_out^T (k = channel), conflict-free 16-byte reads
+  Bw2Buf<NH> buf;
 };
+// (after the loop) the output layer's gradient per wave, over the dY images
+typedef float Bw2Red[kBw2Waves][3][64];
 
 __device__ __forceinline__ half4_t lds_tr16(const uint32_t* p) {
   return __builtin_bit_cast(half4_t, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -100,14 +104,15 @@ __device__ __forceinline__ float max_abs16(const float4_t (&acc)[4]) {
   return m;
 }
 
-// Owner step of one matrix: acc tiles (row tile = this wave, column tiles ct < CT) += dY X^T over the valid
-// source tiles of this buffer, at the running scale `run`.  XI: the X image (nullptr: X_0, whose columns
-// come from x0 and, for ct = 2, the tile's SH values).
+// Owner step of one matrix: acc tiles (row tile wid / 2, column tiles ct0 + m, m < CT) += dY X^T over the valid
+// source tiles, at the running scale `run`.  XI: the X image (nullptr: X_0, whose column tiles 0, 1 come from x0
+// and 2 from the tiles' SH values).
 template <int NH, int CT>
-__device__ __forceinline__ void bw2_owner(const Bw2Buf<NH>& B, int l, const uint32_t* xi, float4_t (&acc)[4],
-                                          float& run) {
+__device__ __forceinline__ void bw2_owner(const Bw2Buf<NH>& B, int l, const uint32_t* xi, float4_t (&acc)[2],
+                                          float& run, int ct0) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   const int tq = (lane >> 2) & 3, tp = lane & 3;
+  const uint32_t rt = (uint32_t)wid >> 1;
   int vd[kBw2Waves];
   float iv[kBw2Waves];
   float imax = 0.f;
@@ -118,7 +123,7 @@ __device__ __forceinline__ void bw2_owner(const Bw2Buf<NH>& B, int l, const uint
     if (vd[sw]) imax = fmaxf(imax, iv[sw]);
   }
   if (imax == 0.f) return;
-  const float s_new = 1.0f / imax;
+  const float s_new = __builtin_amdgcn_rcpf(imax);  // exact: a power of two
   if (s_new < run) {  // wave-uniform
     if (run != INFINITY) {
       const float f = s_new / run;
@@ -133,14 +138,15 @@ __device__ __forceinline__ void bw2_owner(const Bw2Buf<NH>& B, int l, const uint
     const uint32_t r = 16u * sw + 4u * g + tq;  // the transposed read's row (sample) for this lane
     const _Float16 f = (_Float16)(run * iv[sw]);  // run / s_sw = 2^-k, k >= 0
     const half4_t fv = {f, f, f, f};
-    const half4_t ya = lds_tr16(&B.dy[l][sw64(r, 4u * wid + tp)]) * fv;
+    const half4_t ya = lds_tr16(&B.dy[l][sw64(r, 4u * rt + tp)]) * fv;
 #pragma unroll
     for (int m = 0; m < CT; ++m) {
+      const uint32_t ct = (uint32_t)ct0 + m;
       half4_t xb;
       if (xi != nullptr) {
-        xb = lds_tr16(&xi[sw64(r, 4u * m + tp)]);
-      } else if (m < 2) {
-        xb = lds_tr16(&B.x0[sw32(r, 4u * m + tp)]);
+        xb = lds_tr16(&xi[sw64(r, 4u * ct + tp)]);
+      } else if (ct < 2) {
+        xb = lds_tr16(&B.x0[sw32(r, 4u * ct + tp)]);
       } else {
         const _Float16 v = B.sh[sw][c];
         xb = half4_t{v, v, v, v};
@@ -156,22 +162,24 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
   __shared__ Bw2Lds<NH> sm;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   const int tq = (lane >> 2) & 3, tp = lane & 3;
-  // ---- weights: W_0 and W_l in LDS images, the output layer in registers
+  // ---- weights: W_0, W_l and the output layer's operands in LDS
   const uint16_t* wo = a.w + rgb_layer_offset<NH>(NH + 1);  // (16, 64): rows 0..2 are the colour channels
-  half8_t ao[2], aot[4];
-  {
+  if (wid == 0) {
     const int ch = c & 3;  // every 4-row group of the output tile holds the three channels (row 4g + q = channel q)
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const half8_t z = {};
-      ao[s2] = ch < 3 ? ld_half8_perm(wo + ch * kRgbWidth, s2, g) : z;
+      sm.ao[s2][lane] = ch < 3 ? ld_half8_perm(wo + ch * kRgbWidth, s2, g) : z;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      half8_t v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)  // A = Wout^T: [hid 16t + c][k = output 8g + j], outputs 0..2 only
+        v[j] = (g == 0 && j < 3) ? __builtin_bit_cast(_Float16, wo[j * kRgbWidth + 16 * t + c]) : (_Float16)0.f;
+      sm.aot[t][lane] = v;
     }
   }
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int j = 0; j < 8; ++j)  // A = Wout^T: [hid 16t + c][k = output 8g + j], outputs 0..2 only
-      aot[t][j] = (g == 0 && j < 3) ? __builtin_bit_cast(_Float16, wo[j * kRgbWidth + 16 * t + c]) : (_Float16)0.f;
   for (int i = threadIdx.x; i < NH * 64 * 16; i += 64 * kBw2Waves) {  // W_l images, 8-byte chunks
     const int l = i >> 10, r = (i >> 4) & 63, ch = i & 15;
     const uint16_t* src = a.w + rgb_layer_offset<NH>(l + 1) + r * kRgbWidth + 4 * ch;
@@ -183,10 +191,11 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
     lds_st64(&sm.w0[sw64(r, ch)], ch < 12 ? (uint32_t)src[0] | ((uint32_t)src[1] << 16) : 0u,
              ch < 12 ? (uint32_t)src[2] | ((uint32_t)src[3] << 16) : 0u);
   }
-  // ---- weight-gradient accumulators: rows 16 wid .. of W_0 (3 column tiles) and of each W_l (4)
-  float4_t acc0[4], acch[NH > 0 ? NH : 1][4];
+  // ---- weight-gradient accumulators: rows 16 (wid / 2) .. of W_0 (column tiles 0, 1 or 2) and of each W_l
+  // (column tiles 2 (wid & 1) + m)
+  float4_t acc0[2], acch[NH > 0 ? NH : 1][2];
 #pragma unroll
-  for (int m = 0; m < 4; ++m) {
+  for (int m = 0; m < 2; ++m) {
     acc0[m] = float4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int l = 0; l < NH; ++l) acch[l][m] = float4_t{0.f, 0.f, 0.f, 0.f};
@@ -233,7 +242,7 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
   };
   prefetch();
   for (int64_t it = 0; it < n_iter; ++it) {
-    Bw2Buf<NH>& B = sm.buf[it & 1];
+    Bw2Buf<NH>& B = sm.buf;
     const int64_t tile = it * per_iter + (int64_t)blockIdx.x * kBw2Waves + wid;
     const bool valid = tile < n_tiles;
     bool skip = true;
@@ -269,8 +278,9 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
           bsh[j] = g < 2 ? (_Float16)__uint_as_float(g ? hi : lo) : (_Float16)0.f;
         }
         if (c == 0 && g < 2) *reinterpret_cast<half8_t*>(&B.sh[wid][8 * g]) = bsh;
-        // forward (as k_rgb_render): H_l packed, their ReLU masks; X_{l+1} = H_l staged for l < NH
-        uint32_t hp[NH + 1][8];
+        // forward (as k_rgb_render): H_l packed (hp: the current layer), staged as X_{l+1} for l < NH; H_NH goes to
+        // this wave's rows of dy[NH] (the output layer's gradient reads it there, and the backward its mask)
+        uint32_t hp[8];
         {
           float4_t ac[4];
 #pragma unroll
@@ -281,15 +291,15 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
             ac[t] = float4_t{0.f, 0.f, 0.f, 0.f};
             ac[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, benc, ac[t], 0, 0, 0);
             ac[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as, bsh, ac[t], 0, 0, 0);
-            hp[0][2 * t] = pk_relu(ac[t][0], ac[t][1]);
-            hp[0][2 * t + 1] = pk_relu(ac[t][2], ac[t][3]);
+            hp[2 * t] = pk_relu(ac[t][0], ac[t][1]);
+            hp[2 * t + 1] = pk_relu(ac[t][2], ac[t][3]);
           }
         }
 #pragma unroll
         for (int l = 0; l < NH; ++l) {
 #pragma unroll
-          for (int t = 0; t < 4; ++t) lds_st64(&B.h[l][sw64(row, 4u * t + g)], hp[l][2 * t], hp[l][2 * t + 1]);
-          const half8_t b0 = pk_operand(hp[l], 0), b1 = pk_operand(hp[l], 1);
+          for (int t = 0; t < 4; ++t) lds_st64(&B.h[l][sw64(row, 4u * t + g)], hp[2 * t], hp[2 * t + 1]);
+          const half8_t b0 = pk_operand(hp, 0), b1 = pk_operand(hp, 1);
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             half8_t w[2];
@@ -300,13 +310,13 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
             float4_t ac = {0.f, 0.f, 0.f, 0.f};
             ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(w[0], b0, ac, 0, 0, 0);
             ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(w[1], b1, ac, 0, 0, 0);
-            hp[l + 1][2 * t] = pk_relu(ac[0], ac[1]);
-            hp[l + 1][2 * t + 1] = pk_relu(ac[2], ac[3]);
+            hp[2 * t] = pk_relu(ac[0], ac[1]);
+            hp[2 * t + 1] = pk_relu(ac[2], ac[3]);
           }
         }
         float4_t o = {0.f, 0.f, 0.f, 0.f};
-        o = __builtin_amdgcn_mfma_f32_16x16x32_f16(ao[0], pk_operand(hp[NH], 0), o, 0, 0, 0);
-        o = __builtin_amdgcn_mfma_f32_16x16x32_f16(ao[1], pk_operand(hp[NH], 1), o, 0, 0, 0);
+        o = __builtin_amdgcn_mfma_f32_16x16x32_f16(sm.ao[0][lane], pk_operand(hp, 0), o, 0, 0, 0);
+        o = __builtin_amdgcn_mfma_f32_16x16x32_f16(sm.ao[1][lane], pk_operand(hp, 1), o, 0, 0, 0);
         // dL/dlogit of sample c, in every lane (rows 4g .. 4g+2 of the output tile are the channels)
         float dl[3];
 #pragma unroll
@@ -320,7 +330,7 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
            // scaled dO are staged in this wave's own rows of dy[NH] and dy[0], which its backward overwrites below
           uint32_t* hs = B.dy[NH];
 #pragma unroll
-          for (int t = 0; t < 4; ++t) lds_st64(&hs[sw64(row, 4u * t + g)], hp[NH][2 * t], hp[NH][2 * t + 1]);
+          for (int t = 0; t < 4; ++t) lds_st64(&hs[sw64(row, 4u * t + g)], hp[2 * t], hp[2 * t + 1]);
           // [3 channels][16 samples] in this wave's rows of dy[0] (of the otherwise unused h image when NH = 0,
           // where dy[0] is dy[NH])
           _Float16* ds = reinterpret_cast<_Float16*>(NH > 0 ? &B.dy[0][512u * wid] : &B.h[0][512u * wid]);
@@ -352,7 +362,7 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           ac[t] = float4_t{0.f, 0.f, 0.f, 0.f};
-          ac[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aot[t], bo, ac[t], 0, 0, 0);
+          ac[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(sm.aot[t][lane], bo, ac[t], 0, 0, 0);
         }
         // dH_NH .. dH_0: rescale, mask, stage, propagate
         uint32_t dp[8];
@@ -360,10 +370,12 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
         for (int l = NH; l >= 0; --l) {
           const float k2 = grad_scale(wave_max_nonneg(max_abs16(ac)));
           scale *= k2;
+          const uint32_t* hl = l == NH ? B.dy[NH] : B.h[l < NH ? l : 0];  // H_l, this wave's rows (the mask)
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
-            dp[2 * t] = pk_scaled(ac[t][0], ac[t][1], k2) & pk_nonzero_mask(hp[l][2 * t]);
-            dp[2 * t + 1] = pk_scaled(ac[t][2], ac[t][3], k2) & pk_nonzero_mask(hp[l][2 * t + 1]);
+            const u32x2v_t hv = *reinterpret_cast<const u32x2v_t*>(__builtin_assume_aligned(&hl[sw64(row, 4u * t + g)], 8));
+            dp[2 * t] = pk_scaled(ac[t][0], ac[t][1], k2) & pk_nonzero_mask(hv.x);
+            dp[2 * t + 1] = pk_scaled(ac[t][2], ac[t][3], k2) & pk_nonzero_mask(hv.y);
             lds_st64(&B.dy[l][sw64(row, 4u * t + g)], dp[2 * t], dp[2 * t + 1]);
           }
           if (lane == 0) B.inv[wid][l] = __builtin_amdgcn_rcpf(scale);  // exact: scale is a power of two
@@ -408,38 +420,47 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
       }
     }
     if (lane == 0) B.valid[wid] = (valid && !skip) ? 1 : 0;
-    lds_barrier();  // this buffer's images complete (the other buffer is free: everyone passed its readers)
-    // owners: rows 16 wid .. of dW_l += dY_l X_l^T over the 4 source tiles
-    bw2_owner<NH, 3>(B, 0, nullptr, acc0, run0);
+    lds_barrier();  // the images complete
+    // owners: rows 16 (wid / 2) .. of dW_l += dY_l X_l^T over the 8 source tiles
+    if ((wid & 1) == 0)
+      bw2_owner<NH, 2>(B, 0, nullptr, acc0, run0, 0);
+    else
+      bw2_owner<NH, 1>(B, 0, nullptr, acc0, run0, 2);
 #pragma unroll
-    for (int l = 0; l < NH; ++l) bw2_owner<NH, 4>(B, l + 1, B.h[l], acch[l], runh[l]);
+    for (int l = 0; l < NH; ++l) bw2_owner<NH, 2>(B, l + 1, B.h[l], acch[l], runh[l], 2 * (wid & 1));
+    lds_barrier();  // the images read: the next iteration may write them
   }
   // ---- weight gradients to this workgroup's slab
   float* sb = slab + (int64_t)blockIdx.x * rgb_mlp_params<NH>();
+  const int rt = wid >> 1;
   {
     const float inv = run0 == INFINITY ? 0.f : 1.0f / run0;
+    const int ct0 = (wid & 1) ? 2 : 0, nct = (wid & 1) ? 1 : 2;
 #pragma unroll
-    for (int m = 0; m < 3; ++m)
+    for (int m = 0; m < 2; ++m)
+      if (m < nct) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) sb[(16 * wid + 4 * g + q) * kRgbIn + 16 * m + c] = acc0[m][q] * inv;
+        for (int q = 0; q < 4; ++q) sb[(16 * rt + 4 * g + q) * kRgbIn + 16 * (ct0 + m) + c] = acc0[m][q] * inv;
+      }
   }
 #pragma unroll
   for (int l = 0; l < NH; ++l) {
     float* mat = sb + rgb_layer_offset<NH>(l + 1);
     const float inv = runh[l] == INFINITY ? 0.f : 1.0f / runh[l];
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
+    for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) mat[(16 * wid + 4 * g + q) * kRgbWidth + 16 * m + c] = acch[l][m][q] * inv;
+      for (int q = 0; q < 4; ++q) mat[(16 * rt + 4 * g + q) * kRgbWidth + 16 * (2 * (wid & 1) + m) + c] = acch[l][m][q] * inv;
   }
-  // the output layer: rows 0..2 of each wave's tiles, summed over the waves in a fixed order
-  lds_barrier();  // (sm.red aliases nothing, but every wave is past its last owner step)
+  // the output layer: rows 0..2 of each wave's tiles, summed over the waves in a fixed order (in the dY images:
+  // every wave passed the loop's last barrier, after the last reads of them)
+  Bw2Red& red = *reinterpret_cast<Bw2Red*>(&sm.buf.dy[0][0]);
   if (g == 0) {
     const float inv = runo == INFINITY ? 0.f : 1.0f / runo;
 #pragma unroll
     for (int m = 0; m < 4; ++m)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) sm.red[wid][q][16 * m + c] = acco[m][q] * inv;
+      for (int q = 0; q < 3; ++q) red[wid][q][16 * m + c] = acco[m][q] * inv;
   }
   __syncthreads();
   {
@@ -449,7 +470,7 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
       float v = 0.f;
       if (k < 3) {
 #pragma unroll
-        for (int w = 0; w < kBw2Waves; ++w) v += sm.red[w][k][n];
+        for (int w = 0; w < kBw2Waves; ++w) v += red[w][k][n];
       }
       mo[i] = v;
     }
