@@ -170,7 +170,11 @@ class FieldState:
 
 
 FUSED_ADAM_MAX_N = 1 << 17  # samples up to which the step fuses the table's Adam into the backward ("auto")
-AR_CUT_DEFAULT = 8  # the level at which the two gradient-exchange ranges split: [cut, L) first, then [0, cut) + MLP
+# the level at which the two gradient-exchange ranges split: [cut, L) first, then [0, cut) + MLP.  Modelled per
+# cut from the measured per-range accumulate at C4 shard 1/8 (tools/zero_tail_model.py): the
+# exchange's critical path is 3 us shorter at 6 than at 4 and 13-20 us shorter than at 8 (round 4's cut) for
+# ring bandwidths of 100-400 GB/s
+AR_CUT_DEFAULT = 6
 
 
 class StepEngine:
@@ -196,8 +200,8 @@ class StepEngine:
         self._warned_clip = False
         # level ranges of the bucketed gradient all-reduce, finest first: the first range's exchange
         # overlaps the later range's accumulation.  Every range is its own accumulate + finalize
-        # launch pair, and at world size 1 over RCCL (no peer traffic; tools/dp_overhead.py) the step
-        # costs 2.18-2.25 ms with one range, 2.23-2.30 with two (levels 8-15, then 0-7 + the MLP)
+        # launch pair, and at world size 1 over RCCL (no peer traffic; tools/dp_overhead.py, round 3) the step
+        # cost 2.18-2.25 ms with one range, 2.23-2.30 with two (levels 8-15, then 0-7 + the MLP)
         # and 2.41-2.44 with four, against 2.12 without the hook; two ranges hide about half of the
         # 29.7 MB exchange for a fraction of the four ranges' cost.  LONER_AR_BUCKETS = 1, 2 or 4.
         # With two ranges the cut level is LONER_AR_CUT (default AR_CUT_DEFAULT; the modelled exposure of
@@ -563,7 +567,7 @@ class StepEngine:
         the all-gather of that chunk's fp16 shadow (asynchronous).  Nothing waits for the all-gathers here:
         the next reader of the shadow (the next step's encode, after its ray build and sampling, or
         finish()) does, so the gather overlaps the next step's head.  Exposed per step: the last range's
-        reduce-scatter and its Adam."""
+        reduce-scatter and its Adam (the cut: AR_CUT_DEFAULT)."""
         st, cfg, m = self.state, self.cfg, self._mark
         zr, zw = self.zero
         comm = self.allreduce is not None and zw > 1

@@ -64,7 +64,18 @@ def main():
         def scatter():
             e._grid_bwd(e.rays, R, S, N, L.BWD_COUNTS_READY | L.BWD_LEVEL_MAX_READY | L.BWD_NO_ACCUM, L.stream(dev))
 
-        return dict(enc=enc, field=field, scatter=scatter)
+        # the scan turns the encode's histogram into offsets in place: a scatter timed on its own (no encode before
+        # it) first restores the encode's counts (a ~10 us copy, in the alone times only)
+        nb = sum((int(st.desc.size[l]) + 4095) // 4096 for l in range(cfg.n_levels))
+        hist = e.bwd_ws[256:256 + 4 * nb * ((N + 511) // 512)]
+        enc()
+        snap = hist.clone()
+
+        def scatter_alone():
+            hist.copy_(snap)
+            scatter()
+
+        return dict(enc=enc, field=field, scatter=scatter, scatter_alone=scatter_alone)
 
     def run(seq_fns, reps):
         torch.cuda.synchronize()
@@ -102,7 +113,7 @@ def main():
         main.wait_event(d2)
 
     one = engines(1)[0]
-    base = {k: run(one[k], a.reps) for k in ("enc", "field", "scatter")}
+    base = {k: run(one[k if k != "scatter" else "scatter_alone"], a.reps) for k in ("enc", "field", "scatter")}
     whole = run(lambda: (one["enc"](), one["field"](), one["scatter"]()), a.reps)
     print(f"{a.config} whole batch: enc {base['enc']:.1f} field {base['field']:.1f} scatter {base['scatter']:.1f} us;"
           f" E F S in sequence {whole:.1f} us", flush=True)
@@ -113,7 +124,8 @@ def main():
         for _ in range(2):  # warm both forms
             run(lambda: [f() for c in ch for f in (c["enc"], c["field"], c["scatter"])], 3)
             run(lambda: pipelined(ch), 3)
-        alone = {s: sum(run(c[s], a.reps) for c in ch) for s in ("enc", "field", "scatter")}
+        alone = {s: sum(run(c[s if s != "scatter" else "scatter_alone"], a.reps) for c in ch)
+                 for s in ("enc", "field", "scatter")}
         seq = run(lambda: [f() for c in ch for f in (c["enc"], c["field"], c["scatter"])], a.reps)
         pip = run(lambda: pipelined(ch), a.reps)
         print(f"  K={k}: chunks' stages summed: enc {alone['enc']:.1f} field {alone['field']:.1f} scatter "
