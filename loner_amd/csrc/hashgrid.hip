@@ -22,8 +22,9 @@ namespace lnr {
 __device__ __forceinline__ void store_enc(uint32_t* p, uint32_t v) { __builtin_nontemporal_store(v, p); }
 
 // The 8 corners of a fine (hashed, power-of-two) level: the x-pairs e, e ^ d of the four y/z edges.
-// What bounds this gather is the texture addresser: TA busy 85 % of the launch at C2, about 40
-// TA cycles per wave-wide gather of scattered entries (profiles/r03_l2req_C2.txt).  Reading an
+// What bounds this gather is the texture addresser: TA busy 0.78 of the launch at C2 with the level-grouped
+// encode (profiles/r04_l2req_C2.txt; 0.85 before the grouping, profiles/r03_l2req_C2.txt), about 40 TA cycles
+// per wave-wide gather of scattered entries.  Reading an
 // x-pair through one 16-B load of its aligned quad (3/4 of the pairs; tried) cut the vector-L1 line
 // accesses from 426 M to 288 M per launch but left TA busy where it was (0.743 against 0.720 ms);
 // 8-B pair loads ran 0.86 ms.  Plain dword gathers (here, or lane-paired below).
