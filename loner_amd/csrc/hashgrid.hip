@@ -19,7 +19,15 @@ namespace lnr {
 
 // The encoding is written once, as whole lines, and read by the field kernels after this launch: a
 // nontemporal store keeps it out of the way of the table slices in L2 (step -0.01 ms at C2)
-__device__ __forceinline__ void store_enc(uint32_t* p, uint32_t v) { __builtin_nontemporal_store(v, p); }
+#ifndef LNR_ENC_STORE_NT
+#define LNR_ENC_STORE_NT 1
+#endif
+__device__ __forceinline__ void store_enc(uint32_t* p, uint32_t v) {
+  if (LNR_ENC_STORE_NT)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
 
 // The 8 corners of a fine (hashed, power-of-two) level: the x-pairs e, e ^ d of the four y/z edges.
 // What bounds this gather is the texture addresser: TA busy 0.78 of the launch at C2 with the level-grouped
@@ -361,6 +369,13 @@ static int check_desc(const lnr_grid_desc* d, const char* who) {
   return LNR_OK;
 }
 
+// Levels per workgroup of the live-masked eval encode (C3's colour encode): LONER_ENC_LIVE_LPB 1 (default) or 2
+// (strided pairs, the colour grid's two 2 MB levels per group), read at every launch
+static int live_lpb() {
+  const char* e = getenv("LONER_ENC_LIVE_LPB");
+  return e ? atoi(e) : 1;
+}
+
 template <class PosFn>
 static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16_t* table, uint32_t* enc,
                       int64_t enc_stride, void* bwd_ws, int64_t bwd_ws_bytes, hipStream_t st, const char* who,
@@ -395,6 +410,10 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
     if (live == nullptr)
       hipLaunchKernelGGL(enc_kernel(), dim3(grid.x, d->n_levels / lpb), dim3(kSB), 0, st, a, pos, n, tb, enc, enc_stride,
                          BwdWorkspace{}, live);
+    else if (spt2 && live_lpb() == 2 && d->n_levels % 2 == 0 && enc_levels_per_group(d, grid.x) >= 2)
+      // (two samples per thread over two levels spill at eight waves per SIMD: one sample per thread)
+      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, false, 2>), dim3(grid.x, d->n_levels / 2), dim3(kSB), 0, st, a,
+                         pos, n, tb, enc, enc_stride, BwdWorkspace{}, live);
     else if (spt2)
       hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 2, false>), grid, dim3(kSB / 2), 0, st, a, pos, n, tb, enc,
                          enc_stride, BwdWorkspace{}, live);

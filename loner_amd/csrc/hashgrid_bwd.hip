@@ -812,23 +812,34 @@ __device__ __forceinline__ uint32_t level_of_bucket(const GridArgs& a, uint32_t 
 // (mean run of one cell ~1 sample from level 9 on), so a wave's atomic
 // instruction over 64 records 2 apart meets equal entries only by hash collision: each thread adds
 // the 2 records of its own 16-B load, with no stage write, no barriers and no stage reads.
+// LNR_ACCUM_REVERSE: tiles walked from the end of the range to its start (the int64 sums are order-free: the
+// same bits).  The scatter writes the highest rows last, so a range's last records are the most recently
+// written, the ones still in the Infinity Cache.
+#ifndef LNR_ACCUM_REVERSE
+#define LNR_ACCUM_REVERSE 0
+#endif
+#ifndef LNR_ACCUM_LOAD_NT
+#define LNR_ACCUM_LOAD_NT 1  // the record loads nontemporal (read once)
+#endif
 __device__ __forceinline__ void accum_records(unsigned long long* acc, uint2* stage, const BwdWorkspace& ws,
                                               uint64_t beg, uint64_t end, float fs, bool direct = false) {
   const int lane = threadIdx.x & 63;
   const uint64_t beg2 = beg & ~1ull;
   const float ftx = fs * kInvU16;
   const uint64_t n_tiles = (end - beg2 + kTile - 1) / kTile;
+  auto tix = [&](uint64_t t) { return LNR_ACCUM_REVERSE ? n_tiles - 1 - t : t; };  // (t < n_tiles)
   auto load_tile = [&](uint64_t tile) {  // this thread's 2 records of a tile: {w0, v0, w1, v1}
-    const uint64_t rr = beg2 + (tile < n_tiles ? tile : 0) * kTile + 2 * threadIdx.x;
+    const uint64_t rr = beg2 + (tile < n_tiles ? tix(tile) : 0) * kTile + 2 * threadIdx.x;
     const uint64_t rc = rr < end ? rr : beg2;  // unconditional loads
-    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(&ws.rec[rc]));
+    if (LNR_ACCUM_LOAD_NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(&ws.rec[rc]));
+    return *reinterpret_cast<const u32x4*>(&ws.rec[rc]);
   };
   const uint32_t q0 = 32u * lane + 2u * (threadIdx.x >> 6);  // this lane's records in a tile
   auto run_tile = [&](uint64_t tile, const u32x4& cur) {
     lds_barrier();  // the previous tile's stage reads are done
     *reinterpret_cast<u32x4*>(&stage[stage_pos(2 * threadIdx.x)]) = cur;
     lds_barrier();
-    const uint64_t base = beg2 + tile * kTile;
+    const uint64_t base = beg2 + tix(tile) * kTile;
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const uint2 rec = stage[stage_pos(q0 + r)];
@@ -885,7 +896,7 @@ __device__ __forceinline__ void accum_records(unsigned long long* acc, uint2* st
         if (tile + d < n_tiles) {  // block-uniform
           const u32x4 c = buf[d];
           buf[d] = load_tile(tile + d + kAccumTrip);
-          const uint64_t rr = beg2 + (tile + d) * kTile + 2 * threadIdx.x;
+          const uint64_t rr = beg2 + tix(tile + d) * kTile + 2 * threadIdx.x;
           if (rr >= beg && rr < end) add_rec(c.x, c.y);
           if (rr + 1 >= beg && rr + 1 < end) add_rec(c.z, c.w);
         }
