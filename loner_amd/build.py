@@ -31,7 +31,8 @@ FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-ffp-contract=
 # copies wait for the loads before the barrier.
 # rgb_train.hip: MFMA results in VGPRs (the colour-head backward's VALU reads every one of them; the default
 # heuristic put them in AGPRs and paid a v_accvgpr_read per value).
-FILE_FLAGS = {"hashgrid_bwd.hip": ["-fno-slp-vectorize"], "rgb_train.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+FILE_FLAGS = {"hashgrid_bwd.hip": ["-fno-slp-vectorize"], "rgb_train.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"],
+              "field.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
 def _sources():
@@ -42,12 +43,13 @@ def _deps():
     return sorted(glob.glob(os.path.join(CSRC, "*.hpp")) + [os.path.join(ROOT, "include", "loner_amd.h")])
 
 
-def _compile(src, objdir=OBJDIR, extra=()):
+def _compile(src, objdir=OBJDIR, extra=(), file_flags=None):
     obj = os.path.join(objdir, os.path.basename(src).replace(".hip", ".o"))
     newest_dep = max(os.path.getmtime(p) for p in _deps() + [src])
     if os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
         return obj, ""
-    cmd = [HIPCC, *FLAGS, *FILE_FLAGS.get(os.path.basename(src), []), *extra, "-c", src, "-o", obj]
+    ff = FILE_FLAGS if file_flags is None else file_flags
+    cmd = [HIPCC, *FLAGS, *ff.get(os.path.basename(src), []), *extra, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
@@ -56,10 +58,17 @@ def _compile(src, objdir=OBJDIR, extra=()):
 
 def build(jobs=8, force=False, verbose=False, defines=(), out=None):
     """Build the library.  ``defines``/``out``: an experiment variant (-D flags) linked to ``out``
-    with its own object directory (tools/exp_variants.py); the default build has neither."""
+    with its own object directory (tools/exp_variants.py); the default build has neither.  A define
+    ``FLAGS@<file>.hip@<flag>@<flag>...`` adds compiler flags for one source file instead."""
     lib_path = out or LIB
-    objdir = OBJDIR if not defines else os.path.join(ROOT, "build", "obj_" + "_".join(sorted(defines)).lower())
-    extra = [f"-D{d}" for d in defines]
+    objdir = OBJDIR if not defines else os.path.join(
+        ROOT, "build", "obj_" + "_".join(sorted(defines)).lower().replace("@", "_").replace("-", "").replace("=", ""))
+    file_flags = {k: list(v) for k, v in FILE_FLAGS.items()}
+    for d in defines:
+        if d.startswith("FLAGS@"):
+            f, *fl = d.split("@")[1:]
+            file_flags.setdefault(f, []).extend(fl)
+    extra = [f"-D{d}" for d in defines if not d.startswith("FLAGS@")]
     os.makedirs(objdir, exist_ok=True)
     os.makedirs(os.path.dirname(lib_path), exist_ok=True)
     if force:
@@ -67,7 +76,7 @@ def build(jobs=8, force=False, verbose=False, defines=(), out=None):
             os.remove(o)
     srcs = _sources()
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        results = list(ex.map(lambda s: _compile(s, objdir, extra), srcs))
+        results = list(ex.map(lambda s: _compile(s, objdir, extra, file_flags), srcs))
     objs = [o for o, _ in results]
     if verbose:
         for o, err in results:

@@ -61,13 +61,43 @@ enum : uint32_t { kStreamJitter = 1, kStreamPdf = 2, kStreamNoise = 3 };
 
 // ------------------------------------------------------------------ fp16
 typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
+typedef _Float16 half2v_t __attribute__((ext_vector_type(2)));
 typedef float float4_t __attribute__((ext_vector_type(4)));
+typedef short v4i16_t __attribute__((__vector_size__(8)));
+typedef uint16_t u16x2v_t __attribute__((ext_vector_type(2)));
+typedef int16_t i16x2v_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float h2f(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
 __device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
 __device__ __forceinline__ float round_f16(float f) { return (float)(_Float16)f; }
 __device__ __forceinline__ float2 half2_to_float2(uint32_t v) {
   return make_float2(h2f((uint16_t)(v & 0xFFFFu)), h2f((uint16_t)(v >> 16)));
+}
+
+__device__ __forceinline__ float pk_lo(uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v & 0xFFFFu)); }
+__device__ __forceinline__ float pk_hi(uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v >> 16)); }
+// fp32 pair -> packed fp16 (round to nearest even), ReLU on the halves (the ReLU of the rounded value is the
+// rounding of the ReLU; a negative value may give -0, which every consumer treats as 0)
+__device__ __forceinline__ uint32_t pk_relu(float x, float y) {
+  half2v_t h = {(_Float16)x, (_Float16)y};
+  const half2v_t z = {(_Float16)0.f, (_Float16)0.f};
+  h = __builtin_elementwise_max(h, z);
+  return __builtin_bit_cast(uint32_t, h);
+}
+// 0xFFFF in each half whose value is not +-0: bit 15 of (|h| + 0x7FFF) per half, spread by an arithmetic shift
+// (v_and, v_pk_add_u16, v_pk_ashrrev_i16: no carries between the halves, |h| <= 0x7FFF)
+__device__ __forceinline__ uint32_t pk_nonzero_mask(uint32_t h) {
+  const u16x2v_t t = __builtin_bit_cast(u16x2v_t, h & 0x7FFF7FFFu) + (u16x2v_t){0x7FFF, 0x7FFF};
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(i16x2v_t, t) >> (i16x2v_t){15, 15});
+}
+// ds_read_b64_tr_b16: in each 16-lane group, lane 4q + p gives the address of 4 halves (columns 4p .. 4p + 3 of
+// row q); lane i receives column i of the 4 rows
+__device__ __forceinline__ half4_t lds_tr16(const uint32_t* p) {
+  return __builtin_bit_cast(half4_t, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                                         (__attribute__((address_space(3))) v4i16_t*)(p)));
 }
 
 // ------------------------------------------------------------------ barriers

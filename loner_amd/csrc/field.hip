@@ -785,13 +785,15 @@ __global__ void __launch_bounds__(NT) k_sigma_fwd_tiles(FieldArgs a) {
     half8_t b[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) b[t] = load_enc_operand(a.enc, a.enc_stride, n0 + 16 * t + c, true);
+    bool clipped = false;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       SigmaHidden h;
       const float sgm = sigma_tile_fwd(sw, b[t], h);
       if (g == 0) a.d_sigma[n0 + 16 * t + c] = sigma_to_f16(sgm);
-      if (a.lp.dev_status && __any(!isfinite(round_f16(sgm))) && lane == 0) atomicOr(a.lp.dev_status, LNR_STATUS_SIGMA_CLIPPED);
+      clipped |= !isfinite(round_f16(sgm));
     }
+    if (a.lp.dev_status && __any(clipped) && lane == 0) atomicOr(a.lp.dev_status, LNR_STATUS_SIGMA_CLIPPED);
   }
 }
 
@@ -828,7 +830,42 @@ __device__ __forceinline__ void st_off(T* base, uint32_t byte_off, T v) {
 
 // fp16 pair (round to nearest) in one word, low half first
 __device__ __forceinline__ uint32_t pack_h2(float x, float y) {
-  return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)x) | ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)y) << 16);
+  const half2v_t h = {(_Float16)x, (_Float16)y};  // (one v_cvt_pk_f16_f32)
+  return __builtin_bit_cast(uint32_t, h);
+}
+
+// Packed-half pair for k_mlp_bwd_tiles (LNR_MLP_PK): the hidden layer kept as 8 fp16-pair words per tile
+// (v_cvt_pk + v_pk_max: the ReLU of the rounded value), the ReLU masks taken from those words by integer ops
+// (pk_nonzero_mask), and dW0's operands staged as [sample][neuron] rows of 8-byte chunks read back transposed
+// (ds_read_b64_tr_b16) instead of one 2-byte LDS store per value.  Same operands at the same MFMA k
+// positions as dw0_pair_mfma (the k order matters: tools/ubench/ubench_mfma_korder.hip), bitwise the same sums
+// except where the scaled ds * Enc operand rounds a tie differently (below).
+// Wave image of a pair: the ReLU mask (1.0 / 0.0), 32 sample rows x 16 chunks (64 hid), and ds * Enc at the
+// pair's scale, 32 rows x 8 chunks (32 inputs).  Chunk swizzles: the transposed reads of rows 8g + q
+// (g = 0..3, q = 0..3 or 4..7) x 4 chunks meet 64 distinct banks per 32 lanes.
+__device__ __forceinline__ uint32_t mk_dw(uint32_t r, uint32_t ch) {
+  return 32u * r + 2u * (ch ^ ((((r >> 1) & 1u) | (((r >> 3) & 1u) << 1)) << 2));
+}
+__device__ __forceinline__ uint32_t en_dw(uint32_t r, uint32_t ch) { return 1024u + 16u * r + 2u * (ch ^ (((r >> 3) & 1u) << 2)); }
+// forward of one tile: hw[2t + (r >> 1)] holds relu(H)[hid 16t + 4g + r] (r = 0..3) for sample l & 15
+template <class W>
+__device__ __forceinline__ void sigma_tile_fwd_pk(const W& sw, const uint32_t (&x)[4], uint32_t (&hw)[8]) {
+  const half8_t e = __builtin_bit_cast(half8_t, (u32x4){x[0], x[1], x[2], x[3]});
+  float4_t acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(sw.A0(t), e, (float4_t){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    hw[2 * t] = pk_relu(acc[t][0], acc[t][1]);
+    hw[2 * t + 1] = pk_relu(acc[t][2], acc[t][3]);
+  }
+}
+// max |e_j| over a tile's 8 encoding halves (non-negative halves order as their bits), as fp32
+__device__ __forceinline__ float enc_absmax(const uint32_t (&x)[4]) {
+  u16x2v_t m = __builtin_bit_cast(u16x2v_t, x[0] & 0x7FFF7FFFu);
+#pragma unroll
+  for (int q = 1; q < 4; ++q) m = __builtin_elementwise_max(m, __builtin_bit_cast(u16x2v_t, x[q] & 0x7FFF7FFFu));
+  return h2f(m[0] > m[1] ? m[0] : m[1]);
 }
 
 // Phase 2, tile-parallel: sigma MLP backward over 32-sample tile pairs (no per-ray structure):
@@ -842,6 +879,9 @@ __device__ __forceinline__ uint32_t pack_h2(float x, float y) {
 #endif
 #ifndef LNR_MLP_SPLIT_PAIR
 #define LNR_MLP_SPLIT_PAIR 0  // k_mlp_bwd_tiles: one tile of the pair live at a time (pair_split)
+#endif
+#ifndef LNR_MLP_PK
+#define LNR_MLP_PK 1  // k_mlp_bwd_tiles: the packed-half pair (pair_pk)
 #endif
 #ifndef LNR_MLP_BWD_WAVES
 #define LNR_MLP_BWD_WAVES 2  // waves per SIMD (3 spills 113 registers with the weights in registers)
@@ -1000,7 +1040,115 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(LNR_MLP
     }
     if (dw0) dw0_mfma(lds, acc);
   };
-#if LNR_MLP_SPLIT_PAIR
+  auto pair_pk = [&](int64_t n0, const Pre& p) {
+    uint32_t hw[2][8];
+    sigma_tile_fwd_pk(sw, p.x0, hw[0]);
+    sigma_tile_fwd_pk(sw, p.x1, hw[1]);
+    const float ds[2] = {p.d0, p.d1};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const float h0 = (k & 1) ? pk_hi(hw[0][k >> 1]) : pk_lo(hw[0][k >> 1]);
+      const float h1 = (k & 1) ? pk_hi(hw[1][k >> 1]) : pk_lo(hw[1][k >> 1]);
+      dw1[k] = fmaf(ds[0], h0, dw1[k]);
+      dw1[k] = fmaf(ds[1], h1, dw1[k]);
+    }
+    // max |e ds| over the pair: |ds| max |e| (rounding is monotonic: the same value)
+    // (on DPP, wave-uniform; the same value as dw0_pair_mfma's wave_max for finite inputs)
+    const float pair_max = wave_max_nonneg(fmaxf(enc_absmax(p.x0) * fabsf(ds[0]), enc_absmax(p.x1) * fabsf(ds[1])));
+    const uint32_t* w1w = reinterpret_cast<const uint32_t*>(&sw.w1h[0]);
+    uint32_t mk[2][8];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) mk[t][i] = pk_nonzero_mask(hw[t][i]);
+      uint32_t bw[8];  // the backward's B operand: w1 where the hidden unit is live
+#pragma unroll
+      for (int i = 0; i < 8; ++i) bw[i] = mk[t][i] & w1w[i];
+      const half8_t b0 = __builtin_bit_cast(half8_t, (u32x4){bw[0], bw[1], bw[2], bw[3]});
+      const half8_t b1 = __builtin_bit_cast(half8_t, (u32x4){bw[4], bw[5], bw[6], bw[7]});
+      const float dst = ds[t];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        float4_t acc = {0.f, 0.f, 0.f, 0.f};
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(sw.BT(m, 0), b0, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(sw.BT(m, 1), b1, acc, 0, 0, 0);
+        const int lvl = 8 * m + 2 * g;
+        if (JAC) {
+          const uint32_t o = row_j + 8u * (uint32_t)m * st4 + (uint32_t)(n0 + 16 * t + c) * 4u;
+          st_off(a.d_jac, o, pack_h2(acc[0], acc[1]));
+          st_off(a.d_jac, o + st4, pack_h2(acc[2], acc[3]));
+          // max |d ds| = |ds| max |d| (monotonic rounding)
+          const float ads = fabsf(dst);
+          lmax[2 * m] = fmaxf(lmax[2 * m], fmaxf(fabsf(acc[0]), fabsf(acc[1])) * ads);
+          lmax[2 * m + 1] = fmaxf(lmax[2 * m + 1], fmaxf(fabsf(acc[2]), fabsf(acc[3])) * ads);
+        } else {
+          const float2 q0 = make_float2(acc[0] * dst, acc[1] * dst), q1 = make_float2(acc[2] * dst, acc[3] * dst);
+          denc[(int64_t)lvl * a.enc_stride + n0 + 16 * t + c] = q0;
+          denc[(int64_t)(lvl + 1) * a.enc_stride + n0 + 16 * t + c] = q1;
+          lmax[2 * m] = fmaxf(lmax[2 * m], fmaxf(fabsf(q0.x), fabsf(q0.y)));
+          lmax[2 * m + 1] = fmaxf(lmax[2 * m + 1], fmaxf(fabsf(q1.x), fabsf(q1.y)));
+        }
+      }
+    }
+#ifdef LNR_MLP_PK_OLDDW0
+    {
+      SigmaHidden H[2];
+      half8_t E[2];
+      for (int t = 0; t < 2; ++t) {
+        H[t].q[0] = __builtin_bit_cast(half8_t, (u32x4){hw[t][0], hw[t][1], hw[t][2], hw[t][3]});
+        H[t].q[1] = __builtin_bit_cast(half8_t, (u32x4){hw[t][4], hw[t][5], hw[t][6], hw[t][7]});
+        const uint32_t* x = t ? p.x1 : p.x0;
+        E[t] = __builtin_bit_cast(half8_t, (u32x4){x[0], x[1], x[2], x[3]});
+      }
+      dw0_pair_mfma(lds, H[0], H[1], E[0], E[1], ds[0], ds[1], pair_max, acc);
+      return;
+    }
+#endif
+    float scale = 1.f;
+    if (!dw0_scale(pair_max, acc, scale)) return;  // (wave-uniform) the pair adds nothing to dW0
+    uint32_t* img = reinterpret_cast<uint32_t*>(lds);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const uint32_t r = 16u * t + c;
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt)  // hid 16 tt + 4 g .. + 3: chunk 4 tt + g
+        *reinterpret_cast<u32x2*>(&img[mk_dw(r, 4u * tt + g)]) =
+            (u32x2){mk[t][2 * tt] & 0x3C003C00u, mk[t][2 * tt + 1] & 0x3C003C00u};
+      const float st = ds[t] * scale;
+      const uint32_t* x = t ? p.x1 : p.x0;
+      // (fp32 product, then rounded to fp16, as written: dw0_pair_mfma's same expression compiles to v_fma_mixlo,
+      // one rounding of the exact product, so a rare tie rounds differently there: tools/mlp_bwd_dump.py)
+      const half8_t e = __builtin_bit_cast(half8_t, (u32x4){x[0], x[1], x[2], x[3]});
+      half8_t es;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) es[j] = (_Float16)((float)e[j] * st);
+      *reinterpret_cast<half8_t*>(&img[en_dw(r, 2u * g)]) = es;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-local hand-off through LDS
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t tq = ((uint32_t)lane >> 2) & 3u, tp = (uint32_t)lane & 3u;
+    const uint32_t r0 = 8u * g + tq;
+    half8_t av[4], bv[2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const half4_t lo = lds_tr16(&img[mk_dw(r0, 4u * t + tp)]), hi = lds_tr16(&img[mk_dw(r0 + 4u, 4u * t + tp)]);
+      av[t] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const half4_t lo = lds_tr16(&img[en_dw(r0, 4u * m + tp)]), hi = lds_tr16(&img[en_dw(r0 + 4u, 4u * m + tp)]);
+      bv[m] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int m = 0; m < 2; ++m) acc.v[t][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[t], bv[m], acc.v[t][m], 0, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+  };
+#if LNR_MLP_PK
+#define LNR_MLP_PAIR pair_pk
+#elif LNR_MLP_SPLIT_PAIR
 #define LNR_MLP_PAIR pair_split
 #else
 #define LNR_MLP_PAIR pair

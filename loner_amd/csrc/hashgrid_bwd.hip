@@ -238,8 +238,6 @@ __device__ __forceinline__ int64_t xcd_row(uint32_t bx, uint32_t n) {
 }  // 4 records per sample at fine levels, plus slack
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // KIND: the levels one launch covers, so each gets only its own code and registers.
 // kLevelsAny: one launch over every level, grid.x = rows x levels with the level fastest, so each CU

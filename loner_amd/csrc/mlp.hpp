@@ -101,20 +101,24 @@ __device__ __forceinline__ half8_t load_enc_operand(const uint32_t* __restrict__
 
 // Forward of one 16-sample tile.  h[4t+r] = fp16(relu(H))[hid 16t+4g+r][sample l&15];
 // returns sigma for sample l&15 (fp32 accumulate of fp16 operands, NOT yet rounded).
+// The ReLU on the rounded halves (pk_relu: one v_cvt_pk + one v_pk_max per two values) is the rounding of the
+// ReLU; a -0 it may leave adds nothing below and counts as inactive everywhere (h > 0, pk_nonzero_mask).
 template <class W>
 __device__ __forceinline__ float sigma_tile_fwd(const W& sw, const half8_t& benc, SigmaHidden& h) {
-  float part = 0.f;
+  float4_t acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(sw.A0(t), benc, (float4_t){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+  uint32_t hw[8];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    float4_t acc = {0.f, 0.f, 0.f, 0.f};
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(sw.A0(t), benc, acc, 0, 0, 0);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const _Float16 v16 = (_Float16)fmaxf(acc[r], 0.f);
-      h.q[(4 * t + r) >> 3][(4 * t + r) & 7] = v16;
-      part = fmaf(sw.w1(4 * t + r), (float)v16, part);
-    }
+    hw[2 * t] = pk_relu(acc[t][0], acc[t][1]);
+    hw[2 * t + 1] = pk_relu(acc[t][2], acc[t][3]);
   }
+  h.q[0] = __builtin_bit_cast(half8_t, (u32x4){hw[0], hw[1], hw[2], hw[3]});
+  h.q[1] = __builtin_bit_cast(half8_t, (u32x4){hw[4], hw[5], hw[6], hw[7]});
+  float part = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) part = fmaf(sw.w1(k), (k & 1) ? pk_hi(hw[k >> 1]) : pk_lo(hw[k >> 1]), part);
   part += __shfl_xor(part, 16, 64);
   part += __shfl_xor(part, 32, 64);
   return part;
@@ -269,8 +273,15 @@ __device__ __forceinline__ void dw0_pair_mfma(_Float16* __restrict__ lds, const 
   const float s0 = ds0 * scale, s1 = ds1 * scale;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
+#ifdef LNR_DW0_DOUBLE_ROUND
+    float p0 = (float)e0[j] * s0, p1 = (float)e1[j] * s1;
+    asm volatile("" : "+v"(p0), "+v"(p1));
+    ens[(8 * g + j) * 32 + c] = (_Float16)p0;
+    ens[(8 * g + j) * 32 + 16 + c] = (_Float16)p1;
+#else
     ens[(8 * g + j) * 32 + c] = (_Float16)((float)e0[j] * s0);
     ens[(8 * g + j) * 32 + 16 + c] = (_Float16)((float)e1[j] * s1);
+#endif
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-local hand-off through LDS
   __builtin_amdgcn_wave_barrier();

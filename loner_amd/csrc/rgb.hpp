@@ -10,7 +10,6 @@ namespace lnr {
 constexpr int kRgbWaves = 4;
 
 constexpr int kRgbIn = 48, kRgbWidth = 64, kRgbOutPad = 16;
-typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
 
 struct RgbArgs {
   const uint16_t* w;      // tcnn flat params of the colour network

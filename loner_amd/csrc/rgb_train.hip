@@ -25,8 +25,6 @@ namespace lnr {
 //    wave's own rows of the dY images (before its backward writes them) into 16x16x16 MFMAs at a running scale.
 // Scales: a layer's scale comes from the wave's largest |gradient| before the ReLU mask (k_rgb_bwd_tiles:
 // after), so it is at most one power of two finer than it could be; deterministic either way.
-typedef short v4i16_t __attribute__((__vector_size__(8)));
-typedef _Float16 half2v_t __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4v_t __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2v_t __attribute__((ext_vector_type(2)));
 constexpr int kBw2Waves = kRgbBwd2Waves;
@@ -61,25 +59,6 @@ struct Bw2Lds {
 // (after the loop) the output layer's gradient per wave, over the dY images
 typedef float Bw2Red[kBw2Waves][3][64];
 
-__device__ __forceinline__ half4_t lds_tr16(const uint32_t* p) {
-  return __builtin_bit_cast(half4_t, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                                         (__attribute__((address_space(3))) v4i16_t*)(p)));
-}
-// fp32 pair -> packed fp16 (round to nearest even), ReLU on the halves
-__device__ __forceinline__ uint32_t pk_relu(float x, float y) {
-  half2v_t h = {(_Float16)x, (_Float16)y};
-  const half2v_t z = {(_Float16)0.f, (_Float16)0.f};
-  h = __builtin_elementwise_max(h, z);
-  return __builtin_bit_cast(uint32_t, h);
-}
-// 0xFFFF in each half whose value is not +-0: bit 15 of (|h| + 0x7FFF) per half, spread by an arithmetic shift
-// (v_and, v_pk_add_u16, v_pk_ashrrev_i16: no carries between the halves, |h| <= 0x7FFF)
-typedef uint16_t u16x2v_t __attribute__((ext_vector_type(2)));
-typedef int16_t i16x2v_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t pk_nonzero_mask(uint32_t h) {
-  const u16x2v_t t = __builtin_bit_cast(u16x2v_t, h & 0x7FFF7FFFu) + (u16x2v_t){0x7FFF, 0x7FFF};
-  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(i16x2v_t, t) >> (i16x2v_t){15, 15});
-}
 __device__ __forceinline__ void lds_st64(uint32_t* p, uint32_t x, uint32_t y) {
   *reinterpret_cast<u32x2v_t*>(__builtin_assume_aligned(p, 8)) = u32x2v_t{x, y};
 }
@@ -91,8 +70,6 @@ __device__ __forceinline__ half8_t pk_operand(const uint32_t (&v)[8], int s) {
   const u32x4v_t u = {v[4 * s], v[4 * s + 1], v[4 * s + 2], v[4 * s + 3]};
   return __builtin_bit_cast(half8_t, u);
 }
-__device__ __forceinline__ float pk_lo(uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v & 0xFFFFu)); }
-__device__ __forceinline__ float pk_hi(uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v >> 16)); }
 template <int CTRL>
 __device__ __forceinline__ float row_dpp(float v) {  // row_shr by CTRL's shift; lanes shifted in read 0
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));

@@ -108,11 +108,13 @@ def test_hashgrid_fwd_table_offset_and_ragged_rows(L, count, n):
     assert np.all(np.abs(got - ref) <= 1.01 * (np.abs(ref) * 2.0 ** -10 + 2.0 ** -24))
 
 
-@pytest.mark.parametrize("R", [24, 520])
-def test_hashgrid_fwd_live_mask_matches_full_encode(L, R):
+@pytest.mark.parametrize("R,lpb", [(24, "1"), (520, "1"), (520, "2")])
+def test_hashgrid_fwd_live_mask_matches_full_encode(L, R, lpb, monkeypatch):
     """The live-masked eval encode (plain gathers, dead samples issue none; two samples per thread
-    from 2^18 samples) equals the full encode (lane-paired gathers) on live samples and is 0 on dead
-    ones, bit for bit: the same entries in the same corner order."""
+    from 2^18 samples, or with LONER_ENC_LIVE_LPB=2 one sample per thread over two strided levels per
+    workgroup) equals the full encode (lane-paired gathers) on live samples and is 0 on dead ones, bit
+    for bit: the same entries in the same corner order."""
+    monkeypatch.setenv("LONER_ENC_LIVE_LPB", lpb)
     rng = np.random.default_rng(11)
     S = 512
     d = L.grid_desc(16, 2, 19, 16)

@@ -22,6 +22,6 @@ int main() {
   hipMemcpy(din, h, sizeof(h), hipMemcpyHostToDevice);
   k<<<1, 64>>>(dout, din);
   float o[256]; hipMemcpy(o, dout, sizeof(o), hipMemcpyDeviceToHost);
-  for (int l = 0; l < 64; l += 5) printf("lane %d: %g %g %g %g\n", l, o[4*l], o[4*l+1], o[4*l+2], o[4*l+3]);
+  for (int l = 0; l < 64; l += 1) printf("lane %d: %g %g %g %g\n", l, o[4*l], o[4*l+1], o[4*l+2], o[4*l+3]);
   return 0;
 }
