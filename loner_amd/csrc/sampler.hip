@@ -250,11 +250,23 @@ __device__ __forceinline__ void wave_bitonic_merge(float (&v)[E]) {
 }
 
 #ifndef LNR_SAMPLER_MERGE
-#define LNR_SAMPLER_MERGE 1  // sort the importance draws alone, then merge with the strata (LONER_SAMPLER_MERGE)
+// LONER_SAMPLER_MERGE: 0 the full bitonic sort; 1 the importance draws' bitonic sort + one merge stage with the
+// strata; 2 (default) the draws sorted before the inverse CDF, merged by rank (k_sampler_rank, from 4 depths
+// per lane; 2 per lane fall back to 1)
+#define LNR_SAMPLER_MERGE 2
 #endif
-static bool sampler_merge() {  // read at every launch
+#ifndef LNR_SAMPLER_RANK_MIN_RAYS
+// fewer rays than SIMDs x 2 leave each wave's longer dependency chains exposed (C4 shard of 8, 1152 rays: sampler
+// 0.0233 ms with the bitonic merge, 0.0246 with the rank merge; C2 0.057 -> 0.049, C3 0.174 -> 0.159)
+#define LNR_SAMPLER_RANK_MIN_RAYS 2048
+#endif
+static int64_t sampler_rank_min_rays() {  // LONER_SAMPLER_RANK_MIN_RAYS, read at every launch
+  const char* e = getenv("LONER_SAMPLER_RANK_MIN_RAYS");
+  return e ? atoll(e) : (int64_t)LNR_SAMPLER_RANK_MIN_RAYS;
+}
+static int sampler_merge() {  // read at every launch
   const char* e = getenv("LONER_SAMPLER_MERGE");
-  return e ? atoi(e) != 0 : LNR_SAMPLER_MERGE != 0;
+  return e ? atoi(e) : LNR_SAMPLER_MERGE;
 }
 
 constexpr int kSamplerWaves = 4;
@@ -412,6 +424,270 @@ __global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_wave(SamplerArgs
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// OGM sampler, one wave per ray, the importance draws sorted BEFORE the inverse CDF (LONER_SAMPLER_MERGE=2,
+// the default from 256 samples): the inverse CDF is non-decreasing in u, so sorting the draws u and mapping
+// them in order gives the sorted importance depths, and the draws are uniform on [0, 1), which a counting
+// sort handles in a few passes instead of a bitonic network (k_sampler_wave's 2048-sample sort is 88 % of its
+// VALU work).  Then:
+//  * counting sort of the H draws into 2H buckets (LDS atomics, a wave scan), the few bucket mates put in
+//    order by odd-even transposition passes in registers;
+//  * the inverse CDF per sorted draw, its searchsorted answer walked on from the previous draw's;
+//  * strata and importance depths merged by rank: stratum i goes to i + #{importance depths < it}, depth j
+//    to j + #{strata <= it} (positions unique; equal values are interchangeable);
+//  * if the strata are not ascending (jitter rounding, checked as k_sampler_wave does) or the mapped depths
+//    are not (one rounding at a bin edge can put a depth an ulp above the next bin's first), the same values
+//    go through the full bitonic sort instead.
+// Either way the output is the sorted multiset of k_sampler_wave's values: bit for bit the same depths
+// (test_ogm_sampler_merge_equals_full_sort).  Q = E / 2 >= 2 strata and draws per lane, lane l holding
+// positions [l Q, (l + 1) Q); the per-wave LDS slice is k_sampler_wave's.
+__device__ __forceinline__ int lower_bound_from(const float* arr, int lo, int n, float x) {  // first j >= lo: arr[j] >= x
+  if (lo >= n || !(arr[lo] < x)) return lo;
+  int hi = n;
+  ++lo;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (arr[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+__device__ __forceinline__ int upper_bound_from(const float* arr, int lo, int n, float x) {  // first j >= lo: arr[j] > x
+  if (lo >= n || arr[lo] > x) return lo;
+  int hi = n;
+  ++lo;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (arr[mid] <= x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");
+}
+
+template <int E>
+__global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_rank(SamplerArgs a) {
+  static_assert(E >= 4, "two or more strata per lane");
+  if (a.dev_step) a.key = a.dev_step->key;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int Q = E / 2, H = 32 * E, NBK = 2 * H;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  constexpr int M = H - 2;
+  float* base = reinterpret_cast<float*>(smem) + (size_t)wid * (4 * H);
+  float* strat = base;                                        // [H] strata
+  float* imp = base + H;                                      // [H] bucketed draws, then importance depths
+  float* cdf = base + 2 * H;                                  // [H - 1]
+  float* bins = cdf + H;                                      // [H - 1]
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(base + 2 * H);  // [2H] bucket counters (before the cdf)
+  float* out = base + 2 * H;                                  // [2H] merged depths (after the inverse CDF)
+  for (int64_t r = (int64_t)blockIdx.x * kSamplerWaves + wid; r < a.n_rays; r += (int64_t)gridDim.x * kSamplerWaves) {
+    const float* ry = a.rays + 13 * r;
+    const float near = ry[11], far = ry[12];
+    const float ox = ry[0], oy = ry[1], oz = ry[2], dx = ry[3], dy = ry[4], dz = ry[5];
+    const uint32_t gr = (uint32_t)(a.ray_offset + r);
+    // 1. the draws' counting sort (first, while no stratum is held in registers): bucket counters, ranks within a
+    // bucket, bucket offsets, scatter
+#pragma unroll
+    for (int e = 0; e < E; e += 4) *reinterpret_cast<uint4*>(&cnt[lane * E + e]) = make_uint4(0u, 0u, 0u, 0u);
+    wave_lds_fence();
+    auto bucket = [&](float u) {
+      const uint32_t k = (uint32_t)(u * (float)NBK);
+      return k < (uint32_t)NBK ? k : (uint32_t)NBK - 1u;
+    };
+    float uq[Q];
+    uint32_t rk[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int i = lane * Q + q;
+      uq[q] = a.u_pdf ? a.u_pdf[r * H + i] : rand_uniform(a.key, kStreamPdf, gr, (uint32_t)i);
+      rk[q] = atomicAdd(&cnt[bucket(uq[q])], 1u);
+    }
+    wave_lds_fence();
+    {  // exclusive scan of the counters, this lane's E of them in two passes of 16-byte reads
+      uint32_t run = 0;
+#pragma unroll
+      for (int e = 0; e < E; e += 4) {
+        const uint4 v = *reinterpret_cast<const uint4*>(&cnt[lane * E + e]);
+        run += v.x + v.y + v.z + v.w;
+      }
+      uint32_t ex = wave_incl_scan_u32(run) - run;
+#pragma unroll
+      for (int e = 0; e < E; e += 4) {
+        const uint4 v = *reinterpret_cast<const uint4*>(&cnt[lane * E + e]);
+        const uint4 o = make_uint4(ex, ex + v.x, ex + v.x + v.y, ex + v.x + v.y + v.z);
+        ex += v.x + v.y + v.z + v.w;
+        *reinterpret_cast<uint4*>(&cnt[lane * E + e]) = o;
+      }
+    }
+    wave_lds_fence();
+#pragma unroll
+    for (int q = 0; q < Q; ++q) imp[cnt[bucket(uq[q])] + rk[q]] = uq[q];
+    wave_lds_fence();
+    float su[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) su[q] = imp[lane * Q + q];
+    // bucket mates into order: odd-even transposition passes until the wave's draws ascend
+    while (true) {
+      bool asc = true;
+#pragma unroll
+      for (int q = 0; q + 1 < Q; ++q) asc = asc && !(su[q + 1] < su[q]);
+      const float nf = __shfl_down(su[0], 1, 64);
+      if (lane < 63) asc = asc && !(nf < su[Q - 1]);
+      if (__all(asc)) break;
+#pragma unroll
+      for (int q = 0; q + 1 < Q; q += 2) {
+        const float x = su[q], y = su[q + 1];
+        su[q] = fminf(x, y);
+        su[q + 1] = fmaxf(x, y);
+      }
+#pragma unroll
+      for (int q = 1; q + 1 < Q; q += 2) {
+        const float x = su[q], y = su[q + 1];
+        su[q] = fminf(x, y);
+        su[q + 1] = fmaxf(x, y);
+      }
+      const float pl = __shfl_up(su[Q - 1], 1, 64), nx = __shfl_down(su[0], 1, 64);
+      if (lane < 63) su[Q - 1] = fminf(su[Q - 1], nx);
+      if (lane > 0) su[0] = fmaxf(su[0], pl);
+    }
+    wave_lds_fence();  // (the counters' reads are done: the strata's probabilities overwrite them)
+    // 2. strata and occupancy probabilities (k_sampler_wave step 1-2), computed lane-contiguous (stratum
+    // 64 q + lane: one gather instruction's lanes read neighbouring strata, mostly the same voxels), then
+    // transposed through LDS to this lane's positions [l Q, (l + 1) Q)
+    float* pscr = bins;  // [H] the probabilities in stratum order (free until step 3)
+#pragma unroll 4
+    for (int q = 0; q < Q; ++q) {  // (4 strata's gathers in flight per lane: all Q of them cost E = 32 its occupancy)
+      const int i = q * 64 + lane;
+      const float tt = linspace01(i, H);
+      float z = near * (1.0f - tt) + far * tt;
+      if (a.perturb > 0.f) {
+        const float tl = linspace01(i > 0 ? i - 1 : 0, H), tu = linspace01(i + 1 < H ? i + 1 : H - 1, H);
+        const float zl = near * (1.0f - tl) + far * tl, zu = near * (1.0f - tu) + far * tu;
+        const float upper = (i + 1 < H) ? 0.5f * (z + zu) : z;
+        const float lower = (i > 0) ? 0.5f * (zl + z) : z;
+        const float u = a.u_jitter ? a.u_jitter[r * H + i] : rand_uniform(a.key, kStreamJitter, gr, (uint32_t)i);
+        z = lower + (upper - lower) * (a.perturb * u);
+      }
+      strat[i] = z;
+      const float l = occ_grid_sample(a.occ, a.occ_res, ox + dx * z, oy + dy * z, oz + dz * z);
+      float p = 1.0f / (1.0f + expf(-l));
+      p = 2.0f * (fminf(fmaxf(p, 0.5f), 1.0f) - 0.5f);
+      pscr[i] = p;
+    }
+    wave_lds_fence();
+    float zq[Q], pq[Q];
+    double wl = 0.0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int i = lane * Q + q;
+      zq[q] = strat[i];
+      pq[q] = pscr[i];
+      if (i >= 1 && i <= M) wl += (double)(pq[q] + 1e-5f);
+    }
+    bool strat_sorted = true;
+#pragma unroll
+    for (int q = 0; q + 1 < Q; ++q) strat_sorted = strat_sorted && !(zq[q + 1] < zq[q]);
+    {
+      const float next_first = __shfl_down(zq[0], 1, 64);
+      if (lane < 63) strat_sorted = strat_sorted && !(next_first < zq[Q - 1]);
+    }
+    wave_lds_fence();
+    // 3. sample_pdf's cdf and bins (k_sampler_wave step 3)
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) wl += __shfl_xor(wl, o, 64);
+    const float wtot = (float)wl;
+    double loc = 0.0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int i = lane * Q + q;
+      if (i >= 1 && i <= M) loc += (double)((pq[q] + 1e-5f) / wtot);
+    }
+    double inc = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    double run = inc - loc;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int i = lane * Q + q;
+      if (i >= 1 && i <= M) {
+        run += (double)((pq[q] + 1e-5f) / wtot);
+        cdf[i] = (float)run;
+      }
+    }
+    if (lane == 0) cdf[0] = 0.f;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int i = lane * Q + q;
+      if (i < H - 1) bins[i] = 0.5f * (zq[q] + strat[i + 1]);
+    }
+    wave_lds_fence();
+    // 4. inverse CDF of the sorted draws (searchsorted(cdf, u, right=True) over [0, H - 1])
+    float fq[Q];
+    int lo = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const float u = su[q];
+      if (lo < H - 1 && cdf[lo] <= u) {  // the previous draw's answer no longer holds: search on from it
+        int hi = H - 1;
+        ++lo;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (cdf[mid] <= u) lo = mid + 1;
+          else hi = mid;
+        }
+      }
+      const int below = lo - 1 > 0 ? lo - 1 : 0;
+      const int above = lo < M ? lo : M;
+      const float c0 = cdf[below], c1 = cdf[above];
+      const float b0 = bins[below], b1 = bins[above];
+      float denom = c1 - c0;
+      if (denom < 1e-5f) denom = 1.0f;
+      fq[q] = b0 + (u - c0) / denom * (b1 - b0);
+    }
+    bool f_asc = true;
+#pragma unroll
+    for (int q = 0; q + 1 < Q; ++q) f_asc = f_asc && !(fq[q + 1] < fq[q]);
+    {
+      const float nf = __shfl_down(fq[0], 1, 64);
+      if (lane < 63) f_asc = f_asc && !(nf < fq[Q - 1]);
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) imp[lane * Q + q] = fq[q];
+    wave_lds_fence();
+    float* zr = a.z + r * (int64_t)(2 * H);
+    if (__all(strat_sorted && f_asc)) {
+      // 5. merge by rank into out, then coalesced stores
+      // (out overlays the cdf and bins, whose reads ended before the fence above)
+      int js = 0, jt = 0;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        js = lower_bound_from(imp, js, H, zq[q]);
+        out[lane * Q + q + js] = zq[q];
+        jt = upper_bound_from(strat, jt, H, fq[q]);
+        out[lane * Q + q + jt] = fq[q];
+      }
+      wave_lds_fence();
+#pragma unroll
+      for (int e = 0; e < E; ++e) zr[e * 64 + lane] = out[e * 64 + lane];
+    } else {
+      // the full bitonic sort of the same values (strata in strat, depths in imp: one contiguous buffer)
+      float v[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) v[e] = base[lane * E + e];
+      wave_bitonic_sort<E>(v);
+#pragma unroll
+      for (int e = 0; e < E; ++e) zr[lane * E + e] = v[e];
+    }
+    wave_lds_fence();  // this wave's slice is rewritten by its next ray
+  }
+}
+
 static size_t sampler_wave_smem(int E, int H) { return (size_t)kSamplerWaves * (64 * E + 2 * H) * 4; }
 
 static size_t sampler_smem(int H, int P2) { return ((size_t)3 * H + P2 + 2) * 4 + (SNT / 64 + 2) * 8 + 16; }
@@ -441,10 +717,20 @@ extern "C" int lnr_sample_ogm(const float* rays, int64_t n_rays, int32_t n_sampl
   LNR_REQUIRE(a.H <= 8 * SNT, "lnr_sample_ogm: too many samples");
   if (a.H % 64 == 0 && p2 >= 128 && p2 <= 2048) {  // one wave per ray
     const int E = p2 / 64;
-    const bool merge = sampler_merge();
+    const int mode = sampler_merge();
+    const bool merge = mode != 0;
     const int64_t nbw = (n_rays + kSamplerWaves - 1) / kSamplerWaves;
     const dim3 g((unsigned)(nbw < 8192 ? nbw : 8192)), b(64 * kSamplerWaves);
     const size_t sm = sampler_wave_smem(E, a.H);
+    if (mode == 2 && E >= 4 && 2 * a.H == 64 * E && n_rays >= sampler_rank_min_rays()) {
+      switch (E) {
+        case 4: hipLaunchKernelGGL(k_sampler_rank<4>, g, b, sm, as_stream(stream), a); break;
+        case 8: hipLaunchKernelGGL(k_sampler_rank<8>, g, b, sm, as_stream(stream), a); break;
+        case 16: hipLaunchKernelGGL(k_sampler_rank<16>, g, b, sm, as_stream(stream), a); break;
+        default: hipLaunchKernelGGL(k_sampler_rank<32>, g, b, sm, as_stream(stream), a); break;
+      }
+      LNR_RETURN_LAUNCH("lnr_sample_ogm");
+    }
     switch (E) {
       case 2: hipLaunchKernelGGL((merge ? k_sampler_wave<2, true> : k_sampler_wave<2, false>), g, b, sm, as_stream(stream), a); break;
       case 4: hipLaunchKernelGGL((merge ? k_sampler_wave<4, true> : k_sampler_wave<4, false>), g, b, sm, as_stream(stream), a); break;

@@ -377,7 +377,8 @@ def test_ogm_sampler_inkernel_rng_matches_oracle(L):
 @pytest.mark.parametrize("perturb", [1.0, 0.0])
 def test_ogm_sampler_merge_equals_full_sort(L, S, perturb, monkeypatch):
     """The one-wave sampler's sort of the importance draws alone + one bitonic merge with the (checked
-    ascending) strata (LONER_SAMPLER_MERGE=1) gives the full bitonic sort's depths bit for bit, for
+    ascending) strata (LONER_SAMPLER_MERGE=1), and the draws sorted before the inverse CDF and merged by rank
+    (LONER_SAMPLER_MERGE=2, k_sampler_rank, from 256 samples), give the full bitonic sort's depths bit for bit, for
     training (jittered strata) and eval (perturb 0) draws, 2 to 32 values per lane; rays whose strata
     rounding would cross fall back to the full sort."""
     g = np.load("tests/golden/samplers.npz")
@@ -386,15 +387,17 @@ def test_ogm_sampler_merge_equals_full_sort(L, S, perturb, monkeypatch):
     rays = np.concatenate([rays] * 4)
     R = rays.shape[0]
     rays[:, 11] = rng.uniform(0.0, 0.05, R)  # a spread of near / far bounds
+    monkeypatch.setenv("LONER_SAMPLER_RANK_MIN_RAYS", "0")  # (the rank path at this test's ray count too)
     outs = []
-    for m in ("0", "1"):
+    for m in ("0", "1", "2"):
         monkeypatch.setenv("LONER_SAMPLER_MERGE", m)
         z = torch.empty(R, S, dtype=torch.float32, device="cuda")
         L.call("lnr_sample_ogm", cu(rays), R, S, cu(occ), 100, perturb, None, None, orng.step_key(5, 2), 0, z, None,
                L.stream())
         outs.append(host(z).copy())
     np.testing.assert_array_equal(outs[0], outs[1])
-    assert np.all(np.diff(outs[1], axis=1) >= 0)
+    np.testing.assert_array_equal(outs[0], outs[2])
+    assert np.all(np.diff(outs[2], axis=1) >= 0)
 
 
 # ------------------------------------------------------------------ compositing + loss
