@@ -256,9 +256,9 @@ __device__ __forceinline__ void wave_bitonic_merge(float (&v)[E]) {
 #define LNR_SAMPLER_MERGE 2
 #endif
 #ifndef LNR_SAMPLER_RANK_MIN_RAYS
-// fewer rays than SIMDs x 2 leave each wave's longer dependency chains exposed (C4 shard of 8, 1152 rays: sampler
-// 0.0233 ms with the bitonic merge, 0.0246 with the rank merge; C2 0.057 -> 0.049, C3 0.174 -> 0.159)
-#define LNR_SAMPLER_RANK_MIN_RAYS 2048
+// fewest rays for the rank merge (smaller launches take the bitonic merge).  With both forms' occupancy lookups
+// lane-contiguous: C4 shard of 8 (1152 rays) 0.0246 ms either way, C2 0.053 -> 0.049, C3 0.178 -> 0.160
+#define LNR_SAMPLER_RANK_MIN_RAYS 0
 #endif
 static int64_t sampler_rank_min_rays() {  // LONER_SAMPLER_RANK_MIN_RAYS, read at every launch
   const char* e = getenv("LONER_SAMPLER_RANK_MIN_RAYS");
@@ -287,13 +287,11 @@ __global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_wave(SamplerArgs
     const float near = ry[11], far = ry[12];
     const float ox = ry[0], oy = ry[1], oz = ry[2], dx = ry[3], dy = ry[4], dz = ry[5];
     const uint32_t gr = (uint32_t)(a.ray_offset + r);
-    // 1. linspace + jitter (ray_sampling.py:59-72); neighbours recomputed, not exchanged
-    float zq[QMAX], pq[QMAX];
-    double wl = 0.0;
-#pragma unroll
-    for (int q = 0; q < QMAX; ++q) {
-      if (q >= Q) break;
-      const int i = lane * Q + q;
+    // 1. linspace + jitter (ray_sampling.py:59-72); neighbours recomputed, not exchanged.  Computed
+    // lane-contiguous (stratum 64 q + lane: one gather instruction's lanes read neighbouring strata, mostly the
+    // same voxels), then transposed through LDS (bins: free until step 3) to this lane's range [l Q, (l + 1) Q)
+    for (int q = 0; q < Q; ++q) {
+      const int i = q * 64 + lane;
       const float tt = linspace01(i, H);
       float z = near * (1.0f - tt) + far * tt;
       if (a.perturb > 0.f) {
@@ -304,15 +302,27 @@ __global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_wave(SamplerArgs
         const float u = a.u_jitter ? a.u_jitter[r * H + i] : rand_uniform(a.key, kStreamJitter, gr, (uint32_t)i);
         z = lower + (upper - lower) * (a.perturb * u);
       }
-      zq[q] = z;
       buf[i] = z;
       // 2. occupancy probability (ray_sampling.py:74-81)
       const float l = occ_grid_sample(a.occ, a.occ_res, ox + dx * z, oy + dy * z, oz + dz * z);
       float p = 1.0f / (1.0f + expf(-l));
       p = 2.0f * (fminf(fmaxf(p, 0.5f), 1.0f) - 0.5f);
-      pq[q] = p;
-      if (i >= 1 && i <= M) wl += (double)(p + 1e-5f);  // weights = prob[1:-1] + eps
+      bins[i] = p;
     }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");
+    float zq[QMAX], pq[QMAX];
+    double wl = 0.0;
+#pragma unroll
+    for (int q = 0; q < QMAX; ++q) {
+      if (q >= Q) break;
+      const int i = lane * Q + q;
+      zq[q] = buf[i];
+      pq[q] = bins[i];
+      if (i >= 1 && i <= M) wl += (double)(pq[q] + 1e-5f);  // weights = prob[1:-1] + eps
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");  // (bins is rewritten in step 3)
     // 3. sample_pdf (rendering_tcnn.py:19-68): wtot, cdf = cumsum(pdf) in double
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) wl += __shfl_xor(wl, o, 64);

@@ -1,6 +1,6 @@
-"""Time lnr_sample_ogm alone (GPU box) on a C2-like (8192 rays x 512) and a C3-like (4096 rays x 2048, no
-jitter) batch, with HIP events over repeated launches, and print a digest of the sorted depths so variants
-can be checked bit for bit:
+"""Time lnr_sample_ogm alone (GPU box) on a C2-like (8192 rays x 512), a C3-like (4096 rays x 2048, no
+jitter) and a C4-shard-like (1152 rays x 512) batch, with HIP events over repeated launches, and print a
+digest of the sorted depths so variants can be checked bit for bit:
     LONER_AMD_LIB=<lib> python tools/sampler_time.py [--reps 50]
 """
 import argparse
@@ -30,7 +30,7 @@ def main():
         r = rng.integers(2, 6)
         g[c[0] - r:c[0] + r, c[1] - r:c[1] + r, c[2] - r:c[2] + r] = rng.uniform(1, 8)
     occ = torch.from_numpy(g).to(dev)
-    for name, R, S, perturb in (("C2-like", 8192, 512, 1.0), ("C3-like", 4096, 2048, 0.0)):
+    for name, R, S, perturb in (("C2-like", 8192, 512, 1.0), ("C3-like", 4096, 2048, 0.0), ("C4s8-like", 1152, 512, 1.0)):
         rays = np.zeros((R, 13), np.float32)
         o = rng.uniform(-0.3, 0.3, (R, 3))
         d = rng.normal(0, 1, (R, 3))
