@@ -409,6 +409,13 @@ __device__ __forceinline__ void reduce_slabs_fixed(const float* __restrict__ sla
   float s = 0.f;
   if (i < LNR_SIGMA_MLP_PARAMS) {
     int b = b0;
+    for (; b + 32 <= b1; b += 32) {  // 32 rows in flight (a wave's whole range at 512 slabs: one load latency)
+      float v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) v[u] = slab[(int64_t)(b + u) * LNR_SIGMA_MLP_PARAMS + i];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) s += v[u];
+    }
     for (; b + 8 <= b1; b += 8) {  // 8 rows in flight
       float v[8];
 #pragma unroll

@@ -477,8 +477,17 @@ __global__ void __launch_bounds__(64 * kSlabWaves) k_rgb_reduce_slabs(const floa
   const int per = (nb + kSlabWaves - 1) / kSlabWaves;
   const int b0 = wid * per, b1 = b0 + per < nb ? b0 + per : nb;
   float s = 0.f;
-  if (i < P)
-    for (int b = b0; b < b1; ++b) s += slab[(int64_t)b * P + i];
+  if (i < P) {
+    int b = b0;
+    for (; b + 16 <= b1; b += 16) {  // 16 rows in flight, added in order
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = slab[(int64_t)(b + u) * P + i];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += v[u];
+    }
+    for (; b < b1; ++b) s += slab[(int64_t)b * P + i];
+  }
   part[wid][lane] = s;
   __syncthreads();
   if (wid == 0 && i < P) {
