@@ -119,9 +119,11 @@ int lnr_hashgrid_fwd_rays(const lnr_grid_desc* d, const float* rays, const float
                           int32_t n_samples, const uint16_t* table, uint32_t* enc, int64_t enc_stride,
                           void* bwd_ws, int64_t bwd_ws_bytes, void* stream);
 /* Forward of samples whose compositing weight can be zero (the colour head: rgb = sum w_i c_i + ...,
- * rendering_tcnn.py:286): samples with live[n] == 0 (exactly) get a zero encoding and issue no
- * gathers, every other sample is encoded exactly as lnr_hashgrid_fwd_rays does.  live = the (R,S)
- * weights of the sigma pass.  No backward histogram. */
+ * rendering_tcnn.py:286): samples with live[n] == 0 (exactly) issue no gathers, every other sample is
+ * encoded exactly as lnr_hashgrid_fwd_rays does.  A dead sample gets a zero encoding when its aligned
+ * 16-sample tile (n / 16) holds a live sample; the encodings of a tile with no live sample are left
+ * unwritten (lnr_rgb_render and lnr_rgb_train skip such tiles).  live = the (R,S) weights of the sigma
+ * pass.  No backward histogram. */
 int lnr_hashgrid_fwd_rays_live(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
                                int32_t n_samples, const uint16_t* table, const float* live, uint32_t* enc,
                                int64_t enc_stride, void* stream);

@@ -149,6 +149,15 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
     x[h] = y[h] = z[h] = 0.f;
     pos.wave(i, n, in[h], x[h], y[h], z[h]);
   }
+  // dead samples (live, use = false) get a zero encoding only where their aligned 16-sample tile holds a live
+  // sample: the colour kernels skip a tile whose weights are all 0 and read every encoding of the others
+  // (lnr_hashgrid_fwd_rays_live's contract, include/loner_amd.h)
+  bool zero[kEncSpt];
+#pragma unroll
+  for (int h = 0; h < kEncSpt; ++h) {
+    const unsigned long long lv = __ballot(use[h]);
+    zero[h] = in[h] && ((lv >> (threadIdx.x & 48)) & 0xFFFFull) != 0ull;
+  }
   // LPB levels per workgroup, y, y + L/LPB, y + 2 L/LPB, ... (grid.y = L / LPB), in level order: the
   // sample's position is decoded and its depth loaded once for them, and a coherent level's VALU-heavy
   // work runs beside a fine level's gathers (head comment)
@@ -186,7 +195,7 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
           f1 = fmaf(w, t.y, f1);
         }
         store_enc(dst, (uint32_t)f2h(f0) | ((uint32_t)f2h(f1) << 16));
-      } else if (in[h]) {
+      } else if (zero[h]) {
         *dst = 0u;
       }
     }
@@ -226,7 +235,7 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
           f1 = fmaf(c.w[k], t.y, f1);
         }
         store_enc(dst, (uint32_t)f2h(f0) | ((uint32_t)f2h(f1) << 16));
-      } else if (in[h]) {
+      } else if (zero[h]) {
         *dst = 0u;
       }
     } else if (use[h]) {
@@ -241,7 +250,7 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
         f1 = fmaf(c.w[k], t.y, f1);
       }
       store_enc(dst, (uint32_t)f2h(f0) | ((uint32_t)f2h(f1) << 16));
-    } else if (in[h]) {
+    } else if (zero[h]) {
       *dst = 0u;
     }
     if (count) {

@@ -112,8 +112,9 @@ def test_hashgrid_fwd_table_offset_and_ragged_rows(L, count, n):
 def test_hashgrid_fwd_live_mask_matches_full_encode(L, R, lpb, monkeypatch):
     """The live-masked eval encode (plain gathers, dead samples issue none; two samples per thread
     from 2^18 samples, or with LONER_ENC_LIVE_LPB=2 one sample per thread over two strided levels per
-    workgroup) equals the full encode (lane-paired gathers) on live samples and is 0 on dead ones, bit
-    for bit: the same entries in the same corner order."""
+    workgroup) equals the full encode (lane-paired gathers) on live samples and is 0 on dead ones whose
+    16-sample tile holds a live sample, bit for bit: the same entries in the same corner order.  A tile
+    with no live sample is left unwritten."""
     monkeypatch.setenv("LONER_ENC_LIVE_LPB", lpb)
     rng = np.random.default_rng(11)
     S = 512
@@ -126,14 +127,20 @@ def test_hashgrid_fwd_live_mask_matches_full_encode(L, R, lpb, monkeypatch):
     rays[:, 0:3], rays[:, 3:6] = o, dr
     z = np.sort(rng.uniform(0.0, 0.45, (R, S)), 1).astype(np.float32)
     live = (rng.uniform(0, 1, (R, S)) < 0.3).astype(np.float32)
+    live.reshape(-1, 16)[rng.uniform(0, 1, R * S // 16) < 0.3] = 0.0  # whole dead tiles too
     table = cu(rng.uniform(-1, 1, (lay.n_entries, 2)).astype(np.float16).view(np.int16))
     full = torch.empty(16, R * S, dtype=torch.int32, device="cuda")
     part = torch.full((16, R * S), -1, dtype=torch.int32, device="cuda")
     L.call("lnr_hashgrid_fwd_rays", ctypes.byref(d), cu(rays), cu(z), R, S, table, full, R * S, None, 0, L.stream())
     L.call("lnr_hashgrid_fwd_rays_live", ctypes.byref(d), cu(rays), cu(z), R, S, table, cu(live), part, R * S,
            L.stream())
-    mask = torch.from_numpy(live.reshape(1, -1) != 0).cuda()
-    assert torch.equal(part, torch.where(mask, full, torch.zeros_like(full)))
+    alive = live.reshape(-1) != 0
+    tile_live = np.repeat(alive.reshape(-1, 16).any(axis=1), 16)
+    mask = torch.from_numpy(alive.reshape(1, -1)).cuda()
+    want = torch.where(mask, full, torch.zeros_like(full))
+    want[:, torch.from_numpy(~tile_live).cuda()] = -1  # unwritten
+    assert tile_live.sum() < alive.size  # (the case is exercised)
+    assert torch.equal(part, want)
 
 
 @pytest.mark.parametrize("S", [512, 64, 40])
