@@ -19,6 +19,7 @@ colour encode (which also counts the backward's records), ``lnr_rgb_train`` (col
 gradient, MLP backward on MFMA, d_enc), the colour hash-grid backward and Adam.  No host sync.
 """
 import math
+import os
 
 import torch
 
@@ -195,7 +196,7 @@ class CameraStepEngine:
     """One colour-head optimiser iteration on preallocated workspaces for up to ``n_rays`` rays."""
 
     def __init__(self, field, color: ColorState, n_rays, n_samples=512, perturb=1.0, raw_noise_std=1.0,
-                 lr=0.01, gamma=1.0, seed=0, allreduce=None, ray_offset=0, skip_zero=False):
+                 lr=0.01, gamma=1.0, seed=0, allreduce=None, ray_offset=0, skip_zero=None):
         if n_samples % 64:
             raise ValueError(f"n_samples={n_samples} must be a multiple of 64")
         self.field, self.color = field, color
@@ -203,7 +204,8 @@ class CameraStepEngine:
         self.perturb, self.noise_std = float(perturb), float(raw_noise_std)
         self.lr, self.gamma, self.seed = float(lr), float(gamma), int(seed)
         self.allreduce, self.ray_offset = allreduce, int(ray_offset)
-        self.skip_zero = bool(skip_zero)
+        # (None: LONER_CAM_SKIP_ZERO, default on)
+        self.skip_zero = (os.environ.get("LONER_CAM_SKIP_ZERO", "1") == "1") if skip_zero is None else bool(skip_zero)
         self.iteration = 0
         dev = field.device
         N = self.R * self.S
@@ -248,9 +250,10 @@ class CameraStepEngine:
         L.call("lnr_field_render", fs.mlp_f16, self.enc, N, rays, self.z, R, S, 0, self.noise_std, None, key,
                self.ray_offset, self.depth, self.opacity, None, self.weights, s)
         # skip_zero: samples of weight exactly 0 have no colour gradient (dL/dc_i = w_i dL/drgb): no
-        # gathers for them, and the backward counts (its own pass) and scatters only non-zero d_enc.
-        # Measured at CAM (half the samples of weight 0): encode 0.34 -> 0.21 ms but the backward
-        # 0.90 -> 0.99 ms (the counting pass; scatter and accumulate barely shrink), so it is off by default.
+        # gathers for them (nor zero stores in tiles without a live sample), and the backward counts (its
+        # own pass) and scatters only non-zero d_enc.  Round 4 measured it slower at CAM (encode 0.34 ->
+        # 0.21 ms, backward 0.90 -> 0.99 ms); with round 5's kernels the encode drops 0.285 -> 0.19 ms and
+        # the backward stays 0.452-0.458 -> 0.456-0.463: CAM 1.806 -> 1.708 ms.  On by default.
         if self.skip_zero:
             L.call("lnr_hashgrid_fwd_rays_live", L.ctypes.byref(cs.desc), rays, self.z, R, S, cs.table_f16,
                    self.weights, self.enc_rgb, N, s)

@@ -222,10 +222,12 @@ def test_camera_two_shards_match_single_batch(L):
 
 
 def test_camera_skip_zero_matches_default(L):
-    """CameraStepEngine(skip_zero=True) (zero-weight samples: no colour gathers, backward counts only
-    non-zero d_enc) gives the default path's gradient: the skipped samples contribute exactly 0."""
+    """CameraStepEngine(skip_zero=True, the default) (zero-weight samples: no colour gathers, backward counts
+    only non-zero d_enc) gives the full path's gradient: the skipped samples contribute exactly 0 (the table
+    gradient to the fixed-point rounding of the smaller buckets)."""
     from loner_amd import camera as C
-    fr, cs_a, eng_a = _camera_setup()
+    fr, cs_a, eng_def = _camera_setup()
+    eng_a = C.CameraStepEngine(eng_def.field, cs_a, n_rays=eng_def.R, n_samples=128, lr=0.01, seed=0, skip_zero=False)
     _, cs_b, eng_ref = _camera_setup()
     eng_b = C.CameraStepEngine(eng_ref.field, cs_b, n_rays=eng_ref.R, n_samples=128, lr=0.01, seed=0, skip_zero=True)
     R = fr.n_rays(1)
