@@ -30,14 +30,30 @@ typedef uint32_t u32x2v_t __attribute__((ext_vector_type(2)));
 constexpr int kBw2Waves = kRgbBwd2Waves;
 constexpr int kBw2Cols = 16 * kBw2Waves;  // samples per workgroup iteration
 
-// [sample][64 halves] rows of 16 8-byte chunks: chunk ch of row r at this dword (conflict-free transposed
-// reads of 8 consecutive rows x 4 chunks: row pairs land in distinct 4-chunk groups)
-__device__ __forceinline__ uint32_t sw64(uint32_t r, uint32_t ch) { return 32u * r + 2u * (ch ^ (((r >> 1) & 3u) << 2)); }
+// Rows of 16 8-byte chunks (64 halves): chunk ch of row r at dword 32 r + 2 (ch ^ f(r)).  The swizzles are chosen
+// per image for every access the kernel makes to it, by the banking rules of MI355X_MICROARCH.md's LDS table (stores:
+// (a/4) mod 32 in 16-lane groups for b64, 8-lane groups for b128; b64 and transposed reads: mod 64 in 32-lane
+// halves; b128 reads: mod 64 in four 16-lane groups); an image read or written 16 bytes at a time keeps f even, so
+// a chunk pair stays adjacent and in order:
+//  * the per-tile images X_l, dY_l ([sample][neuron], 8-byte accesses only): f = bits (r2, r1, r3, r0) of r as chunk
+//    bits 3..0.  A store instruction's 16 rows (one chunk each) meet 16 distinct positions, a transposed read's
+//    rows 16 s + 4 g + q (g = 0, 1 or 2, 3) x 4 chunks and a b64 row read's 16 rows x 2 chunks 64 distinct banks;
+//  * the weight images W_0, W_l: f = 4 ((r >> 1) mod 4), conflict-free for the forward's 16-byte row reads and
+//    W_0's transposed reads; W_l's (wperm-ordered) transposed reads keep a 2-way conflict on half their groups,
+//    which no single-bit-per-position swizzle with an even f removes.
+// The first layout (that f for every image) spent 42 % of the LDS cycles on bank conflicts (profiles/r05_pmc_CAM.txt),
+// mostly the 4-way conflicting stores of the per-tile images.  (tools/lds_banks_rgb.py counts every access.)
+__device__ __forceinline__ uint32_t swt(uint32_t r, uint32_t ch) {
+  const uint32_t f = (((r >> 1) & 3u) << 2) | (((r >> 3) & 1u) << 1) | (r & 1u);
+  return 32u * r + 2u * (ch ^ f);
+}
+__device__ __forceinline__ uint32_t sww(uint32_t r, uint32_t ch) { return 32u * r + 2u * (ch ^ (((r >> 1) & 3u) << 2)); }
 // W_l images: logical in-chunk lc = in / 4 = 8s + 4h + g stored at chunk 8s + 2g + h, so the forward's
 // hid_perm(s, g, .) operand is one 16-byte row read; the transposed read's 4 consecutive in-indices stay one chunk
 __device__ __forceinline__ uint32_t wperm(uint32_t lc) { return 8u * (lc >> 3) + 2u * (lc & 3u) + ((lc >> 2) & 1u); }
-// [sample][32 halves] rows of 8 chunks
-__device__ __forceinline__ uint32_t sw32(uint32_t r, uint32_t ch) { return 16u * r + 2u * (ch ^ (((r >> 2) & 1u) << 2)); }
+// [sample][32 halves] rows of 8 chunks (X_0): f = 2 ((r >> 1) mod 4), conflict-free for the 16-byte stores and the
+// transposed reads
+__device__ __forceinline__ uint32_t sw32(uint32_t r, uint32_t ch) { return 16u * r + 2u * (ch ^ (((r >> 1) & 3u) << 1)); }
 
 template <int NH>
 struct Bw2Buf {
@@ -115,13 +131,13 @@ __device__ __forceinline__ void bw2_owner(const Bw2Buf<NH>& B, int l, const uint
     const uint32_t r = 16u * sw + 4u * g + tq;  // the transposed read's row (sample) for this lane
     const _Float16 f = (_Float16)(run * iv[sw]);  // run / s_sw = 2^-k, k >= 0
     const half4_t fv = {f, f, f, f};
-    const half4_t ya = lds_tr16(&B.dy[l][sw64(r, 4u * rt + tp)]) * fv;
+    const half4_t ya = lds_tr16(&B.dy[l][swt(r, 4u * rt + tp)]) * fv;
 #pragma unroll
     for (int m = 0; m < CT; ++m) {
       const uint32_t ct = (uint32_t)ct0 + m;
       half4_t xb;
       if (xi != nullptr) {
-        xb = lds_tr16(&xi[sw64(r, 4u * ct + tp)]);
+        xb = lds_tr16(&xi[swt(r, 4u * ct + tp)]);
       } else if (ct < 2) {
         xb = lds_tr16(&B.x0[sw32(r, 4u * ct + tp)]);
       } else {
@@ -160,12 +176,12 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
   for (int i = threadIdx.x; i < NH * 64 * 16; i += 64 * kBw2Waves) {  // W_l images, 8-byte chunks
     const int l = i >> 10, r = (i >> 4) & 63, ch = i & 15;
     const uint16_t* src = a.w + rgb_layer_offset<NH>(l + 1) + r * kRgbWidth + 4 * ch;
-    lds_st64(&sm.wt[l][sw64(r, wperm(ch))], (uint32_t)src[0] | ((uint32_t)src[1] << 16), (uint32_t)src[2] | ((uint32_t)src[3] << 16));
+    lds_st64(&sm.wt[l][sww(r, wperm(ch))], (uint32_t)src[0] | ((uint32_t)src[1] << 16), (uint32_t)src[2] | ((uint32_t)src[3] << 16));
   }
   for (int i = threadIdx.x; i < 64 * 16; i += 64 * kBw2Waves) {  // W_0 image, natural order, zero columns 48..63
     const int r = i >> 4, ch = i & 15;
     const uint16_t* src = a.w + r * kRgbIn + 4 * ch;
-    lds_st64(&sm.w0[sw64(r, ch)], ch < 12 ? (uint32_t)src[0] | ((uint32_t)src[1] << 16) : 0u,
+    lds_st64(&sm.w0[sww(r, ch)], ch < 12 ? (uint32_t)src[0] | ((uint32_t)src[1] << 16) : 0u,
              ch < 12 ? (uint32_t)src[2] | ((uint32_t)src[3] << 16) : 0u);
   }
   // ---- weight-gradient accumulators: rows 16 (wid / 2) .. of W_0 (column tiles 0, 1 or 2) and of each W_l
@@ -263,8 +279,8 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
 #pragma unroll
           for (int t = 0; t < 4; ++t) {  // W_0[16t + c][8g + j] and [32 + 8g + j] (SH; zero columns for g >= 2)
             const uint32_t r0 = 16u * t + c;
-            const half8_t a0 = __builtin_bit_cast(half8_t, *reinterpret_cast<const u32x4v_t*>(__builtin_assume_aligned(&sm.w0[sw64(r0, 2u * g)], 16)));
-            const half8_t as = __builtin_bit_cast(half8_t, *reinterpret_cast<const u32x4v_t*>(__builtin_assume_aligned(&sm.w0[sw64(r0, 8u + 2u * g)], 16)));
+            const half8_t a0 = __builtin_bit_cast(half8_t, *reinterpret_cast<const u32x4v_t*>(__builtin_assume_aligned(&sm.w0[sww(r0, 2u * g)], 16)));
+            const half8_t as = __builtin_bit_cast(half8_t, *reinterpret_cast<const u32x4v_t*>(__builtin_assume_aligned(&sm.w0[sww(r0, 8u + 2u * g)], 16)));
             ac[t] = float4_t{0.f, 0.f, 0.f, 0.f};
             ac[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, benc, ac[t], 0, 0, 0);
             ac[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as, bsh, ac[t], 0, 0, 0);
@@ -275,7 +291,7 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
 #pragma unroll
         for (int l = 0; l < NH; ++l) {
 #pragma unroll
-          for (int t = 0; t < 4; ++t) lds_st64(&B.h[l][sw64(row, 4u * t + g)], hp[2 * t], hp[2 * t + 1]);
+          for (int t = 0; t < 4; ++t) lds_st64(&B.h[l][swt(row, 4u * t + g)], hp[2 * t], hp[2 * t + 1]);
           const half8_t b0 = pk_operand(hp, 0), b1 = pk_operand(hp, 1);
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
@@ -283,7 +299,7 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2)  // W_{l+1}[out 16t + c][k = in hid_perm(s2, g, j)]: one 16-byte row read
               w[s2] = __builtin_bit_cast(half8_t, *reinterpret_cast<const u32x4v_t*>(
-                                                      __builtin_assume_aligned(&sm.wt[l][sw64(16u * t + c, 8u * s2 + 2u * g)], 16)));
+                                                      __builtin_assume_aligned(&sm.wt[l][sww(16u * t + c, 8u * s2 + 2u * g)], 16)));
             float4_t ac = {0.f, 0.f, 0.f, 0.f};
             ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(w[0], b0, ac, 0, 0, 0);
             ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(w[1], b1, ac, 0, 0, 0);
@@ -307,7 +323,7 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
            // scaled dO are staged in this wave's own rows of dy[NH] and dy[0], which its backward overwrites below
           uint32_t* hs = B.dy[NH];
 #pragma unroll
-          for (int t = 0; t < 4; ++t) lds_st64(&hs[sw64(row, 4u * t + g)], hp[2 * t], hp[2 * t + 1]);
+          for (int t = 0; t < 4; ++t) lds_st64(&hs[swt(row, 4u * t + g)], hp[2 * t], hp[2 * t + 1]);
           // [3 channels][16 samples] in this wave's rows of dy[0] (of the otherwise unused h image when NH = 0,
           // where dy[0] is dy[NH])
           _Float16* ds = reinterpret_cast<_Float16*>(NH > 0 ? &B.dy[0][512u * wid] : &B.h[0][512u * wid]);
@@ -330,7 +346,7 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
           const uint32_t rr = 16u * wid + 4u * g + tq;
 #pragma unroll
           for (int m = 0; m < 4; ++m)
-            acco[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(ya, lds_tr16(&hs[sw64(rr, 4u * m + tp)]), acco[m], 0, 0, 0);
+            acco[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(ya, lds_tr16(&hs[swt(rr, 4u * m + tp)]), acco[m], 0, 0, 0);
         }
         half8_t bo = {};
 #pragma unroll
@@ -350,10 +366,10 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
           const uint32_t* hl = l == NH ? B.dy[NH] : B.h[l < NH ? l : 0];  // H_l, this wave's rows (the mask)
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
-            const u32x2v_t hv = *reinterpret_cast<const u32x2v_t*>(__builtin_assume_aligned(&hl[sw64(row, 4u * t + g)], 8));
+            const u32x2v_t hv = *reinterpret_cast<const u32x2v_t*>(__builtin_assume_aligned(&hl[swt(row, 4u * t + g)], 8));
             dp[2 * t] = pk_scaled(ac[t][0], ac[t][1], k2) & pk_nonzero_mask(hv.x);
             dp[2 * t + 1] = pk_scaled(ac[t][2], ac[t][3], k2) & pk_nonzero_mask(hv.y);
-            lds_st64(&B.dy[l][sw64(row, 4u * t + g)], dp[2 * t], dp[2 * t + 1]);
+            lds_st64(&B.dy[l][swt(row, 4u * t + g)], dp[2 * t], dp[2 * t + 1]);
           }
           if (lane == 0) B.inv[wid][l] = __builtin_amdgcn_rcpf(scale);  // exact: scale is a power of two
           if (l == 0) break;
@@ -363,8 +379,8 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
             half8_t w[2];
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {  // W_l^T [in 16t + i][k = out hid_perm(s2, g, j)]
-              const half4_t lo = lds_tr16(&sm.wt[l - 1][sw64(32u * s2 + 4u * g + tq, wperm(4u * t + tp))]);
-              const half4_t hi = lds_tr16(&sm.wt[l - 1][sw64(32u * s2 + 16u + 4u * g + tq, wperm(4u * t + tp))]);
+              const half4_t lo = lds_tr16(&sm.wt[l - 1][sww(32u * s2 + 4u * g + tq, wperm(4u * t + tp))]);
+              const half4_t hi = lds_tr16(&sm.wt[l - 1][sww(32u * s2 + 16u + 4u * g + tq, wperm(4u * t + tp))]);
               w[s2] = half8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
             }
             ac[t] = float4_t{0.f, 0.f, 0.f, 0.f};
@@ -380,8 +396,8 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
           half8_t w[2];
 #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2) {  // W_0^T [in 16m + i][k = hid hid_perm(s2, g, j)]
-            const half4_t lo = lds_tr16(&sm.w0[sw64(32u * s2 + 4u * g + tq, 4u * m + tp)]);
-            const half4_t hi = lds_tr16(&sm.w0[sw64(32u * s2 + 16u + 4u * g + tq, 4u * m + tp)]);
+            const half4_t lo = lds_tr16(&sm.w0[sww(32u * s2 + 4u * g + tq, 4u * m + tp)]);
+            const half4_t hi = lds_tr16(&sm.w0[sww(32u * s2 + 16u + 4u * g + tq, 4u * m + tp)]);
             w[s2] = half8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           }
           float4_t e = {0.f, 0.f, 0.f, 0.f};
