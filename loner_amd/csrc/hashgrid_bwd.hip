@@ -482,13 +482,22 @@ constexpr int rows_waves() {
 #ifndef LNR_ROWS_NB128
 #define LNR_ROWS_NB128 1  // the level-looped scatter for grids with up to 128 chunks per level too
 #endif
+#ifndef LNR_ROWS_SOA
+#define LNR_ROWS_SOA 1
+#endif
 template <int NL, int NB, int STG>
 struct RowsLds {  // the small tables first: their addresses fit the 16-bit LDS instruction offset
   uint2 sg[NL][NB];           // per level and bucket: {start in the stage, global slot of the run}
   uint32_t total[NL];         // records of the row at each level
   uint32_t ctr[2][NB];        // rank counters
   LevelParams lv[NL];         // the level table (kernel arguments indexed per level would be loads)
+#if LNR_ROWS_SOA
+  // staged records in bucket order, one array per field: a record's three stores go to bank slot mod 32 each
+  // (with 16-byte records a store's 32 lanes, at random slots, met only 8 banks: 4 slot mod 8 + field)
+  uint32_t st_word[STG][kRowsCap], st_slot[STG][kRowsCap], st_val[STG][kRowsCap];
+#else
   uint4 stage[STG][kRowsCap];  // staged records {word, global slot, fp16 value pair, -}, bucket order
+#endif
 };
 
 // NL levels, the first NM coherent (run-merging) and the rest fine, at most NB buckets per level:
@@ -560,6 +569,14 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
   }
   lds_barrier();
 
+  // staged record t of stage b as {word, global slot, fp16 pair, -}
+  auto staged_rec = [&](int b, uint32_t t) {
+#if LNR_ROWS_SOA
+    return make_uint4(sm.st_word[b][t], sm.st_slot[b][t], sm.st_val[b][t], 0u);
+#else
+    return sm.stage[b][t];
+#endif
+  };
   // copy level l's staged row out (consecutive threads -> consecutive slots of a run)
   auto copy_out = [&](uint32_t l) {
     const int sbuf = kRowsStages == 2 ? (l & 1) : 0;
@@ -569,7 +586,7 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
 #pragma unroll
     for (int u = 0; u < (kRowsCap + kSB - 1) / kSB; ++u) {
       const uint32_t t = threadIdx.x + u * kSB;
-      const uint4 q = sm.stage[sbuf][t < (uint32_t)kRowsCap ? t : kRowsCap - 1];
+      const uint4 q = staged_rec(sbuf, t < (uint32_t)kRowsCap ? t : kRowsCap - 1);
       const uint32_t d = t < lim && q.y < spare ? q.y : spare;  // (the bound: never a store outside the records)
       ws.rec[d] = make_uint2(q.x, q.z);
     }
@@ -581,7 +598,7 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
       if ((uint32_t)(u * kSB) < lim) {
         const uint32_t t = threadIdx.x + u * kSB;
         if (t < lim) {
-          const uint4 q = sm.stage[sbuf][t];
+          const uint4 q = staged_rec(sbuf, t);
           const uint32_t d = q.y < spare ? q.y : spare;  // (the bound: never a store outside the records)
           ws.rec[d] = make_uint2(q.x, q.z);
         }
@@ -622,11 +639,19 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
         for (int k = 0; k < 4; ++k) {
           const uint32_t slot = s4[k].y + rank[k];
           const uint32_t h = rec_half2(val[k].x, val[k].y, rs);
-          if (staged) {  // three 32-bit fields (ds_write2_b32 + ds_write_b32: no register moves for a b128 quad)
+          if (staged) {
+#if LNR_ROWS_SOA
+            const uint32_t t = s4[k].x + rank[k];
+            sm.st_word[stg][t] = word[k];
+            sm.st_slot[stg][t] = slot;
+            sm.st_val[stg][t] = h;
+#else
+            // three 32-bit fields (ds_write2_b32 + ds_write_b32: no register moves for a b128 quad)
             uint32_t* q = reinterpret_cast<uint32_t*>(&sm.stage[stg][s4[k].x + rank[k]]);
             q[0] = word[k];
             q[1] = slot;
             q[2] = h;
+#endif
           } else {  // (block-uniform) more records than the stage holds: each straight to its global slot
             ws.rec[slot < spare ? slot : spare] = make_uint2(word[k], h);
           }
