@@ -434,6 +434,18 @@ __global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_wave(SamplerArgs
   }
 }
 
+#ifndef LNR_GALLOP_JS
+#define LNR_GALLOP_JS 0
+#endif
+#ifndef LNR_GALLOP_JT
+#define LNR_GALLOP_JT 1
+#endif
+#ifndef LNR_GALLOP_CDF
+#define LNR_GALLOP_CDF 0
+#endif
+#ifndef LNR_SAMPLER_LOOKUP_UNROLL
+#define LNR_SAMPLER_LOOKUP_UNROLL 4
+#endif
 // ---------------------------------------------------------------------------------------------
 // OGM sampler, one wave per ray, the importance draws sorted BEFORE the inverse CDF (LONER_SAMPLER_MERGE=2,
 // the default from 256 samples): the inverse CDF is non-decreasing in u, so sorting the draws u and mapping
@@ -473,6 +485,31 @@ __device__ __forceinline__ int upper_bound_from(const float* arr, int lo, int n,
   }
   return lo;
 }
+// The same searches when the answer is known to lie just after lo (the previous, smaller key's answer):
+// exponential steps lo + 1, + 2, + 4, ... then a binary search in the last step's interval: about 2 log2 of the
+// distance LDS reads instead of log2 (n - lo).  UPPER: first j >= lo with arr[j] > x, else arr[j] >= x.
+template <bool UPPER>
+__device__ __forceinline__ int gallop_from(const float* arr, int lo, int n, float x) {
+  auto after = [&](int j) { return UPPER ? !(arr[j] > x) : (arr[j] < x); };  // the answer lies after j
+  if (lo >= n || !after(lo)) return lo;
+  int last = lo, hi = n;
+  for (int b = 1;; b <<= 1) {
+    const int j = lo + b;
+    if (j >= n) break;
+    if (!after(j)) {
+      hi = j;
+      break;
+    }
+    last = j;
+  }
+  int l2 = last + 1;
+  while (l2 < hi) {
+    const int mid = (l2 + hi) >> 1;
+    if (after(mid)) l2 = mid + 1;
+    else hi = mid;
+  }
+  return l2;
+}
 __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");
@@ -498,6 +535,7 @@ __global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_rank(SamplerArgs
     const float near = ry[11], far = ry[12];
     const float ox = ry[0], oy = ry[1], oz = ry[2], dx = ry[3], dy = ry[4], dz = ry[5];
     const uint32_t gr = (uint32_t)(a.ray_offset + r);
+    LNR_STAMP(t0);
     // 1. the draws' counting sort (first, while no stratum is held in registers): bucket counters, ranks within a
     // bucket, bucket offsets, scatter
 #pragma unroll
@@ -564,12 +602,13 @@ __global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_rank(SamplerArgs
       if (lane > 0) su[0] = fmaxf(su[0], pl);
     }
     wave_lds_fence();  // (the counters' reads are done: the strata's probabilities overwrite them)
+    LNR_STAMP(t1);
     // 2. strata and occupancy probabilities (k_sampler_wave step 1-2), computed lane-contiguous (stratum
     // 64 q + lane: one gather instruction's lanes read neighbouring strata, mostly the same voxels), then
     // transposed through LDS to this lane's positions [l Q, (l + 1) Q)
     float* pscr = bins;  // [H] the probabilities in stratum order (free until step 3)
-#pragma unroll 4
-    for (int q = 0; q < Q; ++q) {  // (4 strata's gathers in flight per lane: all Q of them cost E = 32 its occupancy)
+#pragma unroll LNR_SAMPLER_LOOKUP_UNROLL
+    for (int q = 0; q < Q; ++q) {  // (a few strata's gathers in flight per lane: all Q of them cost E = 32 its occupancy)
       const int i = q * 64 + lane;
       const float tt = linspace01(i, H);
       float z = near * (1.0f - tt) + far * tt;
@@ -605,6 +644,7 @@ __global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_rank(SamplerArgs
       if (lane < 63) strat_sorted = strat_sorted && !(next_first < zq[Q - 1]);
     }
     wave_lds_fence();
+    LNR_STAMP(t2);
     // 3. sample_pdf's cdf and bins (k_sampler_wave step 3)
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) wl += __shfl_xor(wl, o, 64);
@@ -637,21 +677,15 @@ __global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_rank(SamplerArgs
       if (i < H - 1) bins[i] = 0.5f * (zq[q] + strat[i + 1]);
     }
     wave_lds_fence();
+    LNR_STAMP(t3);
     // 4. inverse CDF of the sorted draws (searchsorted(cdf, u, right=True) over [0, H - 1])
     float fq[Q];
     int lo = 0;
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const float u = su[q];
-      if (lo < H - 1 && cdf[lo] <= u) {  // the previous draw's answer no longer holds: search on from it
-        int hi = H - 1;
-        ++lo;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (cdf[mid] <= u) lo = mid + 1;
-          else hi = mid;
-        }
-      }
+      // the previous draw's answer, or the first cdf entry above u after it (the answer capped at H - 1)
+      lo = LNR_GALLOP_CDF ? gallop_from<true>(cdf, lo, H - 1, u) : upper_bound_from(cdf, lo, H - 1, u);
       const int below = lo - 1 > 0 ? lo - 1 : 0;
       const int above = lo < M ? lo : M;
       const float c0 = cdf[below], c1 = cdf[above];
@@ -671,15 +705,16 @@ __global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_rank(SamplerArgs
     for (int q = 0; q < Q; ++q) imp[lane * Q + q] = fq[q];
     wave_lds_fence();
     float* zr = a.z + r * (int64_t)(2 * H);
+    LNR_STAMP(t4);
     if (__all(strat_sorted && f_asc)) {
       // 5. merge by rank into out, then coalesced stores
       // (out overlays the cdf and bins, whose reads ended before the fence above)
       int js = 0, jt = 0;
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
-        js = lower_bound_from(imp, js, H, zq[q]);
+        js = (q == 0 || !LNR_GALLOP_JS) ? lower_bound_from(imp, js, H, zq[q]) : gallop_from<false>(imp, js, H, zq[q]);
         out[lane * Q + q + js] = zq[q];
-        jt = upper_bound_from(strat, jt, H, fq[q]);
+        jt = (q == 0 || !LNR_GALLOP_JT) ? upper_bound_from(strat, jt, H, fq[q]) : gallop_from<true>(strat, jt, H, fq[q]);
         out[lane * Q + q + jt] = fq[q];
       }
       wave_lds_fence();
@@ -695,6 +730,12 @@ __global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_rank(SamplerArgs
       for (int e = 0; e < E; ++e) zr[lane * E + e] = v[e];
     }
     wave_lds_fence();  // this wave's slice is rewritten by its next ray
+    LNR_STAMP(t5);
+    LNR_PHASE(0, t1, t0);
+    LNR_PHASE(1, t2, t1);
+    LNR_PHASE(2, t3, t2);
+    LNR_PHASE(3, t4, t3);
+    LNR_PHASE(4, t5, t4);
   }
 }
 
@@ -705,6 +746,8 @@ static size_t sampler_smem(int H, int P2) { return ((size_t)3 * H + P2 + 2) * 4 
 }  // namespace lnr
 
 using namespace lnr;
+
+LNR_PHASE_EXPORT(sampler)
 
 extern "C" uint32_t lnr_step_key(uint32_t seed, uint32_t step) { return mix32(mix32(seed) ^ step); }
 

@@ -53,6 +53,16 @@ def main():
         t1.record()
         torch.cuda.synchronize()
         us = t0.elapsed_time(t1) / a.reps * 1e3
+        fn = getattr(L.lib(), "lnr_debug_phases_sampler", None)  # (a -DLNR_EXP_STAMPS build: per-phase cycles)
+        if fn is not None:
+            import ctypes
+            buf = (ctypes.c_ulonglong * 32)()
+            fn.argtypes = [ctypes.c_void_p]
+            fn(ctypes.cast(buf, ctypes.c_void_p))
+            ph = list(buf)[:5]
+            tot = max(sum(ph), 1)
+            print("  phases (draws sort, strata + occupancy, cdf, inverse CDF, merge + store):",
+                  " ".join(f"{p / tot:.2f}" for p in ph), flush=True)
         zz = z.cpu().numpy()
         ok = bool(np.all(np.diff(zz, axis=1) >= 0))
         print(f"{name}: {us:.1f} us per launch, sorted={ok}, digest {hashlib.sha1(zz.tobytes()).hexdigest()[:16]}",
