@@ -209,6 +209,9 @@ __device__ __forceinline__ unsigned long long stamp() {
 // OccupancyGridModel.interpolate (src/models/model_tcnn.py:126-134): grid_sample of the (R, R, R) grid
 // at (x, y, z) in [-1, 1] (x the fastest axis), trilinear, align_corners=False, zeros padding.  Its
 // corner order and weights are those of the grid-gradient splat (optim.hip).
+#ifndef LNR_OCC_PAIR
+#define LNR_OCC_PAIR 1
+#endif
 __device__ __forceinline__ float occ_grid_sample(const float* __restrict__ occ, int R, float x, float y, float z) {
   const float ix = ((x + 1.f) * (float)R - 1.f) / 2.f;
   const float iy = ((y + 1.f) * (float)R - 1.f) / 2.f;
@@ -219,6 +222,29 @@ __device__ __forceinline__ float occ_grid_sample(const float* __restrict__ occ, 
   const float wy[2] = {(float)(y0 + 1) - iy, iy - (float)y0};
   const float wz[2] = {(float)(z0 + 1) - iz, iz - (float)z0};
   float acc = 0.f;
+#if LNR_OCC_PAIR
+  // The two x-corners of each y/z edge are adjacent floats: one 8-B load per edge (4 gathers, not 8), from
+  // x0 clamped to [0, R - 2] so that a pair with one corner outside the grid reads the other one.  The same
+  // products added in the same order (a corner outside adds nothing, as before): bitwise the 8-load form.
+  if (R >= 2) {
+    typedef float f32x2u __attribute__((ext_vector_type(2), aligned(4)));
+    const bool in0 = x0 >= 0 && x0 < R, in1 = x0 + 1 >= 0 && x0 + 1 < R;
+    const int xb = min(max(x0, 0), R - 2);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int by = e & 1, bz = e >> 1;
+      const int cy = y0 + by, cz = z0 + bz;
+      const bool yz = cy >= 0 && cy < R && cz >= 0 && cz < R;
+      f32x2u v = {0.f, 0.f};
+      if (yz && (in0 || in1)) v = *(const f32x2u*)(occ + ((int64_t)cz * R + cy) * R + xb);
+      const float v0 = xb == x0 ? v.x : v.y, v1 = xb == x0 ? v.y : v.x;
+      const float w0 = wx[0] * wy[by] * wz[bz], w1 = wx[1] * wy[by] * wz[bz];
+      if (yz && in0) acc += v0 * w0;
+      if (yz && in1) acc += v1 * w1;
+    }
+    return acc;
+  }
+#endif
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     const int bx = c & 1, by = (c >> 1) & 1, bz = (c >> 2) & 1;
