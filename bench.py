@@ -494,18 +494,12 @@ def _camera_stages(eng, fr, rays, inten, L):
     L.call("lnr_field_render", fs.mlp_f16, eng.enc, N, rays, eng.z, R, S, 0, 1.0, None, key, 0, eng.depth,
            eng.opacity, None, eng.weights, s)
     mark("encode_rgb")
-    if eng.skip_zero:
-        L.call("lnr_hashgrid_fwd_rays_live", L.ctypes.byref(cs.desc), rays, eng.z, R, S, cs.table_f16, eng.weights,
-               eng.enc_rgb, N, s)
-    else:
-        L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(cs.desc), rays, eng.z, R, S, cs.table_f16, eng.enc_rgb, N,
-               eng.bwd_ws, eng.bwd_ws_bytes, s)
+    eng.colour_encode(rays, R, S, s)
     mark("rgb_train")
     L.call("lnr_rgb_train", cs.mlp_f16, cs.n_hidden_layers, eng.enc_rgb, N, rays, eng.weights, inten, R, S,
            1.0 / (3.0 * R), eng.rgb, eng.loss, eng.d_enc, cs.grad_mlp, eng.ws, eng.ws_bytes, eng.level_max_ptr, s)
     mark("grid_bwd")
-    L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(cs.desc), rays, eng.z, R, S, eng.d_enc, N, cs.grad_table,
-           None, None, eng.bwd_ws, eng.bwd_ws_bytes, (0 if eng.skip_zero else L.BWD_COUNTS_READY) | L.BWD_LEVEL_MAX_READY, s)
+    eng.colour_grid_backward(rays, R, S, s)
     mark("adam")
     L.call("lnr_adam_step", cs.params, cs.shadow, cs.grad, cs.m, cs.v, cs.n_padded, 1, 0.0, 0.9, 0.999, 1e-8, None, s)
     mark("end")

@@ -127,6 +127,13 @@ int lnr_hashgrid_fwd_rays(const lnr_grid_desc* d, const float* rays, const float
 int lnr_hashgrid_fwd_rays_live(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
                                int32_t n_samples, const uint16_t* table, const float* live, uint32_t* enc,
                                int64_t enc_stride, void* stream);
+/* lnr_hashgrid_fwd_rays_live that also records the backward's histogram in `bwd_ws` (as
+ * lnr_hashgrid_fwd_rays does), counting a sample with live[n] == 0 at the coherent levels only (its
+ * zero gradient merges into the runs there) and not at the others: the records of
+ * lnr_hashgrid_bwd_rays_live, which can then be called with LNR_BWD_COUNTS_READY (no counting pass). */
+int lnr_hashgrid_fwd_rays_live_ws(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
+                                  int32_t n_samples, const uint16_t* table, const float* live, uint32_t* enc,
+                                  int64_t enc_stride, void* bwd_ws, int64_t bwd_ws_bytes, void* stream);
 /* Backward: d_table (n_entries,2) fp32 = scatter of corner weights * d_enc, as an atomic-free
  * binned scatter of 8-byte records (fp16 values at a per-level power-of-two scale from max |d_enc|)
  * with int64 fixed-point accumulation.  d_table is OVERWRITTEN (every entry, zero where
@@ -158,6 +165,16 @@ int lnr_hashgrid_bwd_rays(const lnr_grid_desc* d, const float* rays, const float
                           int32_t n_samples, const float* d_enc, int64_t enc_stride, float* d_table,
                           const uint16_t* table, float* d_pos, void* workspace, int64_t workspace_bytes,
                           int32_t flags, void* stream);
+/* The table gradient of samples with a live mask (the colour grid: live = the compositing weights, d_enc
+ * of a weight-0 sample is 0): at the levels that are not coherent, samples with live[n] == 0 emit no records
+ * (the others emit theirs, zero or not).  The same d_table as lnr_hashgrid_bwd_rays (bitwise when no live
+ * sample has d_enc = 0 at such a level; a zero record can move its bucket's fixed-point unit, a rounding
+ * below 2^-44 of the level's largest record).  With LNR_BWD_COUNTS_READY the histogram must come from
+ * lnr_hashgrid_fwd_rays_live_ws with the same mask. */
+int lnr_hashgrid_bwd_rays_live(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
+                               int32_t n_samples, const float* d_enc, int64_t enc_stride, const float* live,
+                               float* d_table, void* workspace, int64_t workspace_bytes, int32_t flags,
+                               void* stream);
 /* The same, from lnr_field_train's compact encoding gradient: d_enc = d_sigma[n] * J[l][n] with J
  * level-major fp16 pairs (one uint32 per level and sample, level stride jac_stride). */
 int lnr_hashgrid_bwd_rays_jac(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,

@@ -159,6 +159,10 @@ _SIGNATURES = {
     "lnr_rgb_render": (ctypes.c_int, [c_p, c_i32, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_p, c_p]),
     "lnr_hashgrid_fwd_rays_live": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_i64,
                                                   c_p]),
+    "lnr_hashgrid_fwd_rays_live_ws": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_p, c_p,
+                                                     c_i64, c_p, c_i64, c_p]),
+    "lnr_hashgrid_bwd_rays_live": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_p,
+                                                  c_p, c_i64, c_i32, c_p]),
     "lnr_status_scan": (ctypes.c_int, [c_p, c_i64, c_u32, c_p, c_p]),
     "lnr_rgb_mlp_params": (c_i64, [c_i32]),
     "lnr_rgb_train_workspace_bytes": (c_i64, [c_i32, c_i64]),

@@ -206,6 +206,9 @@ class CameraStepEngine:
         self.allreduce, self.ray_offset = allreduce, int(ray_offset)
         # (None: LONER_CAM_SKIP_ZERO, default on)
         self.skip_zero = (os.environ.get("LONER_CAM_SKIP_ZERO", "1") == "1") if skip_zero is None else bool(skip_zero)
+        # with skip_zero: the live encode also counts the backward's records (by the weights' mask), so the
+        # backward needs no counting pass of its own (LONER_CAM_LIVE_COUNT, default on)
+        self.live_count = self.skip_zero and os.environ.get("LONER_CAM_LIVE_COUNT", "1") == "1"
         self.iteration = 0
         dev = field.device
         N = self.R * self.S
@@ -226,6 +229,37 @@ class CameraStepEngine:
                                                                                    L.ptr(self.bwd_ws)))
         self.ws_bytes = int(L.lib().lnr_rgb_train_workspace_bytes(color.n_hidden_layers, self.R))
         self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=dev)
+
+    def colour_encode(self, rays, R, S, s):
+        """The colour grid's encode of the R x S samples (after the sigma pass wrote ``weights``).
+        skip_zero: samples of weight exactly 0 have no colour gradient (dL/dc_i = w_i dL/drgb): no gathers
+        for them (nor zero stores in tiles without a live sample), and no records in the backward at the
+        levels that are not coherent.  Round 4 measured it slower at CAM (encode 0.34 -> 0.21 ms, backward
+        0.90 -> 0.99 ms); with round 5's kernels the encode drops 0.285 -> 0.19 ms and the backward stays
+        0.452-0.458 -> 0.456-0.463: CAM 1.806 -> 1.708 ms.  On by default.  live_count: the live encode
+        counts the backward's records too (the backward's own counting pass was 0.12 ms at CAM)."""
+        cs = self.color
+        if self.live_count:
+            L.call("lnr_hashgrid_fwd_rays_live_ws", L.ctypes.byref(cs.desc), rays, self.z, R, S, cs.table_f16,
+                   self.weights, self.enc_rgb, self.N, self.bwd_ws, self.bwd_ws_bytes, s)
+        elif self.skip_zero:
+            L.call("lnr_hashgrid_fwd_rays_live", L.ctypes.byref(cs.desc), rays, self.z, R, S, cs.table_f16,
+                   self.weights, self.enc_rgb, self.N, s)
+        else:
+            L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(cs.desc), rays, self.z, R, S, cs.table_f16, self.enc_rgb,
+                   self.N, self.bwd_ws, self.bwd_ws_bytes, s)
+
+    def colour_grid_backward(self, rays, R, S, s):
+        """The colour table's gradient from ``d_enc`` (lnr_rgb_train's output), in colour_encode's mode."""
+        cs = self.color
+        if self.skip_zero:  # records of live samples only: counted by the encode (live_count) or here
+            flags = (L.BWD_COUNTS_READY if self.live_count else 0) | L.BWD_LEVEL_MAX_READY
+            L.call("lnr_hashgrid_bwd_rays_live", L.ctypes.byref(cs.desc), rays, self.z, R, S, self.d_enc, self.N,
+                   self.weights, cs.grad_table, self.bwd_ws, self.bwd_ws_bytes, flags, s)
+        else:
+            L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(cs.desc), rays, self.z, R, S, self.d_enc, self.N,
+                   cs.grad_table, None, None, self.bwd_ws, self.bwd_ws_bytes,
+                   L.BWD_COUNTS_READY | L.BWD_LEVEL_MAX_READY, s)
 
     def step(self, rays, intensities, global_step=None, n_rays_global=None):
         """rays (R,13), intensities (R,3) on the GPU, R <= n_rays.  Returns the loss (device, local
@@ -249,23 +283,12 @@ class CameraStepEngine:
                None, 0, s)
         L.call("lnr_field_render", fs.mlp_f16, self.enc, N, rays, self.z, R, S, 0, self.noise_std, None, key,
                self.ray_offset, self.depth, self.opacity, None, self.weights, s)
-        # skip_zero: samples of weight exactly 0 have no colour gradient (dL/dc_i = w_i dL/drgb): no
-        # gathers for them (nor zero stores in tiles without a live sample), and the backward counts (its
-        # own pass) and scatters only non-zero d_enc.  Round 4 measured it slower at CAM (encode 0.34 ->
-        # 0.21 ms, backward 0.90 -> 0.99 ms); with round 5's kernels the encode drops 0.285 -> 0.19 ms and
-        # the backward stays 0.452-0.458 -> 0.456-0.463: CAM 1.806 -> 1.708 ms.  On by default.
-        if self.skip_zero:
-            L.call("lnr_hashgrid_fwd_rays_live", L.ctypes.byref(cs.desc), rays, self.z, R, S, cs.table_f16,
-                   self.weights, self.enc_rgb, N, s)
-        else:
-            L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(cs.desc), rays, self.z, R, S, cs.table_f16, self.enc_rgb,
-                   N, self.bwd_ws, self.bwd_ws_bytes, s)
+        self.colour_encode(rays, R, S, s)
         n_glob = R if n_rays_global is None else int(n_rays_global)
         L.call("lnr_rgb_train", cs.mlp_f16, cs.n_hidden_layers, self.enc_rgb, N, rays, self.weights, intensities, R,
                S, 1.0 / (3.0 * n_glob), self.rgb, self.loss, self.d_enc, cs.grad_mlp, self.ws, self.ws_bytes,
                self.level_max_ptr, s)
-        L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(cs.desc), rays, self.z, R, S, self.d_enc, N, cs.grad_table,
-               None, None, self.bwd_ws, self.bwd_ws_bytes, (0 if self.skip_zero else L.BWD_COUNTS_READY) | L.BWD_LEVEL_MAX_READY, s)
+        self.colour_grid_backward(rays, R, S, s)
         if self.allreduce is not None:
             self.allreduce(cs.grad)
         cs.adam_step += 1

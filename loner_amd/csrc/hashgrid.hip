@@ -143,8 +143,8 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
   for (int h = 0; h < kEncSpt; ++h) {
     const int64_t i = i0 + h * H;
     in[h] = i < n;
-    // live (eval only, never when counting): samples whose weight is exactly 0 get a zero encoding
-    // and issue no gathers
+    // live: samples whose weight is exactly 0 get a zero encoding and issue no gathers; when counting
+    // too, they emit no records at the fine levels (the scatter skips them by the same mask)
     use[h] = in[h] && (live == nullptr || live[i] != 0.f);
     x[h] = y[h] = z[h] = 0.f;
     pos.wave(i, n, in[h], x[h], y[h], z[h]);
@@ -202,7 +202,7 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
     if (count) {
       lds_barrier();
 #pragma unroll
-      for (int h = 0; h < kEncSpt; ++h) count_fine_add(c[h], in[h], hist);
+      for (int h = 0; h < kEncSpt; ++h) count_fine_add(c[h], use[h], hist);
       lds_barrier();
       publish_block_counts(a, l, hist, ws);
     }
@@ -255,7 +255,7 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
     }
     if (count) {
       if (h == 0) lds_barrier();  // the zeroed histogram
-      count_add(a, l, c, in[h], in[h], hist);
+      count_add(a, l, c, in[h], use[h], hist);
     }
   }
   if (count) {
@@ -403,35 +403,33 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
          : lpb == 2 ? k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 2>
                     : k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 1>;
   };
+  BwdWorkspace w{};
   if (bwd_ws) {
     LNR_REQUIRE(bwd_ws_bytes >= bwd_workspace_bytes(d, n), "%s: backward workspace too small", who);
     LNR_REQUIRE(a.n_buckets <= (uint32_t)kMaxBuckets, "%s: too many table chunks (%u)", who, a.n_buckets);
     for (uint32_t l = 0; l < d->n_levels; ++l)
       LNR_REQUIRE(a.bucket_base[l + 1] - a.bucket_base[l] <= (uint32_t)kMaxChunksPerLevel,
                   "%s: level %u has more than %d table chunks", who, l, kMaxChunksPerLevel);
-    BwdWorkspace w = carve_workspace(bwd_ws, a, d, n);
-    // one workgroup per histogram row (kSB samples) so the row is written whole
-    dim3 gridc((unsigned)w.n_sb, d->n_levels / lpb);
-    hipLaunchKernelGGL(enc_kernel(), gridc, dim3(kSB), 0, st, a, pos, n, reinterpret_cast<const uint32_t*>(table), enc,
-                       enc_stride, w, nullptr);
-  } else {
-    // kSB-sample workgroups as in training (C2-size eval launch: 1011 us at 256 one-sample threads, 836 at 512)
-    dim3 grid((unsigned)((n + kSB - 1) / kSB), d->n_levels);
-    const uint32_t* tb = reinterpret_cast<const uint32_t*>(table);
-    if (live == nullptr)
-      hipLaunchKernelGGL(enc_kernel(), dim3(grid.x, d->n_levels / lpb), dim3(kSB), 0, st, a, pos, n, tb, enc, enc_stride,
-                         BwdWorkspace{}, live);
-    else if (spt2 && live_lpb() == 2 && d->n_levels % 2 == 0 && enc_levels_per_group(d, grid.x) >= 2)
-      // (two samples per thread over two levels spill at eight waves per SIMD: one sample per thread)
-      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, false, 2>), dim3(grid.x, d->n_levels / 2), dim3(kSB), 0, st, a,
-                         pos, n, tb, enc, enc_stride, BwdWorkspace{}, live);
-    else if (spt2)
-      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 2, false>), grid, dim3(kSB / 2), 0, st, a, pos, n, tb, enc,
-                         enc_stride, BwdWorkspace{}, live);
-    else
-      hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, false>), grid, dim3(kSB), 0, st, a, pos, n, tb, enc,
-                         enc_stride, BwdWorkspace{}, live);
+    w = carve_workspace(bwd_ws, a, d, n);
   }
+  // one workgroup per histogram row (kSB samples), so a counted row is written whole (and kSB-sample
+  // workgroups for the plain eval launch too: C2-size eval 1011 us at 256 one-sample threads, 836 at 512)
+  const unsigned rows = (unsigned)((n + kSB - 1) / kSB);
+  const uint32_t* tb = reinterpret_cast<const uint32_t*>(table);
+  const dim3 grid(rows, d->n_levels);
+  if (live == nullptr)
+    hipLaunchKernelGGL(enc_kernel(), dim3(rows, d->n_levels / lpb), dim3(kSB), 0, st, a, pos, n, tb, enc, enc_stride, w,
+                       live);
+  else if (spt2 && live_lpb() == 2 && d->n_levels % 2 == 0 && enc_levels_per_group(d, rows) >= 2)
+    // (two samples per thread over two levels spill at eight waves per SIMD: one sample per thread)
+    hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, false, 2>), dim3(rows, d->n_levels / 2), dim3(kSB), 0, st, a, pos, n,
+                       tb, enc, enc_stride, w, live);
+  else if (spt2)
+    hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 2, false>), grid, dim3(kSB / 2), 0, st, a, pos, n, tb, enc, enc_stride, w,
+                       live);
+  else
+    hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, false>), grid, dim3(kSB), 0, st, a, pos, n, tb, enc, enc_stride, w,
+                       live);
   LNR_RETURN_LAUNCH(who);
 }
 
@@ -468,6 +466,19 @@ extern "C" int lnr_hashgrid_fwd_rays_live(const lnr_grid_desc* d, const float* r
   LNR_REQUIRE(rays && z && table && enc && live, "lnr_hashgrid_fwd_rays_live: null pointer");
   return launch_fwd(d, PosFromRays{rays, z, n_samples}, n, table, enc, enc_stride, nullptr, 0, as_stream(stream),
                     "lnr_hashgrid_fwd_rays_live", live);
+}
+
+extern "C" int lnr_hashgrid_fwd_rays_live_ws(const lnr_grid_desc* d, const float* rays, const float* z,
+                                             int64_t n_rays, int32_t n_samples, const uint16_t* table,
+                                             const float* live, uint32_t* enc, int64_t enc_stride, void* bwd_ws,
+                                             int64_t bwd_ws_bytes, void* stream) {
+  if (int e = check_desc(d, "lnr_hashgrid_fwd_rays_live_ws")) return e;
+  const int64_t n = n_rays * (int64_t)n_samples;
+  LNR_REQUIRE(n_rays >= 0 && n_samples > 0 && enc_stride >= n, "lnr_hashgrid_fwd_rays_live_ws: bad sizes");
+  if (n == 0) return LNR_OK;
+  LNR_REQUIRE(rays && z && table && enc && live && bwd_ws, "lnr_hashgrid_fwd_rays_live_ws: null pointer");
+  return launch_fwd(d, PosFromRays{rays, z, n_samples}, n, table, enc, enc_stride, bwd_ws, bwd_ws_bytes,
+                    as_stream(stream), "lnr_hashgrid_fwd_rays_live_ws", live);
 }
 
 extern "C" int lnr_hashgrid_bwd_atomic(const lnr_grid_desc* d, const float* pos01, int64_t n, const float* d_enc,

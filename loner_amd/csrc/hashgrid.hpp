@@ -202,9 +202,15 @@ struct PosFromRays {
 // pairs (lnr_field_train's compact output: 4 B per sample and level instead of 8, and d_sigma 4 B
 // per sample).  load_nt: read once (nontemporal).
 typedef float gf32x2 __attribute__((ext_vector_type(2)));
+// live_at(i): whether sample i may emit records at the fine levels.  GradF32's optional ``live`` mask (the
+// colour grid's compositing weights: a sample of weight exactly 0 has d_enc = 0) makes the scatter skip by
+// the mask, the criterion of a forward that counted the histogram with it (lnr_hashgrid_fwd_rays_live_ws);
+// without one every sample may.
 struct GradF32 {
   const float2* g;
   int64_t stride;
+  const float* live = nullptr;
+  __device__ __forceinline__ bool live_at(int64_t i) const { return live == nullptr || live[i] != 0.f; }
   __device__ __forceinline__ float2 load(uint32_t l, int64_t i) const { return g[(int64_t)l * stride + i]; }
   __device__ __forceinline__ float2 load_nt(uint32_t l, int64_t i) const {
     const gf32x2 v = __builtin_nontemporal_load(reinterpret_cast<const gf32x2*>(&g[(int64_t)l * stride + i]));
@@ -220,6 +226,7 @@ struct GradJac {
   const uint32_t* jac;
   const float* dsig;
   int64_t stride;
+  __device__ __forceinline__ static constexpr bool live_at(int64_t) { return true; }
   __device__ __forceinline__ static float2 apply(uint32_t h, float s) {
     return make_float2((float)__builtin_bit_cast(_Float16, (uint16_t)(h & 0xFFFFu)) * s,
                        (float)__builtin_bit_cast(_Float16, (uint16_t)(h >> 16)) * s);

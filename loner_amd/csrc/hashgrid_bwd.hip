@@ -39,7 +39,7 @@ __global__ void __launch_bounds__(kSB) k_bwd_count(GridArgs a, PosFn pos, int64_
   if (in) {
     pos(i, x, y, z);
     const float2 g = grad.load(l, i);
-    act = g.x != 0.f || g.y != 0.f;
+    act = grad.live_at(i) && (g.x != 0.f || g.y != 0.f);
   }
   lds_barrier();
   if (a.lv[l].fine) {
@@ -324,7 +324,7 @@ __device__ __forceinline__ void scatter_row_level(const GridArgs& a, const PosFn
   const float2 g = in ? g_raw : make_float2(0.f, 0.f);
   // fine / generic levels: samples with a zero gradient emit nothing when the histogram was
   // counted after the MLP backward (k_bwd_count, same predicate); coherent levels keep every lane
-  const bool act = in && (!skip_zero || g.x != 0.f || g.y != 0.f);
+  const bool act = in && grad.live_at(ic) && (!skip_zero || g.x != 0.f || g.y != 0.f);
   bool staged = true;
   auto place = [&](bool valid, uint32_t bk, uint32_t rank, uint32_t word, float2 val) {
     if (!valid) return;
@@ -530,6 +530,7 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
   for (int l = 0; l < NL; ++l) g[l] = grad.load_raw_nt(LB + l, ic);  // read once: nontemporal, so they do not
                                                                 // displace the runs' L2 lines
   const float gsc = grad.scale(ic);
+  const bool live = grad.live_at(ic);  // (GradF32's live mask, when the forward counted with it)
   uint32_t h0[2][2], h1[2][2];
   uint64_t seg[2][2];
 #pragma unroll
@@ -623,7 +624,7 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
 #else
     const float2 gv = in ? gl : make_float2(0.f, 0.f);
 #endif
-    const bool act = in && (!skip_zero || gv.x != 0.f || gv.y != 0.f);
+    const bool act = in && live && (!skip_zero || gv.x != 0.f || gv.y != 0.f);
     const float rs = LNR_PRESCALE ? 1.0f : rsc[l];
     // rank (returning LDS atomics) and place: all start reads, then all atomics, then all writes
     // (one lane-level branch for the 4 records: they share their validity)
@@ -1734,6 +1735,19 @@ extern "C" int lnr_hashgrid_bwd_rays(const lnr_grid_desc* d, const float* rays, 
   return bwd_entry(d, PosFromRays{rays, z, n_samples}, n, GradF32{reinterpret_cast<const float2*>(d_enc), enc_stride},
                    d_table, table, d_pos, workspace, workspace_bytes, flags, as_stream(stream),
                    "lnr_hashgrid_bwd_rays");
+}
+
+extern "C" int lnr_hashgrid_bwd_rays_live(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
+                                          int32_t n_samples, const float* d_enc, int64_t enc_stride, const float* live,
+                                          float* d_table, void* workspace, int64_t workspace_bytes, int32_t flags,
+                                          void* stream) {
+  if (int e = check_desc_bwd(d, "lnr_hashgrid_bwd_rays_live")) return e;
+  const int64_t n = n_rays * (int64_t)n_samples;
+  LNR_REQUIRE(n_rays >= 0 && n_samples > 0 && enc_stride >= n, "lnr_hashgrid_bwd_rays_live: bad sizes");
+  LNR_REQUIRE(n == 0 || (rays && z && d_enc && live && d_table), "lnr_hashgrid_bwd_rays_live: null pointer");
+  return bwd_entry(d, PosFromRays{rays, z, n_samples}, n,
+                   GradF32{reinterpret_cast<const float2*>(d_enc), enc_stride, live}, d_table, nullptr, nullptr,
+                   workspace, workspace_bytes, flags, as_stream(stream), "lnr_hashgrid_bwd_rays_live");
 }
 
 // Adam with a zero gradient on every table parameter (the fused entry's empty batch)

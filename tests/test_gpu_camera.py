@@ -240,3 +240,27 @@ def test_camera_skip_zero_matches_default(L):
     assert float((eng_b.weights[:R] == 0).float().mean()) > 0.05  # the path is exercised
     assert torch.equal(cs_a.grad[:cs_a.n_mlp], cs_b.grad[:cs_b.n_mlp])
     assert _rel(host(cs_b.grad), host(cs_a.grad)) < 1e-6
+
+
+def test_camera_live_count_matches_backward_count(L, monkeypatch):
+    """skip_zero with the records counted by the live colour encode (lnr_hashgrid_fwd_rays_live_ws, the
+    default) against counted by the backward's own pass (LONER_CAM_LIVE_COUNT=0): the same records, so the
+    same gradient bit for bit (no live sample of this batch has a zero d_enc), and the same Adam step."""
+    from loner_amd import camera as C
+    fr, cs_a, eng_def = _camera_setup()
+    monkeypatch.setenv("LONER_CAM_LIVE_COUNT", "0")
+    eng_a = C.CameraStepEngine(eng_def.field, cs_a, n_rays=eng_def.R, n_samples=128, lr=0.01, seed=0, skip_zero=True)
+    monkeypatch.setenv("LONER_CAM_LIVE_COUNT", "1")
+    _, cs_b, eng_ref = _camera_setup()
+    eng_b = C.CameraStepEngine(eng_ref.field, cs_b, n_rays=eng_ref.R, n_samples=128, lr=0.01, seed=0, skip_zero=True)
+    assert not eng_a.live_count and eng_b.live_count
+    R = fr.n_rays(1)
+    rays = torch.empty(R, 13, device="cuda:0")
+    inten = torch.empty(R, 3, device="cuda:0")
+    fr.build(1, rays, inten)
+    for it in range(2):
+        la = float(eng_a.step(rays, inten, global_step=5 + it).item())
+        lb = float(eng_b.step(rays, inten, global_step=5 + it).item())
+        assert la == lb
+        assert torch.equal(cs_a.grad, cs_b.grad)
+    assert torch.equal(cs_a.params, cs_b.params)

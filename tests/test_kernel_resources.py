@@ -6,7 +6,9 @@ code object's AMDGPU metadata note carries every kernel's .vgpr_spill_count.  No
 benched step may spill; the allowlist names the few that do, off that path:
   * k_bwd_accum with the fused Adam epilogue (<*, true>): the record-balanced accumulate only takes
     the epilogue above 2^17 samples, where the step keeps Adam separate (step.FUSED_ADAM_MAX_N);
-  * the two-samples-per-thread encode of plain positions (k_hashgrid_fwd<PosFromArray, 2, false, 1>).
+  * the two-samples-per-thread encodes (k_hashgrid_fwd<*, 2, false, 1>): of plain positions, and of rays
+    with a live mask (one VGPR since that encode can count the backward's records of live samples); a
+    live encode takes it only with LONER_ENC_LIVE_LPB=1 or an odd level count (default: <*, 1, false, 2>).
 A spill the allowlist does not name fails here: 20 spilled VGPRs went unnoticed in the C2
 accumulate for a while (the epilogue used to be a runtime branch of the same kernel)."""
 import os
@@ -21,6 +23,7 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 ALLOWED = [
     r"^_ZN3lnr11k_bwd_accumILb[01]ELb1E",
     r"^_ZN3lnr14k_hashgrid_fwdINS_12PosFromArrayELi2ELb0ELi1EE",
+    r"^_ZN3lnr14k_hashgrid_fwdINS_11PosFromRaysELi2ELb0ELi1EE",
 ]
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
