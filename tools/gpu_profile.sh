@@ -14,6 +14,7 @@ rm -rf $OUT/prof $OUT/pmc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
   python3 $R/bench.py --config $CFG ${ARGS:-} --no-cpu-baseline > $OUT/bench_prof.json 2> $OUT/bench_prof.err \
   || { tail -20 $OUT/bench_prof.err; exit 1; }
+[ "${PMC:-1}" = 1 ] || { echo profiles done; exit 0; }  # PMC=0: the bench line and the kernel trace only
 bash $R/tools/pmc_hbm.sh $CFG || exit 1
 bash $R/tools/pmc_mfma.sh $CFG || exit 1
 bash $R/tools/pmc_step.sh $CFG || exit 1
