@@ -143,6 +143,61 @@ def test_hashgrid_fwd_live_mask_matches_full_encode(L, R, lpb, monkeypatch):
     assert torch.equal(part, want)
 
 
+@pytest.mark.parametrize("grid,R,S", [((16, 2, 19, 16), 520, 512), ((6, 2, 19, 16), 61, 40)])
+def test_live_counted_backward(L, grid, R, S):
+    """lnr_hashgrid_fwd_rays_live_ws counts the live samples' records while it encodes, and
+    lnr_hashgrid_bwd_rays_live (LNR_BWD_COUNTS_READY) scatters exactly those: the same table gradient, bit
+    for bit, as the backward counting for itself (by the mask, or by d_enc != 0 with no mask), since here every
+    dead sample's d_enc is 0 and every live one's is not.  The colour grid at 520 rays (the level-looped
+    scatter at 128 chunks per level) and a 6-level grid with a dense level past the merged ones (res 64 at
+    40 samples per ray: the per-(row, level) scatter's generic path); the gradient against the oracle."""
+    rng = np.random.default_rng(23)
+    d = L.grid_desc(*grid)
+    lay = ohg.GridLayout(*grid)
+    nl = grid[0]
+    o = rng.uniform(-0.5, 0.5, (R, 3))
+    dr = rng.normal(0, 1, (R, 3))
+    dr /= np.linalg.norm(dr, axis=1, keepdims=True)
+    rays = np.zeros((R, 13), np.float32)
+    rays[:, 0:3], rays[:, 3:6] = o, dr
+    z = np.sort(rng.uniform(0.0, 0.45, (R, S)), 1).astype(np.float32)
+    n = R * S
+    live = (rng.uniform(0, 1, (R, S)) < 0.4).astype(np.float32)
+    denc = rng.normal(0, 1, (n, 2 * nl)).astype(np.float32) * live.reshape(-1, 1)
+    denc_lm = cu(np.ascontiguousarray(denc.reshape(n, nl, 2).transpose(1, 0, 2)))
+    table = cu(rng.uniform(-1, 1, (lay.n_entries, 2)).astype(np.float16).view(np.int16))
+    nb = int(L.lib().lnr_hashgrid_bwd_workspace_bytes(ctypes.byref(d), n))
+    grads = []
+    for mode in ("fwd_counts", "own_count_live", "own_count_nonzero"):
+        ws = torch.zeros(nb // 4 + 1, dtype=torch.int32, device="cuda")
+        enc = torch.full((nl, n), -1, dtype=torch.int32, device="cuda")
+        gt = torch.full((lay.n_entries * 2,), 7.0, dtype=torch.float32, device="cuda")
+        if mode == "fwd_counts":
+            L.call("lnr_hashgrid_fwd_rays_live_ws", ctypes.byref(d), cu(rays), cu(z), R, S, table, cu(live), enc, n,
+                   ws, nb, L.stream())
+            ref_enc = torch.full((nl, n), -1, dtype=torch.int32, device="cuda")
+            L.call("lnr_hashgrid_fwd_rays_live", ctypes.byref(d), cu(rays), cu(z), R, S, table, cu(live), ref_enc, n,
+                   L.stream())
+            assert torch.equal(enc, ref_enc)  # the counting changes no encoding
+            L.call("lnr_hashgrid_bwd_rays_live", ctypes.byref(d), cu(rays), cu(z), R, S, denc_lm, n, cu(live), gt, ws,
+                   nb, L.BWD_COUNTS_READY, L.stream())
+        elif mode == "own_count_live":
+            L.call("lnr_hashgrid_bwd_rays_live", ctypes.byref(d), cu(rays), cu(z), R, S, denc_lm, n, cu(live), gt, ws,
+                   nb, 0, L.stream())
+        else:
+            L.call("lnr_hashgrid_bwd_rays", ctypes.byref(d), cu(rays), cu(z), R, S, denc_lm, n, gt, None, None, ws, nb,
+                   0, L.stream())
+        torch.cuda.synchronize()
+        grads.append(gt.clone())
+    assert torch.equal(grads[0], grads[1])
+    assert torch.equal(grads[0], grads[2])
+    o32, d32 = rays[:, None, 0:3], rays[:, None, 3:6]  # the kernels' fp32 op order: (o + d z + 1) * 0.5
+    pos = (((o32 + d32 * z[:, :, None]) + np.float32(1)) * np.float32(0.5)).reshape(-1, 3)
+    ref = ohg.encode_backward(pos, denc, lay)
+    got = host(grads[0]).reshape(-1, 2)
+    assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < TABLE_GRAD_RTOL
+
+
 @pytest.mark.parametrize("S", [512, 64, 40])
 def test_hashgrid_fwd_run_head_gathers_bitwise(L, S, monkeypatch):
     """The coherent levels' run-head gathers (LONER_ENC_RUN_LEVELS: one lane per run of lanes in one cell
