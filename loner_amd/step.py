@@ -320,10 +320,13 @@ class StepEngine:
         # in place of ~18 kernel launches (LONER_GRAPH=0 turns it off; the pipelined path then runs)
         # LONER_GRAPH: auto (default: batches of at most 2^18 samples, where the host's launch cost is a
         # visible share of the step; measured C1 0.161 against 0.163 ms eager on a fast host, 0.188 against
-        # 0.236 on a slow one; C2 2.040 against 2.016 and C4 shard 1/8 0.396 against 0.392, where the eager
-        # path's next-step prefetch overlaps more than the launches cost), 1 always, 0 never
+        # 0.236 on a slow one; and from 2^22 samples, where every kernel fills the chip, so the eager path's
+        # next-step prefetch (the sampler: texture-addresser work) slows the encode beside it about as much
+        # as it hides: C2 1.910-1.916 against 1.918-1.923 ms eager since round 5's lighter sampler, 2.040
+        # against 2.016 before it.  In between, the prefetch fills what the smaller kernels leave idle: C4
+        # shard 1/8 0.374-0.381 eager against 0.380-0.381), 1 always, 0 never
         g = os.environ.get("LONER_GRAPH", "auto")
-        self.use_graph = (g == "1") or (g == "auto" and self.N <= (1 << 18))
+        self.use_graph = (g == "1") or (g == "auto" and (self.N <= (1 << 18) or self.N >= (1 << 22)))
         self.graph_prefetch = os.environ.get("LONER_GRAPH_PREFETCH", "0") == "1"
         # two lnr_step_scalars (32 B each): this step's, and the next step's (its prefetched build + sampling)
         self._dev_steps = torch.zeros(16, dtype=torch.int32, device=dev)
