@@ -855,29 +855,35 @@ class StepEngine:
         self._gpp = (dict(window=window, want=(global_step + 1, n, self.ray_offset), parity=1 - p,
                           have=2 if sample_next else 1) if prefetch else None)
 
+        def branch(fork):
+            # step k + 1's build (+ sampling) on the side stream after ``fork``, joined at the graph's end
+            with torch.cuda.stream(self._pp_stream):
+                self._pp_stream.wait_event(fork)
+                window.build(sc[1].key, self.ray_offset, n, bq["rays"][:n], bq["dgt"][:n], bq["valid"][:n], None,
+                             bq["far"], dev_step=self.dev_step_next)
+                if sample_next:
+                    ss = L.stream(st.device)
+                    if cfg.sampler == "OGM":
+                        L.call("lnr_sample_ogm", bq["rays"][:n], n, self.S, st.occ, cfg.occ_res, cfg.perturb, None,
+                               None, sc[1].key, self.ray_offset, bq["z"], self.dev_step_next, ss)
+                    else:
+                        L.call("lnr_sample_uniform", bq["rays"][:n], n, self.S, cfg.perturb, None, sc[1].key,
+                               self.ray_offset, bq["z"], self.dev_step_next, ss)
+                self._gjoin.record(self._pp_stream)
+
         def body():
             main = torch.cuda.current_stream(st.device)
-            if prefetch:
+            if prefetch and self.pipe_at == "start":
                 self._gfork.record(main)
-                with torch.cuda.stream(self._pp_stream):
-                    self._pp_stream.wait_event(self._gfork)
-                    window.build(sc[1].key, self.ray_offset, n, bq["rays"][:n], bq["dgt"][:n], bq["valid"][:n], None,
-                                 bq["far"], dev_step=self.dev_step_next)
-                    if sample_next:
-                        ss = L.stream(st.device)
-                        if cfg.sampler == "OGM":
-                            L.call("lnr_sample_ogm", bq["rays"][:n], n, self.S, st.occ, cfg.occ_res, cfg.perturb, None,
-                                   None, sc[1].key, self.ray_offset, bq["z"], self.dev_step_next, ss)
-                        else:
-                            L.call("lnr_sample_uniform", bq["rays"][:n], n, self.S, cfg.perturb, None, sc[1].key,
-                                   self.ray_offset, bq["z"], self.dev_step_next, ss)
-                    self._gjoin.record(self._pp_stream)
+                branch(self._gfork)
             if have < 1:
                 window.build(sc[0].key, self.ray_offset, n, b["rays"][:n], b["dgt"][:n], b["valid"][:n], None, b["far"],
                              dev_step=self.dev_step)
             out = self.step(b["rays"][:n], b["dgt"][:n], global_step, iteration_idx, scale=window.scale,
                             far_ref=b["far"], n_rays_global=n_glob, update_ogm=ogm, presampled=have >= 2,
                             dev_step=self.dev_step, fork_count=prefetch)
+            if prefetch and self.pipe_at != "start":  # (LONER_PIPE_AT: after the encode or the field kernels)
+                branch(self._pp_mid)
             if prefetch:
                 main.wait_event(self._gjoin)
             return out

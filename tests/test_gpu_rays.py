@@ -251,13 +251,15 @@ def test_graph_replay_equals_eager(L, zero):
     eager path's losses, parameters, moments, occupancy grid and samples, across OGM steps (their own
     graph), a skipped global step, a changed iteration index / learning-rate factor and a second window
     (the graphs are re-captured), with and without the in-graph prefetch of the next step's rays and
-    samples; also with the sharded optimiser's one-rank share (bench --shard-of)."""
+    samples (forked at the step's start, or after its encode or field kernels: LONER_PIPE_AT); also with the
+    sharded optimiser's one-rank share (bench --shard-of)."""
     from loner_amd import step as S_
     from loner_amd.rays import RayWindow
     loss = S_.LossConfig.from_dict(dict(loss_selection="L1_LOS", decay_los_lambda=True, los_lambda=1000.0,
                                         los_lambda_decay_rate=1e-4, los_lambda_decay_steps=30))
     res = []
-    for graph, pipe in ((False, True), (True, True), (True, False)):
+    for graph, pipe, at in ((False, True, "start"), (True, True, "start"), (True, False, "start"), (True, True, "encode"),
+                            (True, True, "field")):
         st = S_.FieldState(S_.StepConfig(n_samples=64, occ_lr=1e-3, loss=loss), device="cuda:0", table_init=0.5)
         eng = None
         outs = []
@@ -266,7 +268,7 @@ def test_graph_replay_equals_eager(L, zero):
             win = RayWindow(scans, wc, rr, n_lidar=128, n_sky=16, strategy="MASK")
             if eng is None:
                 eng = S_.StepEngine(st, win.n_slots, seed=4, zero=zero)
-                eng.use_graph, eng.pipeline, eng.graph_prefetch = graph, pipe, pipe
+                eng.use_graph, eng.pipeline, eng.graph_prefetch, eng.pipe_at = graph, pipe, pipe, at
             st.reset_optimizer()
             for it, g in enumerate(steps):
                 eng.lr_factor = 0.97 ** it
