@@ -443,6 +443,14 @@ __global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_wave(SamplerArgs
 #ifndef LNR_GALLOP_CDF
 #define LNR_GALLOP_CDF 0
 #endif
+#ifndef LNR_SAMPLER_MERGE_FILL
+// the merge places the depths (each one's stratum count from the linspace, corrected by a short walk: no chain
+// of searches) and fills the other positions with the strata in order (a mark per position, a wave scan)
+#define LNR_SAMPLER_MERGE_FILL 1
+#endif
+#ifndef LNR_SAMPLER_CDF_LIFT
+#define LNR_SAMPLER_CDF_LIFT 1
+#endif
 #ifndef LNR_SAMPLER_LOOKUP_UNROLL
 #define LNR_SAMPLER_LOOKUP_UNROLL 4
 #endif
@@ -509,6 +517,18 @@ __device__ __forceinline__ int gallop_from(const float* arr, int lo, int n, floa
     else hi = mid;
   }
   return l2;
+}
+// #{j < N : !(arr[j] > x)} for ascending arr (upper_bound over [0, N)) by binary lifting: a fixed number of steps,
+// no branch, so several independent searches interleave their LDS reads
+template <int N>
+__device__ __forceinline__ int upper_count_lift(const float* arr, float x) {
+  int cnt = 0;
+#pragma unroll
+  for (int st = 1 << (31 - __builtin_clz(N)); st >= 1; st >>= 1) {
+    const int j = cnt + st;
+    if (j <= N && !(arr[j - 1] > x)) cnt = j;
+  }
+  return cnt;
 }
 __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_wave_barrier();
@@ -685,7 +705,11 @@ __global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_rank(SamplerArgs
     for (int q = 0; q < Q; ++q) {
       const float u = su[q];
       // the previous draw's answer, or the first cdf entry above u after it (the answer capped at H - 1)
-      lo = LNR_GALLOP_CDF ? gallop_from<true>(cdf, lo, H - 1, u) : upper_bound_from(cdf, lo, H - 1, u);
+      // (LNR_SAMPLER_CDF_LIFT: each draw's search from scratch, fixed steps, so the Q searches overlap; else
+      // walked on from the previous draw's answer)
+      lo = LNR_SAMPLER_CDF_LIFT ? upper_count_lift<H - 1>(cdf, u)
+           : LNR_GALLOP_CDF     ? gallop_from<true>(cdf, lo, H - 1, u)
+                                : upper_bound_from(cdf, lo, H - 1, u);
       const int below = lo - 1 > 0 ? lo - 1 : 0;
       const int above = lo < M ? lo : M;
       const float c0 = cdf[below], c1 = cdf[above];
@@ -706,7 +730,45 @@ __global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_rank(SamplerArgs
     wave_lds_fence();
     float* zr = a.z + r * (int64_t)(2 * H);
     LNR_STAMP(t4);
-    if (__all(strat_sorted && f_asc)) {
+    if (LNR_SAMPLER_MERGE_FILL && __all(strat_sorted && f_asc)) {
+      // 5. merge into out, then coalesced stores (out overlays the cdf and bins, whose reads ended before the
+      // fence above).  Depth j goes to j + #{strata <= it}: the strata are the linspace's jittered within their
+      // bins, so the count is the linspace position's, up to the stratum of the bin holding the depth (a walk
+      // of a step or two over the sorted strata makes it exact).  Stratum i goes to the i-th position no depth
+      // took (= i + #{depths < it}: the same merge, ties included): positions are marked in a bit per
+      // position (imp's words: the depths are in registers now), and a lane's E positions take their strata
+      // after a wave scan of the marks' counts.
+      uint32_t* mk = reinterpret_cast<uint32_t*>(imp);
+      constexpr int NW = 2 * H / 32;
+      for (int w = lane; w < NW; w += 64) mk[w] = 0u;
+      const float span = far - near;
+      const float per = span > 0.f ? (float)(H - 1) / span : 0.f;
+      wave_lds_fence();
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const float f = fq[q];
+        int e = (int)fminf(fmaxf((f - near) * per + 1.0f, 0.0f), (float)H);
+        while (e > 0 && strat[e - 1] > f) --e;
+        while (e < H && !(strat[e] > f)) ++e;
+        const int pos = lane * Q + q + e;
+        out[pos] = f;
+        atomicOr(&mk[pos >> 5], 1u << (pos & 31));
+      }
+      wave_lds_fence();
+      const uint32_t bits = (mk[(lane * E) >> 5] >> ((lane * E) & 31)) & (E >= 32 ? 0xFFFFFFFFu : ((1u << E) - 1u));
+      const uint32_t nd = (uint32_t)__popc(bits);
+      int k = lane * E - (int)(wave_incl_scan_u32(nd) - nd);  // the stratum of this lane's first free position
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if (!((bits >> e) & 1u)) {
+          out[lane * E + e] = strat[k];
+          ++k;
+        }
+      }
+      wave_lds_fence();
+#pragma unroll
+      for (int e = 0; e < E; ++e) zr[e * 64 + lane] = out[e * 64 + lane];
+    } else if (__all(strat_sorted && f_asc)) {
       // 5. merge by rank into out, then coalesced stores
       // (out overlays the cdf and bins, whose reads ended before the fence above)
       int js = 0, jt = 0;
