@@ -115,15 +115,38 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 // ------------------------------------------------------------------ wave / block reductions
-__device__ __forceinline__ float wave_sum(float v) {
+// The butterfly over lane distances 32, 16, 8, 4, 2, 1 (every lane ends with the total).  LNR_WAVE_RED_DPP: the
+// exchanges without LDS permutes: v_permlane32_swap / v_permlane16_swap (gfx950) for 32 and 16, DPP row_ror:8
+// for 8 (within a row, lane p + 8 mod 16 = p ^ 8), row_ror:4 for 4 (lane p + 4 mod 16 holds the same value as
+// p ^ 4 once the 8-apart lanes are equal), quad_perm for 2 and 1.  Each lane adds the same two values as the
+// __shfl_xor butterfly (operands at most swapped): bitwise the same sums (tools/ubench/ubench_permlane.hip).
+#ifndef LNR_WAVE_RED_DPP
+#define LNR_WAVE_RED_DPP 0
+#endif
+template <class Op>
+__device__ __forceinline__ float wave_butterfly(float v, Op op) {
+  if (LNR_WAVE_RED_DPP) {
+    const uint32_t b = __float_as_uint(v);
+    const auto r32 = __builtin_amdgcn_permlane32_swap(b, b, false, false);  // {lanes 0-31, lanes 32-63} in both halves
+    v = op(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
+    const uint32_t c = __float_as_uint(v);
+    const auto r16 = __builtin_amdgcn_permlane16_swap(c, c, false, false);  // {even row, odd row} of each row pair
+    v = op(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
+    v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false)));  // row_ror:8
+    v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false)));  // row_ror:4
+    v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false)));   // quad [2,3,0,1]
+    v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false)));   // quad [1,0,3,2]
+    return v;
+  }
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  for (int o = 32; o >= 1; o >>= 1) v = op(v, __shfl_xor(v, o, 64));
   return v;
 }
+__device__ __forceinline__ float wave_sum(float v) {
+  return wave_butterfly(v, [](float x, float y) { return x + y; });
+}
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_butterfly(v, [](float x, float y) { return fmaxf(x, y); });
 }
 
 // Max of a NON-NEGATIVE float over the wave on DPP (row shifts, row_bcast15/31: no LDS permutes),
