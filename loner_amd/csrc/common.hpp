@@ -119,9 +119,10 @@ __device__ __forceinline__ void lds_barrier() {
 // exchanges without LDS permutes: v_permlane32_swap / v_permlane16_swap (gfx950) for 32 and 16, DPP row_ror:8
 // for 8 (within a row, lane p + 8 mod 16 = p ^ 8), row_ror:4 for 4 (lane p + 4 mod 16 holds the same value as
 // p ^ 4 once the 8-apart lanes are equal), quad_perm for 2 and 1.  Each lane adds the same two values as the
-// __shfl_xor butterfly (operands at most swapped): bitwise the same sums (tools/ubench/ubench_permlane.hip).
+// __shfl_xor butterfly (operands at most swapped): bitwise the same sums (tools/ubench/ubench_permlane.hip; C2 loss
+// bit-identical, field stage 0.244-0.246 -> 0.242 ms).
 #ifndef LNR_WAVE_RED_DPP
-#define LNR_WAVE_RED_DPP 0
+#define LNR_WAVE_RED_DPP 1
 #endif
 template <class Op>
 __device__ __forceinline__ float wave_butterfly(float v, Op op) {
