@@ -63,6 +63,15 @@ def parse():
     ap.add_argument("--shard-of", type=int, default=None, metavar="N",
                     help="one GPU runs rank 0's shard of the config's batch split N ways (the per-rank step of an "
                          "N-GPU strong-scaling run, without the collective): the shard floor (C4, N in 2/4/8)")
+    ap.add_argument("--field", default=None, choices=["init", "trained"],
+                    help="init: time steps from the tcnn-like random init; trained (default with --rays device, "
+                         "not C5): first time the from-init steps (kept under 'from_init'), then pre-train the field "
+                         "untimed along the synthetic trajectory as the north-star driver does (shuffled windows of "
+                         "the config's keyframe count, a new Adam per window, --pretrain-iters steps each, OGM on), "
+                         "then time --steps on the bench window: the regime the driver spends its steps in")
+    ap.add_argument("--pretrain-windows", type=int, default=12)
+    ap.add_argument("--pretrain-iters", type=int, default=32,
+                    help="steps per pre-training window (examples/fdt_optimize_implicit_map.py:76 NUM_ITERATIONS)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rays", type=int, default=512, help="rays per reduced-config CPU-baseline step (x512 samples)")
     ap.add_argument("--cpu-steps", type=int, default=24)
@@ -507,6 +516,39 @@ def _camera_stages(eng, fr, rays, inten, L):
     return {ev[i][0]: float(ev[i][1].elapsed_time(ev[i + 1][1])) for i in range(len(ev) - 1)}
 
 
+def pretrain(eng, state, kind, n_kf, rpk, spk, strat, dev, r_glob, g_start, n_windows, iters, pool_size=48):
+    """Untimed pre-training of the benched field in the north-star driver's regime
+    (examples/fdt_optimize_implicit_map.py:576-616): the trajectory's keyframes are shuffled once per
+    repetition and cut into windows of ``n_kf`` (MAX_WINDOW_LENGTH_LIDAR = 16 at C2); each window is a new
+    Adam (optimizer.py:255-265) run for ``iters`` (NUM_ITERATIONS = 32) steps through the same engine, rays
+    selected and built on the GPU, the OGM updated every N_iters_acc global steps.  The keyframe pool is
+    ``pool_size`` poses of the config's synthetic trajectory (the quad loop's 48 poses include every pose
+    of the bench window).  Returns (the next global step, a description for the bench line)."""
+    from loner_amd import synthetic as syn
+    from loner_amd.rays import RayWindow
+    pool = syn.make_window(kind, pool_size, seed=2000)
+    rng = np.random.default_rng(5)
+    order, g = [], g_start
+    for _ in range(n_windows):
+        while len(order) < n_kf:
+            order += list(rng.permutation(pool_size))
+        idx, order = order[:n_kf], order[n_kf:]
+        win = RayWindow([pool[i] for i in idx], syn.world_cube(kind), syn.SENSORS[kind]["ray_range"], n_lidar=rpk,
+                        n_sky=spk, strategy=strat, device=dev)
+        state.reset_optimizer()
+        for it in range(iters):
+            eng.step_window(win, global_step=g, iteration_idx=it, n_rays_global=r_glob)
+            g += 1
+        eng.release()
+        del win
+    torch.cuda.synchronize()
+    return g, {"windows": n_windows, "iterations_per_window": iters, "steps": n_windows * iters,
+               "keyframes_per_window": n_kf, "pool": f"{pool_size} poses of the synthetic {kind} trajectory, shuffled "
+                                                    "per repetition (the driver's SCHUFFLE)",
+               "adam": "new per window", "ogm": "updated every N_iters_acc = 10 global steps",
+               "global_step_after": g}
+
+
 def _free_port():
     import socket
     with socket.socket() as s:
@@ -598,6 +640,7 @@ def main():
         scans, cube, submap = syn.submap_window(rank, nkf, seed=1000 + rank)
         window = RayWindow(scans, cube, syn.SENSORS[kind]["ray_range"], n_lidar=rpk, n_sky=spk, strategy=strat,
                            device=dev)
+        win_kf = len(scans)
         del scans
         if not window.all_valid:
             raise RuntimeError("bench window must give a fixed batch")
@@ -610,6 +653,7 @@ def main():
         scans = syn.make_window(kind, nkf, seed=1000)
         window = RayWindow(scans, syn.world_cube(kind), syn.SENSORS[kind]["ray_range"], n_lidar=rpk, n_sky=spk,
                            strategy=strat, device=dev)
+        win_kf = len(scans)
         del scans
         if not window.all_valid or window.n_slots % args.shard_of:
             raise RuntimeError("bench window must give a fixed, evenly sharded batch")
@@ -621,6 +665,7 @@ def main():
         scans = syn.make_window(kind, nkf if args.scaling == "strong" else nkf * world, seed=1000)
         window = RayWindow(scans, syn.world_cube(kind), syn.SENSORS[kind]["ray_range"], n_lidar=rpk, n_sky=spk,
                            strategy=strat, device=dev)
+        win_kf = len(scans)
         del scans
         if not window.all_valid or window.n_slots % world:
             raise RuntimeError("bench window must give a fixed, evenly sharded batch")
@@ -660,39 +705,66 @@ def main():
     if args.shard_of:
         r_glob = R * args.shard_of
 
-    def run(i, prof=None):
+    if args.field is None:
+        args.field = "trained" if args.rays == "device" and not replicas else "init"
+    if args.field == "trained" and (args.rays != "device" or replicas):
+        raise SystemExit("--field trained needs --rays device and a sharded/single config (not C5)")
+
+    def run(i, prof=None, g0=0):
+        # g0: the global step the timed window starts at; the iteration index within the window drives the
+        # depth-eps decay as in the driver's windows (optimizer.py:781-785)
         if args.rays == "device":
-            return eng.step_window(window, global_step=i, n_rays_global=r_glob, prof=prof)
+            return eng.step_window(window, global_step=g0 + i, iteration_idx=i if g0 else 0, n_rays_global=r_glob,
+                                   prof=prof)
         rays, dgt = batches[i % len(batches)]
         return eng.step(rays, dgt, global_step=i, scale=scale, far_ref=far_ref[i % len(batches)],
                         n_rays_global=r_glob, prof=prof)
 
-    for i in range(args.warmup):
-        run(i)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.warmup, args.warmup + args.steps):
-        out = run(i)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if dist is not None:
-        dist.barrier()
-    elapsed = t1 - t0
-    if dist is not None:
-        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
-    loss = out.cpu().numpy()
-    # per-stage HIP events in a separate pass after the timed region (recording them costs host time:
-    # 47 us per step at C1, where the host issues the step faster than the GPU runs it only without them)
-    prof = {}
-    for i in range(args.warmup + args.steps, args.warmup + args.steps + PROF_STEPS):
-        run(i, prof)
-    torch.cuda.synchronize()
-    stage_ms = {k: float(np.mean([v[j].elapsed_time(v[j + 1]) for j in range(0, len(v), 2)])) for k, v in prof.items()}
+    def measure(g0=0):
+        """W untimed warm-up steps, then K timed steps (barrier + synchronize on both sides, the max over ranks),
+        then PROF_STEPS untimed steps with per-stage HIP events; returns (seconds, loss, stage ms, the fraction
+        of ray-samples whose dL/dsigma is exactly 0 in the profiled steps)."""
+        for i in range(args.warmup):
+            run(i, g0=g0)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.warmup, args.warmup + args.steps):
+            out = run(i, g0=g0)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if dist is not None:
+            dist.barrier()
+        elapsed = t1 - t0
+        if dist is not None:
+            e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            elapsed = float(e.item())
+        loss = out.cpu().numpy()
+        # per-stage HIP events in a separate pass after the timed region (recording them costs host time:
+        # 47 us per step at C1, where the host issues the step faster than the GPU runs it only without them)
+        prof = {}
+        zeros = torch.zeros(1, dtype=torch.float64, device=dev)
+        for i in range(args.warmup + args.steps, args.warmup + args.steps + PROF_STEPS):
+            run(i, prof, g0=g0)
+            zeros += (eng.d_sigma(R) == 0).sum()  # (after the step's events: outside every stage)
+        torch.cuda.synchronize()
+        stage = {k: float(np.mean([v[j].elapsed_time(v[j + 1]) for j in range(0, len(v), 2)])) for k, v in prof.items()}
+        return elapsed, loss, stage, float(zeros.item()) / (PROF_STEPS * R * n_samples)
+
+    elapsed, loss, stage_ms, zero_frac = measure()
+    from_init = None
+    if args.field == "trained":
+        from_init = {"ms_per_step": elapsed / args.steps * 1e3, "value": world * R * n_samples * args.steps / elapsed,
+                     "loss": float(loss[0]), "dsigma_zero_frac": zero_frac, "stage_ms": stage_ms}
+        t_pre = time.perf_counter()
+        g0, pre = pretrain(eng, state, kind, win_kf, rpk, spk, strat, dev, r_glob,
+                           args.warmup + args.steps + PROF_STEPS, args.pretrain_windows, args.pretrain_iters)
+        pre["seconds"] = time.perf_counter() - t_pre
+        state.reset_optimizer()  # the timed window: a new Adam (optimizer.py:255-265)
+        elapsed, loss, stage_ms, zero_frac = measure(g0)
 
     if rank != 0:
         if dist is not None:
@@ -730,7 +802,9 @@ def main():
         "dtype": "fp16 params/activations, fp32 accumulate+optimizer",
         "data": f"synthetic {kind} LiDAR scene (analytic ray-cast), "
                 + ("keyframe scans resident in HBM, rays selected + built on the GPU every step"
-                   if args.rays == "device" else "prebuilt rays resident in HBM") + "; random-init sigma field",
+                   if args.rays == "device" else "prebuilt rays resident in HBM")
+                + ("; sigma field pre-trained untimed along the synthetic trajectory (config.field_state)"
+                   if args.field == "trained" else "; random-init sigma field"),
         "config": {"workload": f"{args.config}: {nkf} KF x ({rpk} + {spk} sky) rays x {n_samples} samples "
                                + ("in total, split over the GPUs, " if args.scaling == "strong" else "per GPU, ")
                                + f"L=16 T=2^18 hash grid + 64-wide sigma MLP, {preset} loss (L1_JS)",
@@ -742,6 +816,11 @@ def main():
                    "launch": ("HIP graph replay (one graph per window and OGM-or-not step)"
                               if eng.use_graph and args.rays == "device" and eng.allreduce is None else
                               "eager, next step's ray build + sampling prefetched on a side stream"),
+                   "field_state": ("trained: the steps below follow %d untimed pre-training steps (config.pretrain)"
+                                   % pre["steps"] if args.field == "trained" else
+                                   "from init: tcnn-like U(+-1e-4) table, Xavier MLP, steps %d-%d after it"
+                                   % (args.warmup, args.warmup + args.steps - 1)),
+                   **({"pretrain": pre} if args.field == "trained" else {}),
                    **({"submap_rank0": submap} if submap is not None else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
@@ -770,6 +849,11 @@ def main():
                  "busy": busy, "busy_source": busy_src},
         "stage_ms": stage_ms,
         "loss": float(loss[0]),
+        # the fraction of ray-samples whose dL/dsigma is exactly 0 (alpha = 1 - exp(-delta relu(sigma + n)) with
+        # sigma + n <= 0, rendering_tcnn.py:252,260) over the profiled steps: they contribute exactly nothing
+        "dsigma_zero_frac": zero_frac,
+        # the same bench on the from-init field, timed first in this run (--field trained only)
+        **({"from_init": from_init} if from_init is not None else {}),
         # the process group as torch.distributed reports it (None: a single process, no group)
         "dist": ({"backend": dist.get_backend(), "ranks": dist.get_world_size()} if dist is not None else None),
     }

@@ -154,10 +154,22 @@ int lnr_hashgrid_fwd_rays_live_ws(const lnr_grid_desc* d, const float* rays, con
                                      parallelism: they only pick each level's power-of-two record scale,
                                      fp16 rounding is scale-invariant, and the fixed-point unit sits far
                                      below what reaches Adam */
+#define LNR_BWD_LIVE 8            /* lnr_hashgrid_bwd_rays_jac(_adam) with LNR_BWD_COUNTS_READY: the live backward.
+                                     A sample with d_sigma[n] == 0 (relu(sigma + noise) = 0, rendering_tcnn.py:260)
+                                     adds exactly 0 to every entry, so only samples with d_sigma != 0 emit records
+                                     (coherent levels: only runs holding one), after a histogram pass over those
+                                     samples; the fixed-point units still follow the forward's (every sample's)
+                                     histogram, so d_table is BITWISE the full backward's.  Pays when most samples
+                                     are dead (a trained field: ~80 % at C2); ignored where the level-looped scatter
+                                     does not apply (small batches, other grids). */
 int64_t lnr_hashgrid_bwd_workspace_bytes(const lnr_grid_desc* d, int64_t n);
 /* Device address of the n_levels per-level max |d_enc| floats inside `workspace` (the same for
  * every n: the workspace's first bytes). */
 float* lnr_hashgrid_bwd_level_max(const lnr_grid_desc* d, int64_t n, void* workspace);
+/* Device address of the last backward's bucket segment starts inside `workspace` (n_buckets + 1 uint64,
+ * buckets = the levels' 4096-entry table chunks in level order; the last is the number of records the
+ * scatter placed): for tests and tools that measure the record volume (e.g. of the live backward). */
+const uint64_t* lnr_hashgrid_bwd_seg_start(const lnr_grid_desc* d, int64_t n, void* workspace);
 int lnr_hashgrid_bwd(const lnr_grid_desc* d, const float* pos01, int64_t n, const float* d_enc,
                      int64_t enc_stride, float* d_table, const uint16_t* table, float* d_pos, void* workspace,
                      int64_t workspace_bytes, int32_t flags, void* stream);
@@ -326,6 +338,9 @@ int64_t lnr_field_train_workspace_words(int64_t n_rays, int32_t n_samples);
  * J = d sigma / d enc as level-major fp16 pairs, one uint32 per (level, sample), so that
  * d_enc = d_sigma * J with d_sigma the (n_rays, n_samples) fp32 dL/dsigma this call leaves at
  * workspace + lnr_dw_workspace_words(n_rays); lnr_hashgrid_bwd_rays_jac takes both (half the bytes).
+ * J is written only for the 32-sample tile pairs holding a sample with d_sigma != 0: elsewhere d_enc is 0
+ * whatever J is, and the J entries keep stale values (every consumer of the pair forms d_sigma * J as 0 where
+ * d_sigma == 0).  The MLP gradient is bitwise the one with every pair computed (a dead pair adds exact zeros).
  * workspace: lnr_field_train_workspace_words(n_rays, n_samples) fp32 words. */
 int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, const float* rays, const float* z,
                     const float* depth_gt, int64_t n_rays, int32_t n_samples, float noise_std, const float* noise,

@@ -24,6 +24,7 @@ RENDER_STRATEGIES = {"default": 0, "adjusted": 1}
 BWD_COUNTS_READY = 1
 BWD_NO_ACCUM = 2
 BWD_LEVEL_MAX_READY = 4
+BWD_LIVE = 8  # the live backward: records only for samples with d_sigma != 0 (bitwise the full one)
 
 c_p = ctypes.c_void_p
 c_i64 = ctypes.c_int64
@@ -123,6 +124,7 @@ _SIGNATURES = {
                                              c_i64, c_p]),
     "lnr_hashgrid_bwd_workspace_bytes": (c_i64, [ctypes.POINTER(GridDesc), c_i64]),
     "lnr_hashgrid_bwd_level_max": (c_p, [ctypes.POINTER(GridDesc), c_i64, c_p]),
+    "lnr_hashgrid_bwd_seg_start": (c_p, [ctypes.POINTER(GridDesc), c_i64, c_p]),
     "lnr_hashgrid_bwd": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64,
                                         c_i32, c_p]),
     "lnr_hashgrid_bwd_rays": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_p,

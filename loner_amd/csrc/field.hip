@@ -1177,12 +1177,40 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(LNR_MLP
     }
   }
 #else
-  Pre pa;
-  prefetch(n0, pa);
+  // A pair whose 32 d sigma are all 0 (relu(sigma + noise) = 0 for every sample: most pairs of a trained field's
+  // free space) adds exact zeros to dW1 and to the level maxima and nothing to dW0 (dw0_scale refuses a zero
+  // pair_max), and its d_enc is 0: it is skipped, its encodings not even loaded and its J not written (consumers
+  // form d sigma * J as 0 there, hashgrid.hpp GradJac).  So d sigma runs one pair ahead of the encodings: the
+  // next pair's are loaded only when its d sigma (loaded a pair earlier) has a non-zero.
+  auto load_ds = [&](int64_t m, float& d0, float& d1) {
+    const uint32_t mb = (uint32_t)((m < N ? m : 0) + c) * 4u;
+    d0 = ld_off(a.d_sigma, mb);
+    d1 = ld_off(a.d_sigma, mb + 64u);
+  };
+  auto load_enc = [&](int64_t m, Pre& p) {
+    const uint32_t mb = (uint32_t)((m < N ? m : 0) + c) * 4u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      p.x0[q] = ld_off(a.enc, row_e + (uint32_t)q * st4 + mb);
+      p.x1[q] = ld_off(a.enc, row_e + (uint32_t)q * st4 + mb + 64u);
+    }
+  };
+  (void)prefetch;
+  Pre pa{};
+  float nd0, nd1;
+  load_ds(n0, pa.d0, pa.d1);
+  bool la = n0 < N && __ballot(pa.d0 != 0.f || pa.d1 != 0.f) != 0ull;  // (wave-uniform)
+  if (la) load_enc(n0, pa);
+  load_ds(n0 + step, nd0, nd1);
   for (; n0 < N; n0 += step) {
     const Pre cur = pa;
-    prefetch(n0 + step, pa);
-    LNR_MLP_PAIR(n0, cur);
+    const bool lc = la;
+    pa.d0 = nd0;
+    pa.d1 = nd1;
+    la = n0 + step < N && __ballot(pa.d0 != 0.f || pa.d1 != 0.f) != 0ull;
+    if (la) load_enc(n0 + step, pa);
+    load_ds(n0 + 2 * step, nd0, nd1);
+    if (lc) LNR_MLP_PAIR(n0, cur);
   }
 #endif
 #undef LNR_MLP_PAIR

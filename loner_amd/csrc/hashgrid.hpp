@@ -207,6 +207,7 @@ typedef float gf32x2 __attribute__((ext_vector_type(2)));
 // the mask, the criterion of a forward that counted the histogram with it (lnr_hashgrid_fwd_rays_live_ws);
 // without one every sample may.
 struct GradF32 {
+  static constexpr bool kScaled = false;  // no per-sample scale: scale() is not dL/dsigma
   const float2* g;
   int64_t stride;
   const float* live = nullptr;
@@ -222,12 +223,18 @@ struct GradF32 {
   __device__ __forceinline__ float scale(int64_t) const { return 0.f; }
   __device__ __forceinline__ static float2 finish(const Raw& r, float) { return r; }
 };
+// A sample with dL/dsigma = 0 (relu(sigma + noise) = 0: alpha = 1 - exp(-delta relu(sigma + n)),
+// rendering_tcnn.py:252,260) has d_enc = 0 exactly, and its J is not written: the MLP backward skips the
+// 32-sample tile pairs whose d sigma are all 0 (k_mlp_bwd_tiles), so apply() returns 0 for s = 0 instead of
+// reading a stale J.
 struct GradJac {
+  static constexpr bool kScaled = true;  // scale(i) = dL/dsigma of sample i
   const uint32_t* jac;
   const float* dsig;
   int64_t stride;
   __device__ __forceinline__ static constexpr bool live_at(int64_t) { return true; }
   __device__ __forceinline__ static float2 apply(uint32_t h, float s) {
+    if (s == 0.f) return make_float2(0.f, 0.f);
     return make_float2((float)__builtin_bit_cast(_Float16, (uint16_t)(h & 0xFFFFu)) * s,
                        (float)__builtin_bit_cast(_Float16, (uint16_t)(h >> 16)) * s);
   }
@@ -561,7 +568,9 @@ struct BwdWorkspace {
   uint32_t* hist;        // per level l: [n_sb][nb_l] record counts -> exclusive offsets within bucket
   uint32_t* chunk_sum;   // [L][n_chunks][kMaxChunksPerLevel] per-chunk column sums (k_bwd_chunk_sums)
   float* level_max;      // [LNR_MAX_LEVELS] max |d_enc| per level (as uint bits: k_denc_level_max's atomicMax)
-  uint32_t* counts;      // [kMaxBuckets]
+  uint32_t* counts;      // [kMaxBuckets] records per bucket (the scatter's: placement, work split)
+  uint32_t* k2cnt;       // [kMaxBuckets] the count the fixed-point unit follows (bucket_k2): every sample's
+                         // records (the forward's histogram), also when the live backward places fewer
   uint64_t* seg_start;   // [kMaxBuckets + 1]
   long long* partial;    // [2 kAccumGroups][2 * kChunk] int64 fixed-point partial sums of cut buckets
   uint32_t* bucket_done; // [kMaxBuckets] pieces of a cut bucket accumulated so far (k_bwd_accum<true>)
@@ -577,7 +586,7 @@ inline int64_t bwd_n_chunks(int64_t n) { return (bwd_n_sb(n) + kRowsPerChunk - 1
 inline int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
 
 struct WsLayout {
-  int64_t hist, chunk_sum, level_max, counts, seg_start, partial, bucket_done, units, rec, total;
+  int64_t hist, chunk_sum, level_max, counts, k2cnt, seg_start, partial, bucket_done, units, rec, total;
 };
 
 inline WsLayout ws_layout(const lnr_grid_desc* d, const GridArgs& a, int64_t n) {
@@ -588,6 +597,7 @@ inline WsLayout ws_layout(const lnr_grid_desc* d, const GridArgs& a, int64_t n) 
   w.hist = b;      b += align256((int64_t)a.n_buckets * nsb * 4);
   w.chunk_sum = b; b += align256((int64_t)d->n_levels * nch * kMaxChunksPerLevel * 4);
   w.counts = b;    b += align256(kMaxBuckets * 4);
+  w.k2cnt = b;     b += align256(kMaxBuckets * 4);
   w.seg_start = b; b += align256((kMaxBuckets + 1) * 8);
   w.partial = b;   b += align256((int64_t)2 * kAccumGroups * 2 * kChunk * 8);
   w.bucket_done = b; b += align256(kMaxBuckets * 4);
@@ -608,6 +618,7 @@ inline BwdWorkspace carve_workspace(void* base, const GridArgs& a, const lnr_gri
   w.chunk_sum = reinterpret_cast<uint32_t*>(p + L.chunk_sum);
   w.level_max = reinterpret_cast<float*>(p + L.level_max);
   w.counts = reinterpret_cast<uint32_t*>(p + L.counts);
+  w.k2cnt = reinterpret_cast<uint32_t*>(p + L.k2cnt);
   w.seg_start = reinterpret_cast<uint64_t*>(p + L.seg_start);
   w.partial = reinterpret_cast<long long*>(p + L.partial);
   w.bucket_done = reinterpret_cast<uint32_t*>(p + L.bucket_done);

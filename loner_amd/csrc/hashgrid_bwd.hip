@@ -168,12 +168,18 @@ __device__ __forceinline__ void build_units(UnitTable* ut, uint32_t b0, uint32_t
 
 // Bucket segment starts: exclusive prefix of the bucket totals (records are laid out bucket-major),
 // and the unit accumulation's work list over all buckets.
-__global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint32_t n_buckets) {
+// set_k2: the counts are every sample's records (the forward's histogram): they also set the fixed-point
+// units (ws.k2cnt); the live backward's counts do not (k_bwd_col_totals wrote ws.k2cnt before).
+__global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint32_t n_buckets, bool set_k2) {
   __shared__ uint64_t w_seg[16], w_units[16];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   uint64_t seg[2];  // two buckets per thread (n_buckets <= kMaxBuckets = 2048)
 #pragma unroll
   for (int q = 0; q < 2; ++q) seg[q] = 2 * t + q < (int)n_buckets ? ws.counts[2 * t + q] : 0u;
+  if (set_k2)
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      if (2 * t + q < (int)n_buckets) ws.k2cnt[2 * t + q] = (uint32_t)seg[q];
   uint64_t iseg = seg[0] + seg[1];
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -216,6 +222,84 @@ __global__ void __launch_bounds__(1024) k_bwd_units(BwdWorkspace ws, uint32_t b0
   uint64_t R = 0;
   for (int w = 0; w < 16; ++w) R += w_r[w];
   build_units(ws.units, b0, nb, cnt, R, w_units);
+}
+
+// ---------------------------------------------------------------- the live backward (LNR_BWD_LIVE)
+// A sample whose dL/dsigma is exactly 0 (relu(sigma + noise) = 0, rendering_tcnn.py:252,260: most of a trained
+// field's free-space samples) adds exactly 0 to every table entry.  The live backward places records only for the
+// live samples: fine levels emit a sample's records iff dL/dsigma != 0, coherent levels a run's records iff the run
+// holds a live lane, and a wave without a live lane skips all of its work.  Everything else is the full
+// backward's: the same rows, the same run merging over the same lanes (dead lanes add zeros), the same record
+// values, and the fixed-point unit of a bucket from every sample's count (ws.k2cnt, the forward's histogram), so
+// the int64 sums, and the gradient, are bitwise those of the full backward.
+
+// The forward's per-bucket totals over every sample (ws.k2cnt): the column sums of its histogram, from the
+// per-chunk sums when there are several chunks.  grid (L), one thread per bucket column.
+__global__ void __launch_bounds__(kMaxChunksPerLevel) k_bwd_col_totals(GridArgs a, BwdWorkspace ws) {
+  const uint32_t l = blockIdx.x, c = threadIdx.x;
+  const uint32_t nb = a.bucket_base[l + 1] - a.bucket_base[l];
+  if (c >= nb) return;
+  uint32_t tot = 0;
+  if (ws.n_chunks == 1) {
+    const uint32_t* col = ws.hist + (int64_t)a.bucket_base[l] * ws.n_sb + c;
+    for (int64_t r = 0; r < ws.n_sb; ++r) tot += col[r * nb];
+  } else {
+    const uint32_t* cs = ws.chunk_sum + (int64_t)l * ws.n_chunks * kMaxChunksPerLevel + c;
+    for (int64_t k = 0; k < ws.n_chunks; ++k) tot += cs[k * kMaxChunksPerLevel];
+  }
+  ws.k2cnt[a.bucket_base[l] + c] = tot;
+}
+
+// Whether lane's run [head_lane, lane] holds a live lane (wl: the wave's live lanes)
+__device__ __forceinline__ bool run_live(unsigned long long wl, const RunInfo& ri) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+  return (wl & upto & ~((1ull << ri.head_lane) - 1ull)) != 0ull;
+}
+
+// The live backward's histogram: one workgroup per row (the full backward's rows), every level, the records
+// k_bwd_scatter_rows<LIVE> places (above).  NL levels, the first NM coherent, at most NB buckets per level.
+template <class PosFn, int NL, int NM, int NB>
+__global__ void __launch_bounds__(kSB) k_bwd_count_live(GridArgs a, PosFn pos, int64_t n, const float* __restrict__ dsig,
+                                                        BwdWorkspace ws) {
+  __shared__ uint32_t hist[NL * NB];
+  const int64_t sb = blockIdx.x;
+  const int64_t i = sb * kSB + threadIdx.x;
+  const bool in = i < n;
+  const int64_t ic = in ? i : n - 1;
+  for (int t = threadIdx.x; t < NL * NB; t += kSB) hist[t] = 0u;
+  const bool live = in && dsig[ic] != 0.f;
+  const unsigned long long wl = __ballot(live);
+  lds_barrier();
+  if (wl) {  // (wave-uniform) a wave of dead samples emits nothing
+    float x = 0.f, y = 0.f, z = 0.f;
+    pos.eval(pos.load(ic), x, y, z);
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const LevelParams& lv = a.lv[l];
+      uint32_t* h = hist + l * NB;
+      if (l < NM) {
+        Corners c;
+        level_corners<true>(lv, x, y, z, c);
+        const RunInfo ri = cell_runs_dpp(in, c.cx, c.cy, c.cz);
+        if (in && ri.tail && run_live(wl, ri)) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) atomicAdd(&h[(c.idx[k] - lv.offset) >> kChunkLog2], 1u);
+        }
+      } else {
+        FineCell c;
+        fine_cell(lv, x, y, z, c);
+        count_fine_add(c, live, h);
+      }
+    }
+  }
+  lds_barrier();
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    const uint32_t nb = a.bucket_base[l + 1] - a.bucket_base[l];
+    uint32_t* row = hist_row(a, ws, l, sb);
+    for (uint32_t b = threadIdx.x; b < nb; b += kSB) row[b] = hist[l * NB + b];
+  }
 }
 
 // One workgroup per (histogram row, level): kSB samples, up to 8 records each (hashgrid.hpp).
@@ -504,7 +588,9 @@ struct RowsLds {  // the small tables first: their addresses fit the 16-bit LDS 
 // compile-time, so the level loop unrolls into straight-line code.  Record slots are 32-bit (the
 // launcher checks 8 N L < 2^32).
 // The body walks levels [LB, LB + NL) of histogram row sb (local level l is level LB + l).
-template <class PosFn, class GradFn, int LB, int NL, int NM, int NB, int kRowsStages>
+// LIVE (GradJac only): the live backward (k_bwd_count_live above): records only for samples with dL/dsigma != 0
+// (coherent levels: runs holding one), and a wave without a live lane skips its loads and corner work.
+template <class PosFn, class GradFn, int LB, int NL, int NM, int NB, int kRowsStages, bool LIVE = false>
 __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& sm, const GridArgs& a, const PosFn& pos,
                                                   int64_t n, const GradFn& grad, const BwdWorkspace& ws, bool skip_zero,
                                                   int64_t sb) {
@@ -525,12 +611,21 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
   if (threadIdx.x < 2 * NB) (&sm.ctr[0][0])[threadIdx.x] = 0u;
   // prologue 2: every global load of the kernel
   const typename PosFn::Raw raw = pos.load(ic);
-  typename GradFn::Raw g[NL];  // (GradJac: the fp16 pair, scaled by d sigma at use: half the registers)
-#pragma unroll
-  for (int l = 0; l < NL; ++l) g[l] = grad.load_raw_nt(LB + l, ic);  // read once: nontemporal, so they do not
-                                                                // displace the runs' L2 lines
+  static_assert(!LIVE || GradFn::kScaled, "the live backward takes its criterion from dL/dsigma");
   const float gsc = grad.scale(ic);
   const bool live = grad.live_at(ic);  // (GradF32's live mask, when the forward counted with it)
+  // LIVE: this lane's sample has dL/dsigma != 0, and the wave's live lanes (wave-uniform)
+  const bool lv_live = in && (!GradFn::kScaled || gsc != 0.f);
+  const unsigned long long wl = LIVE ? __ballot(lv_live) : ~0ull;
+  typename GradFn::Raw g[NL];  // (GradJac: the fp16 pair, scaled by d sigma at use: half the registers)
+  if (!LIVE || wl) {
+#pragma unroll
+    for (int l = 0; l < NL; ++l) g[l] = grad.load_raw_nt(LB + l, ic);  // read once: nontemporal, so they do not
+                                                                  // displace the runs' L2 lines
+  } else {
+#pragma unroll
+    for (int l = 0; l < NL; ++l) g[l] = typename GradFn::Raw{};
+  }
   uint32_t h0[2][2], h1[2][2];
   uint64_t seg[2][2];
 #pragma unroll
@@ -624,7 +719,7 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
 #else
     const float2 gv = in ? gl : make_float2(0.f, 0.f);
 #endif
-    const bool act = in && live && (!skip_zero || gv.x != 0.f || gv.y != 0.f);
+    const bool act = LIVE ? lv_live : in && live && (!skip_zero || gv.x != 0.f || gv.y != 0.f);
     const float rs = LNR_PRESCALE ? 1.0f : rsc[l];
     // rank (returning LDS atomics) and place: all start reads, then all atomics, then all writes
     // (one lane-level branch for the 4 records: they share their validity)
@@ -661,7 +756,9 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
     };
     uint32_t bk4[4], w4[4];
     float2 val4[4];
-    if (l >= NM) {  // fine: one record per x-pair (hashgrid.hpp "Backward records")
+    if (LIVE && !wl) {
+      // (wave-uniform) LIVE: no live lane, nothing to place
+    } else if (l >= NM) {  // fine: one record per x-pair (hashgrid.hpp "Backward records")
       FineCell c;
       fine_cell(lv, x, y, z, c);
       const bool split = c.d >= (uint32_t)kChunk;
@@ -694,7 +791,7 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
       RunInfo ri;
       float v[16];
       coherent_run_values(c, in, gv.x, gv.y, ri, v);
-      const bool valid = in && ri.tail;
+      const bool valid = in && ri.tail && (!LIVE || run_live(wl, ri));
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -721,12 +818,13 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
   if (kRowsStages == 2) copy_out(NL - 1);
 }
 
-template <class PosFn, class GradFn, int NL, int NM, int NB>
+template <class PosFn, class GradFn, int NL, int NM, int NB, bool LIVE = false>
 __global__ void __launch_bounds__(kSB)
 __attribute__((amdgpu_waves_per_eu(rows_waves<GradFn, NB>(), rows_waves<GradFn, NB>())))
 k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace ws, bool skip_zero) {
   __shared__ RowsLds<NL, NB, rows_stages<GradFn, NB>()> sm;
-  scatter_rows_body<PosFn, GradFn, 0, NL, NM, NB>(sm, a, pos, n, grad, ws, skip_zero, xcd_row(blockIdx.x, gridDim.x));
+  scatter_rows_body<PosFn, GradFn, 0, NL, NM, NB, rows_stages<GradFn, NB>(), LIVE>(sm, a, pos, n, grad, ws, skip_zero,
+                                                                                  xcd_row(blockIdx.x, gridDim.x));
 }
 
 constexpr size_t kScatterLds = (size_t)kCap * 4 + kMaxChunksPerLevel * 8 + (size_t)kCap * 4 + kMaxChunksPerLevel * 4 +
@@ -767,8 +865,10 @@ constexpr int kAccumThreads = LNR_ACCUM_THREADS;
 // level's largest possible record at C2's bucket sizes.  (Precision here matters beyond the
 // gradients' own: Adam's eps = 1e-8 turns a one-unit difference of a near-zero gradient entry into
 // a visible step, so two runs must round alike far below the gradients' scale.)
+// cnt is the bucket's count over every sample (ws.k2cnt: the forward's histogram), not the records the live
+// backward places (ws.counts), so the unit, and with it every rounding, is the same in both backwards.
 __device__ __forceinline__ int bucket_k2(const BwdWorkspace& ws, uint32_t b) {
-  const uint64_t bcnt = ws.seg_start[b + 1] - ws.seg_start[b];
+  const uint64_t bcnt = ws.k2cnt[b];
   const int lg = 64 - __clzll((long long)(bcnt > 0 ? bcnt : 1));  // ceil-ish log2(cnt + 1)
   return 47 - lg < 36 ? 47 - lg : 36;
 }
@@ -1454,10 +1554,6 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, Gra
                 who);
     hipLaunchKernelGGL(k_denc_level_max<GradFn>, dim3(kMaxBlocks, d->n_levels), dim3(256), 0, st, grad, n, w);
   }
-  if (w.n_chunks > 1)
-    hipLaunchKernelGGL(k_bwd_chunk_sums, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
-  hipLaunchKernelGGL(k_bwd_scan_rows, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
-  hipLaunchKernelGGL(k_bwd_scan_buckets, dim3(1), dim3(1024), 0, st, w, a.n_buckets);
   const uint32_t m = a.merge_levels, L = d->n_levels;
   bool all_fine = true, pow2 = true;
   uint32_t maxnb = 0;
@@ -1473,7 +1569,39 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, Gra
   // workgroup each walking 16 levels in sequence): one workgroup per (row, level) instead.
   const bool rows = L == 16 && all_fine && pow2 && 8 * n * (int64_t)L + 2 < (int64_t(1) << 32) &&
                     w.n_sb >= scatter_rows_min();
-  if (rows && m >= 3 && m <= 7 && maxnb <= 64) {
+  const bool rows64 = rows && m >= 3 && m <= 7 && maxnb <= 64;
+  // the live backward (LNR_BWD_LIVE): dL/dsigma-scaled gradients, the forward's histogram for the units, the
+  // level-looped scatter; otherwise the flag is ignored (the full backward: bitwise the same gradient)
+  const bool live = (flags & LNR_BWD_LIVE) && GradFn::kScaled && (flags & LNR_BWD_COUNTS_READY) && rows64;
+  if (w.n_chunks > 1)
+    hipLaunchKernelGGL(k_bwd_chunk_sums, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
+  if (live) {
+    if constexpr (GradFn::kScaled) {
+      // every sample's bucket totals (the fixed-point units), then the live records' histogram in its place
+      hipLaunchKernelGGL(k_bwd_col_totals, dim3(d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
+      auto cnt = m == 3   ? k_bwd_count_live<PosFn, 16, 3, 64>
+                 : m == 4 ? k_bwd_count_live<PosFn, 16, 4, 64>
+                 : m == 5 ? k_bwd_count_live<PosFn, 16, 5, 64>
+                 : m == 6 ? k_bwd_count_live<PosFn, 16, 6, 64>
+                          : k_bwd_count_live<PosFn, 16, 7, 64>;
+      hipLaunchKernelGGL(cnt, dim3((unsigned)w.n_sb), dim3(kSB), 0, st, a, pos, n, grad.dsig, w);
+      if (w.n_chunks > 1)
+        hipLaunchKernelGGL(k_bwd_chunk_sums, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a,
+                           w);
+    }
+  }
+  hipLaunchKernelGGL(k_bwd_scan_rows, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
+  hipLaunchKernelGGL(k_bwd_scan_buckets, dim3(1), dim3(1024), 0, st, w, a.n_buckets, !live);
+  if (live) {
+    if constexpr (GradFn::kScaled) {
+      auto kern = m == 3   ? k_bwd_scatter_rows<PosFn, GradFn, 16, 3, 64, true>
+                  : m == 4 ? k_bwd_scatter_rows<PosFn, GradFn, 16, 4, 64, true>
+                  : m == 5 ? k_bwd_scatter_rows<PosFn, GradFn, 16, 5, 64, true>
+                  : m == 6 ? k_bwd_scatter_rows<PosFn, GradFn, 16, 6, 64, true>
+                           : k_bwd_scatter_rows<PosFn, GradFn, 16, 7, 64, true>;
+      hipLaunchKernelGGL(kern, dim3((unsigned)w.n_sb), dim3(kSB), 0, st, a, pos, n, grad, w, skip_zero);
+    }
+  } else if (rows64) {
     auto kern = m == 3   ? k_bwd_scatter_rows<PosFn, GradFn, 16, 3, 64>
                 : m == 4 ? k_bwd_scatter_rows<PosFn, GradFn, 16, 4, 64>
                 : m == 5 ? k_bwd_scatter_rows<PosFn, GradFn, 16, 5, 64>
@@ -1679,6 +1807,11 @@ extern "C" int64_t lnr_hashgrid_bwd_workspace_bytes(const lnr_grid_desc* d, int6
 extern "C" float* lnr_hashgrid_bwd_level_max(const lnr_grid_desc* d, int64_t n, void* workspace) {
   if (d == nullptr || n < 0 || workspace == nullptr || check_desc_bwd(d, "lnr_hashgrid_bwd_level_max")) return nullptr;
   return carve_workspace(workspace, make_args(d), d, n).level_max;
+}
+
+extern "C" const uint64_t* lnr_hashgrid_bwd_seg_start(const lnr_grid_desc* d, int64_t n, void* workspace) {
+  if (d == nullptr || n < 0 || workspace == nullptr || check_desc_bwd(d, "lnr_hashgrid_bwd_seg_start")) return nullptr;
+  return carve_workspace(workspace, make_args(d), d, n).seg_start;
 }
 
 // The three backward entry points: d_table (optional: NULL = no table gradient) through the binned

@@ -81,7 +81,11 @@ class StepConfig:
 
 
 class FieldState:
-    """Parameters, Adam moments, fp16 shadow and the occupancy grid, resident on one GPU."""
+    """Parameters, Adam moments, fp16 shadow and the occupancy grid, resident on one GPU.
+
+    With a data-parallel or sharded ``StepEngine`` on this state, the last step's OGM update and shadow
+    all-gathers may still be pending on the device: call the engine's ``finish()`` (or ``drop_prefetch()`` /
+    ``release()``, which call it) before reading ``occ``, ``shadow`` or ``state_dict()`` directly."""
 
     def __init__(self, cfg: StepConfig, device="cuda", seed=1337, table_init=1e-4):
         self.cfg = cfg
@@ -336,6 +340,19 @@ class StepEngine:
         self._gpp = None  # what the last graph step prefetched for the next: window, want, parity, have
         self._capture_stream = torch.cuda.Stream(device=dev)
         self._gfork, self._gjoin = torch.cuda.Event(), torch.cuda.Event()
+        # The live backward (LNR_BWD_LIVE): a sample with dL/dsigma = 0 (relu(sigma + noise) = 0,
+        # rendering_tcnn.py:260) adds exactly 0 to the table gradient, and on a trained field most samples are such
+        # (~80 % at C2 after the driver's windows, bench.py --field trained; ~0 % in the first steps from init).
+        # The live backward places records only for the others, after a histogram pass over them: bitwise the
+        # full backward's gradient, so the choice is a matter of speed only.  LONER_LIVE_BWD: 1 always, 0 never,
+        # auto (default): every live_probe_every steps the share of zero dL/dsigma of the last step is read back
+        # asynchronously (no host sync: an event polled at the next steps), and the live backward runs while the
+        # share exceeds live_on (back to the full one below live_off).
+        self.live_bwd = {"0": False, "1": True}.get(os.environ.get("LONER_LIVE_BWD", "auto"), "auto")
+        self.live_on, self.live_off, self.live_probe_every = 0.35, 0.25, 16
+        self._live = self.live_bwd is True
+        self._probe_ev, self._probe_ctr, self._probe_n = None, self.live_probe_every, 1
+        self._probe_host = torch.zeros(1, dtype=torch.int64).pin_memory() if torch.cuda.is_available() else None
         self._pp_bufs = [dict(rays=self.rays if i == 0 else torch.empty_like(self.rays),
                               dgt=self.depth_gt if i == 0 else torch.empty_like(self.depth_gt),
                               valid=self.ray_valid if i == 0 else torch.empty_like(self.ray_valid),
@@ -497,7 +514,8 @@ class StepEngine:
         self._r_last = R
         # 5. hash-grid backward
         m(prof, "grid_bwd")
-        flags = (L.BWD_COUNTS_READY if self.count_in_forward else 0) | L.BWD_LEVEL_MAX_READY
+        flags = (L.BWD_COUNTS_READY if self.count_in_forward else 0) | L.BWD_LEVEL_MAX_READY | (
+            L.BWD_LIVE if self._live else 0)
         if self.zero is not None:
             return self._step_zero(rays, depth_gt, R, S, N, flags, s, scale, update_ogm, global_step, prof)
         if self.allreduce is None and self.compact_denc and (
@@ -618,6 +636,26 @@ class StepEngine:
             m(prof, "ogm")
         return self.loss_out
 
+    def live_probe(self, n_rays=None):
+        """LONER_LIVE_BWD=auto: pick the backward for the coming steps from the share of zero dL/dsigma (see
+        __init__).  Called after every step by step_window; a probe is a count of the last step's non-zero
+        dL/dsigma copied to pinned host memory behind an event, read when the event has completed."""
+        if self.live_bwd != "auto":
+            return
+        ev = self._probe_ev
+        if ev is not None and ev.query():
+            dead = 1.0 - float(self._probe_host[0]) / self._probe_n
+            self._live = dead > (self.live_off if self._live else self.live_on)
+            self._probe_ev = None
+        self._probe_ctr += 1
+        if ev is None and self._probe_ctr >= self.live_probe_every and self._probe_host is not None:
+            self._probe_ctr = 0
+            r = self._r_last if n_rays is None else n_rays
+            self._probe_host.copy_(torch.count_nonzero(self.d_sigma(r)).view(1), non_blocking=True)
+            self._probe_n = max(r * self.S, 1)
+            self._probe_ev = torch.cuda.Event()
+            self._probe_ev.record()
+
     def finish(self):
         """Order the current stream after the sharded optimiser's pending shadow all-gathers (the shadow is
         then whole again).  step() calls it before its encode; call it before reading the fp16 parameters
@@ -640,8 +678,9 @@ class StepEngine:
         if not self.compact_denc:
             return self.d_enc
         nl, n = self.cfg.n_levels, self._r_last * self.S
-        return (self.d_jac.view(torch.float16).view(nl, self.N, 2)[:, :n].float()
-                * self.d_sigma().view(1, n, 1))
+        ds = self.d_sigma().view(1, n, 1)
+        # (J is not written where a 32-sample pair's dL/dsigma are all 0: d_enc is 0 there, include/loner_amd.h)
+        return torch.where(ds == 0, 0.0, self.d_jac.view(torch.float16).view(nl, self.N, 2)[:, :n].float() * ds)
 
     def _grid_bwd(self, rays, R, S, N, flags, s):
         st = self.state
@@ -714,6 +753,7 @@ class StepEngine:
         self._pf_fork.record(main)  # the other buffer is free once everything enqueued so far is done
         out = self.step(pf["rays"], pf["dgt"], global_step, iteration_idx, scale=window.scale, far_ref=pf["far"],
                         n_rays_global=pf["n_glob"], prof=prof, **kw)
+        self.live_probe(pf["rays"].shape[0])
         if self.prefetch:
             nxt = None if n_rays_global is None else n_rays_global
             with torch.cuda.stream(self._pf_stream):
@@ -750,10 +790,14 @@ class StepEngine:
         self._pp_parity = parity
         # (the buffers of the step in flight: rays, depth_gt, ray_valid, far_ref and z as step() uses them)
         self.z, self.rays, self.depth_gt, self.ray_valid, self.far_ref = b["z"], b["rays"], b["dgt"], b["valid"], b["far"]
+        # the previous step's data-parallel OGM update (its SGD step, pending until the grid's next reader) lands
+        # before the fork: the prefetch below samples the grid on the side stream after waiting on this fork only
+        self._apply_pending_ogm()
         self._pp_fork.record(main)  # the other buffers are free once everything enqueued so far is done
         out = self.step(b["rays"][:n], b["dgt"][:n], global_step, iteration_idx, scale=window.scale, far_ref=b["far"],
                         n_rays_global=window.n_slots if n_rays_global is None else n_rays_global, prof=prof,
                         presampled=presampled, **kw)
+        self.live_probe(n)
         if not self.pipeline or prof is not None or "u_jitter" in kw or "u_pdf" in kw:
             return out  # (a profiled step keeps its stages apart)
         cfg = self.cfg
@@ -843,7 +887,7 @@ class StepEngine:
         # slower than a single-stream graph (C1 0.284 against 0.170 ms eager on one box): off by default
         prefetch = self.pipeline and self.graph_prefetch
         sample_next = prefetch and (cfg.sampler != "OGM" or not ogm)  # the OGM sampler reads the grid step k updates
-        gkey = (p, have, ogm, prefetch, n, self.ray_offset, n_glob, self.zero)
+        gkey = (p, have, ogm, prefetch, n, self.ray_offset, n_glob, self.zero, self._live)
         s = L.stream(st.device)
         sc = (L.StepScalars * 2)()
         sc[0] = self.step_scalars(global_step, iteration_idx)
@@ -893,6 +937,7 @@ class StepEngine:
             g.replay()
             st.adam_step += 1
             self._r_last = n
+            self.live_probe(n)
             return self.loss_out
         out = body()  # this step, eagerly
         saved = st.adam_step
@@ -908,6 +953,7 @@ class StepEngine:
         torch.cuda.current_stream(st.device).wait_stream(cs)
         st.adam_step = saved
         self._graphs[gkey] = g
+        self.live_probe(n)
         return out
 
     def _build_compact(self, window, global_step, n, n_rays_global, parity, stream):

@@ -1,0 +1,117 @@
+"""The live hash-grid backward (LNR_BWD_LIVE) on a trained field (GPU only).
+
+A sample whose dL/dsigma is exactly 0 (alpha = 1 - exp(-delta relu(sigma + n)) with sigma + n <= 0,
+/root/reference/src/models/rendering_tcnn.py:252,260) adds exactly 0 to every gradient.  On a field trained
+through the north-star driver's windowed schedule (examples/fdt_optimize_implicit_map.py:576-616: shuffled
+keyframe windows, a new Adam per window, src/mapping/optimizer.py:255-265, the OGM on) most samples are such.
+The live backward skips them: its records, and the MLP backward's dead tile pairs.  These tests pin that the
+step's table gradient, MLP gradient, Adam state, shadow and occupancy grid are BITWISE those of the full
+backward, over steps that include an OGM update, with the table's Adam separate and fused."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+N_KF, PER_KF, S = 4, 512, 512  # 2048 rays x 512 samples: 2048 histogram rows, the level-looped scatter
+
+
+@pytest.fixture(scope="module")
+def trained():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from loner_amd import step as S_
+    from loner_amd import synthetic as syn
+    from loner_amd.rays import RayWindow
+    dev = torch.device("cuda", 0)
+    cfg = S_.StepConfig(n_samples=S)
+    state = S_.FieldState(cfg, device=dev)
+    pool = syn.make_window("quad", 12, seed=2000)
+    rng = np.random.default_rng(3)
+    R = N_KF * PER_KF
+    eng = S_.StepEngine(state, R, seed=5)
+    eng.live_bwd, eng._live = False, False
+    g = 1
+    for _ in range(8):  # the driver's shuffled windows, 32 iterations each
+        idx = rng.choice(len(pool), N_KF, replace=False)
+        win = RayWindow([pool[i] for i in idx], syn.world_cube("quad"), syn.SENSORS["quad"]["ray_range"],
+                        n_lidar=PER_KF, device=dev)
+        state.reset_optimizer()
+        for it in range(32):
+            eng.step_window(win, global_step=g, iteration_idx=it)
+            g += 1
+        eng.release()
+    window = RayWindow(syn.make_window("quad", N_KF, seed=1000), syn.world_cube("quad"),
+                       syn.SENSORS["quad"]["ray_range"], n_lidar=PER_KF, device=dev)
+    torch.cuda.synchronize()
+    g = (g // 10 + 1) * 10 - 1  # the second of the three compared steps updates the OGM
+    return cfg, state.state_dict(), window, g
+
+
+def _records(L, eng):
+    """Records the last backward placed (the segment starts' last entry)."""
+    st = eng.state
+    nb = sum((int(st.desc.size[l]) + 4095) // 4096 for l in range(st.desc.n_levels))
+    p = L.lib().lnr_hashgrid_bwd_seg_start(L.ctypes.byref(st.desc), eng.N, L.ptr(eng.bwd_ws))
+    off = p - eng.bwd_ws.data_ptr()
+    return int(eng.bwd_ws[off:off + 8 * (nb + 1)].view(torch.int64)[nb].item())
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_live_backward_bitwise_on_trained_field(trained, fused):
+    from loner_amd import _lib as L
+    from loner_amd import step as S_
+    cfg, sd, window, g = trained
+    out = {}
+    for live in (False, True):
+        st = S_.FieldState(cfg, device="cuda")
+        st.load_state_dict(sd)
+        st.reset_optimizer()
+        eng = S_.StepEngine(st, window.n_slots, seed=9)
+        eng.live_bwd, eng._live = live, live
+        eng.fused_adam = fused
+        eng.pipeline, eng.use_graph = False, False
+        recs, zero = [], []
+        for k in range(3):
+            eng.step_window(window, global_step=g + k, iteration_idx=k)
+            torch.cuda.synchronize()
+            recs.append(_records(L, eng))
+            zero.append(float((eng.d_sigma() == 0).float().mean()))
+        eng.finish()
+        torch.cuda.synchronize()
+        o = {k: getattr(st, k).clone() for k in ("params", "m", "v", "shadow", "occ")}
+        o["grad_mlp"] = st.grad_mlp.clone()
+        o["loss"] = eng.loss_out.clone()
+        if not fused:
+            o["grad_table"] = st.table_gradient().clone()
+        out[live] = (o, recs, zero)
+    (full, rec_full, zero_full), (live, rec_live, zero_live) = out[False], out[True]
+    assert zero_full == zero_live
+    assert min(zero_live) > 0.5, f"the pre-trained field should leave most samples dead: {zero_live}"
+    for k in full:
+        assert torch.equal(full[k], live[k]), f"{k} differs between the full and the live backward"
+    # the live backward placed far fewer records (its histogram counts live samples only)
+    for rf, rl in zip(rec_full, rec_live):
+        assert rl < 0.6 * rf, (rec_full, rec_live)
+
+
+def test_live_probe_switches_modes(trained):
+    """LONER_LIVE_BWD=auto: the probe turns the live backward on for the trained field and off again for a
+    freshly initialised one (all samples live after its first steps)."""
+    from loner_amd import step as S_
+    cfg, sd, window, g = trained
+    st = S_.FieldState(cfg, device="cuda")
+    st.load_state_dict(sd)
+    eng = S_.StepEngine(st, window.n_slots, seed=9)
+    eng.live_bwd, eng._live = "auto", False
+    for k in range(4):
+        eng.step_window(window, global_step=g + k, iteration_idx=k)
+        torch.cuda.synchronize()
+    assert eng._live
+    fresh = S_.FieldState(cfg, device="cuda")
+    eng2 = S_.StepEngine(fresh, window.n_slots, seed=9)
+    eng2.live_bwd, eng2._live, eng2.live_probe_every = "auto", True, 1
+    for k in range(40):
+        eng2.step_window(window, global_step=1 + k, iteration_idx=k)
+        torch.cuda.synchronize()
+    assert not eng2._live
