@@ -18,16 +18,9 @@
 namespace lnr {
 
 // The encoding is written once, as whole lines, and read by the field kernels after this launch: a
-// nontemporal store keeps it out of the way of the table slices in L2 (step -0.01 ms at C2)
-#ifndef LNR_ENC_STORE_NT
-#define LNR_ENC_STORE_NT 1
-#endif
-__device__ __forceinline__ void store_enc(uint32_t* p, uint32_t v) {
-  if (LNR_ENC_STORE_NT)
-    __builtin_nontemporal_store(v, p);
-  else
-    *p = v;
-}
+// nontemporal store keeps it out of the way of the table slices in L2 (step -0.01 ms at C2; plain stores
+// re-measured in round 5 within the noise)
+__device__ __forceinline__ void store_enc(uint32_t* p, uint32_t v) { __builtin_nontemporal_store(v, p); }
 
 // The 8 corners of a fine (hashed, power-of-two) level: the x-pairs e, e ^ d of the four y/z edges.
 // What bounds this gather is the texture addresser: TA busy 0.78 of the launch at C2 with the level-grouped
@@ -208,37 +201,15 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
     }
     continue;
   }
-  // coherent levels below a.enc_run_levels: only the head lane of each run of lanes in one cell
-  // gathers the 8 corners, and the run's other lanes take them from it (ds_bpermute, the LDS
-  // crossbar), so the texture addresser sees one active lane per distinct cell; same values, so the
-  // encoding is bit-identical
-  const bool runs = l < a.enc_run_levels;  // block-uniform
+  // (the coherent levels' gathers once per run of lanes in one cell, handed to the run's lanes by ds_bpermute,
+  // measured no faster: the texture addresser charges the lanes' shared lines once either way; removed in round
+  // 6, history before commit e32a0b7)
 #pragma unroll
   for (int h = 0; h < kEncSpt; ++h) {
     Corners c;
     level_corners(lv, x[h], y[h], z[h], c);
     uint32_t* dst = enc + (int64_t)l * stride + i0 + h * H;
-    if (runs) {
-      const RunInfo ri = cell_runs_dpp(use[h], c.cx, c.cy, c.cz);
-      const bool head = ((ri.heads >> (threadIdx.x & 63)) & 1ull) != 0ull;
-      uint32_t v[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = (use[h] && head) ? table[c.idx[k]] : 0u;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = (uint32_t)__builtin_amdgcn_ds_bpermute(ri.head_lane << 2, (int)v[k]);
-      if (use[h]) {
-        float f0 = 0.f, f1 = 0.f;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          float2 t = half2_to_float2(v[k]);
-          f0 = fmaf(c.w[k], t.x, f0);
-          f1 = fmaf(c.w[k], t.y, f1);
-        }
-        store_enc(dst, (uint32_t)f2h(f0) | ((uint32_t)f2h(f1) << 16));
-      } else if (zero[h]) {
-        *dst = 0u;
-      }
-    } else if (use[h]) {
+    if (use[h]) {
       uint32_t v[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] = table[c.idx[k]];

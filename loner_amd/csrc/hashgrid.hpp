@@ -60,28 +60,7 @@ struct GridArgs {
   uint32_t n_levels;
   uint32_t n_buckets;
   uint32_t merge_levels;  // levels [0, merge_levels) merge equal corner indices across lanes
-  uint32_t accum_direct_level;  // the accumulation reads levels from this one on without its tile stage
-  uint32_t enc_run_levels;      // the encode's coherent levels below this gather once per run of lanes in a cell
 };
-
-// Levels from which the accumulation adds each thread's own records (no dealing through an LDS tile
-// stage: hashgrid_bwd.hip accum_records); LONER_ACCUM_DIRECT_LEVEL overrides (read per launch).
-#ifndef LNR_ACCUM_DIRECT_LEVEL
-#define LNR_ACCUM_DIRECT_LEVEL 99  // measured: 9 equal to off (C2 grid_bwd 0.969 vs 0.964 ms), 6 or 0 +0.21 ms (same-entry conflicts)
-#endif
-// Encode levels (of the coherent, non-fine ones) that gather once per run of lanes in one cell and
-// hand the corners to the run's lanes (k_hashgrid_fwd)
-#ifndef LNR_ENC_RUN_LEVELS
-#define LNR_ENC_RUN_LEVELS 0
-#endif
-inline uint32_t enc_run_levels() {
-  const char* e = getenv("LONER_ENC_RUN_LEVELS");
-  return e ? (uint32_t)atoi(e) : (uint32_t)LNR_ENC_RUN_LEVELS;
-}
-inline uint32_t accum_direct_level() {
-  const char* e = getenv("LONER_ACCUM_DIRECT_LEVEL");
-  return e ? (uint32_t)atoi(e) : (uint32_t)LNR_ACCUM_DIRECT_LEVEL;
-}
 
 // Levels whose cell edge spans several consecutive samples of a ray produce runs of equal corner
 // indices.  At the reference's 512 samples per ray (after the OGM has concentrated them) that holds
@@ -121,8 +100,6 @@ inline GridArgs make_args(const lnr_grid_desc* d, int32_t samples_per_ray = 0) {
   a.bucket_base[d->n_levels] = b;
   a.n_buckets = b;
   a.merge_levels = merge_levels_for(d, samples_per_ray);
-  a.accum_direct_level = accum_direct_level();
-  a.enc_run_levels = enc_run_levels();
   for (uint32_t l = 0; l < d->n_levels; ++l)
     a.lv[l].fine = (a.lv[l].hashed && a.lv[l].size_mask && l >= a.merge_levels) ? 1u : 0u;
   return a;

@@ -931,39 +931,26 @@ __device__ __forceinline__ uint32_t level_of_bucket(const GridArgs& a, uint32_t 
 // A pair record (p > 0) adds (1 - tx) v to corner e0 and tx v to e1 = e0 ^ (2^p - 1), a single
 // record (p = 0, tx = 0) adds v to e0.  int64 sums: the result does not depend on the order.
 // fs = 2^k2, the bucket's fixed-point scale (the records carry 2^k_l already).
-// DIRECT (levels >= GridArgs.accum_direct_level, block-uniform per bucket): no tile stage.  At the fine levels
-// consecutive records of a bucket come from consecutive samples of a row, whose cells are unrelated
-// (mean run of one cell ~1 sample from level 9 on), so a wave's atomic
-// instruction over 64 records 2 apart meets equal entries only by hash collision: each thread adds
-// the 2 records of its own 16-B load, with no stage write, no barriers and no stage reads.
-// LNR_ACCUM_REVERSE: tiles walked from the end of the range to its start (the int64 sums are order-free: the
-// same bits).  The scatter writes the highest rows last, so a range's last records are the most recently
-// written, the ones still in the Infinity Cache.
-#ifndef LNR_ACCUM_REVERSE
-#define LNR_ACCUM_REVERSE 0
-#endif
-#ifndef LNR_ACCUM_LOAD_NT
-#define LNR_ACCUM_LOAD_NT 1  // the record loads nontemporal (read once)
-#endif
+// (Measured and dropped, round 5: walking the tiles from the range's end, for the Infinity Cache, and plain
+// instead of nontemporal record loads, both within the noise; adding each thread's own records without the
+// tile stage from some level on, +0.21 ms at C2 from same-entry conflicts.  History before commit e32a0b7.)
 __device__ __forceinline__ void accum_records(unsigned long long* acc, uint2* stage, const BwdWorkspace& ws,
-                                              uint64_t beg, uint64_t end, float fs, bool direct = false) {
+                                              uint64_t beg, uint64_t end, float fs) {
   const int lane = threadIdx.x & 63;
   const uint64_t beg2 = beg & ~1ull;
   const float ftx = fs * kInvU16;
   const uint64_t n_tiles = (end - beg2 + kTile - 1) / kTile;
-  auto tix = [&](uint64_t t) { return LNR_ACCUM_REVERSE ? n_tiles - 1 - t : t; };  // (t < n_tiles)
   auto load_tile = [&](uint64_t tile) {  // this thread's 2 records of a tile: {w0, v0, w1, v1}
-    const uint64_t rr = beg2 + (tile < n_tiles ? tix(tile) : 0) * kTile + 2 * threadIdx.x;
-    const uint64_t rc = rr < end ? rr : beg2;  // unconditional loads
-    if (LNR_ACCUM_LOAD_NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(&ws.rec[rc]));
-    return *reinterpret_cast<const u32x4*>(&ws.rec[rc]);
+    const uint64_t rr = beg2 + (tile < n_tiles ? tile : 0) * kTile + 2 * threadIdx.x;
+    const uint64_t rc = rr < end ? rr : beg2;  // unconditional loads; read once: nontemporal
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(&ws.rec[rc]));
   };
   const uint32_t q0 = 32u * lane + 2u * (threadIdx.x >> 6);  // this lane's records in a tile
   auto run_tile = [&](uint64_t tile, const u32x4& cur) {
     lds_barrier();  // the previous tile's stage reads are done
     *reinterpret_cast<u32x4*>(&stage[stage_pos(2 * threadIdx.x)]) = cur;
     lds_barrier();
-    const uint64_t base = beg2 + tix(tile) * kTile;
+    const uint64_t base = beg2 + tile * kTile;
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const uint2 rec = stage[stage_pos(q0 + r)];
@@ -993,41 +980,6 @@ __device__ __forceinline__ void accum_records(unsigned long long* acc, uint2* st
       }
     }
   };
-  auto add_rec = [&](uint32_t w, uint32_t h) {
-    const float v0 = rec_v0(h), v1 = rec_v1(h);
-    const uint32_t e0 = w & (kChunk - 1);
-    const uint32_t p = (w >> kChunkLog2) & 15u;
-    const float tx = (float)(w >> 16) * ftx;
-    const float s0 = fs - tx;
-    atomicAdd(&acc[e0], fixed_i64(s0 * v0));
-    atomicAdd(&acc[kChunk + e0], fixed_i64(s0 * v1));
-    if (p) {
-#ifdef LNR_BWD_CHECK
-      if (p > kChunkLog2) __builtin_trap();
-#endif
-      const uint32_t e1 = e0 ^ ((1u << p) - 1u);
-      atomicAdd(&acc[e1], fixed_i64(tx * v0));
-      atomicAdd(&acc[kChunk + e1], fixed_i64(tx * v1));
-    }
-  };
-  if (direct) {
-    u32x4 buf[kAccumTrip];
-#pragma unroll
-    for (int d = 0; d < kAccumTrip; ++d) buf[d] = load_tile(d);
-    for (uint64_t tile = 0; tile < n_tiles; tile += kAccumTrip) {
-#pragma unroll
-      for (int d = 0; d < kAccumTrip; ++d) {
-        if (tile + d < n_tiles) {  // block-uniform
-          const u32x4 c = buf[d];
-          buf[d] = load_tile(tile + d + kAccumTrip);
-          const uint64_t rr = beg2 + tix(tile + d) * kTile + 2 * threadIdx.x;
-          if (rr >= beg && rr < end) add_rec(c.x, c.y);
-          if (rr + 1 >= beg && rr + 1 < end) add_rec(c.z, c.w);
-        }
-      }
-    }
-    return;
-  }
   // kAccumTrip tiles per trip, each in a register set of its own (the unrolled loop indexes them
   // statically), its next load issued as soon as it is staged: the loads of the following
   // kAccumTrip tiles are in flight while these accumulate
@@ -1208,7 +1160,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
     lds_barrier();
     // one scale per bucket (the pieces' partials add exactly)
     const int k2 = bucket_k2(ws, b);
-    accum_records(acc, stage, ws, beg, end, ldexpf(1.f, k2), l >= a.accum_direct_level);
+    accum_records(acc, stage, ws, beg, end, ldexpf(1.f, k2));
     lds_barrier();
     if (beg == s0 && end == s1) {  // the whole bucket: the final values
       store_bucket<ADAM>(acc, a, ws, d_table, l, ent0, nent, k2);
@@ -1281,7 +1233,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
   for (int t = threadIdx.x; t < 2 * kChunk; t += blockDim.x) acc[t] = 0ull;
   lds_barrier();
   const int k2 = bucket_k2(ws, b);
-  accum_records(acc, stage, ws, s0, s1, ldexpf(1.f, k2), l >= a.accum_direct_level);
+  accum_records(acc, stage, ws, s0, s1, ldexpf(1.f, k2));
   lds_barrier();
   store_bucket<ADAM>(acc, a, ws, d_table, l, ent0, nent, k2);
 }
@@ -1315,7 +1267,7 @@ __global__ void __launch_bounds__(kAccumThreads, LNR_ACCUM_WAVES_PER_EU) k_bwd_a
   for (int t = threadIdx.x; t < 2 * kChunk; t += blockDim.x) acc[t] = 0ull;
   lds_barrier();
   const int k2 = bucket_k2(ws, b);
-  accum_records(acc, stage, ws, beg, end, ldexpf(1.f, k2), l >= a.accum_direct_level);
+  accum_records(acc, stage, ws, beg, end, ldexpf(1.f, k2));
   lds_barrier();
   if (P == 1) {
     store_bucket<ADAM>(acc, a, ws, d_table, l, ent0, nent, k2);

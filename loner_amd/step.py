@@ -311,12 +311,6 @@ class StepEngine:
         self._pp, self._pp_parity = None, 0
         self._pp_stream = torch.cuda.Stream(device=dev)
         self._pp_fork = torch.cuda.Event()
-        # where in step k the prefetch may start (LONER_PIPE_AT): "start" (beside the encode), "encode"
-        # (after the encode launch: beside the field and the backward) or "field" (beside the backward)
-        self.pipe_at = os.environ.get("LONER_PIPE_AT", "start")
-        if self.pipe_at not in ("start", "encode", "field"):
-            raise ValueError(f"LONER_PIPE_AT={self.pipe_at!r}: expected start, encode or field")
-        self._pp_mid = torch.cuda.Event()
         # step_window on all-valid windows, single process: the whole step (ray build, sampling, encode,
         # field, backward, Adam, and the OGM update on its steps) captured once per (window, OGM or not)
         # in a HIP graph and replayed, its per-step scalars (key, loss scalars, Adam coefficients) set in
@@ -331,15 +325,12 @@ class StepEngine:
         # shard 1/8 0.374-0.381 eager against 0.380-0.381), 1 always, 0 never
         g = os.environ.get("LONER_GRAPH", "auto")
         self.use_graph = (g == "1") or (g == "auto" and (self.N <= (1 << 18) or self.N >= (1 << 22)))
-        self.graph_prefetch = os.environ.get("LONER_GRAPH_PREFETCH", "0") == "1"
-        # two lnr_step_scalars (32 B each): this step's, and the next step's (its prefetched build + sampling)
-        self._dev_steps = torch.zeros(16, dtype=torch.int32, device=dev)
-        self.dev_step, self.dev_step_next = self._dev_steps[:8], self._dev_steps[8:]
+        # the graph step's lnr_step_scalars (32 B)
+        self._dev_steps = torch.zeros(8, dtype=torch.int32, device=dev)
+        self.dev_step = self._dev_steps
         self._dev_step = None
         self._graphs, self._graph_window = {}, None
-        self._gpp = None  # what the last graph step prefetched for the next: window, want, parity, have
         self._capture_stream = torch.cuda.Stream(device=dev)
-        self._gfork, self._gjoin = torch.cuda.Event(), torch.cuda.Event()
         # The live backward (LNR_BWD_LIVE): a sample with dL/dsigma = 0 (relu(sigma + noise) = 0,
         # rendering_tcnn.py:260) adds exactly 0 to the table gradient, and on a trained field most samples are such
         # (~80 % at C2 after the driver's windows, bench.py --field trained; ~0 % in the first steps from init).
@@ -496,8 +487,6 @@ class StepEngine:
             L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(st.desc), rays, self.z, R, S, st.table_f16, self.enc, N,
                    None, 0, s)
         m(prof, "encode")
-        if self.pipe_at == "encode":
-            self._pp_mid.record(main)
         # 4. fused field + loss + backward through compositing and MLP (stores the MLP gradient, and the
         # loss scalars into loss_out)
         if fork_count or self.allreduce is not None:
@@ -509,8 +498,6 @@ class StepEngine:
                self.ray_offset, L.ctypes.byref(lp), self.d_enc, st.grad_mlp, self.ws, self.stats, self.depth,
                self.opacity, None, self.level_max_ptr, self.d_jac if self.compact_denc else None, s)
         m(prof, "field")
-        if self.pipe_at == "field":
-            self._pp_mid.record(main)
         self._r_last = R
         # 5. hash-grid backward
         m(prof, "grid_bwd")
@@ -737,7 +724,6 @@ class StepEngine:
         # Windows with rays the 1 m filter drops: the batch size must reach the host (one sync per step).
         # The build and compaction of step k + 1 run on a side stream while step k runs, so that sync
         # never waits for the main stream: the host stays a step ahead of the GPU (double-buffered).
-        self._gpp = None
         main = torch.cuda.current_stream(self.state.device)
         want = (global_step, n, self.ray_offset, n_rays_global)
         pf, self._pf = self._pf, None
@@ -768,7 +754,6 @@ class StepEngine:
                 any(k in kw for k in ("u_jitter", "u_pdf", "noise", "presampled"))):
             return self._step_window_graph(window, global_step, iteration_idx, n, n_rays_global, kw)
         m = self._mark
-        self._gpp = None  # (the eager path neither uses nor keeps the graph path's prefetched buffers)
         main = torch.cuda.current_stream(self.state.device)
         want = (global_step, n, self.ray_offset)
         pp, self._pp = self._pp, None
@@ -809,7 +794,7 @@ class StepEngine:
         key = L.step_key(self.seed, global_step + 1)
         sample = cfg.sampler != "OGM" or not ogm_now  # the OGM sampler reads the grid step k may update
         with torch.cuda.stream(self._pp_stream):
-            self._pp_stream.wait_event(self._pp_fork if self.pipe_at == "start" else self._pp_mid)
+            self._pp_stream.wait_event(self._pp_fork)
             window.build(key, self.ray_offset, n, bq["rays"][:n], bq["dgt"][:n], bq["valid"][:n], None, bq["far"])
             if sample:
                 s = L.stream(self.state.device)
@@ -831,7 +816,7 @@ class StepEngine:
         for pend in (self._pp, self._pf):
             if pend is not None:
                 main.wait_event(pend["done"])
-        self._pp = self._pf = self._gpp = None
+        self._pp = self._pf = None
         self.finish()
 
     def release(self):
@@ -858,14 +843,13 @@ class StepEngine:
         return sc
 
     def _step_window_graph(self, window, global_step, iteration_idx, n, n_rays_global, kw):
-        """step_window as a replayed HIP graph (see __init__), with the pipelined path's prefetch inside it:
-        a second branch, forked at the graph's start and joined at its end, builds step k + 1's rays (and
-        samples them, unless step k updates the OGM the sampler reads) into the other buffers, keyed by
-        the next step's scalars.  Graphs are captured per (buffer parity, what the previous step
-        prefetched, OGM step or not, batch) and per window: the first step of each runs eagerly with the
-        device scalars (every kernel loaded; the step's own result) and is then captured without
+        """step_window as a replayed HIP graph (see __init__): the whole step, ray build included, on one stream.
+        Graphs are captured per (OGM step or not, batch, backward) and per window: the first step of each runs
+        eagerly with the device scalars (every kernel loaded; the step's own result) and is then captured without
         executing; later steps set their scalars (one small launch) and replay.  Bitwise the eager path
-        (tests/test_gpu_rays.py::test_graph_replay_equals_eager)."""
+        (tests/test_gpu_rays.py::test_graph_replay_equals_eager).  (The next step's build + sampling as a forked
+        branch of the graph measured slower than the single-stream graph at every fork point, round 5: DESIGN.md
+        section 4d; removed in round 6, commit history before e32a0b7.)"""
         st, cfg = self.state, self.cfg
         if self._pp is not None or self._pf is not None:
             self.drop_prefetch()
@@ -878,59 +862,21 @@ class StepEngine:
         if self._graph_window is not window:  # a new window: its tensors back the captured pointers
             self._graphs.clear()
             self._graph_window = window
-        gp = self._gpp
-        if gp is not None and gp["window"] is window and gp["want"] == (global_step, n, self.ray_offset):
-            p, have = gp["parity"], gp["have"]
-        else:
-            p, have = self._pp_parity, 0
-        # the next step's build + sampling as a forked branch of the graph (LONER_GRAPH_PREFETCH=1) measured
-        # slower than a single-stream graph (C1 0.284 against 0.170 ms eager on one box): off by default
-        prefetch = self.pipeline and self.graph_prefetch
-        sample_next = prefetch and (cfg.sampler != "OGM" or not ogm)  # the OGM sampler reads the grid step k updates
-        gkey = (p, have, ogm, prefetch, n, self.ray_offset, n_glob, self.zero, self._live)
+        p = self._pp_parity
+        gkey = (p, ogm, n, self.ray_offset, n_glob, self.zero, self._live)
         s = L.stream(st.device)
-        sc = (L.StepScalars * 2)()
+        sc = (L.StepScalars * 1)()
         sc[0] = self.step_scalars(global_step, iteration_idx)
-        sc[1].key = L.step_key(self.seed, global_step + 1)
-        L.call("lnr_step_scalars_set", sc, 2, self._dev_steps, s)
-        b, bq = self._pp_bufs[p], self._pp_bufs[1 - p]
-        self._pp_parity = p
+        L.call("lnr_step_scalars_set", sc, 1, self._dev_steps, s)
+        b = self._pp_bufs[p]
         self.z, self.rays, self.depth_gt, self.ray_valid, self.far_ref = b["z"], b["rays"], b["dgt"], b["valid"], b["far"]
-        self._gpp = (dict(window=window, want=(global_step + 1, n, self.ray_offset), parity=1 - p,
-                          have=2 if sample_next else 1) if prefetch else None)
-
-        def branch(fork):
-            # step k + 1's build (+ sampling) on the side stream after ``fork``, joined at the graph's end
-            with torch.cuda.stream(self._pp_stream):
-                self._pp_stream.wait_event(fork)
-                window.build(sc[1].key, self.ray_offset, n, bq["rays"][:n], bq["dgt"][:n], bq["valid"][:n], None,
-                             bq["far"], dev_step=self.dev_step_next)
-                if sample_next:
-                    ss = L.stream(st.device)
-                    if cfg.sampler == "OGM":
-                        L.call("lnr_sample_ogm", bq["rays"][:n], n, self.S, st.occ, cfg.occ_res, cfg.perturb, None,
-                               None, sc[1].key, self.ray_offset, bq["z"], self.dev_step_next, ss)
-                    else:
-                        L.call("lnr_sample_uniform", bq["rays"][:n], n, self.S, cfg.perturb, None, sc[1].key,
-                               self.ray_offset, bq["z"], self.dev_step_next, ss)
-                self._gjoin.record(self._pp_stream)
 
         def body():
-            main = torch.cuda.current_stream(st.device)
-            if prefetch and self.pipe_at == "start":
-                self._gfork.record(main)
-                branch(self._gfork)
-            if have < 1:
-                window.build(sc[0].key, self.ray_offset, n, b["rays"][:n], b["dgt"][:n], b["valid"][:n], None, b["far"],
-                             dev_step=self.dev_step)
-            out = self.step(b["rays"][:n], b["dgt"][:n], global_step, iteration_idx, scale=window.scale,
-                            far_ref=b["far"], n_rays_global=n_glob, update_ogm=ogm, presampled=have >= 2,
-                            dev_step=self.dev_step, fork_count=prefetch)
-            if prefetch and self.pipe_at != "start":  # (LONER_PIPE_AT: after the encode or the field kernels)
-                branch(self._pp_mid)
-            if prefetch:
-                main.wait_event(self._gjoin)
-            return out
+            window.build(sc[0].key, self.ray_offset, n, b["rays"][:n], b["dgt"][:n], b["valid"][:n], None, b["far"],
+                         dev_step=self.dev_step)
+            return self.step(b["rays"][:n], b["dgt"][:n], global_step, iteration_idx, scale=window.scale,
+                             far_ref=b["far"], n_rays_global=n_glob, update_ogm=ogm, dev_step=self.dev_step,
+                             fork_count=False)
 
         g = self._graphs.get(gkey)
         if g is not None:

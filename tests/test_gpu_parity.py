@@ -199,11 +199,11 @@ def test_live_counted_backward(L, grid, R, S):
 
 
 @pytest.mark.parametrize("S", [512, 64, 40])
-def test_hashgrid_fwd_run_head_gathers_bitwise(L, S, monkeypatch):
-    """The coherent levels' run-head gathers (LONER_ENC_RUN_LEVELS: one lane per run of lanes in one cell
-    gathers, the run's other lanes take its values through ds_bpermute) give the same encodings and
-    record histograms as every lane gathering, for the training, plain eval and live-masked launches;
-    40 samples per ray puts rays and ragged rows across waves."""
+def test_hashgrid_fwd_train_eval_live_agree(L, S):
+    """The training launch (with the record histogram) and the plain eval launch give the same encodings, and
+    the live-masked launch those encodings on its live samples; 40 samples per ray puts rays and ragged rows
+    across waves.  (Round 5's run-head gathers on the coherent levels, which this test also pinned, were
+    removed in round 6: measured no faster)"""
     rng = np.random.default_rng(5)
     R = 37
     d = L.grid_desc(16, 2, 18, 16)
@@ -220,22 +220,17 @@ def test_hashgrid_fwd_run_head_gathers_bitwise(L, S, monkeypatch):
     table = cu(rng.uniform(-1, 1, (lay.n_entries, 2)).astype(np.float16).view(np.int16))
     n = R * S
     nb = int(L.lib().lnr_hashgrid_bwd_workspace_bytes(ctypes.byref(d), n))
-    outs = {}
-    for rl in ("0", "16"):
-        monkeypatch.setenv("LONER_ENC_RUN_LEVELS", rl)
-        ws = torch.zeros(nb // 4 + 1, dtype=torch.int32, device="cuda")
-        e_train = torch.full((16, n), -1, dtype=torch.int32, device="cuda")
-        e_eval = torch.full((16, n), -1, dtype=torch.int32, device="cuda")
-        e_live = torch.full((16, n), -1, dtype=torch.int32, device="cuda")
-        L.call("lnr_hashgrid_fwd_rays", ctypes.byref(d), cu(rays), cu(z), R, S, table, e_train, n, ws, nb, L.stream())
-        L.call("lnr_hashgrid_fwd_rays", ctypes.byref(d), cu(rays), cu(z), R, S, table, e_eval, n, None, 0, L.stream())
-        L.call("lnr_hashgrid_fwd_rays_live", ctypes.byref(d), cu(rays), cu(z), R, S, table, live, e_live, n,
-               L.stream())
-        torch.cuda.synchronize()
-        outs[rl] = (e_train, ws, e_eval, e_live)
-    for a, b in zip(outs["0"], outs["16"]):
-        assert torch.equal(a, b)
-    assert torch.equal(outs["0"][0], outs["0"][2])
+    ws = torch.zeros(nb // 4 + 1, dtype=torch.int32, device="cuda")
+    e_train = torch.full((16, n), -1, dtype=torch.int32, device="cuda")
+    e_eval = torch.full((16, n), -1, dtype=torch.int32, device="cuda")
+    e_live = torch.full((16, n), -1, dtype=torch.int32, device="cuda")
+    L.call("lnr_hashgrid_fwd_rays", ctypes.byref(d), cu(rays), cu(z), R, S, table, e_train, n, ws, nb, L.stream())
+    L.call("lnr_hashgrid_fwd_rays", ctypes.byref(d), cu(rays), cu(z), R, S, table, e_eval, n, None, 0, L.stream())
+    L.call("lnr_hashgrid_fwd_rays_live", ctypes.byref(d), cu(rays), cu(z), R, S, table, live, e_live, n, L.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(e_train, e_eval)
+    m = live.reshape(-1) != 0
+    assert torch.equal(e_live[:, m], e_eval[:, m])
 
 
 @pytest.mark.parametrize("R", [520, 2060])

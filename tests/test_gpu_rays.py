@@ -178,17 +178,17 @@ def test_pipelined_build_and_sampling_equals_plain(L):
     """step_window's pipeline (step k + 1's ray build and sampling enqueued on a side stream after
     step k, double-buffered; no sampling prefetch after an OGM step) gives bitwise the plain path's
     losses, parameters, occupancy grid and last samples, across OGM steps (global steps 10, 20) and a
-    skipped step (the prefetch is discarded), for every fork point of the prefetch (LONER_PIPE_AT)."""
+    skipped step (the prefetch is discarded)."""
     from loner_amd import step as S_
     from loner_amd.rays import RayWindow
     scans, wc, rr = _window("forest", 2, seed=8)
     win = RayWindow(scans, wc, rr, n_lidar=128, n_sky=16, strategy="MASK")
     assert win.all_valid
     res = []
-    for pipeline, at in ((False, "start"), (True, "start"), (True, "encode"), (True, "field")):
+    for pipeline in (False, True):
         st = S_.FieldState(S_.StepConfig(n_samples=128, occ_lr=1e-3), device="cuda:0", table_init=0.5)
         eng = S_.StepEngine(st, win.n_slots, seed=7)
-        eng.pipeline, eng.pipe_at = pipeline, at
+        eng.pipeline = pipeline
         outs = [eng.step_window(win, global_step=g).clone() for g in (8, 9, 10, 11, 13, 14, 19, 20, 21)]
         torch.cuda.synchronize()
         res.append(([host(o) for o in outs], host(st.params).copy(), host(st.occ).copy(), host(eng.z).copy(),
@@ -250,16 +250,14 @@ def test_graph_replay_equals_eager(L, zero):
     and the ExponentialLR factor read from device memory, set by one launch per step) gives bitwise the
     eager path's losses, parameters, moments, occupancy grid and samples, across OGM steps (their own
     graph), a skipped global step, a changed iteration index / learning-rate factor and a second window
-    (the graphs are re-captured), with and without the in-graph prefetch of the next step's rays and
-    samples (forked at the step's start, or after its encode or field kernels: LONER_PIPE_AT); also with the
-    sharded optimiser's one-rank share (bench --shard-of)."""
+    (the graphs are re-captured), against the eager path with and without its pipelined prefetch; also with
+    the sharded optimiser's one-rank share (bench --shard-of)."""
     from loner_amd import step as S_
     from loner_amd.rays import RayWindow
     loss = S_.LossConfig.from_dict(dict(loss_selection="L1_LOS", decay_los_lambda=True, los_lambda=1000.0,
                                         los_lambda_decay_rate=1e-4, los_lambda_decay_steps=30))
     res = []
-    for graph, pipe, at in ((False, True, "start"), (True, True, "start"), (True, False, "start"), (True, True, "encode"),
-                            (True, True, "field")):
+    for graph, pipe in ((False, True), (False, False), (True, True)):
         st = S_.FieldState(S_.StepConfig(n_samples=64, occ_lr=1e-3, loss=loss), device="cuda:0", table_init=0.5)
         eng = None
         outs = []
@@ -268,7 +266,7 @@ def test_graph_replay_equals_eager(L, zero):
             win = RayWindow(scans, wc, rr, n_lidar=128, n_sky=16, strategy="MASK")
             if eng is None:
                 eng = S_.StepEngine(st, win.n_slots, seed=4, zero=zero)
-                eng.use_graph, eng.pipeline, eng.graph_prefetch, eng.pipe_at = graph, pipe, pipe, at
+                eng.use_graph, eng.pipeline = graph, pipe
             st.reset_optimizer()
             for it, g in enumerate(steps):
                 eng.lr_factor = 0.97 ** it
