@@ -72,6 +72,10 @@ def parse():
     ap.add_argument("--pretrain-windows", type=int, default=12)
     ap.add_argument("--pretrain-iters", type=int, default=32,
                     help="steps per pre-training window (examples/fdt_optimize_implicit_map.py:76 NUM_ITERATIONS)")
+    ap.add_argument("--field-cache", default=None, metavar="PATH",
+                    help="--field trained: save the pre-trained field here, or load it if PATH exists and skip the "
+                         "from-init steps and the pre-training (profiling runs: kernel statistics of the trained "
+                         "window only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rays", type=int, default=512, help="rays per reduced-config CPU-baseline step (x512 samples)")
     ap.add_argument("--cpu-steps", type=int, default=24)
@@ -125,6 +129,32 @@ def pmc_mfma(cfg_name):
         return None, None
     rec = json.load(open(files[-1]))
     return {k: v["mfma_busy_frac"] for k, v in rec["kernels"].items()}, os.path.relpath(files[-1], ROOT)
+
+
+def pmc_kernel_traffic(cfg_name, kernel):
+    """HBM bytes per launch of one kernel of the step, from the newest committed per-step PMC pass
+    (profiles/<round>_traffic_<cfg>_step.json); (None, None) if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_traffic_{cfg_name}_step.json")))
+    if not files:
+        return None, None
+    rec = json.load(open(files[-1]))
+    hits = [v for k, v in rec["kernels"].items() if kernel in k]
+    if not hits:
+        return None, None
+    per_step = sum(v["bytes_per_step"] for v in hits)
+    launches = sum(v["dispatches"] for v in hits) / max(rec.get("steps_profiled", 1), 1)
+    return per_step / max(launches, 1.0), os.path.relpath(files[-1], ROOT)
+
+
+def pmc_ta_busy(cfg_name):
+    """The encode's texture-addresser busy fraction (TA_BUSY_avr / GRBM_GUI_ACTIVE of k_hashgrid_fwd) from the
+    newest committed profiles/<round>_ta_<cfg>.json (tools/pmc_l2req.sh + tools/refresh_profiles.py)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_ta_{cfg_name}.json")))
+    if not files:
+        return None, None
+    return json.load(open(files[-1])).get("ta_busy_frac"), os.path.relpath(files[-1], ROOT)
 
 
 def host_cpu_share():
@@ -754,15 +784,30 @@ def main():
         stage = {k: float(np.mean([v[j].elapsed_time(v[j + 1]) for j in range(0, len(v), 2)])) for k, v in prof.items()}
         return elapsed, loss, stage, float(zeros.item()) / (PROF_STEPS * R * n_samples)
 
-    elapsed, loss, stage_ms, zero_frac = measure()
+    cache = args.field_cache if args.field == "trained" else None
     from_init = None
+    if cache and os.path.exists(cache):
+        # a profiling run: the pre-trained field of an earlier run (no from-init steps, no pre-training here, so
+        # the kernel statistics hold the trained window's steps only)
+        ck = torch.load(cache, map_location=dev, weights_only=True)
+        state.params.copy_(ck["params"])
+        state.occ.copy_(ck["occ"])
+        state.refresh_shadow()
+        g0, pre = int(ck["g0"]), dict(json.loads(ck["pre"]), loaded_from=cache)
+    else:
+        elapsed, loss, stage_ms, zero_frac = measure()
     if args.field == "trained":
-        from_init = {"ms_per_step": elapsed / args.steps * 1e3, "value": world * R * n_samples * args.steps / elapsed,
-                     "loss": float(loss[0]), "dsigma_zero_frac": zero_frac, "stage_ms": stage_ms}
-        t_pre = time.perf_counter()
-        g0, pre = pretrain(eng, state, kind, win_kf, rpk, spk, strat, dev, r_glob,
-                           args.warmup + args.steps + PROF_STEPS, args.pretrain_windows, args.pretrain_iters)
-        pre["seconds"] = time.perf_counter() - t_pre
+        if not (cache and os.path.exists(cache)):
+            from_init = {"ms_per_step": elapsed / args.steps * 1e3,
+                         "value": world * R * n_samples * args.steps / elapsed,
+                         "loss": float(loss[0]), "dsigma_zero_frac": zero_frac, "stage_ms": stage_ms}
+            t_pre = time.perf_counter()
+            g0, pre = pretrain(eng, state, kind, win_kf, rpk, spk, strat, dev, r_glob,
+                               args.warmup + args.steps + PROF_STEPS, args.pretrain_windows, args.pretrain_iters)
+            pre["seconds"] = time.perf_counter() - t_pre
+            if cache and rank == 0:
+                torch.save({"params": state.params.cpu(), "occ": state.occ.cpu(), "g0": g0, "pre": json.dumps(pre)},
+                           cache)
         state.reset_optimizer()  # the timed window: a new Adam (optimizer.py:255-265)
         elapsed, loss, stage_ms, zero_frac = measure(g0)
 
@@ -778,15 +823,24 @@ def main():
     # so the stage's algorithmic bytes add Adam's 32 B per table parameter
     fused_adam = eng.allreduce is None and eng.zero is None and eng.compact_denc and (
         eng.fused_adam is True or (eng.fused_adam == "auto" and N <= S_.FUSED_ADAM_MAX_N))
-    bwd_bytes = 1024.0 * N + (32.0 * 2 * state.n_entries if fused_adam else 0.0)
+    # algorithmic work counts the samples that have it: every sample is encoded and goes through the MLP forward
+    # (its sigma decides whether it is dead), but a sample with dL/dsigma = 0 has no scatter-adds and no MLP
+    # backward to do (its contributions are exactly 0; the reference's tcnn path does them all the same)
+    n_live = N * (1.0 - zero_frac)
+    bwd_bytes = 1024.0 * n_live + (32.0 * 2 * state.n_entries if fused_adam else 0.0)
     achieved = bwd_bytes / (bwd_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args.config)
     traffic_step, traffic_step_src = pmc_step_traffic(args.config)
-    # the whole step against the HBM bound: 1536 B per ray-sample (hash-grid gathers and
-    # scatter-adds) + 32 B per parameter (Adam) + 52 B per ray
-    step_bytes = 1536.0 * N + 32.0 * state.n_params + 52.0 * R
+    enc_traffic, enc_traffic_src = pmc_kernel_traffic(args.config, "k_hashgrid_fwd")
+    # the whole step against the HBM bound: 512 B per ray-sample of gathers, 1024 B per live
+    # ray-sample of scatter-adds, 32 B per parameter (Adam), 52 B per ray
+    step_bytes = 512.0 * N + 1024.0 * n_live + 32.0 * state.n_params + 52.0 * R
     busy, busy_src = pmc_mfma(args.config)
-    mlp_tflops = MLP_FLOP_PER_SAMPLE * N / (stage_ms["field"] * 1e-3) / 1e12
+    mlp_flop = 4224.0 * N + 8448.0 * n_live
+    mlp_tflops = mlp_flop / (stage_ms["field"] * 1e-3) / 1e12
+    enc_ms = stage_ms["encode"]
+    enc_achieved = 512.0 * N / (enc_ms * 1e-3) / 1e9
+    ta, ta_src = pmc_ta_busy(args.config)
     line = {
         # BASELINE.json metric: the rate here, the rendered-depth L1 in cpu_baseline.rendered_depth_vs_oracle
         "metric": "ray-samples/sec per optimizer step; rendered-depth L1 vs reference",
@@ -822,30 +876,37 @@ def main():
                                    % (args.warmup, args.warmup + args.steps - 1)),
                    **({"pretrain": pre} if args.field == "trained" else {}),
                    **({"submap_rank0": submap} if submap is not None else {})},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": "hash-grid backward stage (k_bwd_chunk_sums, k_bwd_scan_*, k_bwd_scatter_rows, " + (
-                         "k_bwd_accum_buckets)" if N <= (1 << 17) else
-                         "k_bwd_accum_units: whole buckets and pieces of the large ones)" if N <= (1 << 21) else
-                         "k_bwd_accum: record-balanced, k_bwd_finalize)") + (
-                         "; the table's Adam fused into the accumulation" if fused_adam else ""),
-                     "algorithmic_bytes_per_launch": bwd_bytes, "ms_per_launch": bwd_ms,
+        # the dominant kernel, the training encode (k_hashgrid_fwd: 8 gathers per sample and level, 512 B per
+        # ray-sample algorithmic; the longest kernel of the step from init and trained), against HBM peak; what
+        # bounds it is the texture addresser, not bytes ("What bounds the forward encode")
+        "roofline": {"bound": "hbm", "achieved": enc_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": enc_achieved / HBM_PEAK_GBS, "traffic": enc_traffic, "traffic_source": enc_traffic_src,
+                     "kernel": "k_hashgrid_fwd (training encode + the backward's record histogram)",
+                     "algorithmic_bytes_per_launch": 512 * N, "ms_per_launch": enc_ms,
+                     "limiter": "texture addresser: TA busy %s of the launch (%s)" % (
+                         "n/a" if ta is None else "%.2f" % ta, ta_src or "no committed PMC pass"),
                      "step_algorithmic_bytes": step_bytes,
                      "step_frac": step_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "traffic_step": traffic_step, "traffic_step_source": traffic_step_src},
-        # the longest single kernel, the training encode (k_hashgrid_fwd: 8 gathers per sample and level,
-        # 512 B/sample algorithmic), against HBM peak; what bounds it is the texture addresser, not bytes
-        # ("What bounds the forward encode")
-        "dominant_kernel": {"kernel": "k_hashgrid_fwd (training encode + record histogram)",
-                            "ms_per_launch": stage_ms["encode"], "algorithmic_bytes_per_launch": 512 * N,
-                            "achieved": 512.0 * N / (stage_ms["encode"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                            "unit": "GB/s", "frac": 512.0 * N / (stage_ms["encode"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                            "bound": "texture addresser + the coherent levels' VALU: TA busy 0.78 of the launch at C2 "
-                                     "(rocprofv3 TA_BUSY_avr, profiles/r04_l2req_C2.txt)"},
+        # the hash-grid backward stage (the scatter-adds: 1024 B per live ray-sample)
+        "backward_stage": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                           "kernel": "hash-grid backward stage (" + (
+                               "live: k_bwd_col_totals, k_bwd_count_live, " if eng._live else "") +
+                               "k_bwd_chunk_sums, k_bwd_scan_*, k_bwd_scatter_rows, " + (
+                               "k_bwd_accum_buckets)" if N <= (1 << 17) else
+                               "k_bwd_accum_units: whole buckets and pieces of the large ones)" if N <= (1 << 21) else
+                               "k_bwd_accum: record-balanced, k_bwd_finalize)") + (
+                               "; the table's Adam fused into the accumulation" if fused_adam else ""),
+                           "backward": "live (records for samples with dL/dsigma != 0 only)" if eng._live else "full",
+                           "algorithmic_bytes_per_launch": bwd_bytes, "live_samples_per_launch": n_live,
+                           "ms_per_launch": bwd_ms},
         # the sigma MLP (fwd 4224 + bwd 8448 FLOP/sample) over the field stage
         # (k_sigma_fwd_tiles + k_composite_wave + k_mlp_bwd_tiles), against the dense fp16 MFMA peak
         "mfma": {"achieved": mlp_tflops, "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": mlp_tflops / MFMA_PEAK_TFLOPS,
-                 "flop_per_sample": MLP_FLOP_PER_SAMPLE, "ms_per_launch": stage_ms["field"],
+                 "flop_per_sample": MLP_FLOP_PER_SAMPLE, "flop_per_launch": mlp_flop,
+                 "flop_note": "forward 4224 per ray-sample, backward 8448 per live ray-sample",
+                 "ms_per_launch": stage_ms["field"],
                  "busy": busy, "busy_source": busy_src},
         "stage_ms": stage_ms,
         "loss": float(loss[0]),

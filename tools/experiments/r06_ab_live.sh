@@ -1,0 +1,10 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/r06b
+for v in 0 1 0 1; do
+  LONER_LIVE_BWD=$v timeout -k 10 200 python bench.py --no-cpu-baseline --steps 40 > gpurun_out/r06b/live$v.json 2>/dev/null || exit 1
+  python -c "
+import json; d=json.loads(open('gpurun_out/r06b/live$v.json').read().strip().splitlines()[-1]); f=d['from_init']
+print('live=$v trained', round(d['ms_per_step'],4), {k: round(x,4) for k,x in d['stage_ms'].items()})
+print('live=$v init   ', round(f['ms_per_step'],4), {k: round(x,4) for k,x in f['stage_ms'].items()})"
+done

@@ -10,15 +10,17 @@ CFG=${1:-C2}
 cd /tmp && export TMPDIR=/tmp
 run() {
   tag=$1; shift
-  mkdir -p $R/gpurun_out/pmcl2${TAG:-}/$tag
+  D=${OUT:-$R/gpurun_out}/pmcl2${TAG:-}
+  mkdir -p $D/$tag
   timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-trace --output-format csv \
-    -d $R/gpurun_out/pmcl2${TAG:-}/$tag -o run -- python3 $R/bench.py --config $CFG --no-cpu-baseline --steps 10 \
-    > $R/gpurun_out/pmcl2${TAG:-}/$tag/out.txt 2>&1
+    -d $D/$tag -o run -- python3 $R/bench.py --config $CFG ${ARGS:-} --no-cpu-baseline --steps 10 \
+    > $D/$tag/out.txt 2>&1
   rc=$?
   echo "pmc $tag rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 }
 run l2a TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TCC_HIT_sum TCC_MISS_sum
 run l2b TCC_REQ_sum TCP_TCC_WRITE_REQ_sum TA_BUSY_avr TA_TA_BUSY_sum GRBM_GUI_ACTIVE
-python3 $R/tools/pmc_summary.py $R/gpurun_out/pmcl2${TAG:-} > $R/gpurun_out/pmcl2${TAG:-}/summary.txt
-grep -A1 -E "k_hashgrid_fwd|k_bwd_scatter_rows|k_bwd_accum|k_mlp_bwd|k_sigma_fwd" $R/gpurun_out/pmcl2${TAG:-}/summary.txt
+D=${OUT:-$R/gpurun_out}/pmcl2${TAG:-}
+python3 $R/tools/pmc_summary.py $D > $D/summary.txt
+grep -A1 -E "k_hashgrid_fwd|k_bwd_scatter_rows|k_bwd_accum|k_mlp_bwd|k_sigma_fwd" $D/summary.txt

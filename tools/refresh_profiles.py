@@ -21,7 +21,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BWD_KERNELS = ("k_bwd_chunk_sums", "k_bwd_scan_rows", "k_bwd_scan_buckets", "k_bwd_scatter_rows",
+BWD_KERNELS = ("k_bwd_col_totals", "k_bwd_count_live", "k_bwd_chunk_sums", "k_bwd_scan_rows", "k_bwd_scan_buckets", "k_bwd_scatter_rows",
                "k_bwd_scatter", "k_denc_level_max", "k_bwd_accum", "k_bwd_finalize", "k_bwd_accum_units",
                "k_bwd_finalize_units", "k_bwd_accum_buckets", "k_bwd_units")
 
@@ -134,6 +134,27 @@ def main(tag, cfg, src=None):
                "formula": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs * 256 CUs * 4 SIMDs)"}
         json.dump(rec, open(os.path.join(prof, f"{tag}_mfma_{cfg}.json"), "w"), indent=1)
         print("mfma busy", {k: round(v["mfma_busy_frac"] or 0.0, 4) for k, v in kern.items()})
+    # texture-addresser busy of the encode (tools/pmc_l2req.sh pass l2b): TA_BUSY_avr per TA instance over the
+    # GPU-active cycles of one XCD (GRBM_GUI_ACTIVE sums the 8 XCDs)
+    t = glob.glob(os.path.join(out, "pmcl2", "l2b", "*counter_collection.csv"))
+    if t:
+        tot = collections.defaultdict(lambda: collections.defaultdict(float))
+        disp = collections.defaultdict(set)
+        for row in csv.DictReader(open(t[0])):
+            if "k_hashgrid_fwd" not in row["Kernel_Name"]:
+                continue
+            tot[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
+        ta = sum(tot["TA_BUSY_avr"].values()) / max(len(tot["TA_BUSY_avr"]), 1)
+        gr = sum(tot["GRBM_GUI_ACTIVE"].values()) / max(len(tot["GRBM_GUI_ACTIVE"]), 1)
+        rec = {"kernel": "k_hashgrid_fwd", "config": cfg, "dispatches": len(tot["TA_BUSY_avr"]),
+               "TA_BUSY_avr": ta, "GRBM_GUI_ACTIVE": gr, "ta_busy_frac": ta / (gr / 8) if gr else None,
+               "formula": "TA_BUSY_avr / (GRBM_GUI_ACTIVE / 8 XCDs)"}
+        json.dump(rec, open(os.path.join(prof, f"{tag}_ta_{cfg}.json"), "w"), indent=1)
+        print("encode TA busy", rec["ta_busy_frac"])
+    for sub, name in (("pmcl2", "l2req"), ("pmcb", "pmc")):
+        f = os.path.join(out, sub, "summary.txt")
+        if os.path.exists(f):
+            shutil.copy(f, os.path.join(prof, f"{tag}_{name}_{cfg}.txt"))
 
 
 if __name__ == "__main__":
