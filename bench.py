@@ -725,12 +725,20 @@ def main():
             return dist.all_reduce(t, async_op=async_op)
         if use_zero and world in (2, 4, 8):
             zero = (rank, world)
+            # LONER_EXCHANGE_GROUPS=2 (default): the shadow all-gathers on a process group of their own, i.e. a
+            # second communicator, so range r's gather runs beside range r + 1's reduce-scatter instead of after it
+            # in one communicator's queue (tools/zero_tail_model.py); 1: one group
+            ag_group = dist.new_group(list(range(world))) if os.environ.get("LONER_EXCHANGE_GROUPS", "2") == "2" else None
             hooks = dict(reduce_scatter=lambda o, i, async_op=False: dist.reduce_scatter_tensor(o, i, async_op=async_op),
-                         all_gather=lambda o, i, async_op=False: dist.all_gather_into_tensor(o, i, async_op=async_op))
+                         all_gather=lambda o, i, async_op=False: dist.all_gather_into_tensor(o, i, group=ag_group,
+                                                                                            async_op=async_op),
+                         two_groups=ag_group is not None)
     elif args.shard_of and use_zero:
         zero = (0, args.shard_of)  # one rank's share of the sharded Adam, no exchange (world size 1)
     eng = S_.StepEngine(state, R, seed=12345 + (rank if replicas else 0), allreduce=allreduce,
-                        ray_offset=0 if replicas else rank * R, zero=zero, **hooks)
+                        ray_offset=0 if replicas else rank * R, zero=zero,
+                        ar_cut=S_.AR_CUT_TWO_GROUPS if hooks.get("two_groups") else None,
+                        **{k: v for k, v in hooks.items() if k != "two_groups"})
     r_glob = R if replicas else R * world
     if args.shard_of:
         r_glob = R * args.shard_of
@@ -866,7 +874,9 @@ def main():
                    "parallelism": (f"replicas{world}" if replicas else f"dp{world}") if world > 1 else
                    (f"shard 0 of {args.shard_of} (one rank's strong-scaling step: its rays, its 1/{args.shard_of} "
                     f"of the sharded Adam; no collective)" if args.shard_of else "single"),
-                   "optimizer": "sharded (ZeRO-1)" if zero is not None else "replicated",
+                   "optimizer": ("sharded (ZeRO-1)" + (", all-gathers on a second communicator" if world > 1 and
+                                 os.environ.get("LONER_EXCHANGE_GROUPS", "2") == "2" else "")
+                                 if zero is not None else "replicated"),
                    "launch": ("HIP graph replay (one graph per window and OGM-or-not step)"
                               if eng.use_graph and args.rays == "device" and eng.allreduce is None else
                               "eager, next step's ray build + sampling prefetched on a side stream"),

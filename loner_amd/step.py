@@ -179,13 +179,18 @@ FUSED_ADAM_MAX_N = 1 << 17  # samples up to which the step fuses the table's Ada
 # exchange's critical path is 3 us shorter at 6 than at 4 and 13-20 us shorter than at 8 (round 4's cut) for
 # ring bandwidths of 100-400 GB/s
 AR_CUT_DEFAULT = 6
+# with the sharded optimiser's all-gathers on a communicator of their own (bench.py LONER_EXCHANGE_GROUPS=2), the
+# gather of range 1 overlaps range 2's reduce-scatter, and the model puts the best cut at 8 (levels 8-15 first):
+# 168 us exposed at 200 GB/s if the two share the link bandwidth, 148 us if not, against 191 / 156 at cut 6
+# (tools/zero_tail_model.py, profiles/r06_zero_tail_model_C4s8.txt)
+AR_CUT_TWO_GROUPS = 8
 
 
 class StepEngine:
     """Preallocated workspaces for a fixed ray-batch size; ``step`` runs one optimiser step."""
 
     def __init__(self, state: FieldState, n_rays: int, seed: int = 0, allreduce=None, ray_offset: int = 0,
-                 count_in_forward: bool = True, zero=None, reduce_scatter=None, all_gather=None):
+                 count_in_forward: bool = True, zero=None, reduce_scatter=None, all_gather=None, ar_cut=None):
         self.state = state
         self.cfg = state.cfg
         self.n_rays = n_rays
@@ -215,7 +220,7 @@ class StepEngine:
         if nbk <= 1:
             cuts = [nl, 0]
         elif nbk == 2:
-            cut = int(os.environ.get("LONER_AR_CUT", str(AR_CUT_DEFAULT)))
+            cut = int(os.environ.get("LONER_AR_CUT", str(AR_CUT_DEFAULT if ar_cut is None else ar_cut)))
             cuts = sorted({nl, min(max(cut, 1), max(nl - 1, 1)), 0}, reverse=True)
         else:
             cuts = sorted({nl, max(nl - 5, 1), max(nl - 10, 1), min(3, nl), 0}, reverse=True)

@@ -36,7 +36,7 @@ def test_bench_spawns_two_gloo_ranks():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["LONER_DIST_BACKEND"] = "gloo"
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "C4", "--steps", "3",
-                        "--warmup", "1", "--no-cpu-baseline"], env=env, capture_output=True, text=True, timeout=110,
+                        "--warmup", "1", "--no-cpu-baseline", "--field", "init"], env=env, capture_output=True, text=True, timeout=110,
                        cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     line = _last_json(r.stdout)

@@ -96,12 +96,17 @@ def _zero_worker(rank, world, port, out):
 
     hooks = dict(reduce_scatter=lambda o, i, async_op=False: dist.reduce_scatter_tensor(o, i, async_op=async_op),
                  all_gather=lambda o, i, async_op=False: dist.all_gather_into_tensor(o, i, async_op=async_op))
-    for tag, zero in (("ar", None), ("zero", (rank, world))):
+    # the exchange on two communicators (bench.py's default, LONER_EXCHANGE_GROUPS=2): the all-gathers on a group
+    # of their own, so a range's gather runs beside the next range's reduce-scatter
+    ag_group = dist.new_group(list(range(world)))
+    hooks2 = dict(reduce_scatter=hooks["reduce_scatter"],
+                  all_gather=lambda o, i, async_op=False: dist.all_gather_into_tensor(o, i, group=ag_group,
+                                                                                     async_op=async_op))
+    for tag, zero, hk in (("ar", None, {}), ("zero", (rank, world), hooks), ("zero2", (rank, world), hooks2)):
         S_, syn, rays, dgt, st = _setup()
         R = rays.shape[0]
         s0, s1 = shard_range(R, rank, world)
-        eng = S_.StepEngine(st, s1 - s0, seed=9, allreduce=allreduce, ray_offset=s0, zero=zero,
-                            **(hooks if zero else {}))
+        eng = S_.StepEngine(st, s1 - s0, seed=9, allreduce=allreduce, ray_offset=s0, zero=zero, **hk)
         for k in range(3):
             eng.step(rays[s0:s1].contiguous(), dgt[s0:s1].contiguous(), global_step=9 + k, scale=syn.CUBES["forest"][0],
                      far_ref=float(rays[0, -1]), n_rays_global=R)
@@ -117,7 +122,8 @@ def _zero_worker(rank, world, port, out):
 def test_gloo_two_ranks_sharded_optimizer(tmp_path):
     """ZeRO-1 (reduce-scatter of each level range's gradient, Adam on each rank's half, all-gather of the
     fp16 shadow) gives the all-reduce path's parameters bit for bit, on both ranks, over 3 steps (one an
-    OGM step); after sync_master the fp32 master and the moments agree too."""
+    OGM step); after sync_master the fp32 master and the moments agree too.  The same with the all-gathers
+    on a second process group (two communicators: the exchange's reduce-scatters and gathers unserialised)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import torch.multiprocessing as mp
@@ -136,6 +142,63 @@ def test_gloo_two_ranks_sharded_optimizer(tmp_path):
         assert np.array_equal(ref, np.load(tmp_path / f"ar_{what}1.npy"))
         for r in range(2):
             assert np.array_equal(ref, np.load(tmp_path / f"zero_{what}{r}.npy")), (what, r)
+            assert np.array_equal(ref, np.load(tmp_path / f"zero2_{what}{r}.npy")), (what, r)
+
+
+def _pipe_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from loner_amd import step as S_
+    from loner_amd import synthetic as syn
+    from loner_amd.rays import RayWindow
+
+    def allreduce(t, async_op=False):
+        return dist.all_reduce(t, async_op=async_op)
+
+    win = RayWindow(syn.make_window("forest", 2 * world, seed=4), syn.world_cube("forest"),
+                    syn.SENSORS["forest"]["ray_range"], n_lidar=128, n_sky=16, strategy="MASK", device="cuda:0")
+    assert win.all_valid
+    R = win.n_slots // world
+    for pipeline in (False, True):
+        st = S_.FieldState(S_.StepConfig(n_samples=128, occ_lr=1e-3), device="cuda:0", table_init=0.5, seed=5)
+        eng = S_.StepEngine(st, R, seed=9, allreduce=allreduce, ray_offset=rank * R)
+        eng.pipeline = pipeline
+        zs = []
+        for g in (8, 9, 10, 11, 12):  # step 10 updates the OGM; 11's prefetched sampling must see the update
+            eng.step_window(win, global_step=g, n_rays_global=win.n_slots)
+            zs.append(eng.z.clone())
+        eng.finish()
+        torch.cuda.synchronize()
+        np.save(os.path.join(out, f"pipe{int(pipeline)}_occ{rank}.npy"), st.occ.cpu().numpy())
+        np.save(os.path.join(out, f"pipe{int(pipeline)}_z{rank}.npy"), torch.stack(zs).cpu().numpy())
+        np.save(os.path.join(out, f"pipe{int(pipeline)}_params{rank}.npy"), st.params.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_two_ranks_pipelined_ogm_equals_plain(tmp_path):
+    """The data-parallel OGM update is asynchronous (its SGD step lands before the grid's next reader): with the
+    eager path's pipeline (step k + 1's sampling prefetched on a side stream) the occupancy grid, the samples of
+    the steps after the OGM step and the parameters are bit for bit those of LONER_PIPELINE=0, on both ranks."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_pipe_worker, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=100)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    for r in range(2):
+        for what in ("occ", "z", "params"):
+            assert np.array_equal(np.load(tmp_path / f"pipe0_{what}{r}.npy"), np.load(tmp_path / f"pipe1_{what}{r}.npy")), \
+                (what, r)
 
 
 def test_sharded_optimizer_emulation_single_process():

@@ -12,9 +12,15 @@ Timeline after the scatter (t = 0), collectives serialised in enqueue order on t
 Exposed = max(end of Adam2, end of AG2) - (A1 + A2): the time the exchange adds beyond the accumulation.
 A ring reduce-scatter / all-gather moves (w - 1) / w of the buffer over each rank's link.
 
-    python tools/zero_tail_model.py profiles/r05_bwd_levels_C4s8.json [--world 8]
+Two communicators (round 6, bench.py LONER_EXCHANGE_GROUPS=2): the reduce-scatters on one queue, the all-gathers
+on a second, so AG1 can start as soon as Adam1 is done instead of after RS2.  Whether that helps depends on
+whether concurrent collectives share the link bandwidth: ``--share`` runs a fluid model (collectives that are in
+their transfer phase at the same time split B equally); without it each queue gets B (an upper bound on the gain).
+
+    python tools/zero_tail_model.py profiles/r05_bwd_levels_C4s8.json [--world 8] [--queues 2] [--share]
 """
 import argparse
+import collections
 import json
 import math
 
@@ -50,6 +56,83 @@ def model(cut, a1_ms, a2_ms, world, bw_gbs, alpha_us, adam_tbs=7.0, n_mlp=3072):
                 exposed_us=max(adam2_end, ag2_end) - (A1 + A2), accumulate_us=A1 + A2)
 
 
+def simulate(jobs, bw_gbs, alpha_us, share):
+    """Fluid timeline of collectives.  jobs: name -> (ready_us, queue, bytes over the link, deps); a job starts
+    when ready, its queue is free and its deps are done, spends alpha_us in latency, then transfers its bytes at
+    bw / (number of jobs transferring) if share else at bw.  Returns name -> end time (us)."""
+    B = bw_gbs * 1e3  # bytes per us
+    end, start, rem = {}, {}, {}
+    q_free = collections.defaultdict(float)
+    t = 0.0
+    pending = dict(jobs)
+    active = {}  # name -> transfer-phase start
+    while pending or active:
+        # start every job that can start now (its queue idle, ready, deps done)
+        changed = True
+        while changed:
+            changed = False
+            for nm, (ready, q, nbytes, deps) in sorted(pending.items(), key=lambda kv: kv[1][0]):
+                if any(d not in end for d in deps):
+                    continue
+                st = max(ready, q_free[q], max([end[d] for d in deps], default=0.0))
+                busy_q = any(jobs[a][1] == q for a in active) or any(jobs[a][1] == q and a not in end for a in start)
+                if st <= t + 1e-9 and not busy_q:
+                    start[nm] = t
+                    rem[nm] = nbytes
+                    active[nm] = t + alpha_us  # transfers after the latency
+                    del pending[nm]
+                    changed = True
+                    break
+        # next event: a pending job becoming startable, a latency ending, or a transfer finishing
+        cands = []
+        for nm, (ready, q, nbytes, deps) in pending.items():
+            if all(d in end for d in deps):
+                cands.append(max(ready, q_free[q], max([end[d] for d in deps], default=0.0)))
+        moving = [a for a, t0 in active.items() if t0 <= t + 1e-9]
+        rate = (B / len(moving) if share else B) if moving else 0.0
+        for a in moving:
+            cands.append(t + rem[a] / rate)
+        for a, t0 in active.items():
+            if t0 > t + 1e-9:
+                cands.append(t0)
+        cands = [c for c in cands if c > t + 1e-9]
+        if not cands:
+            break
+        t1 = min(cands)
+        for a in moving:
+            rem[a] -= rate * (t1 - t)
+        t = t1
+        for a in list(active):
+            if active[a] <= t + 1e-9 and rem[a] <= 1e-6:
+                end[a] = t
+                q_free[jobs[a][1]] = t
+                del active[a]
+    return end
+
+
+def model2(cut, a1_ms, a2_ms, world, bw_gbs, alpha_us, queues, share, adam_tbs=7.0, n_mlp=3072):
+    """The same tail as ``model`` with the collectives on ``queues`` communicators (RS on queue 0, AG on queue
+    queues - 1) through the fluid simulation."""
+    off = level_params()
+    p1 = 2 * (off[16] - off[cut])
+    p2 = n_mlp + 2 * off[cut]
+    frac = (world - 1) / world
+    adam = lambda p: 32 * p / world / (adam_tbs * 1e6)
+    A1, A2 = 1e3 * a1_ms, 1e3 * a2_ms
+    qa = queues - 1
+    # Adam1 runs after RS1 and the second accumulate (stream order), Adam2 after Adam1 and RS2: modelled as
+    # pseudo-jobs on a compute queue with zero link bytes and their duration as latency
+    jobs = {"RS1": (A1, "A", 4 * p1 * frac, []), "RS2": (A1 + A2, "A", 4 * p2 * frac, ["RS1"])}
+    e = simulate(jobs, bw_gbs, alpha_us, share)
+    adam1_end = max(A1 + A2, e["RS1"]) + adam(p1)
+    adam2_end = max(adam1_end, e["RS2"]) + adam(p2)
+    jobs.update({"AG1": (adam1_end, "A" if qa == 0 else "B", 2 * p1 * frac, ["RS2"] if qa == 0 else []),
+                 "AG2": (adam2_end, "A" if qa == 0 else "B", 2 * p2 * frac, ["AG1"])})
+    e = simulate(jobs, bw_gbs, alpha_us, share)
+    return dict(cut=cut, queues=queues, share=share, step_end_us=adam2_end, gather_end_us=e["AG2"],
+                exposed_us=max(adam2_end, e["AG2"]) - (A1 + A2), accumulate_us=A1 + A2)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("levels_json")
@@ -69,7 +152,18 @@ def main():
     for r in rows:
         print(f"{r['cut']:>3} {r['bw_GBs']:>7.0f} {r['A1_us']:>12.1f} {r['A2_us']:>11.1f} {r['rs2_MB']:>7.2f} "
               f"{r['step_end_us']:>9.1f} {r['gather_end_us']:>8.1f} {r['exposed_us']:>8.1f}")
-    print(json.dumps(dict(world=a.world, alpha_us=a.alpha, rows=rows)))
+    rows2 = []
+    print(f"\n{'cut':>3} {'B GB/s':>7} {'1 queue':>8} {'2 queues, shared B':>19} {'2 queues, B each':>17}   exposed us "
+          f"(fluid model; the 1-queue column reproduces the table above)")
+    cuts = sorted(int(k.split('-')[0]) for k in rng if k.endswith('-16'))
+    for cut in cuts:
+        for bw in (100.0, 200.0, 400.0):
+            r1 = model2(cut, rng[f"{cut}-16"], rng[f"0-{cut}"], a.world, bw, a.alpha, 1, True)
+            r2s = model2(cut, rng[f"{cut}-16"], rng[f"0-{cut}"], a.world, bw, a.alpha, 2, True)
+            r2 = model2(cut, rng[f"{cut}-16"], rng[f"0-{cut}"], a.world, bw, a.alpha, 2, False)
+            rows2 += [dict(r1, bw_GBs=bw), dict(r2s, bw_GBs=bw), dict(r2, bw_GBs=bw)]
+            print(f"{cut:>3} {bw:>7.0f} {r1['exposed_us']:>8.1f} {r2s['exposed_us']:>19.1f} {r2['exposed_us']:>17.1f}")
+    print(json.dumps(dict(world=a.world, alpha_us=a.alpha, rows=rows, two_queue_rows=rows2)))
 
 
 if __name__ == "__main__":
