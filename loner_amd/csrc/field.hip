@@ -1180,37 +1180,41 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(LNR_MLP
   // A pair whose 32 d sigma are all 0 (relu(sigma + noise) = 0 for every sample: most pairs of a trained field's
   // free space) adds exact zeros to dW1 and to the level maxima and nothing to dW0 (dw0_scale refuses a zero
   // pair_max), and its d_enc is 0: it is skipped, its encodings not even loaded and its J not written (consumers
-  // form d sigma * J as 0 there, hashgrid.hpp GradJac).  So d sigma runs one pair ahead of the encodings: the
-  // next pair's are loaded only when its d sigma (loaded a pair earlier) has a non-zero.
-  auto load_ds = [&](int64_t m, float& d0, float& d1) {
-    const uint32_t mb = (uint32_t)((m < N ? m : 0) + c) * 4u;
-    d0 = ld_off(a.d_sigma, mb);
-    d1 = ld_off(a.d_sigma, mb + 64u);
-  };
-  auto load_enc = [&](int64_t m, Pre& p) {
-    const uint32_t mb = (uint32_t)((m < N ? m : 0) + c) * 4u;
+  // form d sigma * J as 0 there, hashgrid.hpp GradJac).  The wave finds its live pairs 16 at a time (lane l reads 8
+  // of pair l / 4's d sigma: one load round trip per 16 pairs, not per pair) and walks them with the next live
+  // pair's loads in flight during this one's work.
+  int64_t lb = -16;  // the wave's current batch of 16 pairs (pair n0 + (lb + j) step)
+  uint32_t pm = 0u;  // its live pairs not yet taken
+  auto next_live = [&]() -> int64_t {
+    while (pm == 0u) {
+      lb += 16;
+      if (n0 + lb * step >= N) return -1;  // (wave-uniform)
+      const int64_t m = n0 + (lb + (lane >> 2)) * step;
+      bool lv = false;
+      if (m < N) {
+        const float* dp = a.d_sigma + m + 8 * (lane & 3);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      p.x0[q] = ld_off(a.enc, row_e + (uint32_t)q * st4 + mb);
-      p.x1[q] = ld_off(a.enc, row_e + (uint32_t)q * st4 + mb + 64u);
+        for (int k = 0; k < 8; ++k) lv = lv || dp[k] != 0.f;
+      }
+      const unsigned long long bl = __ballot(lv);
+      uint32_t q = 0u;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) q |= ((bl >> (4 * j)) & 0xFull) ? (1u << j) : 0u;
+      pm = q;
     }
+    const int j = __builtin_ctz(pm);
+    pm &= pm - 1u;
+    return n0 + (lb + j) * step;
   };
-  (void)prefetch;
   Pre pa{};
-  float nd0, nd1;
-  load_ds(n0, pa.d0, pa.d1);
-  bool la = n0 < N && __ballot(pa.d0 != 0.f || pa.d1 != 0.f) != 0ull;  // (wave-uniform)
-  if (la) load_enc(n0, pa);
-  load_ds(n0 + step, nd0, nd1);
-  for (; n0 < N; n0 += step) {
+  int64_t nm = next_live();
+  if (nm >= 0) prefetch(nm, pa);
+  while (nm >= 0) {
     const Pre cur = pa;
-    const bool lc = la;
-    pa.d0 = nd0;
-    pa.d1 = nd1;
-    la = n0 + step < N && __ballot(pa.d0 != 0.f || pa.d1 != 0.f) != 0ull;
-    if (la) load_enc(n0 + step, pa);
-    load_ds(n0 + 2 * step, nd0, nd1);
-    if (lc) LNR_MLP_PAIR(n0, cur);
+    const int64_t m = nm;
+    nm = next_live();
+    if (nm >= 0) prefetch(nm, pa);
+    LNR_MLP_PAIR(m, cur);
   }
 #endif
 #undef LNR_MLP_PAIR

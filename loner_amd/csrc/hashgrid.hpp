@@ -553,8 +553,14 @@ struct BwdWorkspace {
   uint32_t* bucket_done; // [kMaxBuckets] pieces of a cut bucket accumulated so far (k_bwd_accum<true>)
   UnitTable* units;      // the unit accumulation's work list (k_bwd_scan_buckets / k_bwd_units)
   uint2* rec;            // [8 * N * L] records {word, half2} (see "Backward records")
+  // the live backward (LNR_BWD_LIVE): its histogram rows are groups of 8 live waves (64-sample groups holding a
+  // sample with dL/dsigma != 0), listed in sample order
+  uint8_t* wflags;       // [ceil(N / 64)] wave w holds a live sample
+  uint32_t* wlist;       // [ceil(N / 64)] the live waves, ascending
+  uint32_t* live;        // [2] live waves, live rows (= ceil(live waves / 8))
   int64_t n_sb;
   int64_t n_chunks;
+  bool use_live;         // the scans cover live[1] rows instead of n_sb (the live histogram)
 };
 
 inline int64_t bwd_n_sb(int64_t n) { return (n + kSB - 1) / kSB; }
@@ -563,7 +569,8 @@ inline int64_t bwd_n_chunks(int64_t n) { return (bwd_n_sb(n) + kRowsPerChunk - 1
 inline int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
 
 struct WsLayout {
-  int64_t hist, chunk_sum, level_max, counts, k2cnt, seg_start, partial, bucket_done, units, rec, total;
+  int64_t hist, chunk_sum, level_max, counts, k2cnt, seg_start, partial, bucket_done, units, wflags, wlist, live, rec,
+      total;
 };
 
 inline WsLayout ws_layout(const lnr_grid_desc* d, const GridArgs& a, int64_t n) {
@@ -579,6 +586,9 @@ inline WsLayout ws_layout(const lnr_grid_desc* d, const GridArgs& a, int64_t n) 
   w.partial = b;   b += align256((int64_t)2 * kAccumGroups * 2 * kChunk * 8);
   w.bucket_done = b; b += align256(kMaxBuckets * 4);
   w.units = b;     b += align256(sizeof(UnitTable));
+  w.wflags = b;    b += align256((n + 63) / 64);
+  w.wlist = b;     b += align256((n + 63) / 64 * 4);
+  w.live = b;      b += align256(2 * 4);
   // +2 records: the accumulate loads records in pairs
   w.rec = b;       b += align256((8 * n * (int64_t)d->n_levels + 2) * 8);
   w.total = b;
@@ -600,6 +610,9 @@ inline BwdWorkspace carve_workspace(void* base, const GridArgs& a, const lnr_gri
   w.partial = reinterpret_cast<long long*>(p + L.partial);
   w.bucket_done = reinterpret_cast<uint32_t*>(p + L.bucket_done);
   w.units = reinterpret_cast<UnitTable*>(p + L.units);
+  w.wflags = reinterpret_cast<uint8_t*>(p + L.wflags);
+  w.wlist = reinterpret_cast<uint32_t*>(p + L.wlist);
+  w.live = reinterpret_cast<uint32_t*>(p + L.live);
   w.rec = reinterpret_cast<uint2*>(p + L.rec);
   w.n_sb = bwd_n_sb(n);
   w.n_chunks = bwd_n_chunks(n);

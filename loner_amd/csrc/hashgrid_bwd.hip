@@ -59,8 +59,9 @@ __global__ void __launch_bounds__(kMaxChunksPerLevel) k_bwd_chunk_sums(GridArgs 
   const uint32_t nb = a.bucket_base[l + 1] - a.bucket_base[l];
   if (c >= nb) return;
   const uint32_t* col = ws.hist + (int64_t)a.bucket_base[l] * ws.n_sb + c;
+  const int64_t nrows = ws.use_live ? (int64_t)ws.live[1] : ws.n_sb;  // (the live histogram's rows)
   const int64_t r0 = (int64_t)ch * kRowsPerChunk;
-  const int64_t r1 = r0 + kRowsPerChunk < ws.n_sb ? r0 + kRowsPerChunk : ws.n_sb;
+  const int64_t r1 = r0 + kRowsPerChunk < nrows ? r0 + kRowsPerChunk : nrows;
   uint32_t s = 0;
   for (int64_t r = r0; r < r1; r += 16) {  // 16 row loads in flight
     uint32_t v[16];
@@ -81,14 +82,15 @@ __global__ void __launch_bounds__(kMaxChunksPerLevel) k_bwd_scan_rows(GridArgs a
   if (c >= nb) return;
   const uint32_t* cs = ws.chunk_sum + (int64_t)l * ws.n_chunks * kMaxChunksPerLevel + c;
   uint32_t base = 0, tot = 0;  // the preceding chunks' sum; all chunks' (the bucket total, chunk 0)
+  const int64_t nrows = ws.use_live ? (int64_t)ws.live[1] : ws.n_sb;  // (the live histogram's rows)
   // one chunk (a small batch): no k_bwd_chunk_sums launch, the total is this chunk's own column sum
   const int64_t kend = ws.n_chunks == 1 ? 0 : ch == 0 ? ws.n_chunks : ch;
   if (ws.n_chunks == 1) {
     const uint32_t* col = ws.hist + (int64_t)a.bucket_base[l] * ws.n_sb + c;
-    for (int64_t r = 0; r < ws.n_sb; r += 16) {
+    for (int64_t r = 0; r < nrows; r += 16) {
       uint32_t v[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = r + u < ws.n_sb ? col[(r + u) * nb] : 0u;
+      for (int u = 0; u < 16; ++u) v[u] = r + u < nrows ? col[(r + u) * nb] : 0u;
 #pragma unroll
       for (int u = 0; u < 16; ++u) tot += v[u];
     }
@@ -106,7 +108,7 @@ __global__ void __launch_bounds__(kMaxChunksPerLevel) k_bwd_scan_rows(GridArgs a
   if (ch == 0) ws.counts[a.bucket_base[l] + c] = tot;
   uint32_t* col = ws.hist + (int64_t)a.bucket_base[l] * ws.n_sb + c;
   const int64_t r0 = (int64_t)ch * kRowsPerChunk;
-  const int64_t r1 = r0 + kRowsPerChunk < ws.n_sb ? r0 + kRowsPerChunk : ws.n_sb;
+  const int64_t r1 = r0 + kRowsPerChunk < nrows ? r0 + kRowsPerChunk : nrows;
   for (int64_t r = r0; r < r1; r += 16) {  // 16 row loads in flight
     uint32_t v[16];
 #pragma unroll
@@ -234,20 +236,35 @@ __global__ void __launch_bounds__(1024) k_bwd_units(BwdWorkspace ws, uint32_t b0
 // the int64 sums, and the gradient, are bitwise those of the full backward.
 
 // The forward's per-bucket totals over every sample (ws.k2cnt): the column sums of its histogram, from the
-// per-chunk sums when there are several chunks.  grid (L), one thread per bucket column.
-__global__ void __launch_bounds__(kMaxChunksPerLevel) k_bwd_col_totals(GridArgs a, BwdWorkspace ws) {
-  const uint32_t l = blockIdx.x, c = threadIdx.x;
+// per-chunk sums when there are several chunks.  grid (L), 1024 threads: column c = t % 128 of group g = t / 128
+// sums chunks (or rows) g, g + 8, ... with 16 loads in flight, then the 8 groups add in LDS.
+__global__ void __launch_bounds__(1024) k_bwd_col_totals(GridArgs a, BwdWorkspace ws) {
+  __shared__ uint32_t part[8][kMaxChunksPerLevel];
+  const uint32_t l = blockIdx.x, c = threadIdx.x & (kMaxChunksPerLevel - 1), gq = threadIdx.x / kMaxChunksPerLevel;
   const uint32_t nb = a.bucket_base[l + 1] - a.bucket_base[l];
-  if (c >= nb) return;
   uint32_t tot = 0;
-  if (ws.n_chunks == 1) {
-    const uint32_t* col = ws.hist + (int64_t)a.bucket_base[l] * ws.n_sb + c;
-    for (int64_t r = 0; r < ws.n_sb; ++r) tot += col[r * nb];
-  } else {
-    const uint32_t* cs = ws.chunk_sum + (int64_t)l * ws.n_chunks * kMaxChunksPerLevel + c;
-    for (int64_t k = 0; k < ws.n_chunks; ++k) tot += cs[k * kMaxChunksPerLevel];
+  if (c < nb) {
+    const bool rows = ws.n_chunks == 1;
+    const int64_t cnt = rows ? ws.n_sb : ws.n_chunks;
+    const uint32_t* src = rows ? ws.hist + (int64_t)a.bucket_base[l] * ws.n_sb + c
+                               : ws.chunk_sum + (int64_t)l * ws.n_chunks * kMaxChunksPerLevel + c;
+    const int64_t stride = rows ? (int64_t)nb : (int64_t)kMaxChunksPerLevel;
+    for (int64_t k = gq; k < cnt; k += 8 * 16) {
+      uint32_t v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = k + 8 * u < cnt ? src[(k + 8 * u) * stride] : 0u;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) tot += v[u];
+    }
   }
-  ws.k2cnt[a.bucket_base[l] + c] = tot;
+  part[gq][c] = tot;
+  __syncthreads();
+  if (gq == 0 && c < nb) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) t += part[g][c];
+    ws.k2cnt[a.bucket_base[l] + c] = t;
+  }
 }
 
 // Whether lane's run [head_lane, lane] holds a live lane (wl: the wave's live lanes)
@@ -257,23 +274,77 @@ __device__ __forceinline__ bool run_live(unsigned long long wl, const RunInfo& r
   return (wl & upto & ~((1ull << ri.head_lane) - 1ull)) != 0ull;
 }
 
-// The live backward's histogram: one workgroup per row (the full backward's rows), every level, the records
-// k_bwd_scatter_rows<LIVE> places (above).  NL levels, the first NM coherent, at most NB buckets per level.
+// The live waves: wflags[w] = some sample of the 64-sample group w has dL/dsigma != 0 (16 threads of 4 samples
+// per group), then k_bwd_live_list lists them in order and counts them (ws.live: waves, rows of 8).
+__global__ void __launch_bounds__(256) k_bwd_live_flags(const float* __restrict__ dsig, int64_t n, BwdWorkspace ws) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t i = 4 * t;
+  bool lv = false;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) lv = lv || (i + k < n && dsig[i + k] != 0.f);
+  const unsigned long long b = __ballot(lv);
+  const int lane = threadIdx.x & 63;
+  if ((lane & 15) == 0 && i < n) ws.wflags[t >> 4] = ((b >> lane) & 0xFFFFull) != 0ull ? 1 : 0;
+}
+// One workgroup: passes of 1024 x 64 wave flags, each thread listing the live ones among its 64 in order.
+__global__ void __launch_bounds__(1024) k_bwd_live_list(int64_t n_waves, BwdWorkspace ws) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t carry;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  if (t == 0) carry = 0u;
+  for (int64_t p0 = 0; p0 < n_waves; p0 += 1024 * 64) {
+    const int64_t f0 = p0 + 64 * (int64_t)t;
+    unsigned long long m = 0ull;
+    for (int k = 0; k < 64; ++k)
+      if (f0 + k < n_waves && ws.wflags[f0 + k]) m |= 1ull << k;
+    const uint32_t c = (uint32_t)__popcll(m);
+    const uint32_t inc = wave_incl_scan_u32(c);
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    uint32_t off = carry, tot = carry;
+    for (int w = 0; w < 16; ++w) {
+      if (w < wid) off += wsum[w];
+      tot += wsum[w];
+    }
+    off += inc - c;
+    while (m) {
+      const int k = __builtin_ctzll(m);
+      m &= m - 1ull;
+      ws.wlist[off++] = (uint32_t)(f0 + k);
+    }
+    __syncthreads();
+    if (t == 0) carry = tot;
+    __syncthreads();
+  }
+  if (t == 0) {
+    ws.live[0] = carry;
+    ws.live[1] = (carry + 7u) / 8u;
+  }
+}
+
+// The live backward's histogram: row r = the live waves 8r .. 8r + 7 (one per wave of the workgroup), every level,
+// the records k_bwd_scatter_rows<LIVE> places (above).  NL levels, the first NM coherent, at most NB buckets per
+// level.  Rows past the live ones return at once (the scans stop at ws.live[1]).
 template <class PosFn, int NL, int NM, int NB>
 __global__ void __launch_bounds__(kSB) k_bwd_count_live(GridArgs a, PosFn pos, int64_t n, const float* __restrict__ dsig,
                                                         BwdWorkspace ws) {
   __shared__ uint32_t hist[NL * NB];
   const int64_t sb = blockIdx.x;
-  const int64_t i = sb * kSB + threadIdx.x;
-  const bool in = i < n;
+  if (sb >= (int64_t)ws.live[1]) return;  // (block-uniform)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t wi = 8u * (uint32_t)sb + (uint32_t)wid;
+  const bool wok = wi < ws.live[0];
+  const int64_t i = (int64_t)(wok ? ws.wlist[wi] : 0u) * 64 + lane;
+  const bool in = wok && i < n;
   const int64_t ic = in ? i : n - 1;
   for (int t = threadIdx.x; t < NL * NB; t += kSB) hist[t] = 0u;
+  const typename PosFn::Raw raw = pos.load(ic);  // (with d sigma: one round trip)
   const bool live = in && dsig[ic] != 0.f;
   const unsigned long long wl = __ballot(live);
   lds_barrier();
-  if (wl) {  // (wave-uniform) a wave of dead samples emits nothing
+  if (wl) {  // (wave-uniform) the row's tail waves hold no live sample
     float x = 0.f, y = 0.f, z = 0.f;
-    pos.eval(pos.load(ic), x, y, z);
+    pos.eval(raw, x, y, z);
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
       const LevelParams& lv = a.lv[l];
@@ -598,10 +669,14 @@ __device__ __forceinline__ void scatter_rows_body(RowsLds<NL, NB, kRowsStages>& 
   static_assert(NB <= 128, "two buckets per lane");
   static_assert(kRowsStages == 1 || kRowsStages == 2, "one or two stages");
   static_assert(NM <= NL, "coherent levels come first");
-  const int64_t i = sb * kSB + threadIdx.x;
-  const bool in = i < n;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const bool last = sb + 1 >= ws.n_sb;
+  // LIVE: row sb = the live waves 8 sb .. 8 sb + 7 (ws.wlist), each wave its own 64-sample group: the coherent
+  // levels' runs and sums see the lanes the full backward's wave sees
+  const uint32_t wi = 8u * (uint32_t)sb + (uint32_t)wid;
+  const bool wok = !LIVE || wi < ws.live[0];
+  const int64_t i = LIVE ? (int64_t)(wok ? ws.wlist[wi] : 0u) * 64 + lane : sb * kSB + threadIdx.x;
+  const bool in = wok && i < n;
+  const bool last = sb + 1 >= (LIVE ? (int64_t)ws.live[1] : ws.n_sb);
   const int64_t ic = in ? i : n - 1;
   const uint32_t spare = (uint32_t)(8 * n * (int64_t)a.n_levels);  // one of the 2 slack records past the last slot
 
@@ -823,8 +898,14 @@ __global__ void __launch_bounds__(kSB)
 __attribute__((amdgpu_waves_per_eu(rows_waves<GradFn, NB>(), rows_waves<GradFn, NB>())))
 k_bwd_scatter_rows(GridArgs a, PosFn pos, int64_t n, GradFn grad, BwdWorkspace ws, bool skip_zero) {
   __shared__ RowsLds<NL, NB, rows_stages<GradFn, NB>()> sm;
-  scatter_rows_body<PosFn, GradFn, 0, NL, NM, NB, rows_stages<GradFn, NB>(), LIVE>(sm, a, pos, n, grad, ws, skip_zero,
-                                                                                  xcd_row(blockIdx.x, gridDim.x));
+  int64_t sb = xcd_row(blockIdx.x, gridDim.x);
+  if (LIVE) {  // the live rows only, XCD x taking the contiguous rows [x r/8, (x+1) r/8) of them (see xcd_row)
+    const uint32_t r = ws.live[1], r8 = (r + 7u) & ~7u;
+    if (blockIdx.x >= r8) return;
+    sb = (int64_t)(blockIdx.x & 7u) * (r8 >> 3) + (blockIdx.x >> 3);
+    if (sb >= (int64_t)r) return;
+  }
+  scatter_rows_body<PosFn, GradFn, 0, NL, NM, NB, rows_stages<GradFn, NB>(), LIVE>(sm, a, pos, n, grad, ws, skip_zero, sb);
 }
 
 constexpr size_t kScatterLds = (size_t)kCap * 4 + kMaxChunksPerLevel * 8 + (size_t)kCap * 4 + kMaxChunksPerLevel * 4 +
@@ -1530,13 +1611,17 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, Gra
   if (live) {
     if constexpr (GradFn::kScaled) {
       // every sample's bucket totals (the fixed-point units), then the live records' histogram in its place
-      hipLaunchKernelGGL(k_bwd_col_totals, dim3(d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
+      hipLaunchKernelGGL(k_bwd_col_totals, dim3(d->n_levels), dim3(1024), 0, st, a, w);
+      const int64_t n_waves = (n + 63) / 64;
+      hipLaunchKernelGGL(k_bwd_live_flags, dim3((unsigned)((n_waves * 16 + 255) / 256)), dim3(256), 0, st, grad.dsig, n, w);
+      hipLaunchKernelGGL(k_bwd_live_list, dim3(1), dim3(1024), 0, st, n_waves, w);
       auto cnt = m == 3   ? k_bwd_count_live<PosFn, 16, 3, 64>
                  : m == 4 ? k_bwd_count_live<PosFn, 16, 4, 64>
                  : m == 5 ? k_bwd_count_live<PosFn, 16, 5, 64>
                  : m == 6 ? k_bwd_count_live<PosFn, 16, 6, 64>
                           : k_bwd_count_live<PosFn, 16, 7, 64>;
       hipLaunchKernelGGL(cnt, dim3((unsigned)w.n_sb), dim3(kSB), 0, st, a, pos, n, grad.dsig, w);
+      w.use_live = true;  // the scans and the scatter below: the live rows
       if (w.n_chunks > 1)
         hipLaunchKernelGGL(k_bwd_chunk_sums, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a,
                            w);
