@@ -784,13 +784,17 @@ def main():
         # per-stage HIP events in a separate pass after the timed region (recording them costs host time:
         # 47 us per step at C1, where the host issues the step faster than the GPU runs it only without them)
         prof = {}
-        zeros = torch.zeros(1, dtype=torch.float64, device=dev)
+        zeros = torch.zeros(2, dtype=torch.float64, device=dev)
+        nw = R * n_samples // 64
         for i in range(args.warmup + args.steps, args.warmup + args.steps + PROF_STEPS):
             run(i, prof, g0=g0)
-            zeros += (eng.d_sigma(R) == 0).sum()  # (after the step's events: outside every stage)
+            ds = eng.d_sigma(R)  # (after the step's events: outside every stage)
+            zeros[0] += (ds == 0).sum()
+            zeros[1] += (ds[:64 * nw].view(nw, 64) != 0).any(1).logical_not().sum()  # dead 64-sample waves
         torch.cuda.synchronize()
         stage = {k: float(np.mean([v[j].elapsed_time(v[j + 1]) for j in range(0, len(v), 2)])) for k, v in prof.items()}
-        return elapsed, loss, stage, float(zeros.item()) / (PROF_STEPS * R * n_samples)
+        z = zeros.cpu().numpy()
+        return elapsed, loss, stage, (float(z[0]) / (PROF_STEPS * R * n_samples), float(z[1]) / (PROF_STEPS * max(nw, 1)))
 
     cache = args.field_cache if args.field == "trained" else None
     from_init = None
@@ -808,7 +812,8 @@ def main():
         if not (cache and os.path.exists(cache)):
             from_init = {"ms_per_step": elapsed / args.steps * 1e3,
                          "value": world * R * n_samples * args.steps / elapsed,
-                         "loss": float(loss[0]), "dsigma_zero_frac": zero_frac, "stage_ms": stage_ms}
+                         "loss": float(loss[0]), "dsigma_zero_frac": zero_frac[0], "dead_wave_frac": zero_frac[1],
+                         "backward": "live" if eng._live else "full", "stage_ms": stage_ms}
             t_pre = time.perf_counter()
             g0, pre = pretrain(eng, state, kind, win_kf, rpk, spk, strat, dev, r_glob,
                                args.warmup + args.steps + PROF_STEPS, args.pretrain_windows, args.pretrain_iters)
@@ -834,6 +839,7 @@ def main():
     # algorithmic work counts the samples that have it: every sample is encoded and goes through the MLP forward
     # (its sigma decides whether it is dead), but a sample with dL/dsigma = 0 has no scatter-adds and no MLP
     # backward to do (its contributions are exactly 0; the reference's tcnn path does them all the same)
+    zero_frac, dead_wave_frac = zero_frac
     n_live = N * (1.0 - zero_frac)
     bwd_bytes = 1024.0 * n_live + (32.0 * 2 * state.n_entries if fused_adam else 0.0)
     achieved = bwd_bytes / (bwd_ms * 1e-3) / 1e9
@@ -923,6 +929,9 @@ def main():
         # the fraction of ray-samples whose dL/dsigma is exactly 0 (alpha = 1 - exp(-delta relu(sigma + n)) with
         # sigma + n <= 0, rendering_tcnn.py:252,260) over the profiled steps: they contribute exactly nothing
         "dsigma_zero_frac": zero_frac,
+        # the fraction of 64-sample waves without a live sample: the live backward's work skips by wave, and it
+        # runs (LONER_LIVE_BWD=auto) while this share exceeds StepEngine.live_on (backward_stage.backward)
+        "dead_wave_frac": dead_wave_frac,
         # the same bench on the from-init field, timed first in this run (--field trained only)
         **({"from_init": from_init} if from_init is not None else {}),
         # the process group as torch.distributed reports it (None: a single process, no group)

@@ -218,6 +218,10 @@ int lnr_hashgrid_bwd_rays_jac_adam(const lnr_grid_desc* d, const float* rays, co
  * accumulates. */
 int lnr_hashgrid_bwd_accum(const lnr_grid_desc* d, int64_t n, void* workspace, int64_t workspace_bytes,
                            uint32_t level_begin, uint32_t level_end, float* d_table, void* stream);
+/* The same after a live backward (flags: the backward's LNR_BWD_LIVE): picks the accumulation for its smaller
+ * record counts (the unit work list); the result is the same either way. */
+int lnr_hashgrid_bwd_accum_flags(const lnr_grid_desc* d, int64_t n, void* workspace, int64_t workspace_bytes,
+                                 uint32_t level_begin, uint32_t level_end, float* d_table, int32_t flags, void* stream);
 /* Same result with one fp32 atomic pair per corner (coarse levels merged in-wave); d_table
  * accumulates.  Kept as an independent implementation for cross-checking and A/B timing. */
 int lnr_hashgrid_bwd_atomic(const lnr_grid_desc* d, const float* pos01, int64_t n, const float* d_enc,

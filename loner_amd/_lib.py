@@ -134,6 +134,8 @@ _SIGNATURES = {
     "lnr_hashgrid_bwd_rays_jac_adam": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_p, c_i64,
                                                       ctypes.POINTER(AdamEpilogue), c_p, c_i64, c_i32, c_p]),
     "lnr_hashgrid_bwd_accum": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_i64, c_p, c_i64, c_u32, c_u32, c_p, c_p]),
+    "lnr_hashgrid_bwd_accum_flags": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_i64, c_p, c_i64, c_u32, c_u32, c_p,
+                                                     ctypes.c_int32, c_p]),
     "lnr_hashgrid_bwd_atomic": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_i64, c_p, c_i64, c_p, c_p]),
     "lnr_hashgrid_bwd_rays_atomic": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_i64, c_p,
                                                     c_p]),

@@ -551,8 +551,8 @@ class StepEngine:
             self._grid_bwd(rays, R, S, N, flags | L.BWD_NO_ACCUM, s)
             pending = []
             for l0, l1 in self.ar_groups:
-                L.call("lnr_hashgrid_bwd_accum", L.ctypes.byref(st.desc), R * S, self.bwd_ws, self.bwd_ws_bytes, l0,
-                       l1, st.grad_table, s)
+                L.call("lnr_hashgrid_bwd_accum_flags", L.ctypes.byref(st.desc), R * S, self.bwd_ws, self.bwd_ws_bytes,
+                       l0, l1, st.grad_table, flags & L.BWD_LIVE, s)
                 a0, a1 = self._ar_range(l0, l1)
                 pending.append(self._allreduce_async(st.grad[a0:a1]))
             m(prof, "grid_bwd")
@@ -591,8 +591,8 @@ class StepEngine:
         if comm:
             self._grid_bwd(rays, R, S, N, flags | L.BWD_NO_ACCUM, s)
             for i, ((l0, l1), (a0, a1, c), out) in enumerate(zip(self.ar_groups, self.zero_chunks, self.zero_grad)):
-                L.call("lnr_hashgrid_bwd_accum", L.ctypes.byref(st.desc), R * S, self.bwd_ws, self.bwd_ws_bytes, l0,
-                       l1, st.grad_table, s)
+                L.call("lnr_hashgrid_bwd_accum_flags", L.ctypes.byref(st.desc), R * S, self.bwd_ws, self.bwd_ws_bytes,
+                       l0, l1, st.grad_table, flags & L.BWD_LIVE, s)
                 rs[i] = self.reduce_scatter(out, st.grad[a0:a1], async_op=True)
             m(prof, "grid_bwd")
         else:  # one process: this rank's share of the work only (no exchange)

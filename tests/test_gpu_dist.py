@@ -86,7 +86,8 @@ def test_gloo_two_ranks_bucketed_async_allreduce(tmp_path):
 
 def _zero_worker(rank, world, port, out):
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    # the level-looped scatter (and with it the live backward) at this small batch too (read at every launch)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LONER_SCATTER_ROWS_MIN="1")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     from loner_amd.shard import shard_range
@@ -102,11 +103,14 @@ def _zero_worker(rank, world, port, out):
     hooks2 = dict(reduce_scatter=hooks["reduce_scatter"],
                   all_gather=lambda o, i, async_op=False: dist.all_gather_into_tensor(o, i, group=ag_group,
                                                                                      async_op=async_op))
-    for tag, zero, hk in (("ar", None, {}), ("zero", (rank, world), hooks), ("zero2", (rank, world), hooks2)):
+    for tag, zero, hk, live in (("ar", None, {}, False), ("zero", (rank, world), hooks, False),
+                                ("zero2", (rank, world), hooks2, False), ("arlive", None, {}, True),
+                                ("zero2live", (rank, world), hooks2, True)):
         S_, syn, rays, dgt, st = _setup()
         R = rays.shape[0]
         s0, s1 = shard_range(R, rank, world)
         eng = S_.StepEngine(st, s1 - s0, seed=9, allreduce=allreduce, ray_offset=s0, zero=zero, **hk)
+        eng.live_bwd, eng._live = live, live
         for k in range(3):
             eng.step(rays[s0:s1].contiguous(), dgt[s0:s1].contiguous(), global_step=9 + k, scale=syn.CUBES["forest"][0],
                      far_ref=float(rays[0, -1]), n_rays_global=R)
@@ -143,6 +147,10 @@ def test_gloo_two_ranks_sharded_optimizer(tmp_path):
         for r in range(2):
             assert np.array_equal(ref, np.load(tmp_path / f"zero_{what}{r}.npy")), (what, r)
             assert np.array_equal(ref, np.load(tmp_path / f"zero2_{what}{r}.npy")), (what, r)
+            # the live backward (records only for samples with dL/dsigma != 0; ignored where the level-looped scatter
+            # does not apply) through both exchanges: bitwise the same
+            assert np.array_equal(ref, np.load(tmp_path / f"arlive_{what}{r}.npy")), (what, r)
+            assert np.array_equal(ref, np.load(tmp_path / f"zero2live_{what}{r}.npy")), (what, r)
 
 
 def _pipe_worker(rank, world, port, out):
