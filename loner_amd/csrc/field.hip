@@ -1183,13 +1183,20 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(LNR_MLP
   // form d sigma * J as 0 there, hashgrid.hpp GradJac).  The wave finds its live pairs 16 at a time (lane l reads 8
   // of pair l / 4's d sigma: one load round trip per 16 pairs, not per pair) and walks them with the next live
   // pair's loads in flight during this one's work.
-  int64_t lb = -16;  // the wave's current batch of 16 pairs (pair n0 + (lb + j) step)
+  // Round k of the walk gives wave w the pair k W + (w + 7 k) mod W (W waves): every round still covers W
+  // consecutive pairs once, but a wave's position within the rays (16 pairs of 512 samples) changes from round to
+  // round.  With the plain k W + w (W a multiple of 16) a wave met one position in every ray, and the live pairs,
+  // which sit at the positions near the surfaces, went to a few waves (C2 trained: 74 us for 21 % live pairs).
+  const int64_t W = (int64_t)gridDim.x * kWavesPerBlock, w0 = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  const int64_t npairs = N / 32;
+  auto pair_at = [&](int64_t k) { return 32 * (k * W + (w0 + 7 * k) % W); };  // its first sample
+  int64_t lb = -16;  // the wave's current batch of 16 rounds
   uint32_t pm = 0u;  // its live pairs not yet taken
   auto next_live = [&]() -> int64_t {
     while (pm == 0u) {
       lb += 16;
-      if (n0 + lb * step >= N) return -1;  // (wave-uniform)
-      const int64_t m = n0 + (lb + (lane >> 2)) * step;
+      if (lb * W >= npairs) return -1;  // (wave-uniform)
+      const int64_t m = pair_at(lb + (lane >> 2));
       bool lv = false;
       if (m < N) {
         const float* dp = a.d_sigma + m + 8 * (lane & 3);
@@ -1204,7 +1211,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(LNR_MLP
     }
     const int j = __builtin_ctz(pm);
     pm &= pm - 1u;
-    return n0 + (lb + j) * step;
+    return pair_at(lb + j);
   };
   Pre pa{};
   int64_t nm = next_live();
