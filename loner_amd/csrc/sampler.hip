@@ -747,9 +747,14 @@ __global__ void __launch_bounds__(64 * kSamplerWaves) k_sampler_rank(SamplerArgs
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         const float f = fq[q];
-        int e = (int)fminf(fmaxf((f - near) * per + 1.0f, 0.0f), (float)H);
-        while (e > 0 && strat[e - 1] > f) --e;
-        while (e < H && !(strat[e] > f)) ++e;
+        int e;
+        if (span > 0.f) {  // (wave-uniform: one ray per wave)
+          e = (int)fminf(fmaxf((f - near) * per + 1.0f, 0.0f), (float)H);
+          while (e > 0 && strat[e - 1] > f) --e;
+          while (e < H && !(strat[e] > f)) ++e;
+        } else {  // no linspace estimate (far <= near): the same count by binary lifting, not a walk of up to H steps
+          e = upper_count_lift<H>(strat, f);
+        }
         const int pos = lane * Q + q + e;
         out[pos] = f;
         atomicOr(&mk[pos >> 5], 1u << (pos & 31));

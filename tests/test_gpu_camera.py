@@ -120,7 +120,7 @@ def test_camera_rays_vs_oracle(L):
     assert len(set(host(fr.perm[0]).tolist())) == fr.keep
 
 
-def _camera_setup(seed=0, n_kf=2, W=48, H=32, n_per_kf=128):
+def _camera_setup(seed=0, n_kf=2, W=48, H=32, n_per_kf=128, skip_zero=None):
     from loner_amd import camera as C
     from loner_amd import step as S_
     st = S_.FieldState(S_.StepConfig(), device="cuda:0", table_init=0.5, seed=7)
@@ -142,7 +142,7 @@ def _camera_setup(seed=0, n_kf=2, W=48, H=32, n_per_kf=128):
     fr = C.CameraFrames(dirs, W, H, imgs, poses, cube, (0.5, 40.0), n_rays_per_kf=n_per_kf, seed=seed,
                         device="cuda:0")
     cs = C.ColorState(4, device="cuda:0", seed=5)
-    eng = C.CameraStepEngine(st, cs, n_rays=n_kf * n_per_kf, n_samples=128, lr=0.01, seed=seed)
+    eng = C.CameraStepEngine(st, cs, n_rays=n_kf * n_per_kf, n_samples=128, lr=0.01, seed=seed, skip_zero=skip_zero)
     return fr, cs, eng
 
 
@@ -169,13 +169,15 @@ def test_camera_step_learns_and_is_deterministic(L):
     assert torch.equal(cs2.params, cs3.params)
 
 
-def test_camera_two_shards_match_single_batch(L):
+@pytest.mark.parametrize("skip_zero", [True, False])
+def test_camera_two_shards_match_single_batch(L, skip_zero):
     """Data-parallel camera phase: two engines on the two halves of the rays (draws keyed by global
     ray index, loss normalised by the global ray count, one gradient all-reduce) reproduce the
-    single-engine iteration, and both replicas hold identical parameters after Adam."""
+    single-engine iteration, and both replicas hold identical parameters after Adam; with the default
+    zero-weight skipping and with the exact full path (skip_zero=False: every sample's records)."""
     import threading
     from loner_amd import camera as C
-    fr, cs_ref, eng_ref = _camera_setup()
+    fr, cs_ref, eng_ref = _camera_setup(skip_zero=skip_zero)
     R = fr.n_rays(1)
     rays = torch.empty(R, 13, device="cuda:0")
     inten = torch.empty(R, 3, device="cuda:0")
@@ -206,7 +208,7 @@ def test_camera_two_shards_match_single_batch(L):
     def run(rank):
         s0, s1 = (0, R // 2) if rank == 0 else (R // 2, R)
         eng = C.CameraStepEngine(field, states[rank], n_rays=s1 - s0, n_samples=128, lr=0.01, seed=0,
-                                 allreduce=make_allreduce(rank), ray_offset=s0)
+                                 allreduce=make_allreduce(rank), ray_offset=s0, skip_zero=skip_zero)
         losses[rank] = float(eng.step(rays[s0:s1].contiguous(), inten[s0:s1].contiguous(), global_step=7,
                                       n_rays_global=R).item())
 

@@ -437,13 +437,15 @@ def test_ogm_sampler_merge_equals_full_sort(L, S, perturb, monkeypatch):
     ascending) strata (LONER_SAMPLER_MERGE=1), and the draws sorted before the inverse CDF and merged by rank
     (LONER_SAMPLER_MERGE=2, k_sampler_rank, from 256 samples), give the full bitonic sort's depths bit for bit, for
     training (jittered strata) and eval (perturb 0) draws, 2 to 32 values per lane; rays whose strata
-    rounding would cross fall back to the full sort."""
+    rounding would cross fall back to the full sort; rays with far <= near too."""
     g = np.load("tests/golden/samplers.npz")
     rays, occ = g["rays"], g["occ"]
     rng = np.random.default_rng(3)
     rays = np.concatenate([rays] * 4)
     R = rays.shape[0]
     rays[:, 11] = rng.uniform(0.0, 0.05, R)  # a spread of near / far bounds
+    rays[:4, 12] = rays[:4, 11]  # far == near and far < near: no linspace estimate (the rank merge's lifting search)
+    rays[4:8, 12] = rays[4:8, 11] - 0.01
     monkeypatch.setenv("LONER_SAMPLER_RANK_MIN_RAYS", "0")  # (the rank path at this test's ray count too)
     outs = []
     for m in ("0", "1", "2"):
