@@ -8,7 +8,8 @@
 
 Traffic per the MI355X guide's HBM section: bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024, FETCH_SIZE
 doubled on gfx950 (it counts 128-B requests as 64 B), averaged per dispatch and summed over the
-backward stage's kernels for one launch of the stage.
+backward stage's kernels per step, over the steps after the bench's warmup (the first steps run the
+full backward until the live switch's probe lands).
 
     python tools/refresh_profiles.py r01 C2 [source dir, default gpurun_out]
 """
@@ -21,24 +22,38 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BWD_KERNELS = ("k_bwd_col_totals", "k_bwd_count_live", "k_bwd_chunk_sums", "k_bwd_scan_rows", "k_bwd_scan_buckets", "k_bwd_scatter_rows",
-               "k_bwd_scatter", "k_denc_level_max", "k_bwd_accum", "k_bwd_finalize", "k_bwd_accum_units",
-               "k_bwd_finalize_units", "k_bwd_accum_buckets", "k_bwd_units")
+BWD_KERNELS = ("k_bwd_col_totals", "k_bwd_live_flags", "k_bwd_live_list", "k_bwd_count_live", "k_bwd_chunk_sums",
+               "k_bwd_scan_rows", "k_bwd_scan_buckets", "k_bwd_scatter_rows", "k_bwd_scatter", "k_denc_level_max",
+               "k_bwd_accum", "k_bwd_finalize", "k_bwd_accum_units", "k_bwd_finalize_units", "k_bwd_accum_buckets",
+               "k_bwd_units")
 
 
-def per_dispatch(path):
-    """kernel short name -> mean counter value per dispatch."""
-    tot = collections.defaultdict(float)
-    disp = collections.defaultdict(set)
-    for row in csv.DictReader(open(path)):
-        name = row["Kernel_Name"]
-        base = name.split("(")[0].split("<")[0].replace("void ", "").replace("lnr::", "").strip()
-        key = base if base in BWD_KERNELS else None
-        if key is None:
-            continue
-        tot[key] += float(row["Counter_Value"])
-        disp[key].add(row["Dispatch_Id"])
-    return {k: tot[k] / len(disp[k]) for k in tot}
+def _short(name):
+    return name.split("(")[0].replace("void ", "").replace("lnr::", "").strip()
+
+
+def _base(name):
+    return _short(name).split("<")[0]
+
+
+def _timed_rows(paths_mults, warmup):
+    """Rows (short kernel name, bytes) of the steps after the bench's warmup: a step ends with its Adam
+    (k_adam), so the dispatches after the warmup-th k_adam are the timed and profiled steps.  Returns
+    (steps counted, {name: [bytes, dispatch ids]})."""
+    out = collections.defaultdict(lambda: [0.0, set()])
+    n_steps = None
+    for path, mult in paths_mults:
+        rows = list(csv.DictReader(open(path)))
+        adam = sorted({int(r["Dispatch_Id"]) for r in rows if _base(r["Kernel_Name"]) == "k_adam"})
+        cut = adam[warmup - 1] if 0 < warmup <= len(adam) else -1
+        n = len(adam) - (warmup if 0 < warmup <= len(adam) else 0)
+        n_steps = n if n_steps is None else min(n_steps, n)
+        for r in rows:
+            if int(r["Dispatch_Id"]) > cut:
+                e = out[_short(r["Kernel_Name"])]
+                e[0] += mult * float(r["Counter_Value"]) * 1024
+                e[1].add((path, r["Dispatch_Id"]))
+    return max(n_steps or 0, 1), out
 
 
 MLP_KERNELS = ("k_sigma_fwd_tiles", "k_field_wave", "k_mlp_bwd_tiles")
@@ -70,23 +85,14 @@ def mfma_busy(path):
 OGM_KERNELS = ("k_ogm_grad", "k_sum_replicas", "k_sgd")
 
 
-def step_traffic(fetch_csv, write_csv):
-    """Per kernel name: HBM bytes per optimiser step from a --pmc pass over bench.py.  The step count is
-    k_adam's dispatch count (one Adam per step); kernels dispatched at least once per step are counted
-    whole, the OGM kernels (every 10th step) too, set-up kernels (fewer dispatches) are left out."""
-    vals = collections.defaultdict(float)
-    disp = collections.defaultdict(set)
-    for path, mult in ((fetch_csv, 2.0), (write_csv, 1.0)):  # FETCH_SIZE doubled on gfx950
-        for row in csv.DictReader(open(path)):
-            name = row["Kernel_Name"].split("(")[0].replace("void ", "")
-            vals[name] += mult * float(row["Counter_Value"]) * 1024
-            disp[name].add(row["Dispatch_Id"])
-    n_steps = max((len(d) for k, d in disp.items() if "k_adam" in k), default=0)
-    out = {}
-    for k, v in vals.items():
-        calls = len(disp[k]) // 1
-        if calls >= n_steps or any(o in k for o in OGM_KERNELS):
-            out[k] = {"bytes_per_step": v / n_steps, "dispatches": calls}
+def step_traffic(fetch_csv, write_csv, warmup):
+    """Per kernel: HBM bytes per optimiser step from the --pmc passes over bench.py, over the steps after the
+    warmup (the timed and profiled steps), FETCH_SIZE doubled on gfx950."""
+    n_steps, rows = _timed_rows(((fetch_csv, 2.0), (write_csv, 1.0)), warmup)
+    # (torch's own kernels are the bench's instrumentation around its profiled steps -- the dL/dsigma zero
+    # counts -- and the live switch's probe, not the step)
+    out = {k: {"bytes_per_step": v[0] / n_steps, "dispatches": len(v[1]) // 2} for k, v in rows.items()
+           if not k.startswith("at::")}
     return n_steps, out
 
 
@@ -98,25 +104,27 @@ def main(tag, cfg, src=None):
     stats = glob.glob(os.path.join(out, "prof", "*kernel_stats.csv"))
     if stats:
         shutil.copy(stats[0], os.path.join(prof, f"{tag}_bench_{cfg}_kernel_stats.csv"))
+    bench = json.load(open(os.path.join(out, "bench.json")))
+    warmup = int(bench.get("warmup", 10))
     f = glob.glob(os.path.join(out, "pmc", "FETCH_SIZE", "*counter_collection.csv"))
     w = glob.glob(os.path.join(out, "pmc", "WRITE_SIZE", "*counter_collection.csv"))
     if f and w:
-        fk, wk = per_dispatch(f[0]), per_dispatch(w[0])
-        kern = {k: {"FETCH_SIZE_kB": fk.get(k, 0.0), "WRITE_SIZE_kB": wk.get(k, 0.0),
-                    "hbm_bytes": (2 * fk.get(k, 0.0) + wk.get(k, 0.0)) * 1024} for k in sorted(set(fk) | set(wk))}
-        total = sum(v["hbm_bytes"] for v in kern.values())
-        bench = json.load(open(os.path.join(out, "bench.json")))
-        rec = {"stage": "hash-grid backward (one launch of the stage per step)", "config": cfg,
-               "hbm_bytes_per_launch": total, "algorithmic_bytes_per_launch": bench["roofline"]["algorithmic_bytes_per_launch"],
-               "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving, validated per access pattern in profiles/r04_fetch_calibration.json)",
-               "kernels": kern}
+        n_steps, rows = _timed_rows(((f[0], 2.0), (w[0], 1.0)), warmup)
+        kern = {k: {"bytes_per_step": v[0] / n_steps, "dispatches": len(v[1]) // 2} for k, v in rows.items()
+                if _base(k) in BWD_KERNELS}
+        total = sum(v["bytes_per_step"] for v in kern.values())
+        alg = (bench.get("backward_stage") or {}).get("algorithmic_bytes_per_launch")
+        rec = {"stage": "hash-grid backward, every kernel of the stage, per step (one launch of the stage per step)",
+               "config": cfg, "steps_profiled": n_steps, "hbm_bytes_per_launch": total,
+               "algorithmic_bytes_per_launch": alg, "ratio_to_algorithmic": total / alg if alg else None,
+               "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving, validated per access pattern in profiles/r04_fetch_calibration.json); the steps after the bench's warmup",
+               "kernels": dict(sorted(kern.items(), key=lambda kv: -kv[1]["bytes_per_step"]))}
         json.dump(rec, open(os.path.join(prof, f"{tag}_traffic_{cfg}.json"), "w"), indent=1)
-        print(f"traffic {total / 1e9:.3f} GB per launch vs algorithmic {rec['algorithmic_bytes_per_launch'] / 1e9:.3f} GB")
+        print(f"backward traffic {total / 1e9:.3f} GB per step vs algorithmic {(alg or 0) / 1e9:.3f} GB")
     f = glob.glob(os.path.join(out, "pmc_step", "FETCH_SIZE", "*counter_collection.csv"))
     w = glob.glob(os.path.join(out, "pmc_step", "WRITE_SIZE", "*counter_collection.csv"))
     if f and w:
-        n_steps, kern = step_traffic(f[0], w[0])
-        bench = json.load(open(os.path.join(out, "bench.json")))
+        n_steps, kern = step_traffic(f[0], w[0], warmup)
         total = sum(v["bytes_per_step"] for v in kern.values())
         alg = bench["roofline"].get("step_algorithmic_bytes")
         rec = {"what": "HBM bytes per optimiser step, every kernel of the step (rocprofv3 --pmc FETCH_SIZE and "
