@@ -76,6 +76,9 @@ def parse():
                     help="--field trained: save the pre-trained field here, or load it if PATH exists and skip the "
                          "from-init steps and the pre-training (profiling runs: kernel statistics of the trained "
                          "window only)")
+    ap.add_argument("--joint-poses", action="store_true",
+                    help="the timed window optimises the keyframe poses with the map (the joint config of the "
+                         "reference's default mapper schedule, cfg/defaults.yaml:93-97; keyframe 0 anchored)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rays", type=int, default=512, help="rays per reduced-config CPU-baseline step (x512 samples)")
     ap.add_argument("--cpu-steps", type=int, default=24)
@@ -796,8 +799,24 @@ def main():
         z = zeros.cpu().numpy()
         return elapsed, loss, stage, (float(z[0]) / (PROF_STEPS * R * n_samples), float(z[1]) / (PROF_STEPS * max(nw, 1)))
 
+    poses_desc = "fixed (ground-truth poses, use_gt_poses: the north-star driver)"
+
+    def arm_poses(n_iter):
+        """--joint-poses: the keyframes' pose tensors (keyframe 0 anchored) in an Adam at lrate_pose 1e-3."""
+        nonlocal poses_desc
+        if not args.joint_poses:
+            return
+        from loner_amd.pose import PoseWindow
+        pw = PoseWindow(window, [k > 0 for k in range(window.n_kf)], 1e-3, allreduce=allreduce, n_iter=n_iter)
+        eng.set_poses(pw)
+        poses_desc = (f"joint pose + map: {window.n_kf - 1} keyframe poses in an Adam at 1e-3 beside the map "
+                      f"(keyframe 0 anchored; optimizer.py:258-262)"
+                      + ("" if pw.stay_valid else ", rays filtered every step (window near the cube's faces)"))
+
     cache = args.field_cache if args.field == "trained" else None
     from_init = None
+    if args.field != "trained":
+        arm_poses(args.warmup + args.steps + PROF_STEPS)
     if cache and os.path.exists(cache):
         # a profiling run: the pre-trained field of an earlier run (no from-init steps, no pre-training here, so
         # the kernel statistics hold the trained window's steps only)
@@ -822,6 +841,7 @@ def main():
                 torch.save({"params": state.params.cpu(), "occ": state.occ.cpu(), "g0": g0, "pre": json.dumps(pre)},
                            cache)
         state.reset_optimizer()  # the timed window: a new Adam (optimizer.py:255-265)
+        arm_poses(args.warmup + args.steps + PROF_STEPS)
         elapsed, loss, stage_ms, zero_frac = measure(g0)
 
     if rank != 0:
@@ -890,6 +910,7 @@ def main():
                                    % pre["steps"] if args.field == "trained" else
                                    "from init: tcnn-like U(+-1e-4) table, Xavier MLP, steps %d-%d after it"
                                    % (args.warmup, args.warmup + args.steps - 1)),
+                   "poses": poses_desc,
                    **({"pretrain": pre} if args.field == "trained" else {}),
                    **({"submap_rank0": submap} if submap is not None else {})},
         # the dominant kernel, the training encode (k_hashgrid_fwd: 8 gathers per sample and level, 512 B per

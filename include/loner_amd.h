@@ -293,6 +293,11 @@ typedef struct lnr_loss_params {
                                 here, in its last launch (one launch less per step) */
   int32_t flags;             /* LNR_LP_* */
   const lnr_step_scalars* dev_step; /* optional DEVICE: key (the noise), los_lambda and los_eps from here */
+  float* dev_d_ray;          /* optional DEVICE (R,2), lnr_field_train: [dL/d|d|, dL/dfar] per ray, the loss's
+                                dependence on the ray itself when the poses are optimised (optimizer.py:258-262;
+                                rendering_tcnn.py:248,274-278; the samples z are detached, ray_sampling.py:75-90).
+                                With the hash grid's input gradient (lnr_hashgrid_bwd_rays_jac's d_pos) it gives
+                                dL/d{origin, direction, far} of every ray (joint pose + map) */
 } lnr_loss_params;
 #define LNR_LP_DW_OVERWRITE 1  /* lnr_field_train STORES d_w (the MLP gradient) instead of adding to it */
 

@@ -384,15 +384,26 @@ __device__ void composite_ray(const FieldArgs& a, const RayShared& sh, int64_t r
   float redD[1] = {(float)acc_los};
   block_sum<NT, 1>(redD, sh.red);
   float X = block_suffix_affine(FA, FB, sh.fscan);
+  double acc_dn = 0.0;
 #pragma unroll
   for (int c = C - 1; c >= 0; --c) {
     if (active && i0 + c < S) {
       const float dA = T[c] * (G[c] - X);
       X = G[c] * alpha[c] + s[c] * X;
       const float sr = fmaxf(x[c], 0.f);
-      const float dsig = (x[c] > 0.f) ? dA * (delta[c] * expf(-(delta[c] * sr))) : 0.f;
+      const float ex = expf(-(delta[c] * sr));
+      const float dsig = (x[c] > 0.f) ? dA * (delta[c] * ex) : 0.f;
       sh.sig[i0 + c] = dsig;
       if (a.d_sigma) a.d_sigma[r * S + i0 + c] = dsig;
+      acc_dn += (double)((dA * (ex * sr)) * dlr[c]);
+    }
+  }
+  if (a.d_ray) {  // the loss's dependence on the ray (poses under optimisation): see composite_loss_wave
+    float rd[1] = {(float)acc_dn};
+    block_sum<NT, 1>(rd, sh.red);
+    if (t == 0) {
+      a.d_ray[2 * r + 0] = rd[0];
+      a.d_ray[2 * r + 1] = ADJ ? 0.f : g_depth * (1.0f - wsum);
     }
   }
   if (a.weights && active)
@@ -722,12 +733,36 @@ __device__ void composite_loss_wave(const FieldArgs& a, float* sig, int64_t r) {
   }
   const float los = wave_sum((float)acc_los);
   float X = wave_suffix_affine(FA, FB);
+  if (a.d_ray) {
+    // poses under optimisation (optimizer.py:258-262): the loss's dependence on the ray itself.  deltas =
+    // dl * |d| (rendering_tcnn.py:248), so dL/d|d| = sum dA * dl * relu(x) * exp(-delta relu(x)); depth =
+    // sum w z + (1 - sum w) far (:274-278), so dL/dfar = g_depth (1 - sum w).  The z are detached
+    // (ray_sampling.py:75-90 samples under no_grad).  (A wave-uniform branch: the default step keeps
+    // the loop below.)
+    double acc_dn = 0.0;
+    const float inv_dn = dnorm > 0.f ? 1.0f / dnorm : 0.f;
 #pragma unroll
-  for (int c = C - 1; c >= 0; --c) {
-    const float dA = T[c] * (G[c] - X);
-    X = G[c] * alpha[c] + s[c] * X;
-    const float sr = fmaxf(x[c], 0.f);
-    sig[i0 + c] = (x[c] > 0.f) ? dA * (delta[c] * expf(-(delta[c] * sr))) : 0.f;
+    for (int c = C - 1; c >= 0; --c) {
+      const float dA = T[c] * (G[c] - X);
+      X = G[c] * alpha[c] + s[c] * X;
+      const float sr = fmaxf(x[c], 0.f);
+      const float ex = expf(-(delta[c] * sr));
+      sig[i0 + c] = (x[c] > 0.f) ? dA * (delta[c] * ex) : 0.f;
+      acc_dn += (double)((dA * (ex * sr)) * (delta[c] * inv_dn));
+    }
+    const float dn = wave_sum((float)acc_dn);
+    if (lane == 0) {
+      a.d_ray[2 * r + 0] = dn;
+      a.d_ray[2 * r + 1] = g_depth * (1.0f - wsum);
+    }
+  } else {
+#pragma unroll
+    for (int c = C - 1; c >= 0; --c) {
+      const float dA = T[c] * (G[c] - X);
+      X = G[c] * alpha[c] + s[c] * X;
+      const float sr = fmaxf(x[c], 0.f);
+      sig[i0 + c] = (x[c] > 0.f) ? dA * (delta[c] * expf(-(delta[c] * sr))) : 0.f;
+    }
   }
   if (a.weights)
 #pragma unroll
@@ -1482,6 +1517,7 @@ extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t e
   a.n_rays = n_rays; a.S = n_samples; a.noise_std = noise_std; a.noise = noise; a.key = key;
   a.ray_offset = ray_offset; a.lp = *lp; a.d_enc = d_enc; a.dw_slab = workspace; a.ray_stats = ray_stats;
   a.depth = depth; a.opacity = opacity; a.weights = weights; a.denc_max = d_enc_level_max; a.d_jac = d_enc_jac;
+  a.d_ray = lp->dev_d_ray;
   hipStream_t st = as_stream(stream);
   int nb;
   const int C = n_samples / 64;

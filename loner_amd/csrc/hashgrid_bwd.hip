@@ -1690,8 +1690,8 @@ static int check_desc_bwd(const lnr_grid_desc* d, const char* who) {
 // dL/dy * dy/dx[dim]).  Table values are the fp16 forward operand; the arithmetic is fp32.
 // One thread per sample walks every level, so each sample's gradient is one fixed-order sum (no
 // atomics): deterministic.  The 8 corner gathers of a level are issued before any arithmetic.
-// Only launched when the caller asks for d_pos: the training step (which holds the poses fixed)
-// never pays for it.
+// Only launched when the caller asks for d_pos: the map-only step (poses fixed) never pays for it; the
+// joint pose + map step (loner_amd/pose.py) does, over its live samples only (dL/dsigma != 0).
 constexpr int kDposThreads = 256;
 #ifndef LNR_DPOS_LEVELS_PER_PASS
 #define LNR_DPOS_LEVELS_PER_PASS 2  // C2 (tools/k3_metrics.py): 1.47 ms at 16, 1.35 at 8, 1.23 at 4, 1.13 at 2, 1.25 at 1
@@ -1757,6 +1757,15 @@ __global__ void __launch_bounds__(kDposThreads) k_hashgrid_dpos(GridArgs a, PosF
                                                                 float* __restrict__ d_pos, uint32_t l0, uint32_t l1) {
   const int64_t i = (int64_t)blockIdx.x * kDposThreads + threadIdx.x;
   if (i >= n) return;
+  if constexpr (GradFn::kScaled) {
+    // a sample with dL/dsigma = 0 has d_enc = 0 at every level, so d_pos = 0 (every term is +-0 * a finite
+    // difference of fp16 values): skip its gathers (most samples of a trained field: the live backward's
+    // dead samples, hashgrid.hpp) -- bitwise the full sum
+    if (grad.scale(i) == 0.f) {
+      if (l0 == 0) d_pos[3 * i + 0] = d_pos[3 * i + 1] = d_pos[3 * i + 2] = 0.f;
+      return;
+    }
+  }
   float x, y, z;
   pos(i, x, y, z);
   float r0 = 0.f, r1 = 0.f, r2 = 0.f;
@@ -1792,7 +1801,9 @@ __global__ void __launch_bounds__(kDposThreads) k_hashgrid_dpos_k(GridArgs a, Po
       const bool in = i < n;
       float x = 0.f, y = 0.f, z = 0.f;
       pos.wave(i, n, in, x, y, z);
-      if (in) dpos_level(p, l, i, x, y, z, table, grad, r[k][0], r[k][1], r[k][2]);
+      bool live = in;
+      if constexpr (GradFn::kScaled) live = live && grad.scale(i) != 0.f;  // (as k_hashgrid_dpos)
+      if (live) dpos_level(p, l, i, x, y, z, table, grad, r[k][0], r[k][1], r[k][2]);
     }
   }
 #pragma unroll

@@ -15,17 +15,18 @@ The schedule logic follows the reference:
 Rays are selected and built on the device from the window held in HBM (``RayWindow``). Each
 iteration is ``StepEngine.step``: no host synchronisation until the window's final loss is read.
 
-Scope: the map, i.e. the sigma head.
-* Pose optimisation (tracking, joint refinement) is out of scope. An iteration config that asks
-  for it with a frozen sigma head (tracking only) raises ``NotImplementedError``.  A joint config
-  (``freeze_poses: False`` with the sigma head trained, the reference's default mapper schedule,
-  cfg/defaults.yaml:93-97) also raises, unless the caller opts in with ``fixed_poses=True``: then the
-  map part runs with the poses held fixed, a different optimisation problem from the reference's
-  joint one (optimizer.py:258-262 puts the pose tensors in the same Adam), so it is never silent.
-  ``use_gt_poses=True`` (the north-star driver, fdt_optimize_implicit_map.py:355) freezes the poses as
-  the reference does and needs no opt-in.
-* The colour head trains in the camera phase: ``iterate_optimizer_camera(frames)`` over a
-  ``loner_amd.camera.CameraFrames`` window (``loner_amd.camera``).
+Poses (optimizer.py:235-262): an iteration config with ``freeze_poses: False`` optimises the pose
+tensors [t, axis-angle] of the active window's un-anchored keyframes (a window of one keyframe anchors
+it, :196-197) in an Adam at ``lrate_pose`` beside the map's, with the same ExponentialLR; the joint
+config of the default mapper schedule (cfg/defaults.yaml:93-97) and pose tracking (both heads frozen,
+:252-257: the map's Adam steps at lr 0) both run on the fused step (``loner_amd.pose``: the step writes
+dL/d{ray} and dL/dpos, chained to the poses on the device).  The optimised poses are written back into
+the keyframes (scan dicts: ``pose6`` and ``pose``; objects: their pose tensor).  ``fixed_poses=True``
+keeps the poses fixed instead (a map-only run of such configs, with a warning); ``use_gt_poses=True``
+(the north-star driver, fdt_optimize_implicit_map.py:355) freezes them as the reference does.
+
+The colour head trains in the camera phase: ``iterate_optimizer_camera(frames)`` over a
+``loner_amd.camera.CameraFrames`` window (``loner_amd.camera``).
 
 Keyframes are ``loner_amd`` scan dicts (``directions`` (3,P), ``distances`` (P,), optional
 ``sky_directions`` (3,Q), ``pose`` (4,4)), or objects with the reference's KeyFrame accessors
@@ -65,6 +66,54 @@ class OptimizationSettings:
         return OptimizationSettings(d.get("num_iterations", 1), d.get("freeze_poses", False),
                                     d.get("latest_kf_only", False), d.get("freeze_sigma_mlp", False),
                                     d.get("freeze_rgb_mlp", False))
+
+
+def _kf_time(kf):
+    t = kf.get("time") if isinstance(kf, dict) else getattr(kf, "get_time", lambda: None)()
+    return None if t is None else float(t)
+
+
+def _is_anchored(kf):
+    return bool(kf.get("anchored", False)) if isinstance(kf, dict) else bool(getattr(kf, "is_anchored", False))
+
+
+def _set_anchored(kf):
+    if isinstance(kf, dict):
+        kf["anchored"] = True
+    else:
+        kf.is_anchored = True
+
+
+def _pose6_of(kf, scan):
+    """The keyframe's pose tensor [t, axis-angle] (Pose.get_pose_tensor), or transform_to_tensor of its matrix."""
+    from .pose import matrix_to_pose6
+    if isinstance(kf, dict):
+        if kf.get("pose6") is not None:
+            return torch.as_tensor(kf["pose6"], dtype=torch.float32).reshape(6).cpu()
+        return matrix_to_pose6(scan["pose"])
+    p = kf.get_lidar_pose()
+    if hasattr(p, "get_pose_tensor") and p.get_pose_tensor() is not None:
+        return p.get_pose_tensor().detach().float().reshape(6).cpu()
+    return matrix_to_pose6(scan["pose"])
+
+
+def _write_poses(keyframes, scans, pw):
+    """The optimised poses back into their keyframes (the reference's pose tensors change in place):
+    scan dicts get ``pose6`` and ``pose`` (4x4), objects with a pose tensor get it overwritten."""
+    p6 = pw.p6.detach().cpu()
+    M = pw.matrices()
+    moved = pw.optimise.cpu().tolist()
+    for k, (kf, sc) in enumerate(zip(keyframes, scans)):
+        if not moved[k]:
+            continue  # an anchored keyframe keeps its pose as it was
+        if isinstance(kf, dict):
+            kf["pose6"] = p6[k].clone()
+            kf["pose"] = M[k].clone()
+        else:
+            p = kf.get_lidar_pose()
+            if hasattr(p, "get_pose_tensor") and p.get_pose_tensor() is not None:
+                with torch.no_grad():
+                    p.get_pose_tensor().copy_(p6[k].to(p.get_pose_tensor().device))
 
 
 def _scan_dict(kf):
@@ -121,6 +170,7 @@ class Optimizer:
             n_iters_acc=int(_g(occ, "N_iters_acc", 10)), sampler=self._samples_strategy,
             loss=LossConfig.from_dict(dict(loss)) if loss is not None else LossConfig())
         self._lr_gamma = float(_g(train, "lrate_gamma", 1.0))
+        self._lr_pose = float(_g(train, "lrate_pose", 0.001))
         self.state = FieldState(self.cfg, device=self._device, seed=seed)
         self._seed = int(seed)
         self._allreduce, self._rank, self._world = allreduce, int(rank), int(world)
@@ -170,39 +220,37 @@ class Optimizer:
         return result
 
     def _do_iterate_optimizer(self, keyframe_window, iteration_schedule, optimizer_settings=None) -> float:
+        if len(keyframe_window) == 1:
+            _set_anchored(keyframe_window[0])  # optimizer.py:196-197 (persists on the keyframe)
         if len(iteration_schedule) > 1 and _g(self._settings, "skip_pose_refinement", False):
             iteration_schedule = iteration_schedule[1:]
         if optimizer_settings is not None:
             iteration_schedule = [None]
-        scans = [_scan_dict(kf) for kf in keyframe_window]
         loss = None
         for config in iteration_schedule:
             os_ = optimizer_settings if config is None else OptimizationSettings.from_dict(config)
             freeze_poses = os_.freeze_poses or bool(_g(self._settings, "freeze_poses", False)) or self._use_gt_poses
-            if not freeze_poses:
-                if os_.freeze_sigma_mlp:
-                    raise NotImplementedError("pose tracking (frozen sigma head, free poses) is outside this build's "
-                                              "scope (SURVEY.md §8)")
-                if not self._fixed_poses:
-                    raise NotImplementedError(
-                        "joint pose + map optimisation (freeze_poses: False) is outside this build's scope: the "
-                        "reference optimises the poses in the same Adam (optimizer.py:258-262). Pass "
-                        "Optimizer(..., fixed_poses=True) to optimise the map with the poses held fixed, or "
-                        "use_gt_poses=True / freeze_poses: True as the north-star driver does")
+            if not freeze_poses and self._fixed_poses:
                 if not self._warned_poses:
                     self._warned_poses = True
-                    warnings.warn("fixed_poses=True: the joint config's poses stay fixed and only the map is "
-                                  "optimised")
-            if os_.freeze_sigma_mlp:
-                continue  # nothing of the map to optimise in this config
-            window_scans = scans
-            if os_.latest_kf_only and len(scans) > 1:
-                window_scans = scans[-1:]
+                    warnings.warn("fixed_poses=True: the config's poses stay fixed and only the map is optimised")
+                freeze_poses = True
+            # optimizer.py:252-253: poses free with both heads frozen is pose tracking (the map's Adam
+            # steps at lr 0 here: the map does not move)
+            tracking = (not freeze_poses) and os_.freeze_sigma_mlp and os_.freeze_rgb_mlp
+            if os_.freeze_sigma_mlp and not tracking:
+                continue  # nothing of the map or the poses to optimise in this config
+            # the active window (optimizer.py:237-246): the most recent keyframe only, or all of them
+            active = list(keyframe_window)
+            if os_.latest_kf_only and len(active) > 1:
+                active = [max(active, key=_kf_time)] if all(_kf_time(k) is not None for k in active) else active[-1:]
             self.state.reset_optimizer()  # a new torch.optim.Adam per iteration config (:255-265)
-            loss = self._run_config(window_scans, int(os_.num_iterations))
+            loss = self._run_config(active, int(os_.num_iterations), optimise_poses=not freeze_poses,
+                                    tracking=tracking)
         return float(loss[0].item()) if loss is not None else float("nan")
 
-    def _run_config(self, scans, num_iterations):
+    def _run_config(self, keyframes, num_iterations, optimise_poses=False, tracking=False):
+        scans = [_scan_dict(kf) for kf in keyframes]
         n_sky = self._num_sky_samples if self._enable_sky_segmentation else 0
         fixed = self._rays_strategy == "FIXED"
         window = RayWindow(scans, self._world_cube, self._ray_range, n_lidar=self._num_lidar_samples, n_sky=n_sky,
@@ -211,15 +259,33 @@ class Optimizer:
         out = None
         if fixed:
             given, num_iterations = self._fixed_schedule(scans, window)
-        for it in range(num_iterations):
-            eng.lr_factor = self._lr_gamma ** it  # ExponentialLR stepped after every iteration
-            if fixed:
-                out = self._fixed_step(eng, window, given, it)
-            else:
-                out = eng.step_window(window, global_step=self._global_step, iteration_idx=it,
-                                      n_rays_global=window.n_slots, n_slots=n_local)
-            self._global_step += 1
-        eng.lr_factor = 1.0
+        pw = None
+        if optimise_poses:
+            # joint pose + map (optimizer.py:258-262) or tracking (:255-257): the un-anchored keyframes' pose
+            # tensors in an Adam at lrate_pose beside the map's, same ExponentialLR (loner_amd.pose)
+            from .pose import PoseWindow
+            p6 = [_pose6_of(kf, sc) for kf, sc in zip(keyframes, scans)]
+            pw = PoseWindow(window, [not _is_anchored(kf) for kf in keyframes], self._lr_pose,
+                            pose6=torch.stack(p6), allreduce=self._allreduce if self._world > 1 else None,
+                            n_iter=num_iterations, lr_gamma=self._lr_gamma)
+            eng.set_poses(pw)
+            eng.map_frozen = bool(tracking)
+        try:
+            for it in range(num_iterations):
+                eng.lr_factor = self._lr_gamma ** it  # ExponentialLR stepped after every iteration
+                if fixed:
+                    out = self._fixed_step(eng, window, given, it)
+                else:
+                    out = eng.step_window(window, global_step=self._global_step, iteration_idx=it,
+                                          n_rays_global=window.n_slots, n_slots=n_local)
+                self._global_step += 1
+        finally:
+            eng.lr_factor = 1.0
+            if pw is not None:
+                eng.set_poses(None)
+                eng.map_frozen = False
+        if pw is not None:
+            _write_poses(keyframes, scans, pw)
         eng.release()  # the next window is a new object: this one's prefetched step and graphs are dropped
         return out
 
@@ -314,5 +380,11 @@ class Optimizer:
             s0, s1 = shard_range(n_glob, self._rank, self._world)
             rays, depth = rays[s0:s1], depth[s0:s1]
             eng.ray_offset = s0
-        return eng.step(rays.contiguous(), depth.contiguous(), self._global_step, it, scale=window.scale,
-                        far_ref=far_ref, n_rays_global=n_glob)
+        out = eng.step(rays.contiguous(), depth.contiguous(), self._global_step, it, scale=window.scale,
+                       far_ref=far_ref, n_rays_global=n_glob)
+        if eng.poses is not None:
+            slots = torch.nonzero(sel).squeeze(1)
+            if self._world > 1:
+                slots = slots[s0:s1]
+            eng.poses.step(eng, rays, slots, eng.lr_factor)
+        return out

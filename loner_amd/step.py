@@ -352,12 +352,38 @@ class StepEngine:
         self._live = self.live_bwd is True
         self._probe_ev, self._probe_ctr, self._probe_n = None, self.live_probe_every, 1
         self._probe_host = torch.zeros(1, dtype=torch.int64).pin_memory() if torch.cuda.is_available() else None
+        # Joint pose + map (loner_amd.pose): with pose_grad on, the step also writes per ray [dL/d|d|, dL/dfar]
+        # (d_ray, from the field kernel) and per sample dL/dpos01 (d_pos, the hash grid's input gradient,
+        # before the table's Adam); ``poses`` (a pose.PoseWindow) then takes its Adam step after every
+        # step_window step and rewrites the window's pose rows, which the next step's ray build reads
+        self.pose_grad = False
+        self.map_frozen = False
+        self.poses = None
+        self.d_ray = self.d_pos = None
+        self._last_batch, self._slots_cache = None, None
         self._pp_bufs = [dict(rays=self.rays if i == 0 else torch.empty_like(self.rays),
                               dgt=self.depth_gt if i == 0 else torch.empty_like(self.depth_gt),
                               valid=self.ray_valid if i == 0 else torch.empty_like(self.ray_valid),
                               far=self.far_ref if i == 0 else torch.empty_like(self.far_ref),
                               z=self.z if i == 0 else torch.empty_like(self.z))
                          for i in range(2)]
+
+    def map_lr(self):
+        """The map's Adam learning rate this step: lrate_sigma_mlp x the ExponentialLR factor, or 0 while the
+        map is frozen (``map_frozen``: pose tracking, optimizer.py:232,255-257; Adam with a zero step size
+        leaves every parameter bit for bit as it is)."""
+        return 0.0 if self.map_frozen else self.cfg.lr * self.lr_factor
+
+    def set_poses(self, poses):
+        """Optimise the window's poses with the map (``poses``: a loner_amd.pose.PoseWindow), or stop (None).
+        The pose gradient's buffers are allocated on first use."""
+        self.poses = poses
+        self.pose_grad = poses is not None
+        if self.pose_grad and self.d_ray is None:
+            dev = self.state.device
+            self.d_ray = torch.zeros(self.n_rays, 2, dtype=torch.float32, device=dev)
+            self.d_pos = torch.zeros(self.N, 3, dtype=torch.float32, device=dev)
+        self.drop_prefetch()  # a prefetched build read the poses before this step's update
 
     def loss_params(self, global_step, iteration_idx, scale, far_ref, n_rays_global, dev_far_ref=None):
         lc = self.cfg.loss
@@ -471,6 +497,7 @@ class StepEngine:
         lp = self.loss_params(global_step, iteration_idx, scale, far_h, n_glob, dev_far)
         dsp = None if dev_step is None else dev_step.data_ptr()
         lp.dev_step = dsp
+        lp.dev_d_ray = self.d_ray.data_ptr() if self.pose_grad else None
         self._dev_step = dsp
         # 2. sampling (``presampled``: step_window's pipeline already drew self.z for these rays); the previous
         # step's data-parallel OGM update lands first (the sampler reads the grid)
@@ -507,6 +534,17 @@ class StepEngine:
                self.opacity, None, self.level_max_ptr, self.d_jac if self.compact_denc else None, s)
         m(prof, "field")
         self._r_last = R
+        if self.pose_grad:
+            # 4b. the poses' share: dL/dpos01 per sample (tcnn's input gradient) from the table the forward read,
+            # before the table's Adam (below) changes it
+            m(prof, "pose_grad")
+            if self.compact_denc:
+                L.call("lnr_hashgrid_bwd_rays_jac", L.ctypes.byref(st.desc), rays, self.z, R, S, self.d_jac,
+                       self.d_sigma(R), N, None, st.table_f16, self.d_pos, None, 0, 0, s)
+            else:
+                L.call("lnr_hashgrid_bwd_rays", L.ctypes.byref(st.desc), rays, self.z, R, S, self.d_enc, N, None,
+                       st.table_f16, self.d_pos, None, 0, 0, s)
+            m(prof, "pose_grad")
         # 5. hash-grid backward
         m(prof, "grid_bwd")
         flags = (L.BWD_COUNTS_READY if self.count_in_forward else 0) | L.BWD_LEVEL_MAX_READY | (
@@ -522,17 +560,17 @@ class StepEngine:
             st.grad_table_current = False
             nm, nt = st.n_mlp, 2 * st.n_entries
             epi = L.AdamEpilogue(L.ptr(st.params[nm:nm + nt]), L.ptr(st.shadow[nm:nm + nt]), L.ptr(st.m[nm:nm + nt]),
-                                 L.ptr(st.v[nm:nm + nt]), st.adam_step, cfg.lr * self.lr_factor, 0.9, 0.999, 1e-8, dsp)
+                                 L.ptr(st.v[nm:nm + nt]), st.adam_step, self.map_lr(), 0.9, 0.999, 1e-8, dsp)
             L.call("lnr_hashgrid_bwd_rays_jac_adam", L.ctypes.byref(st.desc), rays, self.z, R, S, self.d_jac,
                    self.d_sigma(R), N, L.ctypes.byref(epi), self.bwd_ws, self.bwd_ws_bytes, flags, s)
             m(prof, "grid_bwd")
             m(prof, "adam")
             L.call("lnr_adam_step", st.params[:nm], st.shadow[:nm], st.grad[:nm], st.m[:nm], st.v[:nm], nm,
-                   st.adam_step, cfg.lr * self.lr_factor, 0.9, 0.999, 1e-8, dsp, s)
+                   st.adam_step, self.map_lr(), 0.9, 0.999, 1e-8, dsp, s)
             if st.n_padded > nm + nt:
                 o = nm + nt
                 L.call("lnr_adam_step", st.params[o:], st.shadow[o:], st.grad[o:], st.m[o:], st.v[o:], st.n_padded - o,
-                       st.adam_step, cfg.lr * self.lr_factor, 0.9, 0.999, 1e-8, dsp, s)
+                       st.adam_step, self.map_lr(), 0.9, 0.999, 1e-8, dsp, s)
             m(prof, "adam")
             if update_ogm is None:
                 update_ogm = (global_step % cfg.n_iters_acc == 0)
@@ -565,7 +603,7 @@ class StepEngine:
         st.adam_step += 1
         m(prof, "adam")
         L.call("lnr_adam_step", st.params, st.shadow, st.grad, st.m, st.v, st.n_padded, st.adam_step,
-               cfg.lr * self.lr_factor, 0.9, 0.999, 1e-8, dsp, s)
+               self.map_lr(), 0.9, 0.999, 1e-8, dsp, s)
         m(prof, "adam")
         # 8. OGM every N_iters_acc global steps (optimizer.py:466-469)
         if update_ogm is None:
@@ -600,7 +638,7 @@ class StepEngine:
             m(prof, "grid_bwd")
         st.adam_step += 1
         m(prof, "adam")
-        lr = cfg.lr * self.lr_factor
+        lr = self.map_lr()
         if not comm:
             # this rank's chunk of every level range, one launch (lnr_adam_step_ranges)
             rng = (L.AdamRange * len(self.zero_chunks))()
@@ -729,9 +767,32 @@ class StepEngine:
         if not 0 <= n <= self.n_rays or self.ray_offset + n > window.n_slots:
             raise ValueError(f"slots [{self.ray_offset}, {self.ray_offset + n}) outside the window "
                              f"({window.n_slots}) or the engine capacity ({self.n_rays})")
+        if self.poses is not None and self.poses.window is not window:
+            raise ValueError("step_window: the engine's PoseWindow belongs to another window (set_poses)")
+        out = self._step_window_any(window, global_step, iteration_idx, n, n_rays_global, prof, kw)
+        if self.poses is not None:
+            # joint pose + map: the poses' Adam step on this step's gradient; the next build reads the new poses
+            m = self._mark
+            m(prof, "pose_adam")
+            rays, slots = self._last_batch
+            self.poses.step(self, rays, slots, self.lr_factor)
+            m(prof, "pose_adam")
+        return out
+
+    def _slot_range(self, n):
+        r = self._slots_cache
+        if r is None or r[0] != (self.ray_offset, n):
+            idx = torch.arange(self.ray_offset, self.ray_offset + n, dtype=torch.int64, device=self.state.device)
+            self._slots_cache = r = ((self.ray_offset, n), idx)
+        return r[1]
+
+    def _step_window_any(self, window, global_step, iteration_idx, n, n_rays_global, prof, kw):
         m = self._mark
-        if window.all_valid:
-            return self._step_window_pipelined(window, global_step, iteration_idx, n, n_rays_global, prof, kw)
+        if window.all_valid and (self.poses is None or self.poses.stay_valid):
+            out = self._step_window_pipelined(window, global_step, iteration_idx, n, n_rays_global, prof, kw)
+            if self.poses is not None:
+                self._last_batch = (self.rays[:n], self._slot_range(n))
+            return out
         # Windows with rays the 1 m filter drops: the batch size must reach the host (one sync per step).
         # The build and compaction of step k + 1 run on a side stream while step k runs, so that sync
         # never waits for the main stream: the host stays a step ahead of the GPU (double-buffered).
@@ -751,6 +812,9 @@ class StepEngine:
         out = self.step(pf["rays"], pf["dgt"], global_step, iteration_idx, scale=window.scale, far_ref=pf["far"],
                         n_rays_global=pf["n_glob"], prof=prof, **kw)
         self.live_probe(pf["rays"].shape[0])
+        if self.poses is not None:
+            self._last_batch = (pf["rays"], pf["slots"])
+            return out  # (no prefetch: the next build must read the poses this step's pose update writes)
         if self.prefetch:
             nxt = None if n_rays_global is None else n_rays_global
             with torch.cuda.stream(self._pf_stream):
@@ -794,8 +858,8 @@ class StepEngine:
                         n_rays_global=window.n_slots if n_rays_global is None else n_rays_global, prof=prof,
                         presampled=presampled, **kw)
         self.live_probe(n)
-        if not self.pipeline or prof is not None or "u_jitter" in kw or "u_pdf" in kw:
-            return out  # (a profiled step keeps its stages apart)
+        if not self.pipeline or prof is not None or "u_jitter" in kw or "u_pdf" in kw or self.poses is not None:
+            return out  # (a profiled step keeps its stages apart; a pose step's update precedes the next build)
         cfg = self.cfg
         ogm_now = kw.get("update_ogm")
         if ogm_now is None:
@@ -848,7 +912,7 @@ class StepEngine:
         sc.los_eps = float(cfg.loss.los_eps_at(iteration_idx))
         t = st.adam_step + 1 if adam_step is None else adam_step
         a, b = L.ctypes.c_float(), L.ctypes.c_float()
-        L.check(L.lib().lnr_adam_coefficients(t, cfg.lr * self.lr_factor, 0.9, 0.999, L.ctypes.byref(a),
+        L.check(L.lib().lnr_adam_coefficients(t, self.map_lr(), 0.9, 0.999, L.ctypes.byref(a),
                                               L.ctypes.byref(b)), "lnr_adam_coefficients")
         sc.adam_step_size, sc.adam_bc2_sqrt = a.value, b.value
         return sc
@@ -874,7 +938,7 @@ class StepEngine:
             self._graphs.clear()
             self._graph_window = window
         p = self._pp_parity
-        gkey = (p, ogm, n, self.ray_offset, n_glob, self.zero, self._live)
+        gkey = (p, ogm, n, self.ray_offset, n_glob, self.zero, self._live, self.pose_grad)
         s = L.stream(st.device)
         sc = (L.StepScalars * 1)()
         sc[0] = self.step_scalars(global_step, iteration_idx)
@@ -923,6 +987,7 @@ class StepEngine:
                          b["valid"][:n], None, b["far"])
             idx = torch.nonzero(b["valid"][:n]).squeeze(1)
             k = int(idx.numel())  # (the sync)
+            slots = idx + self.ray_offset  # (the window slots of the kept rays: the pose gradient's keyframes)
             torch.index_select(b["rays"][:n], 0, idx, out=b["rays_c"][:k])
             torch.index_select(b["dgt"][:n], 0, idx, out=b["dgt_c"][:k])
             cnt = torch.tensor([float(k)], device=self.state.device)
@@ -932,5 +997,5 @@ class StepEngine:
             done = torch.cuda.Event()
             done.record(stream)
         return dict(window=window, want=(global_step, n, self.ray_offset, n_rays_global), rays=b["rays_c"][:k],
-                    dgt=b["dgt_c"][:k], far=b["far"], n_glob=n_glob, done=done, parity=parity)
+                    dgt=b["dgt_c"][:k], far=b["far"], n_glob=n_glob, done=done, parity=parity, slots=slots)
 

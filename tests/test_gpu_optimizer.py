@@ -72,24 +72,24 @@ def test_schedule_selection_and_skips(L):
     opt.iterate_optimizer(scans)           # then: tracking config skipped (skip_pose_refinement), 2 mapping its
     assert opt._global_step == 5
     opt._settings["skip_pose_refinement"] = False
-    with pytest.raises(NotImplementedError):
-        opt.iterate_optimizer(scans)       # pose tracking is out of scope
+    opt.iterate_optimizer(scans)           # pose tracking (7, map frozen) then mapping (2): tests/test_gpu_pose.py
+    assert opt._global_step == 14
 
 
-def test_joint_pose_config_raises_unless_fixed_poses(L):
+def test_joint_pose_config_fixed_poses_opt_in(L):
     """The reference's default mapper schedule optimises poses and map jointly (cfg/defaults.yaml:93-97,
-    optimizer.py:258-262).  The fused Optimizer keeps the poses fixed, so such a config raises through
-    iterate_optimizer unless the caller opts in with fixed_poses=True (then it warns and optimises the map
-    exactly as with freeze_poses: True); use_gt_poses freezes them as the reference does."""
+    optimizer.py:258-262): the fused Optimizer does so (tests/test_gpu_pose.py), and moves the poses.
+    fixed_poses=True opts out (a warning, then the map optimised exactly as with freeze_poses: True);
+    use_gt_poses freezes them as the reference does."""
     import warnings
     from loner_amd.optimizer import Optimizer
     scans, cube = _window()
     joint = [dict(num_keyframes=-1, iteration_schedule=[dict(num_iterations=3, freeze_poses=False,
                                                              freeze_sigma_mlp=False, freeze_rgb_mlp=True)])]
-    opt = Optimizer(_settings(schedule=joint), None, cube, "cuda:0", seed=2)
-    with pytest.raises(NotImplementedError, match="fixed_poses=True"):
-        opt.iterate_optimizer(scans)
-    assert opt._global_step == 0
+    p0 = [s["pose"].clone() for s in scans]
+    loss_joint = Optimizer(_settings(schedule=joint), None, cube, "cuda:0", seed=2).iterate_optimizer(scans)
+    assert np.isfinite(loss_joint) and all(not torch.equal(s["pose"], p) for s, p in zip(scans, p0))
+    scans, cube = _window()
     with pytest.warns(UserWarning, match="fixed_poses=True"):
         loss_fixed = Optimizer(_settings(schedule=joint), None, cube, "cuda:0", seed=2,
                                fixed_poses=True).iterate_optimizer(scans)
@@ -101,6 +101,7 @@ def test_joint_pose_config_raises_unless_fixed_poses(L):
         loss_gt = Optimizer(_settings(schedule=joint), None, cube, "cuda:0", seed=2,
                             use_gt_poses=True).iterate_optimizer(scans)
     assert loss_fixed == loss_frozen == loss_gt
+    assert all(torch.equal(s["pose"], p) for s, p in zip(scans, p0))
 
 
 @pytest.mark.parametrize("strategy,sky", [("MASK", 8), ("FIXED", 0), ("FIXED", 8)])
