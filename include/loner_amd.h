@@ -118,6 +118,15 @@ int lnr_hashgrid_fwd(const lnr_grid_desc* d, const float* pos01, int64_t n, cons
 int lnr_hashgrid_fwd_rays(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
                           int32_t n_samples, const uint16_t* table, uint32_t* enc, int64_t enc_stride,
                           void* bwd_ws, int64_t bwd_ws_bytes, void* stream);
+/* Early ray termination, the encode of one phase: samples [lo, hi) (multiples of 64; n_samples % 64 == 0) of
+ * every ray whose alive[r] != 0 (alive NULL: every ray), as lnr_hashgrid_fwd_rays encodes them; the other
+ * samples' encodings are left unwritten.  bwd_ws (the first phase only, lo == 0): the backward's record
+ * histogram of EVERY sample, as lnr_hashgrid_fwd_rays records it (so the backward's fixed-point units are the
+ * full step's).  Without bwd_ws only the phase's samples are launched.  See lnr_field_sigma_phase. */
+int lnr_hashgrid_fwd_rays_phase(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
+                                int32_t n_samples, const uint16_t* table, uint32_t* enc, int64_t enc_stride,
+                                void* bwd_ws, int64_t bwd_ws_bytes, const uint8_t* alive, int32_t lo, int32_t hi,
+                                void* stream);
 /* Forward of samples whose compositing weight can be zero (the colour head: rgb = sum w_i c_i + ...,
  * rendering_tcnn.py:286): samples with live[n] == 0 (exactly) issue no gathers, every other sample is
  * encoded exactly as lnr_hashgrid_fwd_rays does.  A dead sample gets a zero encoding when its aligned
@@ -300,6 +309,8 @@ typedef struct lnr_loss_params {
                                 dL/d{origin, direction, far} of every ray (joint pose + map) */
 } lnr_loss_params;
 #define LNR_LP_DW_OVERWRITE 1  /* lnr_field_train STORES d_w (the MLP gradient) instead of adding to it */
+#define LNR_LP_SIGMA_READY 2   /* lnr_field_train: sigma is already in its workspace (lnr_field_sigma_phase), the
+                                  MLP forward is not run again (n_samples in {64, 128, 256, 512}) */
 
 /* Status bits (replace the reference's per-step host checks):
  *   LNR_STATUS_NAN_LOSS     loss is NaN: optimizer.py:854 asserts "NaN Loss Encountered"
@@ -356,6 +367,39 @@ int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, 
                     uint32_t key, int64_t ray_offset, const lnr_loss_params* lp, float* d_enc, float* d_w,
                     float* workspace, float* ray_stats, float* depth, float* opacity, float* weights,
                     float* d_enc_level_max, uint32_t* d_enc_jac, void* stream);
+/* Early ray termination (the training step on a trained field): the sigma MLP forward of samples [lo, hi) of
+ * each ray (multiples of 64) into lnr_field_train's workspace, where lnr_field_train with LNR_LP_SIGMA_READY
+ * reads it; rays with alive[r] == 0 (read when lo > 0) get sigma 0 there and no encoding is read.  When
+ * hi < n_samples it also updates, per ray, transmittance[r] (fp64; = 1 before lo == 0) by the product over the
+ * phase of s = 1 - alpha + 1e-10 (the compositing's own arithmetic: noise, deltas as lnr_field_train draws
+ * them; key, noise_std, noise, ray_offset, lp->dev_step as there) and alive[r] = transmittance[r] >= 1e-50.
+ * A ray whose product fell below 1e-50 has every later sample's float transmittance exactly 0 in the
+ * compositing, so its later samples' sigma and encodings cannot change any output: the phases
+ * lnr_hashgrid_fwd_rays_phase -> lnr_field_sigma_phase, phase by phase, then lnr_field_train with
+ * LNR_LP_SIGMA_READY, give the step's results without evaluating them (csrc/field.hip, kErtTMin).
+ * lp: optional (dev_status: LNR_STATUS_SIGMA_CLIPPED for the evaluated samples; dev_step: the key). */
+int lnr_field_sigma_phase(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, const float* rays,
+                          const float* z, int64_t n_rays, int32_t n_samples, int32_t lo, int32_t hi, float noise_std,
+                          const float* noise, uint32_t key, int64_t ray_offset, const lnr_loss_params* lp,
+                          float* workspace, uint8_t* alive, double* transmittance, void* stream);
+/* Joint pose + map (optimizer.py:235-262): the per-keyframe gradient of the pose tensors [t, axis-angle] (K, 6)
+ * from a step's per-sample dL/dpos01 d_pos (n_rays * n_samples, 3) (lnr_hashgrid_bwd_rays_jac) and per-ray
+ * [dL/d|d|, dL/dfar] d_ray (n_rays, 2) (lnr_loss_params.dev_d_ray), for rays built as
+ * LidarRayDirections.build_lidar_rays builds them (o = (t + shift) / scale, d = R v / |R v|, far = min(r_max /
+ * scale, get_far_val(o, d)); ray_utils.py:31-60,269-322): ray r is window slot slots[r] (slots NULL: slot0 + r),
+ * of keyframe slot_kf[slot], and carries slot_pose[slot] (1: a LiDAR ray of an optimised pose, 0: a sky ray --
+ * built from the detached pose, keyframe.py:98 -- or an anchored keyframe).  grad (K, 6) is OVERWRITTEN (a
+ * fixed-order, deterministic sum); ray_ws: n_rays * 12 floats.  far_range = r_max / scale. */
+int lnr_pose_grad(const float* rays, const float* z, const float* d_pos, const float* d_ray, int64_t n_rays,
+                  int32_t n_samples, const int64_t* slots, int64_t slot0, const int32_t* slot_kf, const float* slot_pose,
+                  const float* pose6, int32_t n_kf, float scale, float far_range, float* ray_ws, float* grad,
+                  void* stream);
+/* The poses' Adam step (torch.optim.Adam, the pose group of optimizer.py:262: betas, eps, lr = lrate_pose x the
+ * ExponentialLR factor; step = this Adam's step count, from 1) on pose6 with moments m, v (K, 6), for keyframes
+ * with optimise[k] != 0 (NULL: all), then rows (K, 12) = [R | t] of every pose (the RayWindow's pose layout; may
+ * be NULL).  grad NULL: only the rows are written (m, v, step unused). */
+int lnr_pose_adam(float* pose6, float* m, float* v, const float* grad, const uint8_t* optimise, int32_t n_kf,
+                  int64_t step, float lr, float beta1, float beta2, float eps, float* rows, void* stream);
 /* Forward-only render from enc (inference path, C3 shape): sigma MLP + compositing.  With weights
  * (R,S) given, the sigma MLP runs tile-parallel first and stages sigma in weights, which the
  * compositing then overwrites with the weights (weights must not alias the other buffers); without,

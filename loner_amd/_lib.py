@@ -75,6 +75,7 @@ class LossParams(ctypes.Structure):
 
 
 LP_DW_OVERWRITE = 1
+LP_SIGMA_READY = 2
 
 
 STATUS_NAN_LOSS, STATUS_INF_LOSS, STATUS_SIGMA_CLIPPED, STATUS_NONFINITE_OUTPUT = 1, 2, 4, 8
@@ -158,9 +159,16 @@ _SIGNATURES = {
     "lnr_field_train": (ctypes.c_int, [c_p, c_p, c_i64, c_p, c_p, c_p, c_i64, c_i32, c_f, c_p, c_u32, c_i64,
                                        ctypes.POINTER(LossParams), c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
                                        c_p]),
+    "lnr_field_sigma_phase": (ctypes.c_int, [c_p, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_i32, c_i32, c_f, c_p, c_u32,
+                                             c_i64, ctypes.POINTER(LossParams), c_p, c_p, c_p, c_p]),
+    "lnr_pose_grad": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_p, c_p, c_i32, c_f, c_f, c_p,
+                                     c_p, c_p]),
+    "lnr_pose_adam": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i32, c_i64, c_f, c_f, c_f, c_f, c_p, c_p]),
     "lnr_field_render": (ctypes.c_int, [c_p, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_i32, c_f, c_p, c_u32, c_i64, c_p,
                                         c_p, c_p, c_p, c_p]),
     "lnr_rgb_render": (ctypes.c_int, [c_p, c_i32, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_p, c_p]),
+    "lnr_hashgrid_fwd_rays_phase": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_p, c_i64,
+                                                   c_p, c_i64, c_p, c_i32, c_i32, c_p]),
     "lnr_hashgrid_fwd_rays_live": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_i64,
                                                   c_p]),
     "lnr_hashgrid_fwd_rays_live_ws": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_p, c_p,

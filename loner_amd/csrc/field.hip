@@ -832,6 +832,84 @@ __global__ void __launch_bounds__(NT) k_sigma_fwd_tiles(FieldArgs a) {
   }
 }
 
+// Early ray termination (lnr_field_sigma_phase).  A sample behind enough opaque ones has transmittance exactly 0
+// in the compositing (T = (float) of a double product, rendering_tcnn.py:262-266): its weight alpha T is 0 whatever
+// its sigma, so it contributes nothing to the render, the loss or any gradient (dL/dalpha = T (G - X) = 0), and its
+// sigma need not be evaluated -- nor its encoding gathered.  The step evaluates a ray in phases of samples [lo, hi):
+// after each phase the ray's product of s = 1 - alpha + 1e-10 over its samples so far (the compositing's own
+// per-sample float arithmetic, in double); a ray whose product fell below kErtTMin skips the later phases (its
+// sigma there is 0, so alpha stays finite and its T stays 0: s <= 1).  The compositing's double products
+// associate differently but agree to ~1e-13 relative, so every later sample's float T is 0 there too.  The
+// margin (1e-50 against float's 7e-46) also keeps the later samples' alpha, which still enters the suffix sums
+// X of the samples before them through factors below 1e-50 / T, out of every float result in practice
+// (tests/test_gpu_live.py: bitwise the step without termination).
+constexpr double kErtTMin = 1e-50;
+
+// One wave per ray: the sigma of its samples [lo, hi) (64-sample units, 4 MFMA tiles each) and, when
+// hi < S, its transmittance product over them: T <- T * prod s (T = 1 before the first phase), alive = T >= t_min.
+// sigma_tile_fwd leaves sample 16 t + c's sigma in every lane c + 16 g, so lane l finds its own sample's in
+// tile t = l / 16.  A terminated ray (alive 0, lo > 0) gets sigma 0 and reads no encoding.
+__global__ void __launch_bounds__(NT) k_sigma_phase(FieldArgs a, uint8_t* __restrict__ alive,
+                                                    double* __restrict__ trans, int32_t lo, int32_t hi,
+                                                    double t_min) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+  const int S = a.S;
+  const bool upd = hi < S;
+  SigmaWeights sw;
+  load_sigma_weights(a.w, sw);
+  for (int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + wid; r < a.n_rays; r += (int64_t)gridDim.x * kWavesPerBlock) {
+    if (lo > 0 && alive[r] == 0) {  // (wave-uniform) terminated: sigma 0, no encoding read
+      for (int i = lo + lane; i < hi; i += 64) a.d_sigma[r * S + i] = 0.f;
+      continue;
+    }
+    const float* ry = a.rays + 13 * r;
+    const float dx = ry[3], dy = ry[4], dz = ry[5];
+    const float dnorm = sqrtf(dx * dx + dy * dy + dz * dz);
+    const float* zr = a.z + r * S;
+    const uint32_t gr = (uint32_t)(a.ray_offset + r);
+    double P = 1.0;
+    bool clipped = false;
+    for (int u0 = lo; u0 < hi; u0 += kSigmaFwdUnit) {
+      const int64_t n0 = r * S + u0;
+      half8_t b[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) b[t] = load_enc_operand(a.enc, a.enc_stride, n0 + 16 * t + c, true);
+      float mine = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        SigmaHidden h;
+        const float sgm = sigma_tile_fwd(sw, b[t], h);
+        const float sg16 = sigma_to_f16(sgm);
+        if (g == 0) a.d_sigma[n0 + 16 * t + c] = sg16;
+        if (g == t) mine = sg16;
+        clipped |= !isfinite(round_f16(sgm));
+      }
+      if (upd) {  // the compositing's per-sample arithmetic (composite_loss_wave)
+        const int i = u0 + lane;
+        const float zi = zr[i];
+        const float dl = (i + 1 < S) ? (zr[i + 1] - zi) : 1e10f;
+        const float delta = dl * dnorm;
+        float nz = 0.f;
+        if (a.noise) nz = a.noise[r * S + i] * a.noise_std;
+        else if (a.noise_std > 0.f) nz = rand_normal(step_key_of(a), kStreamNoise, gr, (uint32_t)i) * a.noise_std;
+        const float sr = fmaxf(mine + nz, 0.f);
+        const float alpha = 1.0f - expf(-(delta * sr));
+        P *= (double)((1.0f - alpha) + 1e-10f);
+      }
+    }
+    if (a.lp.dev_status && __any(clipped) && lane == 0) atomicOr(a.lp.dev_status, LNR_STATUS_SIGMA_CLIPPED);
+    if (upd) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) P *= __shfl_xor(P, o, 64);
+      if (lane == 0) {
+        const double t = (lo == 0 ? 1.0 : trans[r]) * P;
+        trans[r] = t;
+        alive[r] = t >= t_min ? 1 : 0;
+      }
+    }
+  }
+}
+
 // Phase 1b, one wave per ray: compositing -> loss -> compositing backward on the sigma of phase 1a,
 // dL/dsigma written over it (a.d_sigma, (R, S) fp32).
 template <int C>
@@ -1529,7 +1607,7 @@ extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t e
     const int nr = (int)(want < 2048 ? want : 2048);
     const size_t sm = wave_smem_bytes(n_samples);
 #if LNR_FIELD_SPLIT
-    {
+    if (!(lp->flags & LNR_LP_SIGMA_READY)) {  // (early ray termination: lnr_field_sigma_phase wrote sigma)
       const int64_t units = n_rays * (int64_t)n_samples / kSigmaFwdUnit;
       const int64_t wantu = (units + kWavesPerBlock - 1) / kWavesPerBlock;
       hipLaunchKernelGGL(k_sigma_fwd_tiles, dim3((int)(wantu < 8192 ? wantu : 8192)), dim3(NT), 0, st, a);
@@ -1572,6 +1650,33 @@ extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t e
   hipLaunchKernelGGL(k_reduce_slabs, dim3(nred), dim3(64 * kSlabWaves), 0, st, workspace, nb, d_w,
                      (lp->flags & LNR_LP_DW_OVERWRITE) != 0, ray_stats, n_rays, *lp);
   LNR_RETURN_LAUNCH("lnr_field_train(reduce)");
+}
+
+extern "C" int lnr_field_sigma_phase(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, const float* rays,
+                                     const float* z, int64_t n_rays, int32_t n_samples, int32_t lo, int32_t hi,
+                                     float noise_std, const float* noise, uint32_t key, int64_t ray_offset,
+                                     const lnr_loss_params* lp, float* workspace, uint8_t* alive,
+                                     double* transmittance, void* stream) {
+  if (int e = check_rays(rays, z, n_rays, n_samples, "lnr_field_sigma_phase")) return e;
+  LNR_REQUIRE(n_samples % 64 == 0 && lo >= 0 && lo < hi && hi <= n_samples && lo % 64 == 0 && hi % 64 == 0,
+              "lnr_field_sigma_phase: phase [%d, %d) of %d samples must be whole 64-sample waves", lo, hi, n_samples);
+  LNR_REQUIRE(enc_stride >= n_rays * (int64_t)n_samples && enc_stride < (int64_t(1) << 26),
+              "lnr_field_sigma_phase: bad enc_stride");
+  if (n_rays == 0) return LNR_OK;
+  LNR_REQUIRE(w && enc && workspace && (hi == n_samples || (alive && transmittance)) && (lo == 0 || alive),
+              "lnr_field_sigma_phase: null pointer");
+  FieldArgs a{};
+  a.w = w; a.enc = enc; a.enc_stride = enc_stride; a.rays = rays; a.z = z; a.n_rays = n_rays; a.S = n_samples;
+  a.noise_std = noise_std; a.noise = noise; a.key = key; a.ray_offset = ray_offset;
+  if (lp) a.lp = *lp;
+  a.d_sigma = workspace + lnr_dw_workspace_words(n_rays);
+  hipStream_t st = as_stream(stream);
+  const char* e = getenv("LONER_ERT_TMIN");  // (experiments: tools/experiments/r06_ert_tmin.py)
+  const double t_min = e ? atof(e) : kErtTMin;
+  const int64_t want = (n_rays + kWavesPerBlock - 1) / kWavesPerBlock;
+  hipLaunchKernelGGL(k_sigma_phase, dim3((int)(want < 8192 ? want : 8192)), dim3(NT), 0, st, a, alive, transmittance, lo,
+                     hi, t_min);
+  LNR_RETURN_LAUNCH("lnr_field_sigma_phase");
 }
 
 extern "C" int lnr_field_render(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, const float* rays,

@@ -117,6 +117,25 @@ inline int enc_levels_per_group(const lnr_grid_desc* d, int64_t n_sb) {
       return g;
   return 1;
 }
+// Early ray termination (lnr_hashgrid_fwd_rays_phase): the encode of samples [lo, hi) of each ray, for the
+// rays still ``alive`` (per-ray bytes, or every ray).  With the record histogram (the first phase) the grid
+// is the plain one, every sample's records are counted (the backward's fixed-point units follow the full
+// counts) and only the phase's samples gather; without it the grid covers just the phase's samples
+// (``compact``: workgroup sample g -> ray g / (hi - lo), ray sample lo + g % (hi - lo); a wave stays
+// within one ray, as lo and hi are multiples of 64).
+struct EncPhase {
+  const uint8_t* alive;  // per ray; null: every ray
+  int32_t lo, hi;        // ray-local sample range; hi == 0: no phase (every sample)
+  int32_t S;             // samples per ray
+  bool compact;
+  __device__ __forceinline__ bool on() const { return hi > 0; }
+  __device__ __forceinline__ int64_t sample(int64_t g) const {
+    if (!compact) return g;
+    const int32_t w = hi - lo;
+    return (g / w) * S + lo + g % w;
+  }
+};
+
 #ifndef LNR_ENC_WAVES
 #define LNR_ENC_WAVES 8  // waves per SIMD asked of the encode (68 registers would allow 7)
 #endif
@@ -124,23 +143,38 @@ template <class PosFn, int kEncSpt, bool PAIRED, int LPB = 1>
 __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per_eu(LNR_ENC_WAVES, LNR_ENC_WAVES))) k_hashgrid_fwd(GridArgs a, PosFn pos, int64_t n,
                                                                const uint32_t* __restrict__ table,
                                                                uint32_t* __restrict__ enc, int64_t stride,
-                                                               BwdWorkspace ws, const float* __restrict__ live) {
+                                                               BwdWorkspace ws, const float* __restrict__ live,
+                                                               EncPhase ph) {
   constexpr int H = kSB / kEncSpt;
-  const int64_t i0 = (int64_t)blockIdx.x * kSB + threadIdx.x;
+  const int64_t g0 = (int64_t)blockIdx.x * kSB + threadIdx.x;  // (the compact phase grid: g0 < n counts its samples)
+  const int64_t i0 = ph.sample(g0);
   const bool count = ws.hist != nullptr;
-  if (!count && (i0 & ~(int64_t)1) >= n) return;  // (lane pairs leave together: fine_gather_paired)
+  if (!count && (g0 & ~(int64_t)1) >= n) return;  // (lane pairs leave together: fine_gather_paired)
   __shared__ uint32_t hist[kMaxChunksPerLevel];
-  bool in[kEncSpt], use[kEncSpt];
+  bool in[kEncSpt], use[kEncSpt], cnt[kEncSpt];
   float x[kEncSpt], y[kEncSpt], z[kEncSpt];
+  const int64_t n_in = ph.compact ? (int64_t)(n / (ph.hi - ph.lo)) * ph.S : n;  // pos.wave's bound
 #pragma unroll
   for (int h = 0; h < kEncSpt; ++h) {
-    const int64_t i = i0 + h * H;
-    in[h] = i < n;
+    const int64_t i = ph.sample(g0 + h * H);
+    in[h] = (g0 + h * H) < n;
     // live: samples whose weight is exactly 0 get a zero encoding and issue no gathers; when counting
     // too, they emit no records at the fine levels (the scatter skips them by the same mask)
     use[h] = in[h] && (live == nullptr || live[i] != 0.f);
+    cnt[h] = use[h];
+    if (ph.on()) {  // early ray termination: the phase's samples of the live rays gather, every sample counts
+      const int32_t j = (int32_t)(i % ph.S);
+      use[h] = in[h] && j >= ph.lo && j < ph.hi && (ph.alive == nullptr || ph.alive[i / ph.S] != 0);
+      cnt[h] = in[h];
+    }
     x[h] = y[h] = z[h] = 0.f;
-    pos.wave(i, n, in[h], x[h], y[h], z[h]);
+    pos.wave(i, n_in, in[h], x[h], y[h], z[h]);
+  }
+  if (ph.on() && !count) {
+    bool any = false;
+#pragma unroll
+    for (int h = 0; h < kEncSpt; ++h) any |= use[h];
+    if (!__any(any)) return;  // a terminated ray's wave (no histogram: no barriers to keep)
   }
   // dead samples (live, use = false) get a zero encoding only where their aligned 16-sample tile holds a live
   // sample: the colour kernels skip a tile whose weights are all 0 and read every encoding of the others
@@ -177,7 +211,7 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
     }
 #pragma unroll
     for (int h = 0; h < kEncSpt; ++h) {
-      uint32_t* dst = enc + (int64_t)l * stride + i0 + h * H;
+      uint32_t* dst = enc + (int64_t)l * stride + ph.sample(g0 + h * H);
       if (use[h]) {
         float f0 = 0.f, f1 = 0.f;
 #pragma unroll
@@ -195,7 +229,7 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
     if (count) {
       lds_barrier();
 #pragma unroll
-      for (int h = 0; h < kEncSpt; ++h) count_fine_add(c[h], use[h], hist);
+      for (int h = 0; h < kEncSpt; ++h) count_fine_add(c[h], cnt[h], hist);
       lds_barrier();
       publish_block_counts(a, l, hist, ws);
     }
@@ -208,7 +242,7 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
   for (int h = 0; h < kEncSpt; ++h) {
     Corners c;
     level_corners(lv, x[h], y[h], z[h], c);
-    uint32_t* dst = enc + (int64_t)l * stride + i0 + h * H;
+    uint32_t* dst = enc + (int64_t)l * stride + ph.sample(g0 + h * H);
     if (use[h]) {
       uint32_t v[8];
 #pragma unroll
@@ -226,7 +260,7 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
     }
     if (count) {
       if (h == 0) lds_barrier();  // the zeroed histogram
-      count_add(a, l, c, in[h], use[h], hist);
+      count_add(a, l, c, in[h], cnt[h], hist);
     }
   }
   if (count) {
@@ -361,7 +395,7 @@ static int live_lpb() {
 template <class PosFn>
 static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16_t* table, uint32_t* enc,
                       int64_t enc_stride, void* bwd_ws, int64_t bwd_ws_bytes, hipStream_t st, const char* who,
-                      const float* live = nullptr) {
+                      const float* live = nullptr, EncPhase ph = EncPhase{nullptr, 0, 0, 1, false}) {
   GridArgs a = make_args(d, pos.samples_per_ray());
   LNR_REQUIRE(n < (int64_t(1) << 31), "%s: n=%lld samples exceeds 2^31", who, (long long)n);
   // training and plain eval launches: one sample per thread, lane-paired fine gathers; the eval launch
@@ -388,19 +422,30 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
   const unsigned rows = (unsigned)((n + kSB - 1) / kSB);
   const uint32_t* tb = reinterpret_cast<const uint32_t*>(table);
   const dim3 grid(rows, d->n_levels);
+  if (ph.compact) {  // a later phase of early ray termination: the grid covers the phase's samples only
+    const int64_t ng = (n / ph.S) * (ph.hi - ph.lo);
+    const unsigned rows_c = (unsigned)((ng + kSB - 1) / kSB);
+    const int lpb_c = enc_levels_per_group(d, rows_c);
+    auto k = lpb_c == 4 ? k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 4>
+           : lpb_c == 2 ? k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 2>
+                        : k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 1>;
+    hipLaunchKernelGGL(k, dim3(rows_c, d->n_levels / lpb_c), dim3(kSB), 0, st, a, pos, ng, tb, enc, enc_stride,
+                       BwdWorkspace{}, nullptr, ph);
+    LNR_RETURN_LAUNCH(who);
+  }
   if (live == nullptr)
     hipLaunchKernelGGL(enc_kernel(), dim3(rows, d->n_levels / lpb), dim3(kSB), 0, st, a, pos, n, tb, enc, enc_stride, w,
-                       live);
+                       live, ph);
   else if (spt2 && live_lpb() == 2 && d->n_levels % 2 == 0 && enc_levels_per_group(d, rows) >= 2)
     // (two samples per thread over two levels spill at eight waves per SIMD: one sample per thread)
     hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, false, 2>), dim3(rows, d->n_levels / 2), dim3(kSB), 0, st, a, pos, n,
-                       tb, enc, enc_stride, w, live);
+                       tb, enc, enc_stride, w, live, ph);
   else if (spt2)
     hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 2, false>), grid, dim3(kSB / 2), 0, st, a, pos, n, tb, enc, enc_stride, w,
-                       live);
+                       live, ph);
   else
     hipLaunchKernelGGL((k_hashgrid_fwd<PosFn, 1, false>), grid, dim3(kSB), 0, st, a, pos, n, tb, enc, enc_stride, w,
-                       live);
+                       live, ph);
   LNR_RETURN_LAUNCH(who);
 }
 
@@ -425,6 +470,24 @@ extern "C" int lnr_hashgrid_fwd_rays(const lnr_grid_desc* d, const float* rays, 
   LNR_REQUIRE(rays && z && table && enc, "lnr_hashgrid_fwd_rays: null pointer");
   return launch_fwd(d, PosFromRays{rays, z, n_samples}, n, table, enc, enc_stride, bwd_ws, bwd_ws_bytes,
                     as_stream(stream), "lnr_hashgrid_fwd_rays");
+}
+
+extern "C" int lnr_hashgrid_fwd_rays_phase(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
+                                           int32_t n_samples, const uint16_t* table, uint32_t* enc, int64_t enc_stride,
+                                           void* bwd_ws, int64_t bwd_ws_bytes, const uint8_t* alive, int32_t lo,
+                                           int32_t hi, void* stream) {
+  if (int e = check_desc(d, "lnr_hashgrid_fwd_rays_phase")) return e;
+  const int64_t n = n_rays * (int64_t)n_samples;
+  LNR_REQUIRE(n_rays >= 0 && n_samples > 0 && enc_stride >= n, "lnr_hashgrid_fwd_rays_phase: bad sizes");
+  LNR_REQUIRE(n_samples % 64 == 0 && lo >= 0 && lo < hi && hi <= n_samples && lo % 64 == 0 && hi % 64 == 0,
+              "lnr_hashgrid_fwd_rays_phase: phase [%d, %d) of %d samples must be whole 64-sample waves", lo, hi,
+              n_samples);
+  LNR_REQUIRE(bwd_ws == nullptr || lo == 0, "lnr_hashgrid_fwd_rays_phase: the record histogram comes with the first phase");
+  if (n == 0) return LNR_OK;
+  LNR_REQUIRE(rays && z && table && enc, "lnr_hashgrid_fwd_rays_phase: null pointer");
+  const EncPhase ph{alive, lo, hi, n_samples, bwd_ws == nullptr};
+  return launch_fwd(d, PosFromRays{rays, z, n_samples}, n, table, enc, enc_stride, bwd_ws, bwd_ws_bytes,
+                    as_stream(stream), "lnr_hashgrid_fwd_rays_phase", nullptr, ph);
 }
 
 extern "C" int lnr_hashgrid_fwd_rays_live(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,

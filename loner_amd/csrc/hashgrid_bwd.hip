@@ -1699,6 +1699,9 @@ constexpr int kDposThreads = 256;
 #ifndef LNR_DPOS_SPT
 #define LNR_DPOS_SPT 0  // samples per thread of the one-launch, level-outer kernel (k_hashgrid_dpos_k: 2, 4, 8); 0: passes
 #endif
+#ifndef LNR_DPOS_SPT_SPARSE
+#define LNR_DPOS_SPT_SPARSE 2  // the same for the compact (d_sigma J) gradient, whose dead waves leave at once
+#endif
 // Levels [l0, l1) per launch, added to the running sums d_pos holds (l0 > 0) in level order: the same
 // fp32 additions in the same order as one pass over every level, so the result does not depend on the
 // split, while each launch's gathers stay within a few levels' table slices (L2-resident: the whole
@@ -1793,6 +1796,22 @@ __global__ void __launch_bounds__(kDposThreads) k_hashgrid_dpos_k(GridArgs a, Po
   float r[K][3];
 #pragma unroll
   for (int k = 0; k < K; ++k) r[k][0] = r[k][1] = r[k][2] = 0.f;
+  if constexpr (GradFn::kScaled) {  // a wave with no live sample (dL/dsigma = 0 throughout): zeros, no work
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int64_t i = base + (int64_t)k * kDposThreads;
+      any |= i < n && grad.scale(i) != 0.f;
+    }
+    if (!__any(any)) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int64_t i = base + (int64_t)k * kDposThreads;
+        if (i < n) d_pos[3 * i + 0] = d_pos[3 * i + 1] = d_pos[3 * i + 2] = 0.f;
+      }
+      return;
+    }
+  }
   for (uint32_t l = 0; l < a.n_levels; ++l) {
     const LevelParams& p = a.lv[l];
 #pragma unroll
@@ -1825,8 +1844,11 @@ static int launch_dpos(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint1
   const GridArgs a = make_args(d, pos.samples_per_ray());
   const int64_t nb = (n + kDposThreads - 1) / kDposThreads;
   LNR_REQUIRE(nb < (int64_t(1) << 31), "%s: n=%lld too large", who, (long long)n);
+  // the compact encoding gradient (GradJac) is sparse on a trained field (most samples' dL/dsigma = 0): one
+  // level-outer launch whose dead waves leave at once (LNR_DPOS_SPT_SPARSE samples per thread) instead of the
+  // passes, which re-read every sample per pass (C2 joint pose + map: tools/experiments/r06_ert.sh)
   const char* ek = getenv("LONER_DPOS_SPT");
-  const int spt = ek ? atoi(ek) : LNR_DPOS_SPT;
+  const int spt = ek ? atoi(ek) : (GradFn::kScaled ? LNR_DPOS_SPT_SPARSE : LNR_DPOS_SPT);
   if (spt == 2 || spt == 4 || spt == 8) {
     const unsigned g = (unsigned)((n + (int64_t)spt * kDposThreads - 1) / ((int64_t)spt * kDposThreads));
     const uint32_t* tb = reinterpret_cast<const uint32_t*>(table);

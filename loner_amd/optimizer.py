@@ -383,8 +383,8 @@ class Optimizer:
         out = eng.step(rays.contiguous(), depth.contiguous(), self._global_step, it, scale=window.scale,
                        far_ref=far_ref, n_rays_global=n_glob)
         if eng.poses is not None:
-            slots = torch.nonzero(sel).squeeze(1)
+            slots = torch.nonzero(sel).squeeze(1)  # (FIXED: one host sync per step already, above)
             if self._world > 1:
                 slots = slots[s0:s1]
-            eng.poses.step(eng, rays, slots, eng.lr_factor)
+            eng.poses.step(eng, rays, slots.contiguous(), eng.lr_factor)
         return out

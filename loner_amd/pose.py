@@ -25,9 +25,12 @@ On the fused step (``StepEngine`` with ``pose_grad=True``):
   directions: with u = R v and d = u / |u|, dL/dR = (1/|u|) (I - d d^T) g_d v^T = (I - d d^T) g_d d^T R;
 * autograd through ``axis_angle_to_matrix`` (K 3x3 matrices) gives dL/d(axis-angle).
 
-``PoseWindow`` holds the window's pose tensors (K, 6) on the device, applies the pose Adam after each
-step and rewrites the window's (K, 12) pose rows, which the next step's ray build (or HIP graph replay)
-reads: no host synchronisation.
+``PoseWindow`` holds the window's pose tensors (K, 6) on the device and, after each step, runs the chain
+(``lnr_pose_grad``, csrc/pose.hip: the per-ray reduction, the far term and the per-keyframe sums in one pass
+over the step's d_pos, then the axis-angle derivative in closed form) and the poses' Adam
+(``lnr_pose_adam``), which rewrites the window's (K, 12) pose rows the next step's ray build (or HIP graph
+replay) reads: three launches, no host synchronisation.  The torch functions below state the same chain;
+they are the tests' reference for the kernels.
 """
 import numpy as np
 import torch
@@ -126,13 +129,17 @@ class PoseWindow:
     (``tensor_to_transform``: the reference builds every ray from the pose tensor's matrix).
     ``optimise``: (K,) bools, the keyframes whose pose is optimised (the reference's un-anchored
     keyframes of the active window, optimizer.py:248-262).  ``lr``: lrate_pose; the step's
-    ``lr_factor`` (ExponentialLR) scales it as it scales the map's.  Each ``step`` after an engine step:
-    the pose gradient of that step's rays (``ray_slots``: their window slots) and one Adam step
-    (torch.optim.Adam over the (K, 6) tensor: a keyframe held fixed keeps a zero gradient, so its Adam
-    moments stay 0 and its pose does not move), then the window's pose rows.  DP: ``allreduce`` sums
-    the (K, 6) gradient over ranks (each holds a slice of the rays)."""
+    ``lr_factor`` (ExponentialLR) scales it as it scales the map's.  Each ``step`` after an engine step,
+    three launches and no host synchronisation: ``lnr_pose_grad`` (the pose gradient of that step's rays:
+    ``slots`` their window slots, or None for the engine's slots [ray_offset, ray_offset + n)), the all-reduce
+    of the (K, 6) gradient when data-parallel (``allreduce``), and ``lnr_pose_adam`` (torch.optim.Adam's step on
+    the (K, 6) tensor: a keyframe held fixed has a zero gradient, its pose does not move; then the window's
+    pose rows).  ``ray_gradients`` / ``keyframe_gradients`` above state the same chain in torch
+    (tests/test_gpu_pose.py compares the two)."""
 
     def __init__(self, window, optimise, lr, pose6=None, allreduce=None, n_iter=None, lr_gamma=1.0):
+        from . import _lib as L
+        self._L = L
         dev = window.device
         K = window.n_kf
         if pose6 is None:
@@ -140,13 +147,17 @@ class PoseWindow:
             M[:, :3, :4] = window.poses.detach().cpu().view(K, 3, 4)
             M[:, 3, 3] = 1.0
             pose6 = matrix_to_pose6(M)
-        self.p6 = torch.nn.Parameter(torch.as_tensor(pose6, dtype=torch.float32).reshape(K, 6).to(dev).clone())
+        self.p6 = torch.as_tensor(pose6, dtype=torch.float32).reshape(K, 6).to(dev).clone()
         self.optimise = torch.as_tensor(optimise, dtype=torch.bool).reshape(K).to(dev)
+        self._opt_u8 = self.optimise.to(torch.uint8)
         self.window = window
         self.lr = float(lr)
         self.allreduce = allreduce
-        self.adam = torch.optim.Adam([self.p6], lr=self.lr)
+        self.m = torch.zeros(K, 6, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(K, 6, dtype=torch.float32, device=dev)
+        self.adam_step = 0
         self.grad = torch.zeros(K, 6, device=dev)
+        self._ray_ws = None
         # per window slot: its keyframe, and whether the ray follows the pose (a LiDAR ray of an
         # optimised keyframe; sky rays use the detached pose)
         off, nsel = window.ray_off_host, window.n_sel_host
@@ -165,48 +176,49 @@ class PoseWindow:
         # when every keyframe keeps 1 - max|o| above near + 1 m after that, no ray can turn invalid and the
         # step needs no per-step host check (StepEngine.step_window's fixed-size path); otherwise it
         # filters every step (one host synchronisation per step).
-        t = self.p6.detach().cpu().numpy()[:, 0:3].astype(np.float64)
+        t = self.p6.cpu().numpy()[:, 0:3].astype(np.float64)
         shift = np.array([window.desc.shift[i] for i in range(3)], np.float64)
         o = (t + shift[None]) / window.scale
         travel = adam_travel_bound(self.lr, n_iter if n_iter is not None else 10 ** 6, lr_gamma) / window.scale
         need = (window.ray_range[0] + 1.0) / window.scale
-        margin = 1.0 - np.abs(o).max(1) - np.where(self.optimise.cpu().numpy(), travel, 0.0)
+        margin = 1.0 - np.abs(o).max(1) - np.where(opt, travel, 0.0)
         self.stay_valid = bool((margin > need).all() and self.far_range > need)
         self.write_window()
 
     def write_window(self):
-        with torch.no_grad():
-            self.window.poses.copy_(pose6_to_rows(self.p6.detach()))
+        L = self._L
+        L.call("lnr_pose_adam", self.p6, None, None, None, None, self.window.n_kf, 0, 0.0, 0.9, 0.999, 1e-8,
+               self.window.poses, L.stream(self.p6.device))
 
     def matrices(self):
         """(K, 4, 4) float32 on the host: the current poses (``Pose.get_transformation_matrix``)."""
-        rows = pose6_to_rows(self.p6.detach()).cpu().view(-1, 3, 4)
+        rows = self.window.poses.detach().cpu().view(-1, 3, 4)
         M = torch.zeros(rows.shape[0], 4, 4)
         M[:, :3, :] = rows
         M[:, 3, 3] = 1.0
         return M
 
-    def gradient(self, engine, rays, slots):
-        """dL/d(pose tensors) (K, 6) of the engine's last step (``pose_grad`` on): ``rays`` the step's
-        (R, 13) rays, ``slots`` their window slots (R,) int64."""
+    def gradient(self, engine, rays, slots=None, slot0=None):
+        """dL/d(pose tensors) (K, 6), written into ``self.grad``, of the engine's last step (``pose_grad`` on):
+        ``rays`` the step's (R, 13) rays, ``slots`` their window slots (R,) int64, or None for slot0 + r."""
+        L = self._L
         n = rays.shape[0]
-        g_o, g_d = ray_gradients(rays, engine.z[:n], engine.d_pos, engine.d_ray, self.far_range)
-        g = keyframe_gradients(rays, g_o, g_d, self.slot_kf[slots], self.slot_pose[slots], self.p6.detach(),
-                               self.window.scale, self.window.n_kf)
+        if self._ray_ws is None or self._ray_ws.numel() < 12 * max(n, 1):
+            self._ray_ws = torch.empty(12 * max(n, 1), dtype=torch.float32, device=rays.device)
+        L.call("lnr_pose_grad", rays, engine.z, engine.d_pos, engine.d_ray, n, engine.S, slots,
+               engine.ray_offset if slot0 is None else int(slot0), self.slot_kf, self.slot_pose, self.p6,
+               self.window.n_kf, self.window.scale, self.far_range, self._ray_ws, self.grad, L.stream(rays.device))
         if self.allreduce is not None:
-            self.allreduce(g)
-        return g
+            self.allreduce(self.grad)
+        return self.grad
 
-    def step(self, engine, rays, slots, lr_factor=1.0):
-        g = self.gradient(engine, rays, slots)
-        self.grad.copy_(g)
-        self.p6.grad = g * self.optimise[:, None].to(g.dtype)
-        for pg in self.adam.param_groups:
-            pg["lr"] = self.lr * lr_factor
-        self.adam.step()
-        self.p6.grad = None
-        self.write_window()
-        return g
+    def step(self, engine, rays, slots=None, lr_factor=1.0):
+        L = self._L
+        self.gradient(engine, rays, slots)
+        self.adam_step += 1
+        L.call("lnr_pose_adam", self.p6, self.m, self.v, self.grad, self._opt_u8, self.window.n_kf, self.adam_step,
+               self.lr * lr_factor, 0.9, 0.999, 1e-8, self.window.poses, L.stream(rays.device))
+        return self.grad
 
 
 def adam_travel_bound(lr, n_iter, gamma=1.0, beta1=0.9, beta2=0.999):

@@ -360,13 +360,37 @@ class StepEngine:
         self.map_frozen = False
         self.poses = None
         self.d_ray = self.d_pos = None
-        self._last_batch, self._slots_cache = None, None
+        self._last_batch = None
+        # Early ray termination (LONER_ERT: auto (default) = with the live backward, 1 always, 0 never): a sample
+        # behind enough opaque ones has float transmittance exactly 0 in the compositing, so its weight is 0 and
+        # neither its sigma nor its encoding can change any output (csrc/field.hip, kErtTMin; 45 % of a trained C2
+        # batch lies behind T = 0, tools/dead_bound.py).  The forward then runs in phases of samples per ray
+        # (ert_bounds): each phase encodes and evaluates the rays still alive and updates their transmittance,
+        # and a ray below 1e-50 skips the later phases.  Bitwise the step without it (tests/test_gpu_live.py).
+        # LONER_ERT_CUTS: the phase boundaries inside a ray, as fractions of n_samples (default "0.5,0.625,0.75": at C2,
+        # trained, 73 / 34 / 12 % of the rays are still alive at them; tools/experiments/r06_ert_tmin.py).
+        self.ert = {"0": False, "1": True}.get(os.environ.get("LONER_ERT", "auto"), "auto")
+        self.ert_cuts = [float(v) for v in os.environ.get("LONER_ERT_CUTS", "0.5,0.625,0.75").split(",") if v.strip()]
+        self.ert_alive = torch.ones(n_rays, dtype=torch.uint8, device=dev)
+        self.ert_T = torch.ones(n_rays, dtype=torch.float64, device=dev)
         self._pp_bufs = [dict(rays=self.rays if i == 0 else torch.empty_like(self.rays),
                               dgt=self.depth_gt if i == 0 else torch.empty_like(self.depth_gt),
                               valid=self.ray_valid if i == 0 else torch.empty_like(self.ray_valid),
                               far=self.far_ref if i == 0 else torch.empty_like(self.far_ref),
                               z=self.z if i == 0 else torch.empty_like(self.z))
                          for i in range(2)]
+
+    def ert_bounds(self):
+        """The early-ray-termination phases [0, b1, ..., S) (whole 64-sample waves), or None when they do not apply
+        (n_samples not a multiple of 64 in {64 .. 512}, or fewer than two phases)."""
+        S = self.S
+        if not self.compact_denc or S % 64:
+            return None
+        b = sorted({int(round(f * S / 64)) * 64 for f in self.ert_cuts if 0.0 < f < 1.0} - {0, S})
+        return [0] + b + [S] if b else None
+
+    def _ert_on(self):
+        return self.ert is True or (self.ert == "auto" and self._live)
 
     def map_lr(self):
         """The map's Adam learning rate this step: lrate_sigma_mlp x the ExponentialLR factor, or 0 while the
@@ -515,7 +539,20 @@ class StepEngine:
         # sharded-optimiser all-gathers may still be writing
         self.finish()
         m(prof, "encode")
-        if self.count_in_forward:  # the backward's record histogram, counted from the forward's corners
+        ert = self.ert_bounds() if self._ert_on() else None
+        if ert is not None:
+            # early ray termination (see __init__): phase by phase, the encode and sigma of the rays still alive
+            lp.flags |= L.LP_SIGMA_READY
+            for q in range(len(ert) - 1):
+                lo, hi = ert[q], ert[q + 1]
+                hist = q == 0 and self.count_in_forward
+                L.call("lnr_hashgrid_fwd_rays_phase", L.ctypes.byref(st.desc), rays, self.z, R, S, st.table_f16,
+                       self.enc, N, self.bwd_ws if hist else None, self.bwd_ws_bytes if hist else 0,
+                       self.ert_alive if q > 0 else None, lo, hi, s)
+                L.call("lnr_field_sigma_phase", st.mlp_f16, self.enc, N, rays, self.z, R, S, lo, hi,
+                       cfg.raw_noise_std, noise, key, self.ray_offset, L.ctypes.byref(lp), self.ws, self.ert_alive,
+                       self.ert_T, s)
+        elif self.count_in_forward:  # the backward's record histogram, counted from the forward's corners
             L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(st.desc), rays, self.z, R, S, st.table_f16, self.enc, N,
                    self.bwd_ws, self.bwd_ws_bytes, s)
         else:
@@ -775,23 +812,16 @@ class StepEngine:
             m = self._mark
             m(prof, "pose_adam")
             rays, slots = self._last_batch
-            self.poses.step(self, rays, slots, self.lr_factor)
+            self.poses.step(self, rays, slots, self.lr_factor)  # (slots None: the engine's [ray_offset, + n))
             m(prof, "pose_adam")
         return out
-
-    def _slot_range(self, n):
-        r = self._slots_cache
-        if r is None or r[0] != (self.ray_offset, n):
-            idx = torch.arange(self.ray_offset, self.ray_offset + n, dtype=torch.int64, device=self.state.device)
-            self._slots_cache = r = ((self.ray_offset, n), idx)
-        return r[1]
 
     def _step_window_any(self, window, global_step, iteration_idx, n, n_rays_global, prof, kw):
         m = self._mark
         if window.all_valid and (self.poses is None or self.poses.stay_valid):
             out = self._step_window_pipelined(window, global_step, iteration_idx, n, n_rays_global, prof, kw)
             if self.poses is not None:
-                self._last_batch = (self.rays[:n], self._slot_range(n))
+                self._last_batch = (self.rays[:n], None)
             return out
         # Windows with rays the 1 m filter drops: the batch size must reach the host (one sync per step).
         # The build and compaction of step k + 1 run on a side stream while step k runs, so that sync
@@ -938,7 +968,7 @@ class StepEngine:
             self._graphs.clear()
             self._graph_window = window
         p = self._pp_parity
-        gkey = (p, ogm, n, self.ray_offset, n_glob, self.zero, self._live, self.pose_grad)
+        gkey = (p, ogm, n, self.ray_offset, n_glob, self.zero, self._live, self.pose_grad, self._ert_on())
         s = L.stream(st.device)
         sc = (L.StepScalars * 1)()
         sc[0] = self.step_scalars(global_step, iteration_idx)

@@ -59,40 +59,50 @@ def _records(L, eng):
 
 @pytest.mark.parametrize("fused", [False, True])
 def test_live_backward_bitwise_on_trained_field(trained, fused):
+    """Full backward without early ray termination (the reference's arithmetic) against the live backward, early ray
+    termination (LONER_ERT, csrc/field.hip kErtTMin: the rays whose transmittance fell below 1e-100 skip the encode
+    and sigma of their later samples) and both, eager and graph-replayed: bitwise equal."""
     from loner_amd import _lib as L
     from loner_amd import step as S_
     cfg, sd, window, g = trained
     out = {}
-    for live in (False, True):
+    for live, ert, graph in ((False, False, False), (True, False, False), (False, True, False), (True, True, False),
+                             (True, True, True)):
         st = S_.FieldState(cfg, device="cuda")
         st.load_state_dict(sd)
         st.reset_optimizer()
         eng = S_.StepEngine(st, window.n_slots, seed=9)
         eng.live_bwd, eng._live = live, live
+        eng.ert = ert
         eng.fused_adam = fused
-        eng.pipeline, eng.use_graph = False, False
-        recs, zero = [], []
+        eng.pipeline, eng.use_graph = False, graph
+        recs, zero, alive = [], [], []
         for k in range(3):
             eng.step_window(window, global_step=g + k, iteration_idx=k)
             torch.cuda.synchronize()
             recs.append(_records(L, eng))
             zero.append(float((eng.d_sigma() == 0).float().mean()))
+            alive.append(float(eng.ert_alive.float().mean()))
         eng.finish()
         torch.cuda.synchronize()
         o = {k: getattr(st, k).clone() for k in ("params", "m", "v", "shadow", "occ")}
         o["grad_mlp"] = st.grad_mlp.clone()
         o["loss"] = eng.loss_out.clone()
-        if not fused:
+        o["depth"] = eng.depth[:window.n_slots].clone()
+        if not fused and not graph:
             o["grad_table"] = st.table_gradient().clone()
-        out[live] = (o, recs, zero)
-    (full, rec_full, zero_full), (live, rec_live, zero_live) = out[False], out[True]
-    assert zero_full == zero_live
-    assert min(zero_live) > 0.5, f"the pre-trained field should leave most samples dead: {zero_live}"
-    for k in full:
-        assert torch.equal(full[k], live[k]), f"{k} differs between the full and the live backward"
-    # the live backward placed far fewer records (its histogram counts live samples only)
-    for rf, rl in zip(rec_full, rec_live):
-        assert rl < 0.6 * rf, (rec_full, rec_live)
+        out[(live, ert, graph)] = (o, recs, zero, alive)
+    full, rec_full, zero_full, _ = out[(False, False, False)]
+    assert min(zero_full) > 0.5, f"the pre-trained field should leave most samples dead: {zero_full}"
+    for key, (o, recs, zero, alive) in out.items():
+        assert zero == zero_full, key
+        for k in o:
+            assert torch.equal(full[k], o[k]), f"{k} differs between the full step and {key} (live, ert, graph)"
+        if key[0]:  # the live backward placed far fewer records (its histogram counts live samples only)
+            for rf, rl in zip(rec_full, recs):
+                assert rl < 0.6 * rf, (key, rec_full, recs)
+        if key[1]:  # early ray termination stopped rays before their last phase
+            assert min(alive) < 1.0, (key, alive)
 
 
 def test_live_probe_switches_modes(trained):
