@@ -789,6 +789,7 @@ def main():
         prof = {}
         zeros = torch.zeros(2, dtype=torch.float64, device=dev)
         nw = R * n_samples // 64
+        th0 = eng.term_hist.clone() if eng.term_hist is not None else None
         for i in range(args.warmup + args.steps, args.warmup + args.steps + PROF_STEPS):
             run(i, prof, g0=g0)
             ds = eng.d_sigma(R)  # (after the step's events: outside every stage)
@@ -796,8 +797,21 @@ def main():
             zeros[1] += (ds[:64 * nw].view(nw, 64) != 0).any(1).logical_not().sum()  # dead 64-sample waves
         torch.cuda.synchronize()
         stage = {k: float(np.mean([v[j].elapsed_time(v[j + 1]) for j in range(0, len(v), 2)])) for k, v in prof.items()}
+        ert = {"phases": eng.ert_bounds(), "mode": eng.ert}
+        if ert["phases"] is not None and "sigma_phase" in stage:
+            # early ray termination: the encode stage holds the phases' encode and sigma launches; the sigma ones
+            # are timed on their own (one pair per phase), the rest is the encode kernels'
+            stage["sigma_phases"] = stage.pop("sigma_phase") * (len(ert["phases"]) - 1)
+        if th0 is not None:
+            d = (eng.term_hist.long().sum(0) - th0.long().sum(0)).cpu().numpy()
+            alive = S_.ert_alive(d, n_samples)
+            ert["alive_after"] = {int(64 * k): round(float(alive[k]), 4) for k in range(1, n_samples // 64)}
+            b = ert["phases"] or [0, n_samples]
+            # the share of ray-samples the encode gathered (the rays still alive at each phase's start)
+            ert["encoded_frac"] = float(sum(alive[lo // 64] * (hi - lo) for lo, hi in zip(b[:-1], b[1:])) / n_samples)
         z = zeros.cpu().numpy()
-        return elapsed, loss, stage, (float(z[0]) / (PROF_STEPS * R * n_samples), float(z[1]) / (PROF_STEPS * max(nw, 1)))
+        return elapsed, loss, stage, (float(z[0]) / (PROF_STEPS * R * n_samples), float(z[1]) / (PROF_STEPS * max(nw, 1)),
+                                      ert)
 
     poses_desc = "fixed (ground-truth poses, use_gt_poses: the north-star driver)"
 
@@ -832,6 +846,7 @@ def main():
             from_init = {"ms_per_step": elapsed / args.steps * 1e3,
                          "value": world * R * n_samples * args.steps / elapsed,
                          "loss": float(loss[0]), "dsigma_zero_frac": zero_frac[0], "dead_wave_frac": zero_frac[1],
+                         "ert": zero_frac[2],
                          "backward": "live" if eng._live else "full", "stage_ms": stage_ms}
             t_pre = time.perf_counter()
             g0, pre = pretrain(eng, state, kind, win_kf, rpk, spk, strat, dev, r_glob,
@@ -859,7 +874,7 @@ def main():
     # algorithmic work counts the samples that have it: every sample is encoded and goes through the MLP forward
     # (its sigma decides whether it is dead), but a sample with dL/dsigma = 0 has no scatter-adds and no MLP
     # backward to do (its contributions are exactly 0; the reference's tcnn path does them all the same)
-    zero_frac, dead_wave_frac = zero_frac
+    zero_frac, dead_wave_frac, ert = zero_frac
     n_live = N * (1.0 - zero_frac)
     bwd_bytes = 1024.0 * n_live + (32.0 * 2 * state.n_entries if fused_adam else 0.0)
     achieved = bwd_bytes / (bwd_ms * 1e-3) / 1e9
@@ -868,12 +883,17 @@ def main():
     enc_traffic, enc_traffic_src = pmc_kernel_traffic(args.config, "k_hashgrid_fwd")
     # the whole step against the HBM bound: 512 B per ray-sample of gathers, 1024 B per live
     # ray-sample of scatter-adds, 32 B per parameter (Adam), 52 B per ray
-    step_bytes = 512.0 * N + 1024.0 * n_live + 32.0 * state.n_params + 52.0 * R
+    n_enc = N * ert.get("encoded_frac", 1.0) if ert["phases"] is not None else N
+    step_bytes = 512.0 * n_enc + 1024.0 * n_live + 32.0 * state.n_params + 52.0 * R
     busy, busy_src = pmc_mfma(args.config)
-    mlp_flop = 4224.0 * N + 8448.0 * n_live
-    mlp_tflops = mlp_flop / (stage_ms["field"] * 1e-3) / 1e12
-    enc_ms = stage_ms["encode"]
-    enc_achieved = 512.0 * N / (enc_ms * 1e-3) / 1e9
+    # (with early ray termination the forward runs in the sigma phases, over the encoded samples)
+    mlp_flop = 4224.0 * n_enc + 8448.0 * n_live
+    mlp_ms = stage_ms["field"] + stage_ms.get("sigma_phases", 0.0)
+    mlp_tflops = mlp_flop / (mlp_ms * 1e-3) / 1e12
+    # the encode launches' time: with early ray termination the stage also holds the sigma phases (timed apart);
+    # the algorithmic gathers are those of the samples encoded (512 B each), as the backward counts live samples
+    enc_ms = stage_ms["encode"] - stage_ms.get("sigma_phases", 0.0)
+    enc_achieved = 512.0 * n_enc / (enc_ms * 1e-3) / 1e9
     ta, ta_src = pmc_ta_busy(args.config)
     line = {
         # BASELINE.json metric: the rate here, the rendered-depth L1 in cpu_baseline.rendered_depth_vs_oracle
@@ -919,7 +939,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": enc_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": enc_achieved / HBM_PEAK_GBS, "traffic": enc_traffic, "traffic_source": enc_traffic_src,
                      "kernel": "k_hashgrid_fwd (training encode + the backward's record histogram)",
-                     "algorithmic_bytes_per_launch": 512 * N, "ms_per_launch": enc_ms,
+                     "algorithmic_bytes_per_launch": 512 * n_enc, "ms_per_launch": enc_ms,
+                     "encoded_samples_per_launch": n_enc,
                      "limiter": "texture addresser: TA busy %s of the launch (%s)" % (
                          "n/a" if ta is None else "%.2f" % ta, ta_src or "no committed PMC pass"),
                      "step_algorithmic_bytes": step_bytes,
@@ -942,8 +963,8 @@ def main():
         # (k_sigma_fwd_tiles + k_composite_wave + k_mlp_bwd_tiles), against the dense fp16 MFMA peak
         "mfma": {"achieved": mlp_tflops, "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": mlp_tflops / MFMA_PEAK_TFLOPS,
                  "flop_per_sample": MLP_FLOP_PER_SAMPLE, "flop_per_launch": mlp_flop,
-                 "flop_note": "forward 4224 per ray-sample, backward 8448 per live ray-sample",
-                 "ms_per_launch": stage_ms["field"],
+                 "flop_note": "forward 4224 per encoded ray-sample, backward 8448 per live ray-sample",
+                 "ms_per_launch": mlp_ms,
                  "busy": busy, "busy_source": busy_src},
         "stage_ms": stage_ms,
         "loss": float(loss[0]),
@@ -953,6 +974,9 @@ def main():
         # the fraction of 64-sample waves without a live sample: the live backward's work skips by wave, and it
         # runs (LONER_LIVE_BWD=auto) while this share exceeds StepEngine.live_on (backward_stage.backward)
         "dead_wave_frac": dead_wave_frac,
+        # early ray termination over the profiled steps: the phases in use (None: off), the share of rays still alive
+        # after each 64-sample boundary (the compositing's termination counts), the share of ray-samples encoded
+        "ert": ert,
         # the same bench on the from-init field, timed first in this run (--field trained only)
         **({"from_init": from_init} if from_init is not None else {}),
         # the process group as torch.distributed reports it (None: a single process, no group)

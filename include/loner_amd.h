@@ -307,7 +307,18 @@ typedef struct lnr_loss_params {
                                 rendering_tcnn.py:248,274-278; the samples z are detached, ray_sampling.py:75-90).
                                 With the hash grid's input gradient (lnr_hashgrid_bwd_rays_jac's d_pos) it gives
                                 dL/d{origin, direction, far} of every ray (joint pose + map) */
+  uint32_t* dev_term_hist;   /* optional DEVICE LNR_TERM_HIST_SLOTS x (n_samples / 64 + 1) counters, slot-major,
+                                lnr_field_train with n_samples a multiple of 64: ray r adds 1 to bin c / 64 of slot
+                                r mod LNR_TERM_HIST_SLOTS, c = the number of its samples after which its
+                                transmittance product is still >= LNR_ERT_T_MIN (c = n_samples: it never terminates).
+                                The caller sums the slots (they only spread the atomics) and differences two reads:
+                                the library never clears them.  The rays alive after sample k (a multiple of 64)
+                                are the bins >= k / 64, which is what picks the phases of
+                                lnr_hashgrid_fwd_rays_phase / lnr_field_sigma_phase */
 } lnr_loss_params;
+#define LNR_TERM_HIST_SLOTS 256
+#define LNR_ERT_T_MIN 1e-50      /* early ray termination: a ray whose transmittance product fell below this has
+                                    float transmittance exactly 0 at every later sample (csrc/field.hip) */
 #define LNR_LP_DW_OVERWRITE 1  /* lnr_field_train STORES d_w (the MLP gradient) instead of adding to it */
 #define LNR_LP_SIGMA_READY 2   /* lnr_field_train: sigma is already in its workspace (lnr_field_sigma_phase), the
                                   MLP forward is not run again (n_samples in {64, 128, 256, 512}) */

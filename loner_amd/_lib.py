@@ -71,7 +71,7 @@ class LossParams(ctypes.Structure):
                 ("los_eps", ctypes.c_float), ("far_ref", ctypes.c_float), ("inv_n_opaque", ctypes.c_float),
                 ("inv_rs", ctypes.c_float), ("dev_n_opaque", ctypes.c_void_p), ("dev_far_ref", ctypes.c_void_p),
                 ("dev_status", ctypes.c_void_p), ("dev_loss_out", ctypes.c_void_p), ("flags", ctypes.c_int32),
-                ("dev_step", ctypes.c_void_p), ("dev_d_ray", ctypes.c_void_p)]
+                ("dev_step", ctypes.c_void_p), ("dev_d_ray", ctypes.c_void_p), ("dev_term_hist", ctypes.c_void_p)]
 
 
 LP_DW_OVERWRITE = 1

@@ -641,6 +641,15 @@ __device__ void composite_loss_wave(const FieldArgs& a, float* sig, int64_t r) {
     acc_wz += (double)(w[c] * z[c]);
     acc_wzs += (double)((z[c] * lp.scale) * w[c]);
   }
+  if (lp.dev_term_hist && S % 64 == 0) {
+    // where the ray terminates (lnr_loss_params.dev_term_hist): its samples after which the transmittance product
+    // (the one above, in double) is still >= the early-ray-termination threshold
+    int live = 0;
+#pragma unroll
+    for (int c = 0; c < C; ++c) live += (T0 * tl[c] * (double)s[c] >= LNR_ERT_T_MIN) ? 1 : 0;
+    const int cnt = (int)wave_sum((float)live);  // (exact: at most 512)
+    if (lane == 0) atomicAdd(lp.dev_term_hist + (r % LNR_TERM_HIST_SLOTS) * (S / 64 + 1) + cnt / 64, 1u);
+  }
   const float wsum = wave_sum((float)acc_w);
   const float wzsum = wave_sum((float)acc_wz);
   const float wzssum = wave_sum((float)acc_wzs);
@@ -843,7 +852,7 @@ __global__ void __launch_bounds__(NT) k_sigma_fwd_tiles(FieldArgs a) {
 // margin (1e-50 against float's 7e-46) also keeps the later samples' alpha, which still enters the suffix sums
 // X of the samples before them through factors below 1e-50 / T, out of every float result in practice
 // (tests/test_gpu_live.py: bitwise the step without termination).
-constexpr double kErtTMin = 1e-50;
+constexpr double kErtTMin = LNR_ERT_T_MIN;
 
 // One wave per ray: the sigma of its samples [lo, hi) (64-sample units, 4 MFMA tiles each) and, when
 // hi < S, its transmittance product over them: T <- T * prod s (T = 1 before the first phase), alive = T >= t_min.
@@ -1671,8 +1680,7 @@ extern "C" int lnr_field_sigma_phase(const uint16_t* w, const uint32_t* enc, int
   if (lp) a.lp = *lp;
   a.d_sigma = workspace + lnr_dw_workspace_words(n_rays);
   hipStream_t st = as_stream(stream);
-  const char* e = getenv("LONER_ERT_TMIN");  // (experiments: tools/experiments/r06_ert_tmin.py)
-  const double t_min = e ? atof(e) : kErtTMin;
+  const double t_min = kErtTMin;
   const int64_t want = (n_rays + kWavesPerBlock - 1) / kWavesPerBlock;
   hipLaunchKernelGGL(k_sigma_phase, dim3((int)(want < 8192 ? want : 8192)), dim3(NT), 0, st, a, alive, transmittance, lo,
                      hi, t_min);

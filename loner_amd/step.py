@@ -185,6 +185,62 @@ AR_CUT_DEFAULT = 6
 # (tools/zero_tail_model.py, profiles/r06_zero_tail_model_C4s8.txt)
 AR_CUT_TWO_GROUPS = 8
 
+# Early ray termination's cost model (us; csrc/field.hip, lnr_hashgrid_fwd_rays_phase + lnr_field_sigma_phase),
+# fitted to round 6's kernel traces of the trained C2 and C4 steps: the encode + sigma of
+# one ray-sample ERT_SAMPLE_NS, phased or not; going phased ERT_FIXED_US (the first phase's record histogram over
+# the samples it does not encode, four sigma launches' weight loads); every phase after the first ERT_PHASE_US
+# (one encode and one sigma launch with their tails)
+ERT_SAMPLE_NS, ERT_FIXED_US, ERT_PHASE_US = 0.157, 35.0, 23.0
+TERM_HIST_SLOTS = 256  # LNR_TERM_HIST_SLOTS
+ERT_MAX_CUTS = 4
+ERT_MARGIN = 0.02  # a plan replaces the current one only when it is modelled this much faster (of the full encode)
+
+
+def ert_alive(hist, S):
+    """From a termination histogram (lnr_loss_params.dev_term_hist: bin c // 64 per ray, c its samples before the
+    transmittance product drops below LNR_ERT_T_MIN): the share of rays still alive after sample 64 k, k = 0..S/64."""
+    import numpy as np
+    h = np.asarray(hist, dtype=np.float64)
+    tot = h.sum()
+    if tot <= 0:
+        return np.ones(S // 64 + 1)
+    tail = np.cumsum(h[::-1])[::-1]  # rays with bin >= k
+    return tail / tot
+
+
+def ert_cost_us(bounds, alive, S, n_samples):
+    """Modelled encode + sigma time of one step (n_samples ray-samples) with the phases ``bounds``
+    ([0, c1, .., S]) or, for None, without early ray termination."""
+    full = ERT_SAMPLE_NS * 1e-3 * n_samples
+    if bounds is None:
+        return full
+    t = ERT_FIXED_US + ERT_PHASE_US * (len(bounds) - 2)
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        t += full * float(alive[lo // 64]) * (hi - lo) / S
+    return t
+
+
+def ert_plan(hist, S, n_samples, current=None, max_cuts=ERT_MAX_CUTS, margin=ERT_MARGIN):
+    """The early-ray-termination phases for the coming steps from the last steps' termination histogram: the
+    cheapest under ert_cost_us among no termination and every set of at most ``max_cuts`` cuts at multiples of
+    64 samples, kept only if it beats ``current`` (the plan in use: bounds or None) by ``margin`` of the full
+    encode (so the graphs, captured per plan, are not re-captured for noise).  Returns bounds or None."""
+    import itertools
+    if S % 64 or S < 128:
+        return None
+    alive = ert_alive(hist, S)
+    full = ert_cost_us(None, alive, S, n_samples)
+    pos = list(range(64, S, 64))
+    best, best_t = None, full
+    for k in range(1, min(max_cuts, len(pos)) + 1):
+        for cuts in itertools.combinations(pos, k):
+            b = [0, *cuts, S]
+            t = ert_cost_us(b, alive, S, n_samples)
+            if t < best_t:
+                best, best_t = b, t
+    cur_t = ert_cost_us(current, alive, S, n_samples)
+    return best if best_t < cur_t - margin * full else current
+
 
 class StepEngine:
     """Preallocated workspaces for a fixed ray-batch size; ``step`` runs one optimiser step."""
@@ -361,18 +417,28 @@ class StepEngine:
         self.poses = None
         self.d_ray = self.d_pos = None
         self._last_batch = None
-        # Early ray termination (LONER_ERT: auto (default) = with the live backward, 1 always, 0 never): a sample
-        # behind enough opaque ones has float transmittance exactly 0 in the compositing, so its weight is 0 and
-        # neither its sigma nor its encoding can change any output (csrc/field.hip, kErtTMin; 45 % of a trained C2
-        # batch lies behind T = 0, tools/dead_bound.py).  The forward then runs in phases of samples per ray
-        # (ert_bounds): each phase encodes and evaluates the rays still alive and updates their transmittance,
-        # and a ray below 1e-50 skips the later phases.  Bitwise the step without it (tests/test_gpu_live.py).
-        # LONER_ERT_CUTS: the phase boundaries inside a ray, as fractions of n_samples (default "0.5,0.625,0.75": at C2,
-        # trained, 73 / 34 / 12 % of the rays are still alive at them; tools/experiments/r06_ert_tmin.py).
+        # Early ray termination: a sample behind enough opaque ones has float transmittance exactly 0 in the
+        # compositing, so its weight is 0 and neither its sigma nor its encoding can change any output
+        # (csrc/field.hip, LNR_ERT_T_MIN; 45 % of a trained C2 batch lies behind T = 0, tools/dead_bound.py).  The
+        # forward then runs in phases of samples per ray (ert_bounds): each phase encodes and evaluates the rays still
+        # alive and updates their transmittance, and a ray below 1e-50 skips the later phases.  Bitwise the step
+        # without it (tests/test_gpu_live.py).  LONER_ERT: auto (default): the compositing counts where every ray
+        # terminates (term_hist, lnr_loss_params.dev_term_hist), read back like the live backward's probe (no host
+        # sync), and ert_plan picks the phases, or none, from the last steps' counts under a fitted cost model
+        # (on the trained C2 field three cuts, on C4's forest, where few rays terminate,
+        # none); 1: always, at the fixed cuts LONER_ERT_CUTS (fractions of n_samples, default 0.5,0.625,0.75); 0: never.
         self.ert = {"0": False, "1": True}.get(os.environ.get("LONER_ERT", "auto"), "auto")
         self.ert_cuts = [float(v) for v in os.environ.get("LONER_ERT_CUTS", "0.5,0.625,0.75").split(",") if v.strip()]
         self.ert_alive = torch.ones(n_rays, dtype=torch.uint8, device=dev)
         self.ert_T = torch.ones(n_rays, dtype=torch.float64, device=dev)
+        self._ert_plan = None  # auto: the phases in use, [0, c1, .., S], or None
+        nb = self.S // 64 + 1
+        self.term_hist = (torch.zeros(TERM_HIST_SLOTS, nb, dtype=torch.int32, device=dev) if self.S % 64 == 0
+                          else None)  # (slots spread the compositing's atomics; term_counts() sums them)
+        pin = torch.cuda.is_available() and self.term_hist is not None
+        self._term_host = torch.zeros(TERM_HIST_SLOTS, nb, dtype=torch.int32).pin_memory() if pin else None
+        self._term_prev = [0] * (self.S // 64 + 1)
+        self._term_ev, self._term_ctr = None, self.live_probe_every
         self._pp_bufs = [dict(rays=self.rays if i == 0 else torch.empty_like(self.rays),
                               dgt=self.depth_gt if i == 0 else torch.empty_like(self.depth_gt),
                               valid=self.ray_valid if i == 0 else torch.empty_like(self.ray_valid),
@@ -381,16 +447,41 @@ class StepEngine:
                          for i in range(2)]
 
     def ert_bounds(self):
-        """The early-ray-termination phases [0, b1, ..., S) (whole 64-sample waves), or None when they do not apply
-        (n_samples not a multiple of 64 in {64 .. 512}, or fewer than two phases)."""
+        """The early-ray-termination phases [0, b1, ..., S] (whole 64-sample waves) of the coming step, or None:
+        termination off (LONER_ERT=0, or auto with no plan that pays), or not applicable (n_samples not a multiple
+        of 64 in {64 .. 512}, or fewer than two phases)."""
         S = self.S
-        if not self.compact_denc or S % 64:
+        if not self.compact_denc or S % 64 or self.ert is False:
             return None
+        if self.ert == "auto":
+            return None if self._ert_plan is None else list(self._ert_plan)
         b = sorted({int(round(f * S / 64)) * 64 for f in self.ert_cuts if 0.0 < f < 1.0} - {0, S})
         return [0] + b + [S] if b else None
 
-    def _ert_on(self):
-        return self.ert is True or (self.ert == "auto" and self._live)
+    def _ert_key(self):
+        b = self.ert_bounds()
+        return None if b is None else tuple(b)
+
+    def ert_probe(self):
+        """LONER_ERT=auto: re-plan the phases from the termination counts the steps since the last probe added to
+        term_hist (read back behind an event, no host sync; the first probe after the first step, then every
+        live_probe_every steps)."""
+        if self.ert != "auto" or self._term_host is None:
+            return
+        ev = self._term_ev
+        if ev is not None and ev.query():
+            cur = [int(v) & 0xFFFFFFFF for v in self._term_host.long().sum(0).tolist()]
+            d = [(c - p) & 0xFFFFFFFF for c, p in zip(cur, self._term_prev)]  # (the counters wrap at 2^32)
+            self._term_prev = cur
+            self._term_ev = None
+            if sum(d) > 0:
+                self._ert_plan = ert_plan(d, self.S, self._r_last * self.S, self._ert_plan)
+        self._term_ctr += 1
+        if self._term_ev is None and self._term_ctr >= self.live_probe_every:
+            self._term_ctr = 0
+            self._term_host.copy_(self.term_hist, non_blocking=True)
+            self._term_ev = torch.cuda.Event()
+            self._term_ev.record()
 
     def map_lr(self):
         """The map's Adam learning rate this step: lrate_sigma_mlp x the ExponentialLR factor, or 0 while the
@@ -522,6 +613,7 @@ class StepEngine:
         dsp = None if dev_step is None else dev_step.data_ptr()
         lp.dev_step = dsp
         lp.dev_d_ray = self.d_ray.data_ptr() if self.pose_grad else None
+        lp.dev_term_hist = self.term_hist.data_ptr() if self.ert == "auto" and self.term_hist is not None else None
         self._dev_step = dsp
         # 2. sampling (``presampled``: step_window's pipeline already drew self.z for these rays); the previous
         # step's data-parallel OGM update lands first (the sampler reads the grid)
@@ -539,7 +631,7 @@ class StepEngine:
         # sharded-optimiser all-gathers may still be writing
         self.finish()
         m(prof, "encode")
-        ert = self.ert_bounds() if self._ert_on() else None
+        ert = self.ert_bounds()
         if ert is not None:
             # early ray termination (see __init__): phase by phase, the encode and sigma of the rays still alive
             lp.flags |= L.LP_SIGMA_READY
@@ -549,9 +641,11 @@ class StepEngine:
                 L.call("lnr_hashgrid_fwd_rays_phase", L.ctypes.byref(st.desc), rays, self.z, R, S, st.table_f16,
                        self.enc, N, self.bwd_ws if hist else None, self.bwd_ws_bytes if hist else 0,
                        self.ert_alive if q > 0 else None, lo, hi, s)
+                m(prof, "sigma_phase")
                 L.call("lnr_field_sigma_phase", st.mlp_f16, self.enc, N, rays, self.z, R, S, lo, hi,
                        cfg.raw_noise_std, noise, key, self.ray_offset, L.ctypes.byref(lp), self.ws, self.ert_alive,
                        self.ert_T, s)
+                m(prof, "sigma_phase")
         elif self.count_in_forward:  # the backward's record histogram, counted from the forward's corners
             L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(st.desc), rays, self.z, R, S, st.table_f16, self.enc, N,
                    self.bwd_ws, self.bwd_ws_bytes, s)
@@ -710,7 +804,8 @@ class StepEngine:
         """LONER_LIVE_BWD=auto: pick the backward for the coming steps from the share of dead 64-sample waves
         (see __init__).  Called after every step by step_window; a probe is a count of the last step's waves
         holding a non-zero dL/dsigma, copied to pinned host memory behind an event, read when the event has
-        completed."""
+        completed.  Also runs the early-ray-termination probe (ert_probe)."""
+        self.ert_probe()
         if self.live_bwd != "auto":
             return
         ev = self._probe_ev
@@ -968,7 +1063,7 @@ class StepEngine:
             self._graphs.clear()
             self._graph_window = window
         p = self._pp_parity
-        gkey = (p, ogm, n, self.ray_offset, n_glob, self.zero, self._live, self.pose_grad, self._ert_on())
+        gkey = (p, ogm, n, self.ray_offset, n_glob, self.zero, self._live, self.pose_grad, self._ert_key())
         s = L.stream(st.device)
         sc = (L.StepScalars * 1)()
         sc[0] = self.step_scalars(global_step, iteration_idx)

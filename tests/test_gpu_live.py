@@ -125,3 +125,45 @@ def test_live_probe_switches_modes(trained):
         eng2.step_window(window, global_step=1 + k, iteration_idx=k)
         torch.cuda.synchronize()
     assert not eng2._live
+
+
+def test_ert_auto_plans_from_termination_counts(trained, monkeypatch):
+    """LONER_ERT=auto: the compositing's termination counts (lnr_loss_params.dev_term_hist) reach the planner
+    without a host sync; on the trained field it picks phases, every ray is counted once per step, and the steps
+    stay bitwise those without termination; on a fresh field (no ray terminates) it picks none.  (This batch,
+    2048 rays, is too small for the fitted fixed costs to let phases pay: the test lowers them.)"""
+    from loner_amd import step as S_
+    monkeypatch.setattr(S_, "ERT_FIXED_US", 2.0)
+    monkeypatch.setattr(S_, "ERT_PHASE_US", 2.0)
+    cfg, sd, window, g = trained
+    outs = []
+    for mode in (False, "auto"):
+        st = S_.FieldState(cfg, device="cuda")
+        st.load_state_dict(sd)
+        st.reset_optimizer()
+        eng = S_.StepEngine(st, window.n_slots, seed=9)
+        eng.live_bwd, eng._live = True, True
+        eng.ert = mode
+        eng.pipeline, eng.use_graph = False, False
+        plans = []
+        for k in range(6):
+            eng.step_window(window, global_step=g + k, iteration_idx=k)
+            torch.cuda.synchronize()
+            plans.append(eng.ert_bounds())
+        eng.finish()
+        torch.cuda.synchronize()
+        outs.append({k: getattr(st, k).clone() for k in ("params", "m", "v", "shadow", "occ")})
+        if mode == "auto":
+            assert int(eng.term_hist.sum()) == 6 * window.n_slots
+            assert plans[0] is None and plans[-1] is not None, plans  # off until the first counts arrive
+            alive = S_.ert_alive(eng.term_hist.long().sum(0).cpu().numpy(), S)
+            assert alive[-1] < 0.9, alive
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
+    fresh = S_.FieldState(cfg, device="cuda")
+    eng2 = S_.StepEngine(fresh, window.n_slots, seed=9)
+    eng2.ert = "auto"
+    for k in range(4):
+        eng2.step_window(window, global_step=1 + k, iteration_idx=k)
+        torch.cuda.synchronize()
+    assert eng2.ert_bounds() is None
