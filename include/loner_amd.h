@@ -121,8 +121,9 @@ int lnr_hashgrid_fwd_rays(const lnr_grid_desc* d, const float* rays, const float
 /* Early ray termination, the encode of one phase: samples [lo, hi) (multiples of 64; n_samples % 64 == 0) of
  * every ray whose alive[r] != 0 (alive NULL: every ray), as lnr_hashgrid_fwd_rays encodes them; the other
  * samples' encodings are left unwritten.  bwd_ws (the first phase only, lo == 0): the backward's record
- * histogram of EVERY sample, as lnr_hashgrid_fwd_rays records it (so the backward's fixed-point units are the
- * full step's).  Without bwd_ws only the phase's samples are launched.  See lnr_field_sigma_phase. */
+ * histogram of EVERY sample, as lnr_hashgrid_fwd_rays records it, for a full backward with
+ * LNR_BWD_COUNTS_READY (the live backward counts its own).  Without bwd_ws only the phase's samples are
+ * launched.  See lnr_field_sigma_phase. */
 int lnr_hashgrid_fwd_rays_phase(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
                                 int32_t n_samples, const uint16_t* table, uint32_t* enc, int64_t enc_stride,
                                 void* bwd_ws, int64_t bwd_ws_bytes, const uint8_t* alive, int32_t lo, int32_t hi,
@@ -145,7 +146,7 @@ int lnr_hashgrid_fwd_rays_live_ws(const lnr_grid_desc* d, const float* rays, con
                                   int64_t enc_stride, void* bwd_ws, int64_t bwd_ws_bytes, void* stream);
 /* Backward: d_table (n_entries,2) fp32 = scatter of corner weights * d_enc, as an atomic-free
  * binned scatter of 8-byte records (fp16 values at a per-level power-of-two scale from max |d_enc|)
- * with int64 fixed-point accumulation.  d_table is OVERWRITTEN (every entry, zero where
+ * with int64 fixed-point accumulation at a unit that depends on N alone.  d_table is OVERWRITTEN (every entry, zero where
  * no sample touches it, all zero for N = 0) and the result is bitwise reproducible; `workspace` holds
  * at least lnr_hashgrid_bwd_workspace_bytes(d, N) bytes.
  * Input gradient (tcnn's backward w.r.t. the positions, src/models/nerf_tcnn.py:63,68-71 when pos
@@ -163,14 +164,15 @@ int lnr_hashgrid_fwd_rays_live_ws(const lnr_grid_desc* d, const float* rays, con
                                      parallelism: they only pick each level's power-of-two record scale,
                                      fp16 rounding is scale-invariant, and the fixed-point unit sits far
                                      below what reaches Adam */
-#define LNR_BWD_LIVE 8            /* lnr_hashgrid_bwd_rays_jac(_adam) with LNR_BWD_COUNTS_READY: the live backward.
-                                     A sample with d_sigma[n] == 0 (relu(sigma + noise) = 0, rendering_tcnn.py:260)
-                                     adds exactly 0 to every entry, so only samples with d_sigma != 0 emit records
-                                     (coherent levels: only runs holding one), after a histogram pass over those
-                                     samples; the fixed-point units still follow the forward's (every sample's)
-                                     histogram, so d_table is BITWISE the full backward's.  Pays when most samples
-                                     are dead (a trained field: ~80 % at C2); ignored where the level-looped scatter
-                                     does not apply (small batches, other grids). */
+#define LNR_BWD_LIVE 8            /* lnr_hashgrid_bwd_rays_jac(_adam): the live backward.  A sample with
+                                     d_sigma[n] == 0 (relu(sigma + noise) = 0 or transmittance 0,
+                                     rendering_tcnn.py:252-266) adds exactly 0 to every entry, so only samples with
+                                     d_sigma != 0 emit records (coherent levels: only runs holding one), after its
+                                     own histogram pass over those samples (a forward histogram is not needed and,
+                                     with LNR_BWD_COUNTS_READY, not read).  The fixed-point unit depends on N alone,
+                                     so d_table is BITWISE the full backward's.  Pays when most samples are dead (a
+                                     trained field: ~89 % at C2); ignored where the level-looped scatter does not
+                                     apply (small batches, other grids). */
 int64_t lnr_hashgrid_bwd_workspace_bytes(const lnr_grid_desc* d, int64_t n);
 /* Device address of the n_levels per-level max |d_enc| floats inside `workspace` (the same for
  * every n: the workspace's first bytes). */
@@ -188,9 +190,8 @@ int lnr_hashgrid_bwd_rays(const lnr_grid_desc* d, const float* rays, const float
                           int32_t flags, void* stream);
 /* The table gradient of samples with a live mask (the colour grid: live = the compositing weights, d_enc
  * of a weight-0 sample is 0): at the levels that are not coherent, samples with live[n] == 0 emit no records
- * (the others emit theirs, zero or not).  The same d_table as lnr_hashgrid_bwd_rays (bitwise when no live
- * sample has d_enc = 0 at such a level; a zero record can move its bucket's fixed-point unit, a rounding
- * below 2^-44 of the level's largest record).  With LNR_BWD_COUNTS_READY the histogram must come from
+ * (the others emit theirs, zero or not).  Bitwise the same d_table as lnr_hashgrid_bwd_rays (records of zero
+ * add nothing and the fixed-point unit does not follow the record counts).  With LNR_BWD_COUNTS_READY the histogram must come from
  * lnr_hashgrid_fwd_rays_live_ws with the same mask. */
 int lnr_hashgrid_bwd_rays_live(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
                                int32_t n_samples, const float* d_enc, int64_t enc_stride, const float* live,

@@ -118,9 +118,10 @@ inline int enc_levels_per_group(const lnr_grid_desc* d, int64_t n_sb) {
   return 1;
 }
 // Early ray termination (lnr_hashgrid_fwd_rays_phase): the encode of samples [lo, hi) of each ray, for the
-// rays still ``alive`` (per-ray bytes, or every ray).  With the record histogram (the first phase) the grid
-// is the plain one, every sample's records are counted (the backward's fixed-point units follow the full
-// counts) and only the phase's samples gather; without it the grid covers just the phase's samples
+// rays still ``alive`` (per-ray bytes, or every ray).  With the record histogram (the first phase, for a full
+// backward, which places every sample's records) the grid is the plain one, every sample's records are counted
+// and only the phase's samples gather; without it (the live backward counts its own) the grid covers just the
+// phase's samples
 // (``compact``: workgroup sample g -> ray g / (hi - lo), ray sample lo + g % (hi - lo); a wave stays
 // within one ray, as lo and hi are multiples of 64).
 struct EncPhase {

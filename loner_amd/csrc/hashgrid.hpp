@@ -546,8 +546,6 @@ struct BwdWorkspace {
   uint32_t* chunk_sum;   // [L][n_chunks][kMaxChunksPerLevel] per-chunk column sums (k_bwd_chunk_sums)
   float* level_max;      // [LNR_MAX_LEVELS] max |d_enc| per level (as uint bits: k_denc_level_max's atomicMax)
   uint32_t* counts;      // [kMaxBuckets] records per bucket (the scatter's: placement, work split)
-  uint32_t* k2cnt;       // [kMaxBuckets] the count the fixed-point unit follows (bucket_k2): every sample's
-                         // records (the forward's histogram), also when the live backward places fewer
   uint64_t* seg_start;   // [kMaxBuckets + 1]
   long long* partial;    // [2 kAccumGroups][2 * kChunk] int64 fixed-point partial sums of cut buckets
   uint32_t* bucket_done; // [kMaxBuckets] pieces of a cut bucket accumulated so far (k_bwd_accum<true>)
@@ -560,6 +558,7 @@ struct BwdWorkspace {
   uint32_t* live;        // [2] live waves, live rows (= ceil(live waves / 8))
   int64_t n_sb;
   int64_t n_chunks;
+  int32_t k2;            // the fixed-point exponent of every bucket (bwd_fixed_k2: from N alone)
   bool use_live;         // the scans cover live[1] rows instead of n_sb (the live histogram)
 };
 
@@ -569,7 +568,7 @@ inline int64_t bwd_n_chunks(int64_t n) { return (bwd_n_sb(n) + kRowsPerChunk - 1
 inline int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
 
 struct WsLayout {
-  int64_t hist, chunk_sum, level_max, counts, k2cnt, seg_start, partial, bucket_done, units, wflags, wlist, live, rec,
+  int64_t hist, chunk_sum, level_max, counts, seg_start, partial, bucket_done, units, wflags, wlist, live, rec,
       total;
 };
 
@@ -581,7 +580,6 @@ inline WsLayout ws_layout(const lnr_grid_desc* d, const GridArgs& a, int64_t n) 
   w.hist = b;      b += align256((int64_t)a.n_buckets * nsb * 4);
   w.chunk_sum = b; b += align256((int64_t)d->n_levels * nch * kMaxChunksPerLevel * 4);
   w.counts = b;    b += align256(kMaxBuckets * 4);
-  w.k2cnt = b;     b += align256(kMaxBuckets * 4);
   w.seg_start = b; b += align256((kMaxBuckets + 1) * 8);
   w.partial = b;   b += align256((int64_t)2 * kAccumGroups * 2 * kChunk * 8);
   w.bucket_done = b; b += align256(kMaxBuckets * 4);
@@ -597,6 +595,16 @@ inline WsLayout ws_layout(const lnr_grid_desc* d, const GridArgs& a, int64_t n) 
 
 inline int64_t bwd_workspace_bytes(const lnr_grid_desc* d, int64_t n) { return ws_layout(d, make_args(d), n).total; }
 
+// The backward's fixed-point exponent (records scaled by 2^k2, in the level's record units): the records of one
+// level and feature, |w g| 2^k < 2^9 per sample (2^k = 2^9 / 2^E, level max |d_enc| < 2^E) with corner weights
+// summing to 1 per sample, add up to less than N 2^9 in any bucket, so 2^(53 - lg N) keeps every int64 sum below
+// 2^62 whatever the counts; one record converted stays below 2^51 (|record| < 2^15, k2 <= 36).  C2 (N = 2^22):
+// k2 = 30, finer than a per-bucket count gives (47 - lg cnt: 27 for a fine bucket of every sample's records).  It
+// depends on N alone: the full backward, the live backward and the skip-zero count all round alike.
+inline int32_t bwd_fixed_k2(int64_t n) {
+  const int lg = n > 0 ? 64 - __builtin_clzll((unsigned long long)n) : 1;  // bits of n (>= log2 n)
+  return 53 - lg < 36 ? 53 - lg : 36;
+}
 inline BwdWorkspace carve_workspace(void* base, const GridArgs& a, const lnr_grid_desc* d, int64_t n) {
   const WsLayout L = ws_layout(d, a, n);
   char* p = reinterpret_cast<char*>(base);
@@ -605,7 +613,6 @@ inline BwdWorkspace carve_workspace(void* base, const GridArgs& a, const lnr_gri
   w.chunk_sum = reinterpret_cast<uint32_t*>(p + L.chunk_sum);
   w.level_max = reinterpret_cast<float*>(p + L.level_max);
   w.counts = reinterpret_cast<uint32_t*>(p + L.counts);
-  w.k2cnt = reinterpret_cast<uint32_t*>(p + L.k2cnt);
   w.seg_start = reinterpret_cast<uint64_t*>(p + L.seg_start);
   w.partial = reinterpret_cast<long long*>(p + L.partial);
   w.bucket_done = reinterpret_cast<uint32_t*>(p + L.bucket_done);
@@ -616,6 +623,7 @@ inline BwdWorkspace carve_workspace(void* base, const GridArgs& a, const lnr_gri
   w.rec = reinterpret_cast<uint2*>(p + L.rec);
   w.n_sb = bwd_n_sb(n);
   w.n_chunks = bwd_n_chunks(n);
+  w.k2 = bwd_fixed_k2(n);
   return w;
 }
 

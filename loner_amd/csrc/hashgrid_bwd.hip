@@ -170,18 +170,12 @@ __device__ __forceinline__ void build_units(UnitTable* ut, uint32_t b0, uint32_t
 
 // Bucket segment starts: exclusive prefix of the bucket totals (records are laid out bucket-major),
 // and the unit accumulation's work list over all buckets.
-// set_k2: the counts are every sample's records (the forward's histogram): they also set the fixed-point
-// units (ws.k2cnt); the live backward's counts do not (k_bwd_col_totals wrote ws.k2cnt before).
-__global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint32_t n_buckets, bool set_k2) {
+__global__ void __launch_bounds__(1024) k_bwd_scan_buckets(BwdWorkspace ws, uint32_t n_buckets) {
   __shared__ uint64_t w_seg[16], w_units[16];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   uint64_t seg[2];  // two buckets per thread (n_buckets <= kMaxBuckets = 2048)
 #pragma unroll
   for (int q = 0; q < 2; ++q) seg[q] = 2 * t + q < (int)n_buckets ? ws.counts[2 * t + q] : 0u;
-  if (set_k2)
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-      if (2 * t + q < (int)n_buckets) ws.k2cnt[2 * t + q] = (uint32_t)seg[q];
   uint64_t iseg = seg[0] + seg[1];
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -232,40 +226,9 @@ __global__ void __launch_bounds__(1024) k_bwd_units(BwdWorkspace ws, uint32_t b0
 // live samples: fine levels emit a sample's records iff dL/dsigma != 0, coherent levels a run's records iff the run
 // holds a live lane, and a wave without a live lane skips all of its work.  Everything else is the full
 // backward's: the same rows, the same run merging over the same lanes (dead lanes add zeros), the same record
-// values, and the fixed-point unit of a bucket from every sample's count (ws.k2cnt, the forward's histogram), so
-// the int64 sums, and the gradient, are bitwise those of the full backward.
-
-// The forward's per-bucket totals over every sample (ws.k2cnt): the column sums of its histogram, from the
-// per-chunk sums when there are several chunks.  grid (L), 1024 threads: column c = t % 128 of group g = t / 128
-// sums chunks (or rows) g, g + 8, ... with 16 loads in flight, then the 8 groups add in LDS.
-__global__ void __launch_bounds__(1024) k_bwd_col_totals(GridArgs a, BwdWorkspace ws) {
-  __shared__ uint32_t part[8][kMaxChunksPerLevel];
-  const uint32_t l = blockIdx.x, c = threadIdx.x & (kMaxChunksPerLevel - 1), gq = threadIdx.x / kMaxChunksPerLevel;
-  const uint32_t nb = a.bucket_base[l + 1] - a.bucket_base[l];
-  uint32_t tot = 0;
-  if (c < nb) {
-    const bool rows = ws.n_chunks == 1;
-    const int64_t cnt = rows ? ws.n_sb : ws.n_chunks;
-    const uint32_t* src = rows ? ws.hist + (int64_t)a.bucket_base[l] * ws.n_sb + c
-                               : ws.chunk_sum + (int64_t)l * ws.n_chunks * kMaxChunksPerLevel + c;
-    const int64_t stride = rows ? (int64_t)nb : (int64_t)kMaxChunksPerLevel;
-    for (int64_t k = gq; k < cnt; k += 8 * 16) {
-      uint32_t v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = k + 8 * u < cnt ? src[(k + 8 * u) * stride] : 0u;
-#pragma unroll
-      for (int u = 0; u < 16; ++u) tot += v[u];
-    }
-  }
-  part[gq][c] = tot;
-  __syncthreads();
-  if (gq == 0 && c < nb) {
-    uint32_t t = 0;
-#pragma unroll
-    for (int g = 0; g < 8; ++g) t += part[g][c];
-    ws.k2cnt[a.bucket_base[l] + c] = t;
-  }
-}
+// values, and the same fixed-point unit (bwd_fixed_k2: from N, not from the counts), so the int64 sums, and the
+// gradient, are bitwise those of the full backward.  It counts its own records (k_bwd_count_live): the forward
+// need not record a histogram for it.
 
 // Whether lane's run [head_lane, lane] holds a live lane (wl: the wave's live lanes)
 __device__ __forceinline__ bool run_live(unsigned long long wl, const RunInfo& ri) {
@@ -951,20 +914,15 @@ __global__ void __launch_bounds__(256) k_denc_level_max(GradFn grad, int64_t n, 
 #endif
 constexpr int kAccumThreads = LNR_ACCUM_THREADS;
 
-// Fixed-point exponent of bucket b, in the records' scaled units: |record| < 2^15 and at most cnt
-// records in the bucket.  Each converted value stays below 2^51 (the exact range of the double
-// conversion below: k2 <= 36) and every partial or total sum below 2^62 (k2 <= 47 - lg cnt), so the
-// int64 sums never overflow.  The unit is 2^(lg cnt - 47) of the scaled units, about 2^-44 of the
-// level's largest possible record at C2's bucket sizes.  (Precision here matters beyond the
-// gradients' own: Adam's eps = 1e-8 turns a one-unit difference of a near-zero gradient entry into
-// a visible step, so two runs must round alike far below the gradients' scale.)
-// cnt is the bucket's count over every sample (ws.k2cnt: the forward's histogram), not the records the live
-// backward places (ws.counts), so the unit, and with it every rounding, is the same in both backwards.
-__device__ __forceinline__ int bucket_k2(const BwdWorkspace& ws, uint32_t b) {
-  const uint64_t bcnt = ws.k2cnt[b];
-  const int lg = 64 - __clzll((long long)(bcnt > 0 ? bcnt : 1));  // ceil-ish log2(cnt + 1)
-  return 47 - lg < 36 ? 47 - lg : 36;
-}
+// Fixed-point exponent of bucket b, in the records' scaled units: ws.k2 = bwd_fixed_k2(N) for every bucket
+// (hashgrid.hpp: every partial or total sum stays below 2^62 from the records' magnitudes alone, and each converted
+// value below 2^51, the exact range of the double conversion below).  The unit is 2^-30 of the scaled units at C2,
+// 2^-39 of the level's largest record.  (Precision here matters beyond the gradients' own: Adam's eps = 1e-8 turns
+// a one-unit difference of a near-zero gradient entry into a visible step, so two runs must round alike far below
+// the gradients' scale; they do, as the unit depends on N alone, not on which records a backward places.)
+// (Rounds 1-5 took 47 - lg(count) per bucket, which needed every sample's count, i.e. the forward's record
+// histogram, for the live backward to round like the full one; history before this commit.)
+__device__ __forceinline__ int bucket_k2(const BwdWorkspace& ws, uint32_t) { return ws.k2; }
 // 2^-(k2 + k_l): fixed-point units back to gradient units (double: the exponent may pass fp32's range)
 __device__ __forceinline__ double unit_back(const GridArgs& a, const BwdWorkspace& ws, uint32_t l, int k2) {
   return ldexp(1.0, -(k2 + rec_exp_for(ws.level_max[l])));
@@ -1593,14 +1551,6 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, Gra
   LNR_REQUIRE(n < (int64_t(1) << 31), "%s: n=%lld samples exceeds 2^31", who, (long long)n);
   BwdWorkspace w = carve_workspace(workspace, a, d, n);
   const bool skip_zero = !(flags & LNR_BWD_COUNTS_READY);
-  if (!(flags & LNR_BWD_COUNTS_READY))
-    hipLaunchKernelGGL((k_bwd_count<PosFn, GradFn>), dim3((unsigned)w.n_sb, d->n_levels), dim3(kSB), 0, st, a, pos, n,
-                       grad, w);
-  if (!(flags & LNR_BWD_LEVEL_MAX_READY)) {
-    LNR_REQUIRE(hipMemsetAsync(w.level_max, 0, LNR_MAX_LEVELS * sizeof(float), st) == hipSuccess, "%s: memset failed",
-                who);
-    hipLaunchKernelGGL(k_denc_level_max<GradFn>, dim3(kMaxBlocks, d->n_levels), dim3(256), 0, st, grad, n, w);
-  }
   const uint32_t m = a.merge_levels, L = d->n_levels;
   bool all_fine = true, pow2 = true;
   uint32_t maxnb = 0;
@@ -1617,15 +1567,22 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, Gra
   const bool rows = L == 16 && all_fine && pow2 && 8 * n * (int64_t)L + 2 < (int64_t(1) << 32) &&
                     w.n_sb >= scatter_rows_min();
   const bool rows64 = rows && m >= 3 && m <= 7 && maxnb <= 64;
-  // the live backward (LNR_BWD_LIVE): dL/dsigma-scaled gradients, the forward's histogram for the units, the
-  // level-looped scatter; otherwise the flag is ignored (the full backward: bitwise the same gradient)
-  const bool live = (flags & LNR_BWD_LIVE) && GradFn::kScaled && (flags & LNR_BWD_COUNTS_READY) && rows64;
-  if (w.n_chunks > 1)
+  // the live backward (LNR_BWD_LIVE): dL/dsigma-scaled gradients, the level-looped scatter, its own histogram of
+  // the live records (a forward histogram, if any, is not read); otherwise the flag is ignored (the full backward:
+  // bitwise the same gradient)
+  const bool live = (flags & LNR_BWD_LIVE) && GradFn::kScaled && rows64;
+  if (!(flags & LNR_BWD_COUNTS_READY) && !live)
+    hipLaunchKernelGGL((k_bwd_count<PosFn, GradFn>), dim3((unsigned)w.n_sb, d->n_levels), dim3(kSB), 0, st, a, pos, n,
+                       grad, w);
+  if (!(flags & LNR_BWD_LEVEL_MAX_READY)) {
+    LNR_REQUIRE(hipMemsetAsync(w.level_max, 0, LNR_MAX_LEVELS * sizeof(float), st) == hipSuccess, "%s: memset failed",
+                who);
+    hipLaunchKernelGGL(k_denc_level_max<GradFn>, dim3(kMaxBlocks, d->n_levels), dim3(256), 0, st, grad, n, w);
+  }
+  if (w.n_chunks > 1 && !live)
     hipLaunchKernelGGL(k_bwd_chunk_sums, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
   if (live) {
     if constexpr (GradFn::kScaled) {
-      // every sample's bucket totals (the fixed-point units), then the live records' histogram in its place
-      hipLaunchKernelGGL(k_bwd_col_totals, dim3(d->n_levels), dim3(1024), 0, st, a, w);
       const int64_t n_waves = (n + 63) / 64;
       hipLaunchKernelGGL(k_bwd_live_flags, dim3((unsigned)((n_waves * 16 + 255) / 256)), dim3(256), 0, st, grad.dsig, n, w);
       hipLaunchKernelGGL(k_bwd_live_list, dim3(1), dim3(1024), 0, st, n_waves, w);
@@ -1642,7 +1599,7 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, Gra
     }
   }
   hipLaunchKernelGGL(k_bwd_scan_rows, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
-  hipLaunchKernelGGL(k_bwd_scan_buckets, dim3(1), dim3(1024), 0, st, w, a.n_buckets, !live);
+  hipLaunchKernelGGL(k_bwd_scan_buckets, dim3(1), dim3(1024), 0, st, w, a.n_buckets);
   if (live) {
     if constexpr (GradFn::kScaled) {
       auto kern = m == 3   ? k_bwd_scatter_rows<PosFn, GradFn, 16, 3, 64, true>

@@ -631,13 +631,16 @@ class StepEngine:
         # sharded-optimiser all-gathers may still be writing
         self.finish()
         m(prof, "encode")
+        # the backward's record histogram, counted from the forward's corners, for the full backward (the live one
+        # counts its live records itself)
+        fwd_hist = self.count_in_forward and not self._live
         ert = self.ert_bounds()
         if ert is not None:
             # early ray termination (see __init__): phase by phase, the encode and sigma of the rays still alive
             lp.flags |= L.LP_SIGMA_READY
             for q in range(len(ert) - 1):
                 lo, hi = ert[q], ert[q + 1]
-                hist = q == 0 and self.count_in_forward
+                hist = q == 0 and fwd_hist
                 L.call("lnr_hashgrid_fwd_rays_phase", L.ctypes.byref(st.desc), rays, self.z, R, S, st.table_f16,
                        self.enc, N, self.bwd_ws if hist else None, self.bwd_ws_bytes if hist else 0,
                        self.ert_alive if q > 0 else None, lo, hi, s)
@@ -646,7 +649,7 @@ class StepEngine:
                        cfg.raw_noise_std, noise, key, self.ray_offset, L.ctypes.byref(lp), self.ws, self.ert_alive,
                        self.ert_T, s)
                 m(prof, "sigma_phase")
-        elif self.count_in_forward:  # the backward's record histogram, counted from the forward's corners
+        elif fwd_hist:
             L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(st.desc), rays, self.z, R, S, st.table_f16, self.enc, N,
                    self.bwd_ws, self.bwd_ws_bytes, s)
         else:
@@ -678,7 +681,7 @@ class StepEngine:
             m(prof, "pose_grad")
         # 5. hash-grid backward
         m(prof, "grid_bwd")
-        flags = (L.BWD_COUNTS_READY if self.count_in_forward else 0) | L.BWD_LEVEL_MAX_READY | (
+        flags = (L.BWD_COUNTS_READY if fwd_hist else 0) | L.BWD_LEVEL_MAX_READY | (
             L.BWD_LIVE if self._live else 0)
         if self.zero is not None:
             return self._step_zero(rays, depth_gt, R, S, N, flags, s, scale, update_ogm, global_step, prof)
