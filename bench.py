@@ -135,8 +135,9 @@ def pmc_mfma(cfg_name):
 
 
 def pmc_kernel_traffic(cfg_name, kernel):
-    """HBM bytes per launch of one kernel of the step, from the newest committed per-step PMC pass
-    (profiles/<round>_traffic_<cfg>_step.json); (None, None) if absent."""
+    """HBM bytes per optimiser step of one kernel (every launch of it in the step: early ray termination's encode
+    phases together), from the newest committed per-step PMC pass (profiles/<round>_traffic_<cfg>_step.json);
+    (None, None) if absent."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_traffic_{cfg_name}_step.json")))
     if not files:
@@ -145,9 +146,7 @@ def pmc_kernel_traffic(cfg_name, kernel):
     hits = [v for k, v in rec["kernels"].items() if kernel in k]
     if not hits:
         return None, None
-    per_step = sum(v["bytes_per_step"] for v in hits)
-    launches = sum(v["dispatches"] for v in hits) / max(rec.get("steps_profiled", 1), 1)
-    return per_step / max(launches, 1.0), os.path.relpath(files[-1], ROOT)
+    return sum(v["bytes_per_step"] for v in hits), os.path.relpath(files[-1], ROOT)
 
 
 def pmc_ta_busy(cfg_name):
@@ -938,7 +937,8 @@ def main():
         # bounds it is the texture addresser, not bytes ("What bounds the forward encode")
         "roofline": {"bound": "hbm", "achieved": enc_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": enc_achieved / HBM_PEAK_GBS, "traffic": enc_traffic, "traffic_source": enc_traffic_src,
-                     "kernel": "k_hashgrid_fwd (training encode + the backward's record histogram)",
+                     "kernel": "k_hashgrid_fwd (training encode: every launch of the step, i.e. early ray termination's "
+                               "phases, + the full backward's record histogram when that backward runs)",
                      "algorithmic_bytes_per_launch": 512 * n_enc, "ms_per_launch": enc_ms,
                      "encoded_samples_per_launch": n_enc,
                      "limiter": "texture addresser: TA busy %s of the launch (%s)" % (

@@ -225,8 +225,8 @@ def test_camera_two_shards_match_single_batch(L, skip_zero):
 
 def test_camera_skip_zero_matches_default(L):
     """CameraStepEngine(skip_zero=True, the default) (zero-weight samples: no colour gathers, backward counts
-    only non-zero d_enc) gives the full path's gradient: the skipped samples contribute exactly 0 (the table
-    gradient to the fixed-point rounding of the smaller buckets)."""
+    only non-zero d_enc) gives the full path's gradient bit for bit: the skipped samples contribute exactly 0, and
+    the backward's fixed-point unit depends on the sample count alone, not on how many records it places."""
     from loner_amd import camera as C
     fr, cs_a, eng_def = _camera_setup()
     eng_a = C.CameraStepEngine(eng_def.field, cs_a, n_rays=eng_def.R, n_samples=128, lr=0.01, seed=0, skip_zero=False)
@@ -240,8 +240,7 @@ def test_camera_skip_zero_matches_default(L):
     lb = float(eng_b.step(rays, inten, global_step=5).item())
     assert la == lb
     assert float((eng_b.weights[:R] == 0).float().mean()) > 0.05  # the path is exercised
-    assert torch.equal(cs_a.grad[:cs_a.n_mlp], cs_b.grad[:cs_b.n_mlp])
-    assert _rel(host(cs_b.grad), host(cs_a.grad)) < 1e-6
+    assert torch.equal(cs_a.grad, cs_b.grad)
 
 
 def test_camera_live_count_matches_backward_count(L, monkeypatch):
