@@ -119,14 +119,18 @@ int lnr_hashgrid_fwd_rays(const lnr_grid_desc* d, const float* rays, const float
                           int32_t n_samples, const uint16_t* table, uint32_t* enc, int64_t enc_stride,
                           void* bwd_ws, int64_t bwd_ws_bytes, void* stream);
 /* Early ray termination, the encode of one phase: samples [lo, hi) (multiples of 64; n_samples % 64 == 0) of
- * every ray whose alive[r] != 0 (alive NULL: every ray), as lnr_hashgrid_fwd_rays encodes them; the other
- * samples' encodings are left unwritten.  bwd_ws (the first phase only, lo == 0): the backward's record
- * histogram of EVERY sample, as lnr_hashgrid_fwd_rays records it, for a full backward with
- * LNR_BWD_COUNTS_READY (the live backward counts its own).  Without bwd_ws only the phase's samples are
- * launched.  See lnr_field_sigma_phase. */
+ * the rays ray_list[0 .. *ray_count) (DEVICE; ray_list NULL: every ray), as lnr_hashgrid_fwd_rays encodes them;
+ * the other samples' encodings are left unwritten.  bwd_ws (the first phase only, lo == 0, every ray): the
+ * backward's record histogram of EVERY sample, as lnr_hashgrid_fwd_rays records it, for a full backward with
+ * LNR_BWD_COUNTS_READY (the live backward counts its own).  Without bwd_ws only the listed rays' phase samples
+ * are encoded, by a grid that leaves at once past the list's end.  expect_rays: the caller's estimate of
+ * *ray_count (0: none); a small one selects a grid for a sparse phase (one level per workgroup, walking the
+ * listed rows).  Every grid encodes exactly the listed rays' samples, whatever the count.  See
+ * lnr_field_sigma_phase. */
 int lnr_hashgrid_fwd_rays_phase(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
                                 int32_t n_samples, const uint16_t* table, uint32_t* enc, int64_t enc_stride,
-                                void* bwd_ws, int64_t bwd_ws_bytes, const uint8_t* alive, int32_t lo, int32_t hi,
+                                void* bwd_ws, int64_t bwd_ws_bytes, const uint32_t* ray_list,
+                                const uint32_t* ray_count, int64_t expect_rays, int32_t lo, int32_t hi,
                                 void* stream);
 /* Forward of samples whose compositing weight can be zero (the colour head: rgb = sum w_i c_i + ...,
  * rendering_tcnn.py:286): samples with live[n] == 0 (exactly) issue no gathers, every other sample is
@@ -380,20 +384,24 @@ int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, 
                     float* workspace, float* ray_stats, float* depth, float* opacity, float* weights,
                     float* d_enc_level_max, uint32_t* d_enc_jac, void* stream);
 /* Early ray termination (the training step on a trained field): the sigma MLP forward of samples [lo, hi) of
- * each ray (multiples of 64) into lnr_field_train's workspace, where lnr_field_train with LNR_LP_SIGMA_READY
- * reads it; rays with alive[r] == 0 (read when lo > 0) get sigma 0 there and no encoding is read.  When
- * hi < n_samples it also updates, per ray, transmittance[r] (fp64; = 1 before lo == 0) by the product over the
- * phase of s = 1 - alpha + 1e-10 (the compositing's own arithmetic: noise, deltas as lnr_field_train draws
- * them; key, noise_std, noise, ray_offset, lp->dev_step as there) and alive[r] = transmittance[r] >= 1e-50.
- * A ray whose product fell below 1e-50 has every later sample's float transmittance exactly 0 in the
- * compositing, so its later samples' sigma and encodings cannot change any output: the phases
- * lnr_hashgrid_fwd_rays_phase -> lnr_field_sigma_phase, phase by phase, then lnr_field_train with
- * LNR_LP_SIGMA_READY, give the step's results without evaluating them (csrc/field.hip, kErtTMin).
+ * the rays list_in[0 .. *count_in) (DEVICE; ignored when lo == 0: every ray) (multiples of 64) into
+ * lnr_field_train's workspace, where lnr_field_train with LNR_LP_SIGMA_READY reads it.  When hi < n_samples it
+ * then takes each listed ray's transmittance[r] (fp64; 1 before lo == 0) times the
+ * product over the phase of s = 1 - alpha + 1e-10 (the compositing's own arithmetic: noise, deltas as
+ * lnr_field_train draws them; key, noise_std, noise, ray_offset, lp->dev_step as there), and lists the rays whose
+ * product stays >= LNR_ERT_T_MIN in list_out[0 .. *count_out) in list order (through `scratch`, at least
+ * n_rays 32-bit words); the others get sigma 0 at their samples [hi, n_samples).  A ray whose product fell below
+ * 1e-50 has every later
+ * sample's float transmittance exactly 0 in the compositing, so its later samples' sigma and encodings cannot
+ * change any output: the phases lnr_hashgrid_fwd_rays_phase -> lnr_field_sigma_phase, phase by phase (the lists
+ * alternating between two buffers), then lnr_field_train with LNR_LP_SIGMA_READY, give the step's results without
+ * evaluating them (csrc/field.hip).
  * lp: optional (dev_status: LNR_STATUS_SIGMA_CLIPPED for the evaluated samples; dev_step: the key). */
 int lnr_field_sigma_phase(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, const float* rays,
                           const float* z, int64_t n_rays, int32_t n_samples, int32_t lo, int32_t hi, float noise_std,
                           const float* noise, uint32_t key, int64_t ray_offset, const lnr_loss_params* lp,
-                          float* workspace, uint8_t* alive, double* transmittance, void* stream);
+                          float* workspace, const uint32_t* list_in, const uint32_t* count_in, uint32_t* list_out,
+                          uint32_t* count_out, double* transmittance, void* scratch, void* stream);
 /* Joint pose + map (optimizer.py:235-262): the per-keyframe gradient of the pose tensors [t, axis-angle] (K, 6)
  * from a step's per-sample dL/dpos01 d_pos (n_rays * n_samples, 3) (lnr_hashgrid_bwd_rays_jac) and per-ray
  * [dL/d|d|, dL/dfar] d_ray (n_rays, 2) (lnr_loss_params.dev_d_ray), for rays built as

@@ -160,7 +160,7 @@ _SIGNATURES = {
                                        ctypes.POINTER(LossParams), c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
                                        c_p]),
     "lnr_field_sigma_phase": (ctypes.c_int, [c_p, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_i32, c_i32, c_f, c_p, c_u32,
-                                             c_i64, ctypes.POINTER(LossParams), c_p, c_p, c_p, c_p]),
+                                             c_i64, ctypes.POINTER(LossParams), c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "lnr_pose_grad": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_p, c_p, c_i32, c_f, c_f, c_p,
                                      c_p, c_p]),
     "lnr_pose_adam": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i32, c_i64, c_f, c_f, c_f, c_f, c_p, c_p]),
@@ -168,7 +168,7 @@ _SIGNATURES = {
                                         c_p, c_p, c_p, c_p]),
     "lnr_rgb_render": (ctypes.c_int, [c_p, c_i32, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_p, c_p]),
     "lnr_hashgrid_fwd_rays_phase": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_p, c_i64,
-                                                   c_p, c_i64, c_p, c_i32, c_i32, c_p]),
+                                                   c_p, c_i64, c_p, c_p, c_i64, c_i32, c_i32, c_p]),
     "lnr_hashgrid_fwd_rays_live": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_i64,
                                                   c_p]),
     "lnr_hashgrid_fwd_rays_live_ws": (ctypes.c_int, [ctypes.POINTER(GridDesc), c_p, c_p, c_i64, c_i32, c_p, c_p, c_p,

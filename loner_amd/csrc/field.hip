@@ -846,38 +846,40 @@ __global__ void __launch_bounds__(NT) k_sigma_fwd_tiles(FieldArgs a) {
 // its sigma, so it contributes nothing to the render, the loss or any gradient (dL/dalpha = T (G - X) = 0), and its
 // sigma need not be evaluated -- nor its encoding gathered.  The step evaluates a ray in phases of samples [lo, hi):
 // after each phase the ray's product of s = 1 - alpha + 1e-10 over its samples so far (the compositing's own
-// per-sample float arithmetic, in double); a ray whose product fell below kErtTMin skips the later phases (its
-// sigma there is 0, so alpha stays finite and its T stays 0: s <= 1).  The compositing's double products
-// associate differently but agree to ~1e-13 relative, so every later sample's float T is 0 there too.  The
-// margin (1e-50 against float's 7e-46) also keeps the later samples' alpha, which still enters the suffix sums
-// X of the samples before them through factors below 1e-50 / T, out of every float result in practice
-// (tests/test_gpu_live.py: bitwise the step without termination).
+// per-sample float arithmetic, in double); a ray whose product fell below kErtTMin skips the later phases, and its
+// later samples' sigma is set to 0 where it falls (the compositing reads it), so alpha there stays finite and T
+// stays 0 (s <= 1); the composite kernel itself carries no test for it (a per-sample select there cost 11 us at C4).  The compositing's double products associate differently but agree to ~1e-13 relative, so
+// every later sample's float T is 0 there too.  The margin (1e-50 against float's 1.4e-45) also keeps the later
+// samples' alpha, which still enters the suffix sums X of the samples before them through factors below 1e-50 / T,
+// out of every float result in practice (tests/test_gpu_live.py: bitwise the step without termination).
 constexpr double kErtTMin = LNR_ERT_T_MIN;
 
-// One wave per ray: the sigma of its samples [lo, hi) (64-sample units, 4 MFMA tiles each) and, when
-// hi < S, its transmittance product over them: T <- T * prod s (T = 1 before the first phase), alive = T >= t_min.
-// sigma_tile_fwd leaves sample 16 t + c's sigma in every lane c + 16 g, so lane l finds its own sample's in
-// tile t = l / 16.  A terminated ray (alive 0, lo > 0) gets sigma 0 and reads no encoding.
-__global__ void __launch_bounds__(NT) k_sigma_phase(FieldArgs a, uint8_t* __restrict__ alive,
-                                                    double* __restrict__ trans, int32_t lo, int32_t hi,
+// The sigma of one phase, one wave per listed ray (list null: every ray; grid-stride, a block past the list leaves
+// at once), its 64-sample units in order.  When hi < S the wave also takes the ray's transmittance times the product
+// of s over the phase (per lane over its units, then across the lanes; every lane holds the product), and a ray
+// that falls below t_min gets sigma 0 at its samples [hi, S) (the compositing's input); keep[e] = r for a surviving
+// ray, ~0 for the others (k_ert_compact lists them).  sigma_tile_fwd leaves sample 16 t + c's sigma in every lane c + 16 g, so lane l finds its own sample's in
+// tile t = l / 16.
+__global__ void __launch_bounds__(NT) k_sigma_phase(FieldArgs a, const uint32_t* __restrict__ list,
+                                                    const uint32_t* __restrict__ count, int32_t lo, int32_t hi,
+                                                    double* __restrict__ trans, uint32_t* __restrict__ keep,
                                                     double t_min) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   const int S = a.S;
   const bool upd = hi < S;
+  const int64_t n_e = list ? (int64_t)count[0] : a.n_rays;
+  if ((int64_t)blockIdx.x * kWavesPerBlock >= n_e) return;  // (block-uniform) past the listed rays
   SigmaWeights sw;
   load_sigma_weights(a.w, sw);
-  for (int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + wid; r < a.n_rays; r += (int64_t)gridDim.x * kWavesPerBlock) {
-    if (lo > 0 && alive[r] == 0) {  // (wave-uniform) terminated: sigma 0, no encoding read
-      for (int i = lo + lane; i < hi; i += 64) a.d_sigma[r * S + i] = 0.f;
-      continue;
-    }
+  bool clipped = false;
+  for (int64_t e = (int64_t)blockIdx.x * kWavesPerBlock + wid; e < n_e; e += (int64_t)gridDim.x * kWavesPerBlock) {
+    const int64_t r = list ? (int64_t)list[e] : e;
     const float* ry = a.rays + 13 * r;
     const float dx = ry[3], dy = ry[4], dz = ry[5];
     const float dnorm = sqrtf(dx * dx + dy * dy + dz * dz);
     const float* zr = a.z + r * S;
     const uint32_t gr = (uint32_t)(a.ray_offset + r);
     double P = 1.0;
-    bool clipped = false;
     for (int u0 = lo; u0 < hi; u0 += kSigmaFwdUnit) {
       const int64_t n0 = r * S + u0;
       half8_t b[4];
@@ -906,17 +908,64 @@ __global__ void __launch_bounds__(NT) k_sigma_phase(FieldArgs a, uint8_t* __rest
         P *= (double)((1.0f - alpha) + 1e-10f);
       }
     }
-    if (a.lp.dev_status && __any(clipped) && lane == 0) atomicOr(a.lp.dev_status, LNR_STATUS_SIGMA_CLIPPED);
     if (upd) {
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) P *= __shfl_xor(P, o, 64);
+      const double t = (lo == 0 ? 1.0 : trans[r]) * P;  // (every lane: the butterfly left P in all of them)
+      const bool al = t >= t_min;
       if (lane == 0) {
-        const double t = (lo == 0 ? 1.0 : trans[r]) * P;
         trans[r] = t;
-        alive[r] = t >= t_min ? 1 : 0;
+        keep[e] = al ? (uint32_t)r : ~0u;
       }
+      if (!al)  // (wave-uniform) terminated here: sigma 0 for the samples no later phase evaluates
+        for (int i = hi + lane; i < S; i += 64) a.d_sigma[r * S + i] = 0.f;
     }
   }
+  if (a.lp.dev_status && __any(clipped) && lane == 0) atomicOr(a.lp.dev_status, LNR_STATUS_SIGMA_CLIPPED);
+}
+
+// The surviving rays of a phase listed in list order: keep[e] (k_sigma_phase) != ~0 over the phase's entries, one
+// workgroup, 8 consecutive entries per thread (every load first), a block-wide exclusive scan per 8192 entries.
+constexpr int kErtCompactThreads = 1024, kErtCompactPer = 8;
+__global__ void __launch_bounds__(kErtCompactThreads) k_ert_compact(const uint32_t* __restrict__ keep,
+                                                                     const uint32_t* __restrict__ count_in, int64_t n_rays,
+                                                                     uint32_t* __restrict__ list_out,
+                                                                     uint32_t* __restrict__ count_out) {
+  __shared__ uint32_t wsum[kErtCompactThreads / 64];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int64_t n_e = count_in ? (int64_t)count_in[0] : n_rays;
+  uint32_t base = 0;
+  for (int64_t c0 = 0; c0 < n_e; c0 += (int64_t)kErtCompactThreads * kErtCompactPer) {
+    uint32_t r[kErtCompactPer];
+    uint32_t mine = 0;
+#pragma unroll
+    for (int j = 0; j < kErtCompactPer; ++j) {
+      const int64_t e = c0 + (int64_t)t * kErtCompactPer + j;
+      r[j] = e < n_e ? keep[e] : ~0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kErtCompactPer; ++j) mine += r[j] != ~0u ? 1u : 0u;
+    uint32_t inc = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += v;
+    }
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    uint32_t off = base + inc - mine, tot = 0;
+    for (int w = 0; w < kErtCompactThreads / 64; ++w) {
+      const uint32_t v = wsum[w];
+      if (w < wid) off += v;
+      tot += v;
+    }
+#pragma unroll
+    for (int j = 0; j < kErtCompactPer; ++j)
+      if (r[j] != ~0u) list_out[off++] = r[j];
+    base += tot;
+    __syncthreads();  // wsum is rewritten by the next chunk
+  }
+  if (t == 0) count_out[0] = base;
 }
 
 // Phase 1b, one wave per ray: compositing -> loss -> compositing backward on the sigma of phase 1a,
@@ -929,6 +978,7 @@ __global__ void __launch_bounds__(NT) k_composite_wave(FieldArgs a) {
   constexpr int S = 64 * C;  // == a.S (checked at launch)
   float* sig = reinterpret_cast<float*>(smem) + wid * S;
   for (int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + wid; r < a.n_rays; r += (int64_t)gridDim.x * kWavesPerBlock) {
+    // (early ray termination: the samples from term[r] on were not evaluated, their sigma is 0)
 #pragma unroll
     for (int k = 0; k < C; ++k) sig[64 * k + lane] = a.d_sigma[r * S + 64 * k + lane];  // coalesced
     wave_lds_handoff();
@@ -1664,26 +1714,34 @@ extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t e
 extern "C" int lnr_field_sigma_phase(const uint16_t* w, const uint32_t* enc, int64_t enc_stride, const float* rays,
                                      const float* z, int64_t n_rays, int32_t n_samples, int32_t lo, int32_t hi,
                                      float noise_std, const float* noise, uint32_t key, int64_t ray_offset,
-                                     const lnr_loss_params* lp, float* workspace, uint8_t* alive,
-                                     double* transmittance, void* stream) {
+                                     const lnr_loss_params* lp, float* workspace, const uint32_t* list_in,
+                                     const uint32_t* count_in, uint32_t* list_out, uint32_t* count_out,
+                                     double* transmittance, void* scratch, void* stream) {
   if (int e = check_rays(rays, z, n_rays, n_samples, "lnr_field_sigma_phase")) return e;
   LNR_REQUIRE(n_samples % 64 == 0 && lo >= 0 && lo < hi && hi <= n_samples && lo % 64 == 0 && hi % 64 == 0,
               "lnr_field_sigma_phase: phase [%d, %d) of %d samples must be whole 64-sample waves", lo, hi, n_samples);
   LNR_REQUIRE(enc_stride >= n_rays * (int64_t)n_samples && enc_stride < (int64_t(1) << 26),
               "lnr_field_sigma_phase: bad enc_stride");
+  LNR_REQUIRE(n_rays < (int64_t(1) << 31), "lnr_field_sigma_phase: too many rays");
   if (n_rays == 0) return LNR_OK;
-  LNR_REQUIRE(w && enc && workspace && (hi == n_samples || (alive && transmittance)) && (lo == 0 || alive),
-              "lnr_field_sigma_phase: null pointer");
+  LNR_REQUIRE(w && enc && workspace && (lo == 0 || (list_in && count_in)) && (!list_in || count_in),
+              "lnr_field_sigma_phase: null pointer (a phase after the first needs the list of rays still alive)");
+  LNR_REQUIRE(hi == n_samples || (list_out && count_out && transmittance && scratch),
+              "lnr_field_sigma_phase: null pointer (the phase's transmittance update)");
   FieldArgs a{};
   a.w = w; a.enc = enc; a.enc_stride = enc_stride; a.rays = rays; a.z = z; a.n_rays = n_rays; a.S = n_samples;
   a.noise_std = noise_std; a.noise = noise; a.key = key; a.ray_offset = ray_offset;
   if (lp) a.lp = *lp;
   a.d_sigma = workspace + lnr_dw_workspace_words(n_rays);
   hipStream_t st = as_stream(stream);
-  const double t_min = kErtTMin;
+  const uint32_t* lin = lo == 0 ? nullptr : list_in;
+  const uint32_t* cin = lo == 0 ? nullptr : count_in;
+  uint32_t* keep = reinterpret_cast<uint32_t*>(scratch);  // one word per entry
   const int64_t want = (n_rays + kWavesPerBlock - 1) / kWavesPerBlock;
-  hipLaunchKernelGGL(k_sigma_phase, dim3((int)(want < 8192 ? want : 8192)), dim3(NT), 0, st, a, alive, transmittance, lo,
-                     hi, t_min);
+  hipLaunchKernelGGL(k_sigma_phase, dim3((unsigned)(want < 8192 ? want : 8192)), dim3(NT), 0, st, a, lin, cin, lo, hi,
+                     transmittance, keep, kErtTMin);
+  if (hi < n_samples)
+    hipLaunchKernelGGL(k_ert_compact, dim3(1), dim3(kErtCompactThreads), 0, st, keep, cin, n_rays, list_out, count_out);
   LNR_RETURN_LAUNCH("lnr_field_sigma_phase");
 }
 

@@ -117,55 +117,71 @@ inline int enc_levels_per_group(const lnr_grid_desc* d, int64_t n_sb) {
       return g;
   return 1;
 }
-// Early ray termination (lnr_hashgrid_fwd_rays_phase): the encode of samples [lo, hi) of each ray, for the
-// rays still ``alive`` (per-ray bytes, or every ray).  With the record histogram (the first phase, for a full
-// backward, which places every sample's records) the grid is the plain one, every sample's records are counted
-// and only the phase's samples gather; without it (the live backward counts its own) the grid covers just the
-// phase's samples
-// (``compact``: workgroup sample g -> ray g / (hi - lo), ray sample lo + g % (hi - lo); a wave stays
-// within one ray, as lo and hi are multiples of 64).
+// Early ray termination (lnr_hashgrid_fwd_rays_phase): the encode of samples [lo, hi) of the listed rays (the
+// rays still alive, ascending; every ray in the first phase).  With the record histogram (the first phase, for a
+// full backward, which places every sample's records) the grid is the plain one, every sample's records are
+// counted and only the phase's samples gather; without it (the live backward counts its own) the grid covers the
+// phase's samples of the listed rays (``compact``: workgroup sample g -> ray list[g / (hi - lo)], ray sample
+// lo + g % (hi - lo); a wave stays within one ray, as lo and hi are multiples of 64), sized for every ray, and its
+// samples past the list's end (count x width) leave at once.
 struct EncPhase {
-  const uint8_t* alive;  // per ray; null: every ray
-  int32_t lo, hi;        // ray-local sample range; hi == 0: no phase (every sample)
-  int32_t S;             // samples per ray
+  const uint32_t* list;   // the rays of the phase (compact only); null: every ray
+  const uint32_t* count;  // DEVICE: how many
+  int32_t lo, hi;         // ray-local sample range; hi == 0: no phase (every sample)
+  int32_t S;              // samples per ray
   bool compact;
   __device__ __forceinline__ bool on() const { return hi > 0; }
+  template <bool LISTED>
   __device__ __forceinline__ int64_t sample(int64_t g) const {
     if (!compact) return g;
-    const int32_t w = hi - lo;
-    return (g / w) * S + lo + g % w;
+    if constexpr (LISTED) {
+      const uint32_t w = (uint32_t)(hi - lo), e = (uint32_t)g / w;
+      return (int64_t)list[e] * S + lo + ((uint32_t)g - e * w);
+    } else {
+      const int32_t w = hi - lo;
+      return (g / w) * S + lo + g % w;
+    }
   }
 };
 
+// Early ray termination's sparse phases: fewer expected rows than this take the one-level row-walking grid
+#ifndef LNR_ENC_SPARSE_ROWS
+#define LNR_ENC_SPARSE_ROWS 512
+#endif
+constexpr int64_t kEncSparseRows = LNR_ENC_SPARSE_ROWS;
+#ifndef LNR_ENC_SPARSE_LPB
+#define LNR_ENC_SPARSE_LPB 2  // levels per workgroup of a sparse phase's row-walking grid (C2: 4 and 1 within
+                              // the noise, 4 spills two VGPRs in the loop; tools/gpu_ab_libs.sh, three rounds)
+#endif
 #ifndef LNR_ENC_WAVES
 #define LNR_ENC_WAVES 8  // waves per SIMD asked of the encode (68 registers would allow 7)
 #endif
-template <class PosFn, int kEncSpt, bool PAIRED, int LPB = 1>
-__global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per_eu(LNR_ENC_WAVES, LNR_ENC_WAVES))) k_hashgrid_fwd(GridArgs a, PosFn pos, int64_t n,
-                                                               const uint32_t* __restrict__ table,
-                                                               uint32_t* __restrict__ enc, int64_t stride,
-                                                               BwdWorkspace ws, const float* __restrict__ live,
-                                                               EncPhase ph) {
+// One row (kSB samples) of the encode at the workgroup's levels (the body of k_hashgrid_fwd); false: this thread's
+// samples lie past the end (it has nothing more to do).
+template <class PosFn, int kEncSpt, bool PAIRED, int LPB, bool LISTED>
+__device__ __forceinline__ bool enc_row(const GridArgs& a, PosFn pos, int64_t n, const uint32_t* __restrict__ table,
+                                        uint32_t* __restrict__ enc, int64_t stride, const BwdWorkspace& ws,
+                                        const float* __restrict__ live, const EncPhase& ph, int64_t row) {
   constexpr int H = kSB / kEncSpt;
-  const int64_t g0 = (int64_t)blockIdx.x * kSB + threadIdx.x;  // (the compact phase grid: g0 < n counts its samples)
-  const int64_t i0 = ph.sample(g0);
+  const int64_t g0 = row * kSB + threadIdx.x;  // (the compact phase grid: g0 < n counts its samples)
   const bool count = ws.hist != nullptr;
-  if (!count && (g0 & ~(int64_t)1) >= n) return;  // (lane pairs leave together: fine_gather_paired)
+  const int64_t n_in = ph.compact ? (int64_t)(n / (ph.hi - ph.lo)) * ph.S : n;  // pos.wave's bound (every ray)
+  if constexpr (LISTED) n = (int64_t)ph.count[0] * (ph.hi - ph.lo);  // the listed rays' samples
+  if (!count && (g0 & ~(int64_t)1) >= n) return false;  // (lane pairs leave together: fine_gather_paired)
   __shared__ uint32_t hist[kMaxChunksPerLevel];
   bool in[kEncSpt], use[kEncSpt], cnt[kEncSpt];
   float x[kEncSpt], y[kEncSpt], z[kEncSpt];
-  const int64_t n_in = ph.compact ? (int64_t)(n / (ph.hi - ph.lo)) * ph.S : n;  // pos.wave's bound
 #pragma unroll
   for (int h = 0; h < kEncSpt; ++h) {
-    const int64_t i = ph.sample(g0 + h * H);
+    const int64_t i = ph.template sample<LISTED>(g0 + h * H);
     in[h] = (g0 + h * H) < n;
     // live: samples whose weight is exactly 0 get a zero encoding and issue no gathers; when counting
     // too, they emit no records at the fine levels (the scatter skips them by the same mask)
     use[h] = in[h] && (live == nullptr || live[i] != 0.f);
     cnt[h] = use[h];
-    if (ph.on()) {  // early ray termination: the phase's samples of the live rays gather, every sample counts
+    if (ph.on()) {  // early ray termination: the phase's samples of the listed rays gather, every sample counts
       const int32_t j = (int32_t)(i % ph.S);
-      use[h] = in[h] && j >= ph.lo && j < ph.hi && (ph.alive == nullptr || ph.alive[i / ph.S] != 0);
+      use[h] = in[h] && j >= ph.lo && j < ph.hi;
       cnt[h] = in[h];
     }
     x[h] = y[h] = z[h] = 0.f;
@@ -175,7 +191,7 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
     bool any = false;
 #pragma unroll
     for (int h = 0; h < kEncSpt; ++h) any |= use[h];
-    if (!__any(any)) return;  // a terminated ray's wave (no histogram: no barriers to keep)
+    if (!__any(any)) return true;  // a terminated ray's wave (no histogram: no barriers to keep)
   }
   // dead samples (live, use = false) get a zero encoding only where their aligned 16-sample tile holds a live
   // sample: the colour kernels skip a tile whose weights are all 0 and read every encoding of the others
@@ -212,7 +228,7 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
     }
 #pragma unroll
     for (int h = 0; h < kEncSpt; ++h) {
-      uint32_t* dst = enc + (int64_t)l * stride + ph.sample(g0 + h * H);
+      uint32_t* dst = enc + (int64_t)l * stride + ph.template sample<LISTED>(g0 + h * H);
       if (use[h]) {
         float f0 = 0.f, f1 = 0.f;
 #pragma unroll
@@ -243,7 +259,7 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
   for (int h = 0; h < kEncSpt; ++h) {
     Corners c;
     level_corners(lv, x[h], y[h], z[h], c);
-    uint32_t* dst = enc + (int64_t)l * stride + ph.sample(g0 + h * H);
+    uint32_t* dst = enc + (int64_t)l * stride + ph.template sample<LISTED>(g0 + h * H);
     if (use[h]) {
       uint32_t v[8];
 #pragma unroll
@@ -268,6 +284,25 @@ __global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per
     lds_barrier();
     publish_block_counts(a, l, hist, ws);
   }
+  }
+  return true;
+}
+
+// The training / eval encode (see above); LOOP (early ray termination's later phases over a list of rays): a grid
+// smaller than the rows walks them, a workgroup taking rows blockIdx.x, + gridDim.x, ... until past the list's end.
+template <class PosFn, int kEncSpt, bool PAIRED, int LPB = 1, bool LISTED = false, bool LOOP = false>
+__global__ void __launch_bounds__(kSB / kEncSpt) __attribute__((amdgpu_waves_per_eu(LNR_ENC_WAVES, LNR_ENC_WAVES))) k_hashgrid_fwd(GridArgs a, PosFn pos, int64_t n,
+                                                               const uint32_t* __restrict__ table,
+                                                               uint32_t* __restrict__ enc, int64_t stride,
+                                                               BwdWorkspace ws, const float* __restrict__ live,
+                                                               EncPhase ph) {
+  if constexpr (!LOOP) {
+    enc_row<PosFn, kEncSpt, PAIRED, LPB, LISTED>(a, pos, n, table, enc, stride, ws, live, ph, blockIdx.x);
+  } else {
+    for (int64_t row = blockIdx.x;
+         enc_row<PosFn, kEncSpt, PAIRED, LPB, LISTED>(a, pos, n, table, enc, stride, ws, live, ph, row);
+         row += gridDim.x) {
+    }
   }
 }
 
@@ -396,7 +431,8 @@ static int live_lpb() {
 template <class PosFn>
 static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16_t* table, uint32_t* enc,
                       int64_t enc_stride, void* bwd_ws, int64_t bwd_ws_bytes, hipStream_t st, const char* who,
-                      const float* live = nullptr, EncPhase ph = EncPhase{nullptr, 0, 0, 1, false}) {
+                      const float* live = nullptr, EncPhase ph = EncPhase{nullptr, nullptr, 0, 0, 1, false},
+                      int64_t expect_rays = 0) {
   GridArgs a = make_args(d, pos.samples_per_ray());
   LNR_REQUIRE(n < (int64_t(1) << 31), "%s: n=%lld samples exceeds 2^31", who, (long long)n);
   // training and plain eval launches: one sample per thread, lane-paired fine gathers; the eval launch
@@ -423,14 +459,36 @@ static int launch_fwd(const lnr_grid_desc* d, PosFn pos, int64_t n, const uint16
   const unsigned rows = (unsigned)((n + kSB - 1) / kSB);
   const uint32_t* tb = reinterpret_cast<const uint32_t*>(table);
   const dim3 grid(rows, d->n_levels);
-  if (ph.compact) {  // a later phase of early ray termination: the grid covers the phase's samples only
+  if (ph.compact) {  // a phase of early ray termination: the grid covers the phase's samples only
     const int64_t ng = (n / ph.S) * (ph.hi - ph.lo);
     const unsigned rows_c = (unsigned)((ng + kSB - 1) / kSB);
     const int lpb_c = enc_levels_per_group(d, rows_c);
+    const unsigned groups = d->n_levels / lpb_c;
+    const int64_t exp_rows = (expect_rays * (ph.hi - ph.lo) + kSB - 1) / kSB;
+    if (ph.list && expect_rays > 0 && exp_rows < kEncSparseRows) {
+      // a sparse phase (few rays still alive, by the caller's estimate): latency-bound, its rows fit in one round of
+      // resident workgroups, so a grid of about the expected rows (x 1.25) walks the listed rows, LNR_ENC_SPARSE_LPB
+      // levels per workgroup (a grid sized for every ray launches workgroups only to leave)
+      const unsigned gx = (unsigned)std::min<int64_t>(rows_c, exp_rows + exp_rows / 4 + 8);
+      const int lpb_s = d->n_levels % LNR_ENC_SPARSE_LPB == 0 ? LNR_ENC_SPARSE_LPB : 1;
+      auto k = lpb_s == LNR_ENC_SPARSE_LPB ? k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, LNR_ENC_SPARSE_LPB, true, true>
+                                           : k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 1, true, true>;
+      hipLaunchKernelGGL(k, dim3(gx, d->n_levels / lpb_s), dim3(kSB), 0, st, a, pos, ng, tb, enc, enc_stride,
+                         BwdWorkspace{}, nullptr, ph);
+      LNR_RETURN_LAUNCH(who);
+    }
+    if (ph.list) {
+      auto k = lpb_c == 4 ? k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 4, true>
+             : lpb_c == 2 ? k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 2, true>
+                          : k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 1, true>;
+      hipLaunchKernelGGL(k, dim3(rows_c, groups), dim3(kSB), 0, st, a, pos, ng, tb, enc, enc_stride,
+                         BwdWorkspace{}, nullptr, ph);
+      LNR_RETURN_LAUNCH(who);
+    }
     auto k = lpb_c == 4 ? k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 4>
            : lpb_c == 2 ? k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 2>
                         : k_hashgrid_fwd<PosFn, 1, LNR_ENC_PAIRED, 1>;
-    hipLaunchKernelGGL(k, dim3(rows_c, d->n_levels / lpb_c), dim3(kSB), 0, st, a, pos, ng, tb, enc, enc_stride,
+    hipLaunchKernelGGL(k, dim3(rows_c, groups), dim3(kSB), 0, st, a, pos, ng, tb, enc, enc_stride,
                        BwdWorkspace{}, nullptr, ph);
     LNR_RETURN_LAUNCH(who);
   }
@@ -475,20 +533,23 @@ extern "C" int lnr_hashgrid_fwd_rays(const lnr_grid_desc* d, const float* rays, 
 
 extern "C" int lnr_hashgrid_fwd_rays_phase(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,
                                            int32_t n_samples, const uint16_t* table, uint32_t* enc, int64_t enc_stride,
-                                           void* bwd_ws, int64_t bwd_ws_bytes, const uint8_t* alive, int32_t lo,
-                                           int32_t hi, void* stream) {
+                                           void* bwd_ws, int64_t bwd_ws_bytes, const uint32_t* ray_list,
+                                           const uint32_t* ray_count, int64_t expect_rays, int32_t lo, int32_t hi,
+                                           void* stream) {
   if (int e = check_desc(d, "lnr_hashgrid_fwd_rays_phase")) return e;
   const int64_t n = n_rays * (int64_t)n_samples;
   LNR_REQUIRE(n_rays >= 0 && n_samples > 0 && enc_stride >= n, "lnr_hashgrid_fwd_rays_phase: bad sizes");
   LNR_REQUIRE(n_samples % 64 == 0 && lo >= 0 && lo < hi && hi <= n_samples && lo % 64 == 0 && hi % 64 == 0,
               "lnr_hashgrid_fwd_rays_phase: phase [%d, %d) of %d samples must be whole 64-sample waves", lo, hi,
               n_samples);
-  LNR_REQUIRE(bwd_ws == nullptr || lo == 0, "lnr_hashgrid_fwd_rays_phase: the record histogram comes with the first phase");
+  LNR_REQUIRE(bwd_ws == nullptr || (lo == 0 && ray_list == nullptr),
+              "lnr_hashgrid_fwd_rays_phase: the record histogram comes with the first phase, over every ray");
+  LNR_REQUIRE(ray_list == nullptr || ray_count != nullptr, "lnr_hashgrid_fwd_rays_phase: a ray list needs its count");
   if (n == 0) return LNR_OK;
   LNR_REQUIRE(rays && z && table && enc, "lnr_hashgrid_fwd_rays_phase: null pointer");
-  const EncPhase ph{alive, lo, hi, n_samples, bwd_ws == nullptr};
+  const EncPhase ph{ray_list, ray_count, lo, hi, n_samples, bwd_ws == nullptr};
   return launch_fwd(d, PosFromRays{rays, z, n_samples}, n, table, enc, enc_stride, bwd_ws, bwd_ws_bytes,
-                    as_stream(stream), "lnr_hashgrid_fwd_rays_phase", nullptr, ph);
+                    as_stream(stream), "lnr_hashgrid_fwd_rays_phase", nullptr, ph, expect_rays);
 }
 
 extern "C" int lnr_hashgrid_fwd_rays_live(const lnr_grid_desc* d, const float* rays, const float* z, int64_t n_rays,

@@ -186,11 +186,10 @@ AR_CUT_DEFAULT = 6
 AR_CUT_TWO_GROUPS = 8
 
 # Early ray termination's cost model (us; csrc/field.hip, lnr_hashgrid_fwd_rays_phase + lnr_field_sigma_phase),
-# fitted to round 6's kernel traces of the trained C2 and C4 steps: the encode + sigma of
-# one ray-sample ERT_SAMPLE_NS, phased or not; going phased ERT_FIXED_US (the first phase's record histogram over
-# the samples it does not encode, four sigma launches' weight loads); every phase after the first ERT_PHASE_US
-# (one encode and one sigma launch with their tails)
-ERT_SAMPLE_NS, ERT_FIXED_US, ERT_PHASE_US = 0.157, 35.0, 23.0
+# fitted to round 6's kernel traces of the trained C2 step: the encode + sigma of one
+# ray-sample ERT_SAMPLE_NS, phased or not; going phased ERT_FIXED_US; every phase after the first ERT_PHASE_US (its
+# encode, sigma and list launches, latency-bound when few rays are left)
+ERT_SAMPLE_NS, ERT_FIXED_US, ERT_PHASE_US = 0.150, 5.0, 28.0
 TERM_HIST_SLOTS = 256  # LNR_TERM_HIST_SLOTS
 ERT_MAX_CUTS = 4
 ERT_MARGIN = 0.02  # a plan replaces the current one only when it is modelled this much faster (of the full encode)
@@ -429,12 +428,18 @@ class StepEngine:
         # none); 1: always, at the fixed cuts LONER_ERT_CUTS (fractions of n_samples, default 0.5,0.625,0.75); 0: never.
         self.ert = {"0": False, "1": True}.get(os.environ.get("LONER_ERT", "auto"), "auto")
         self.ert_cuts = [float(v) for v in os.environ.get("LONER_ERT_CUTS", "0.5,0.625,0.75").split(",") if v.strip()]
-        self.ert_alive = torch.ones(n_rays, dtype=torch.uint8, device=dev)
+        # the phases' device state: the lists of rays still alive (two buffers, alternating), their counts, the
+        # transmittance products and a scratch word per ray
+        self.ert_lists = torch.zeros(2, max(n_rays, 1), dtype=torch.int32, device=dev)
+        self.ert_counts = torch.zeros(2, dtype=torch.int32, device=dev)
         self.ert_T = torch.ones(n_rays, dtype=torch.float64, device=dev)
+        self.ert_keep = torch.zeros(max(n_rays, 1), dtype=torch.int32, device=dev)
+        self._ert_est = None  # auto: the plan's alive shares after each 64-sample boundary (the encode's grid hints)
+        self._ert_last = None  # the phases of the last step (tests, tools)
         self._ert_plan = None  # auto: the phases in use, [0, c1, .., S], or None
         nb = self.S // 64 + 1
         self.term_hist = (torch.zeros(TERM_HIST_SLOTS, nb, dtype=torch.int32, device=dev) if self.S % 64 == 0
-                          else None)  # (slots spread the compositing's atomics; term_counts() sums them)
+                          else None)  # (slots spread the compositing's atomics; ert_probe sums them)
         pin = torch.cuda.is_available() and self.term_hist is not None
         self._term_host = torch.zeros(TERM_HIST_SLOTS, nb, dtype=torch.int32).pin_memory() if pin else None
         self._term_prev = [0] * (self.S // 64 + 1)
@@ -458,6 +463,14 @@ class StepEngine:
         b = sorted({int(round(f * S / 64)) * 64 for f in self.ert_cuts if 0.0 < f < 1.0} - {0, S})
         return [0] + b + [S] if b else None
 
+    def ert_alive_last(self):
+        """The share of the last step's rays still alive after its last cut (early ray termination), or 1.0
+        without phases (a host sync: tests and tools)."""
+        b = self._ert_last
+        if b is None or len(b) < 3:
+            return 1.0
+        return int(self.ert_counts[(len(b) - 3) % 2].item()) / max(self._r_last, 1)
+
     def _ert_key(self):
         b = self.ert_bounds()
         return None if b is None else tuple(b)
@@ -475,7 +488,12 @@ class StepEngine:
             self._term_prev = cur
             self._term_ev = None
             if sum(d) > 0:
-                self._ert_plan = ert_plan(d, self.S, self._r_last * self.S, self._ert_plan)
+                plan = ert_plan(d, self.S, self._r_last * self.S, self._ert_plan)
+                if plan != self._ert_plan or self._ert_est is None:
+                    # the alive shares behind the encode's grid hints: refreshed with the plan only (the graphs,
+                    # captured per plan, hold the hints of their capture)
+                    self._ert_est = [float(v) for v in ert_alive(d, self.S)]
+                self._ert_plan = plan
         self._term_ctr += 1
         if self._term_ev is None and self._term_ctr >= self.live_probe_every:
             self._term_ctr = 0
@@ -635,19 +653,25 @@ class StepEngine:
         # counts its live records itself)
         fwd_hist = self.count_in_forward and not self._live
         ert = self.ert_bounds()
+        self._ert_last = ert
         if ert is not None:
             # early ray termination (see __init__): phase by phase, the encode and sigma of the rays still alive
+            # (the list phase q - 1 left; every ray in phase 0; a ray that terminates gets sigma 0 at its later samples)
             lp.flags |= L.LP_SIGMA_READY
             for q in range(len(ert) - 1):
                 lo, hi = ert[q], ert[q + 1]
                 hist = q == 0 and fwd_hist
+                lin = None if q == 0 else self.ert_lists[(q - 1) % 2]
+                cin = None if q == 0 else self.ert_counts[(q - 1) % 2:(q - 1) % 2 + 1]
+                est = self._ert_est
+                expect = 0 if (q == 0 or est is None) else int(est[lo // 64] * R) + 64
                 L.call("lnr_hashgrid_fwd_rays_phase", L.ctypes.byref(st.desc), rays, self.z, R, S, st.table_f16,
-                       self.enc, N, self.bwd_ws if hist else None, self.bwd_ws_bytes if hist else 0,
-                       self.ert_alive if q > 0 else None, lo, hi, s)
+                       self.enc, N, self.bwd_ws if hist else None, self.bwd_ws_bytes if hist else 0, lin, cin,
+                       expect, lo, hi, s)
                 m(prof, "sigma_phase")
                 L.call("lnr_field_sigma_phase", st.mlp_f16, self.enc, N, rays, self.z, R, S, lo, hi,
-                       cfg.raw_noise_std, noise, key, self.ray_offset, L.ctypes.byref(lp), self.ws, self.ert_alive,
-                       self.ert_T, s)
+                       cfg.raw_noise_std, noise, key, self.ray_offset, L.ctypes.byref(lp), self.ws, lin, cin,
+                       self.ert_lists[q % 2], self.ert_counts[q % 2:q % 2 + 1], self.ert_T, self.ert_keep, s)
                 m(prof, "sigma_phase")
         elif fwd_hist:
             L.call("lnr_hashgrid_fwd_rays", L.ctypes.byref(st.desc), rays, self.z, R, S, st.table_f16, self.enc, N,

@@ -82,7 +82,7 @@ def test_live_backward_bitwise_on_trained_field(trained, fused):
             torch.cuda.synchronize()
             recs.append(_records(L, eng))
             zero.append(float((eng.d_sigma() == 0).float().mean()))
-            alive.append(float(eng.ert_alive.float().mean()))
+            alive.append(eng.ert_alive_last())
         eng.finish()
         torch.cuda.synchronize()
         o = {k: getattr(st, k).clone() for k in ("params", "m", "v", "shadow", "occ")}

@@ -22,8 +22,8 @@ LIB = os.path.join(ROOT, "loner_amd", "_lib", "libloner_amd.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 ALLOWED = [
     r"^_ZN3lnr11k_bwd_accumILb[01]ELb1E",
-    r"^_ZN3lnr14k_hashgrid_fwdINS_12PosFromArrayELi2ELb0ELi1EE",
-    r"^_ZN3lnr14k_hashgrid_fwdINS_11PosFromRaysELi2ELb0ELi1EE",
+    r"^_ZN3lnr14k_hashgrid_fwdINS_12PosFromArrayELi2ELb0ELi1E(E|Lb0ELb0EE)",
+    r"^_ZN3lnr14k_hashgrid_fwdINS_11PosFromRaysELi2ELb0ELi1E(E|Lb0ELb0EE)",
 ]
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 

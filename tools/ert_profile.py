@@ -43,8 +43,8 @@ def main():
     rays, z = eng.rays[:n], eng.z
     s = L.stream(dev)
     lp = eng.loss_params(g, 0, window.scale, 0.0, n)
-    alive = torch.ones(n, dtype=torch.uint8, device=dev)
-    T = torch.ones(n, dtype=torch.float64, device=dev)
+    T, keep = eng.ert_T, eng.ert_keep
+    lists, counts = eng.ert_lists, eng.ert_counts
     sky = torch.zeros(n, dtype=torch.bool)
     off, nsel = window.ray_off_host, window.n_sel_host
     for k in range(window.n_kf):
@@ -52,16 +52,20 @@ def main():
     sky = sky[:n].to(dev)
     print(f"{name}: {n} rays ({int(sky.sum())} sky), {S} samples; cfg.raw_noise_std {cfg.raw_noise_std}")
     key = L.step_key(eng.seed, g)
-    for lo in range(0, S, 64):
+    for q, lo in enumerate(range(0, S, 64)):
         hi = lo + 64
+        lin = None if q == 0 else lists[(q - 1) % 2]
+        cin = None if q == 0 else counts[(q - 1) % 2:(q - 1) % 2 + 1]
         L.call("lnr_hashgrid_fwd_rays_phase", L.ctypes.byref(state.desc), rays, z, n, S, state.table_f16, eng.enc,
-               eng.N, None, 0, alive if lo > 0 else None, lo, hi, s)
+               eng.N, None, 0, lin, cin, 0, lo, hi, s)
         L.call("lnr_field_sigma_phase", state.mlp_f16, eng.enc, eng.N, rays, z, n, S, lo, hi, cfg.raw_noise_std, None,
-               key, eng.ray_offset, L.ctypes.byref(lp), eng.ws, alive, T, s)
+               key, eng.ray_offset, L.ctypes.byref(lp), eng.ws, lin, cin, lists[q % 2], counts[q % 2:q % 2 + 1], T,
+               keep, s)
         if hi < S:
             torch.cuda.synchronize()
-            a = alive.bool()
-            lt = T[~sky].clamp(min=1e-300).log10()
+            a = torch.zeros(n, dtype=torch.bool, device=dev)
+            a[lists[q % 2][:int(counts[q % 2].item())].long()] = True  # (the rays still alive)
+            lt = T[:n][~sky].clamp(min=1e-300).log10()
             print(f"  after sample {hi:4d}: alive {float(a.float().mean()):.3f}  lidar {float(a[~sky].float().mean()):.3f}"
                   f"  sky {float(a[sky].float().mean()) if bool(sky.any()) else float('nan'):.3f}   lidar log10 T"
                   f" median {float(lt.median()):8.1f} p90 {float(lt.quantile(0.9)):8.1f}", flush=True)

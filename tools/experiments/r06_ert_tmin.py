@@ -4,6 +4,9 @@ the share of rays still alive after each phase, the encode + field time, and whe
 step without termination (params, moments, shadow, occupancy, loss, depth over three steps).  GPU.
 
     python tools/experiments/r06_ert_tmin.py
+
+(Ran against the first early-ray-termination version, commit 7de94c3: per-ray alive bytes and the LONER_ERT_TMIN
+switch, both gone since; the phases now run over lists of the rays still alive)
 """
 import os
 import sys
