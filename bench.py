@@ -453,7 +453,10 @@ def bench_camera(args):
                               0.3 + 0.2 * np.sin((xx + yy) / 50.0)], -1).reshape(-1, 3).astype(np.float32))
     fr = C.CameraFrames(dirs, W, H, imgs, poses, syn.world_cube(kind), syn.SENSORS[kind]["ray_range"],
                         n_rays_per_kf=per_kf, seed=0, device=dev)
-    state = S_.FieldState(S_.StepConfig(n_samples=S), device=dev)
+    # the sigma field (frozen during the camera phase) in the LiDAR phase's configuration of this scene (C4's)
+    _, nkf4, rpk4, spk4, strat4, S4, preset4 = syn.CONFIGS["C4"]
+    state = S_.FieldState(S_.StepConfig(n_samples=S, occ_lr=1e-3 if preset4 == "haveri" else 1e-4,
+                                        loss=S_.LossConfig.from_dict(LOSS_PRESETS[preset4])), device=dev)
     color = C.ColorState(4, device=dev)
     R = n_kf * per_kf
     eng = C.CameraStepEngine(state, color, n_rays=R, n_samples=S, seed=0)
@@ -476,19 +479,45 @@ def bench_camera(args):
             mark("iteration")
         return n
 
-    for i in range(args.warmup):
-        run(i, False)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    n_tot = 0
-    for i in range(args.steps):
-        n_tot += run(args.warmup + i, False)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    for i in range(PROF_STEPS):  # whole-iteration events, untimed
-        run(args.warmup + args.steps + i, True)
-    # one extra profiled iteration split by stage (events between the engine's launches)
-    stage_ms = _camera_stages(eng, fr, rays, inten, L)
+    def measure():
+        for i in range(args.warmup):
+            run(i, False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n_tot = 0
+        for i in range(args.steps):
+            n_tot += run(args.warmup + i, False)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        for i in range(PROF_STEPS):  # whole-iteration events, untimed
+            run(args.warmup + args.steps + i, True)
+        # one extra profiled iteration split by stage (events between the engine's launches)
+        stage = _camera_stages(eng, fr, rays, inten, L)
+        live = float((eng.weights[:R * S] != 0).float().mean())
+        return elapsed, n_tot, stage, live
+
+    field = args.field or "trained"
+    from_init, pre = None, None
+    if field == "trained":
+        # the driver's camera phase runs on a sigma field its LiDAR phase has trained: most samples have weight 0
+        # there (free space, and everything behind the surface), which the colour kernels skip (zero-weight tiles,
+        # the live colour encode).  Timed first from init, then after the LiDAR phase's windows (bench.pretrain over
+        # the scene's trajectory, C4's shape), with a fresh colour head for the timed iterations.
+        elapsed, n_tot, stage_i, live_i = measure()
+        from_init = {"ms_per_step": elapsed / args.steps * 1e3, "value": n_tot * S / elapsed, "stage_ms": stage_i,
+                     "live_sample_frac": live_i}
+        R4 = nkf4 * (rpk4 + spk4)
+        leng = S_.StepEngine(state, R4, seed=12345)
+        t_pre = time.perf_counter()
+        _, pre = pretrain(leng, state, kind, nkf4, rpk4, spk4, strat4, dev, R4, 1, args.pretrain_windows,
+                          args.pretrain_iters)
+        pre["seconds"] = time.perf_counter() - t_pre
+        leng.release()
+        del leng
+        color = C.ColorState(4, device=dev)  # a fresh colour head (and its engine) for the timed iterations
+        eng = C.CameraStepEngine(state, color, n_rays=R, n_samples=S, seed=0)
+        torch.cuda.synchronize()
+    elapsed, n_tot, stage_ms, live_frac = measure()
     N = n_tot * S
     bwd_ms = stage_ms["rgb_train"]
     flop = 2 * 3 * (64 * 48 + 3 * 64 * 64 + 16 * 64) * R * S  # forward (x2: recomputed) + backward GEMMs
@@ -498,15 +527,22 @@ def bench_camera(args):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "fp16 params/activations, fp32 accumulate+optimizer",
             "data": "synthetic 1280x720 images resident in HBM, camera rays built on the GPU each iteration; "
-                    "random-init sigma field (frozen) and colour head",
+                    + ("sigma field (frozen) pre-trained untimed by the LiDAR phase's windows (config.field_state)"
+                       if field == "trained" else "random-init sigma field (frozen)") + ", random-init colour head",
             "config": {"workload": f"CAM: {n_kf} KF x {per_kf} camera rays x {S} samples, colour head SH4 + L=16 "
                                    f"T=2^19 + 48->64x4->3 MLP, L1 loss, Adam",
-                       "rays": R, "samples_per_ray": S, "parallelism": "single"},
+                       "rays": R, "samples_per_ray": S, "parallelism": "single",
+                       "field_state": ("trained: the sigma field after %d untimed LiDAR steps (config.pretrain)"
+                                       % pre["steps"] if field == "trained" else "from init"),
+                       **({"pretrain": pre} if pre is not None else {})},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / MFMA_PEAK_TFLOPS, "traffic": None,
                          "kernel": "lnr_rgb_train (colour forward x2 + L1 + MLP backward, MFMA fp16)",
                          "algorithmic_flop_per_launch": flop, "ms_per_launch": bwd_ms},
-            "stage_ms": stage_ms}
+            "stage_ms": stage_ms,
+            # the share of ray-samples with a non-zero compositing weight (the colour kernels' live samples)
+            "live_sample_frac": live_frac,
+            **({"from_init": from_init} if from_init is not None else {})}
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_camera(96, S, 4)
     print(json.dumps(line), flush=True)
