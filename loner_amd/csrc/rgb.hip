@@ -47,7 +47,17 @@ __global__ void __launch_bounds__(64 * kRgbWaves) k_rgb_render(RgbArgs a) {
       const float w = a.weights[base + tb + c];
       // a tile whose 16 weights are all exactly 0 adds nothing to rgb (w * colour = 0): skipped
       // (its encodings may be the zeros of lnr_hashgrid_fwd_rays_live)
-      if (__ballot(w != 0.f) == 0ull) continue;
+      const bool live = __ballot(w != 0.f) != 0ull;
+      if (TRAIN) {  // the tile list of k_rgb_bwd2, and the dead tile's encoding gradient (16 levels x 16 samples)
+        const int64_t tile = (base + tb) / 16;
+        if (lane == 0) a.tile_live[tile] = live ? 1 : 0;
+        if (!live) {
+          float2* de = reinterpret_cast<float2*>(a.d_enc);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) de[(int64_t)(4 * k + g) * a.enc_stride + base + tb + c] = make_float2(0.f, 0.f);
+        }
+      }
+      if (!live) continue;
       const half8_t benc = load_enc_operand(a.enc, a.enc_stride, base + tb + c, true);
       float h[16];
 #pragma unroll
@@ -157,6 +167,53 @@ __global__ void __launch_bounds__(1024) k_rgb_loss_sum(const float* __restrict__
 
 constexpr int kRgbBwdMaxBlocks = 256;
 
+// The live tiles (tile_live, k_rgb_render<NH, true>) in order: one workgroup, 16 consecutive tiles per thread per
+// chunk of 16 K, a block-wide exclusive scan per chunk.
+constexpr int kTileListThreads = 1024, kTileListPer = 16;
+__global__ void __launch_bounds__(kTileListThreads) k_rgb_tile_list(const uint8_t* __restrict__ live, int64_t n_tiles,
+                                                                   uint32_t* __restrict__ list,
+                                                                   uint32_t* __restrict__ count) {
+  __shared__ uint32_t wsum[kTileListThreads / 64];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  uint32_t base = 0;
+  for (int64_t c0 = 0; c0 < n_tiles; c0 += (int64_t)kTileListThreads * kTileListPer) {
+    const int64_t e0 = c0 + (int64_t)t * kTileListPer;
+    uint8_t f[kTileListPer];
+    if (e0 + kTileListPer <= n_tiles) {
+      const uint4 v = *reinterpret_cast<const uint4*>(live + e0);  // (n_tiles padded to 16 in the workspace)
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < kTileListPer; ++j) f[j] = (uint8_t)((w4[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kTileListPer; ++j) f[j] = e0 + j < n_tiles ? live[e0 + j] : 0;
+    }
+    uint32_t mine = 0;
+#pragma unroll
+    for (int j = 0; j < kTileListPer; ++j) mine += f[j] ? 1u : 0u;
+    uint32_t inc = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += v;
+    }
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    uint32_t off = base + inc - mine, tot = 0;
+    for (int w = 0; w < kTileListThreads / 64; ++w) {
+      const uint32_t v = wsum[w];
+      if (w < wid) off += v;
+      tot += v;
+    }
+#pragma unroll
+    for (int j = 0; j < kTileListPer; ++j)
+      if (f[j]) list[off++] = (uint32_t)(e0 + j);
+    base += tot;
+    __syncthreads();
+  }
+  if (t == 0) count[0] = base;
+}
+
 }  // namespace lnr
 
 using namespace lnr;
@@ -190,9 +247,13 @@ extern "C" int64_t lnr_rgb_mlp_params(int32_t n_hidden_layers) {
   return 64 * kRgbIn + (int64_t)(n_hidden_layers - 1) * 64 * 64 + kRgbOutPad * 64;
 }
 
+// slabs | g (3R) | ray_loss (R) | the live-tile flags, list and count (tiles = R x S / 16; n_samples <= 2048)
+static int64_t rgb_tiles_cap(int64_t n_rays) { return ((n_rays * 128 + 63) / 64) * 64; }
 extern "C" int64_t lnr_rgb_train_workspace_bytes(int32_t n_hidden_layers, int64_t n_rays) {
   const int64_t P = lnr_rgb_mlp_params(n_hidden_layers);
-  return (int64_t)kRgbBwdMaxBlocks * P * 4 + ((3 * n_rays + 63) / 64) * 64 * 4 + ((n_rays + 63) / 64) * 64 * 4;
+  const int64_t tc = rgb_tiles_cap(n_rays);
+  return (int64_t)kRgbBwdMaxBlocks * P * 4 + ((3 * n_rays + 63) / 64) * 64 * 4 + ((n_rays + 63) / 64) * 64 * 4 +
+         tc + tc * 4 + 64;
 }
 
 template <int NH>
@@ -201,6 +262,8 @@ static int rgb_train_launch(RgbArgs a, float* d_enc, float* d_w, float* slab, fl
   hipLaunchKernelGGL((k_rgb_render<NH, true>), dim3((unsigned)(nb_r < 4096 ? nb_r : 4096)), dim3(64 * kRgbWaves), 0,
                      st, a);
   const int64_t tiles = a.n_rays * (int64_t)(a.S / 16);
+  hipLaunchKernelGGL(k_rgb_tile_list, dim3(1), dim3(kTileListThreads), 0, st, a.tile_live, tiles, a.tile_list,
+                     a.tile_count);
   const int64_t want = (tiles + kRgbBwd2Waves - 1) / kRgbBwd2Waves;  // a tile per wave per iteration
   const int nb = (int)(want < kRgbBwdMaxBlocks ? want : kRgbBwdMaxBlocks);
   launch_rgb_bwd2(NH, a, d_enc, slab, nb, st);
@@ -217,8 +280,9 @@ extern "C" int lnr_rgb_train(const uint16_t* w_rgb, int32_t n_hidden_layers, con
                              float* d_enc_level_max, void* stream) {
   LNR_REQUIRE(n_hidden_layers >= 1 && n_hidden_layers <= 4,
               "lnr_rgb_train: n_hidden_layers=%d not supported (1..4, 64 neurons)", n_hidden_layers);
-  LNR_REQUIRE(n_rays >= 0 && n_samples > 0 && n_samples % 16 == 0,
-              "lnr_rgb_train: n_samples=%d must be a positive multiple of 16", n_samples);
+  LNR_REQUIRE(n_rays >= 0 && n_samples > 0 && n_samples % 16 == 0 && n_samples <= 2048,
+              "lnr_rgb_train: n_samples=%d must be a positive multiple of 16, at most 2048", n_samples);
+  LNR_REQUIRE(n_rays * (int64_t)n_samples < (int64_t(1) << 35), "lnr_rgb_train: too many samples");
   LNR_REQUIRE(enc_stride >= n_rays * (int64_t)n_samples, "lnr_rgb_train: enc_stride too small");
   LNR_REQUIRE(workspace_bytes >= lnr_rgb_train_workspace_bytes(n_hidden_layers, n_rays),
               "lnr_rgb_train: workspace too small (%lld < %lld bytes)", (long long)workspace_bytes,
@@ -230,10 +294,14 @@ extern "C" int lnr_rgb_train(const uint16_t* w_rgb, int32_t n_hidden_layers, con
   float* slab = reinterpret_cast<float*>(workspace);
   float* g = slab + (int64_t)kRgbBwdMaxBlocks * P;
   float* ray_loss = g + ((3 * n_rays + 63) / 64) * 64;
+  uint8_t* tile_live = reinterpret_cast<uint8_t*>(ray_loss + ((n_rays + 63) / 64) * 64);
+  uint32_t* tile_list = reinterpret_cast<uint32_t*>(tile_live + rgb_tiles_cap(n_rays));
+  uint32_t* tile_count = tile_list + rgb_tiles_cap(n_rays);
   RgbArgs a{};
   a.w = w_rgb; a.enc = enc_rgb; a.enc_stride = enc_stride; a.rays = rays; a.weights = weights; a.n_rays = n_rays;
   a.S = n_samples; a.rgb = rgb; a.gt = intensities; a.g = g; a.ray_loss = ray_loss; a.inv_count = inv_count;
   a.denc_max = d_enc_level_max;
+  a.d_enc = d_enc; a.tile_live = tile_live; a.tile_list = tile_list; a.tile_count = tile_count;
   hipStream_t st = as_stream(stream);
   switch (n_hidden_layers - 1) {
     case 0: rgb_train_launch<0>(a, d_enc, d_w, slab, loss, st); break;

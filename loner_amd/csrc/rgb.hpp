@@ -26,6 +26,13 @@ struct RgbArgs {
   float* ray_loss;        // (R) sum_k |rgb_k - gt_k|
   float inv_count;
   float* denc_max;        // optional [16]: max |d_enc| per level (float bits, atomicMax; zeroed by the render)
+  // training: the 16-sample tiles with a non-zero weight.  The render flags them (tile_live) and writes d_enc = 0
+  // for the others (d_enc); k_rgb_tile_list lists them (tile_list, tile_count) for k_rgb_bwd2, which visits
+  // only those
+  float* d_enc;
+  uint8_t* tile_live;     // (R * S / 16)
+  uint32_t* tile_list;    // (R * S / 16)
+  uint32_t* tile_count;   // [1]
 };
 
 template <int NH>

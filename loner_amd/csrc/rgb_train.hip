@@ -202,42 +202,37 @@ __global__ void __launch_bounds__(64 * kBw2Waves) k_rgb_bwd2(RgbArgs a, float* _
   float runo = INFINITY;
   __syncthreads();
 
-  const int64_t n_tiles = a.n_rays * (int64_t)(a.S / 16);
+  // the live tiles only (k_rgb_render flagged them and zeroed the others' d_enc; k_rgb_tile_list listed them)
+  const int64_t n_tiles = (int64_t)a.tile_count[0];
   const int64_t per_iter = (int64_t)gridDim.x * kBw2Waves;
   const int64_t n_iter = (n_tiles + per_iter - 1) / per_iter;
   float2* denc = reinterpret_cast<float2*>(d_enc);
   float lmax[4] = {0.f, 0.f, 0.f, 0.f};  // max |d_enc| of this lane's levels 2g, 2g + 1, 8 + 2g, 9 + 2g
   uint32_t nx[4];
   float nw = 0.f, ng[3] = {0.f, 0.f, 0.f}, nd[3] = {0.f, 0.f, 0.f};
-  // the prefetched tile's ray, tracked incrementally (wave-uniform; no 64-bit division per tile)
-  const int64_t tpr = a.S / 16;
-  int64_t pf_tile = (int64_t)blockIdx.x * kBw2Waves + wid, pf_ray = pf_tile / tpr, pf_rem = pf_tile % tpr;
-  const int64_t step_q = per_iter / tpr, step_r = per_iter % tpr;
+  const uint32_t tpr = (uint32_t)(a.S / 16);
+  int64_t pf_pos = (int64_t)blockIdx.x * kBw2Waves + wid, pf_tile = 0;
   auto prefetch = [&]() {
-    if (pf_tile < n_tiles) {
-      const int64_t m0 = pf_tile * 16;
+    if (pf_pos < n_tiles) {
+      pf_tile = a.tile_list[pf_pos];
+      const int64_t m0 = pf_tile * 16, ray = (int64_t)((uint32_t)pf_tile / tpr);
 #pragma unroll
       for (int q = 0; q < 4; ++q) nx[q] = a.enc[(int64_t)(4 * g + q) * a.enc_stride + m0 + c];
       nw = a.weights[m0 + c];
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        ng[k] = a.g[3 * pf_ray + k];
-        nd[k] = a.rays[13 * pf_ray + 6 + k];
+        ng[k] = a.g[3 * ray + k];
+        nd[k] = a.rays[13 * ray + 6 + k];
       }
     }
-    pf_tile += per_iter;
-    pf_ray += step_q;
-    pf_rem += step_r;
-    if (pf_rem >= tpr) {
-      pf_rem -= tpr;
-      ++pf_ray;
-    }
+    pf_pos += per_iter;
   };
   prefetch();
   for (int64_t it = 0; it < n_iter; ++it) {
     Bw2Buf<NH>& B = sm.buf;
-    const int64_t tile = it * per_iter + (int64_t)blockIdx.x * kBw2Waves + wid;
-    const bool valid = tile < n_tiles;
+    const int64_t pos = it * per_iter + (int64_t)blockIdx.x * kBw2Waves + wid;
+    const bool valid = pos < n_tiles;
+    const int64_t tile = pf_tile;  // (the prefetch below moves pf_tile on)
     bool skip = true;
     if (valid) {
       uint32_t ex[4];
