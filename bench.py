@@ -904,8 +904,7 @@ def main():
     bwd_ms = stage_ms["grid_bwd"]
     # one GPU: the table's Adam runs inside the backward's accumulation (lnr_hashgrid_bwd_rays_jac_adam),
     # so the stage's algorithmic bytes add Adam's 32 B per table parameter
-    fused_adam = eng.allreduce is None and eng.zero is None and eng.compact_denc and (
-        eng.fused_adam is True or (eng.fused_adam == "auto" and N <= S_.FUSED_ADAM_MAX_N))
+    fused_adam = eng.fuses_adam(N)
     # algorithmic work counts the samples that have it: every sample is encoded and goes through the MLP forward
     # (its sigma decides whether it is dead), but a sample with dL/dsigma = 0 has no scatter-adds and no MLP
     # backward to do (its contributions are exactly 0; the reference's tcnn path does them all the same)

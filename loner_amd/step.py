@@ -463,6 +463,16 @@ class StepEngine:
         b = sorted({int(round(f * S / 64)) * 64 for f in self.ert_cuts if 0.0 < f < 1.0} - {0, S})
         return [0] + b + [S] if b else None
 
+    def fuses_adam(self, N=None):
+        """Whether the step runs the table's Adam inside the backward's accumulation (LONER_FUSED_ADAM: 1, 0, auto):
+        one GPU (no exchange), the compact encoding gradient, and (auto) a batch of at most FUSED_ADAM_MAX_N samples
+        or the live backward, whose unit accumulation takes the epilogue without spilling (the record-balanced one
+        of a large full backward does not: k_bwd_accum<*, true>); C2 trained 0.949 -> 0.934 ms, C4 1.199 -> 1.182
+        (the separate Adam's 237 MB of table traffic moves under the LDS-bound accumulation)."""
+        N = self.N if N is None else N
+        return self.allreduce is None and self.zero is None and self.compact_denc and (
+            self.fused_adam is True or (self.fused_adam == "auto" and (N <= FUSED_ADAM_MAX_N or self._live)))
+
     def ert_alive_last(self):
         """The share of the last step's rays still alive after its last cut (early ray termination), or 1.0
         without phases (a host sync: tests and tools)."""
@@ -709,8 +719,7 @@ class StepEngine:
             L.BWD_LIVE if self._live else 0)
         if self.zero is not None:
             return self._step_zero(rays, depth_gt, R, S, N, flags, s, scale, update_ogm, global_step, prof)
-        if self.allreduce is None and self.compact_denc and (
-                self.fused_adam is True or (self.fused_adam == "auto" and N <= FUSED_ADAM_MAX_N)):
+        if self.fuses_adam(N):
             # 5 + 7. the table's Adam inside the backward (lnr_hashgrid_bwd_rays_jac_adam: each entry's
             # gradient updates its parameter where the accumulation finishes it, bitwise lnr_adam_step's
             # result), then Adam on the MLP's parameters alone
