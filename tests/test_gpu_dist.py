@@ -103,14 +103,16 @@ def _zero_worker(rank, world, port, out):
     hooks2 = dict(reduce_scatter=hooks["reduce_scatter"],
                   all_gather=lambda o, i, async_op=False: dist.all_gather_into_tensor(o, i, group=ag_group,
                                                                                      async_op=async_op))
-    for tag, zero, hk, live in (("ar", None, {}, False), ("zero", (rank, world), hooks, False),
-                                ("zero2", (rank, world), hooks2, False), ("arlive", None, {}, True),
-                                ("zero2live", (rank, world), hooks2, True)):
+    for tag, zero, hk, live, ert in (("ar", None, {}, False, False), ("zero", (rank, world), hooks, False, False),
+                                     ("zero2", (rank, world), hooks2, False, False), ("arlive", None, {}, True, False),
+                                     ("zero2live", (rank, world), hooks2, True, False),
+                                     ("zero2ert", (rank, world), hooks2, True, True)):
         S_, syn, rays, dgt, st = _setup()
         R = rays.shape[0]
         s0, s1 = shard_range(R, rank, world)
         eng = S_.StepEngine(st, s1 - s0, seed=9, allreduce=allreduce, ray_offset=s0, zero=zero, **hk)
         eng.live_bwd, eng._live = live, live
+        eng.ert = ert  # early ray termination at the fixed cuts through the sharded exchange
         for k in range(3):
             eng.step(rays[s0:s1].contiguous(), dgt[s0:s1].contiguous(), global_step=9 + k, scale=syn.CUBES["forest"][0],
                      far_ref=float(rays[0, -1]), n_rays_global=R)
@@ -151,6 +153,8 @@ def test_gloo_two_ranks_sharded_optimizer(tmp_path):
             # does not apply) through both exchanges: bitwise the same
             assert np.array_equal(ref, np.load(tmp_path / f"arlive_{what}{r}.npy")), (what, r)
             assert np.array_equal(ref, np.load(tmp_path / f"zero2live_{what}{r}.npy")), (what, r)
+            # and with early ray termination on top (the phases over the rays still alive): bitwise the same
+            assert np.array_equal(ref, np.load(tmp_path / f"zero2ert_{what}{r}.npy")), (what, r)
 
 
 def _pipe_worker(rank, world, port, out):
