@@ -168,6 +168,10 @@ int lnr_hashgrid_fwd_rays_live_ws(const lnr_grid_desc* d, const float* rays, con
                                      parallelism: they only pick each level's power-of-two record scale,
                                      fp16 rounding is scale-invariant, and the fixed-point unit sits far
                                      below what reaches Adam */
+#define LNR_BWD_PREPARE_ONLY 16   /* stop before the scatter: the live records' histogram (or, with
+                                     LNR_BWD_COUNTS_READY, the forward's) scanned into bucket offsets; needs
+                                     LNR_BWD_LIVE or LNR_BWD_COUNTS_READY (reads d_sigma, not J) */
+#define LNR_BWD_PREPARED 32       /* a LNR_BWD_PREPARE_ONLY call with the same arguments ran: scatter + accumulate */
 #define LNR_BWD_LIVE 8            /* lnr_hashgrid_bwd_rays_jac(_adam): the live backward.  A sample with
                                      d_sigma[n] == 0 (relu(sigma + noise) = 0 or transmittance 0,
                                      rendering_tcnn.py:252-266) adds exactly 0 to every entry, so only samples with
@@ -327,6 +331,12 @@ typedef struct lnr_loss_params {
 #define LNR_LP_DW_OVERWRITE 1  /* lnr_field_train STORES d_w (the MLP gradient) instead of adding to it */
 #define LNR_LP_SIGMA_READY 2   /* lnr_field_train: sigma is already in its workspace (lnr_field_sigma_phase), the
                                   MLP forward is not run again (n_samples in {64, 128, 256, 512}) */
+#define LNR_LP_FORWARD_ONLY 4  /* lnr_field_train (n_samples in {64, 128, 256, 512}, d_enc_jac): the sigma forward and
+                                  the compositing + loss + its backward only (dL/dsigma in the workspace); a second
+                                  call with the same arguments and LNR_LP_BACKWARD_ONLY runs the MLP backward and the
+                                  reductions.  Between the two, work that needs dL/dsigma but not J (the live
+                                  backward's LNR_BWD_PREPARE_ONLY) can run on another stream */
+#define LNR_LP_BACKWARD_ONLY 8
 
 /* Status bits (replace the reference's per-step host checks):
  *   LNR_STATUS_NAN_LOSS     loss is NaN: optimizer.py:854 asserts "NaN Loss Encountered"

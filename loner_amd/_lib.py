@@ -25,6 +25,8 @@ BWD_COUNTS_READY = 1
 BWD_NO_ACCUM = 2
 BWD_LEVEL_MAX_READY = 4
 BWD_LIVE = 8  # the live backward: records only for samples with d_sigma != 0 (bitwise the full one)
+BWD_PREPARE_ONLY = 16  # stop before the scatter (histogram + scans); needs BWD_LIVE or BWD_COUNTS_READY
+BWD_PREPARED = 32  # a BWD_PREPARE_ONLY call with the same arguments ran
 
 c_p = ctypes.c_void_p
 c_i64 = ctypes.c_int64
@@ -76,6 +78,8 @@ class LossParams(ctypes.Structure):
 
 LP_DW_OVERWRITE = 1
 LP_SIGMA_READY = 2
+LP_FORWARD_ONLY = 4
+LP_BACKWARD_ONLY = 8
 
 
 STATUS_NAN_LOSS, STATUS_INF_LOSS, STATUS_SIGMA_CLIPPED, STATUS_NONFINITE_OUTPUT = 1, 2, 4, 8

@@ -1659,6 +1659,9 @@ extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t e
   int nb;
   const int C = n_samples / 64;
   float* dsig_ws = workspace + lnr_dw_workspace_words(n_rays);
+  const bool fwd_only = (lp->flags & LNR_LP_FORWARD_ONLY) != 0, bwd_only = (lp->flags & LNR_LP_BACKWARD_ONLY) != 0;
+  LNR_REQUIRE(!(fwd_only || bwd_only) || (d_enc_jac && (C == 1 || C == 2 || C == 4 || C == 8) && !(fwd_only && bwd_only)),
+              "lnr_field_train: LNR_LP_FORWARD_ONLY / BACKWARD_ONLY need d_enc_jac, n_samples in {64 .. 512}, one of them");
   if ((C == 1 || C == 2 || C == 4 || C == 8) && dsig_ws) {
     // one wave per ray (the reference's 512 samples: C = 8), then the tile-parallel MLP backward
     a.d_sigma = dsig_ws;
@@ -1666,6 +1669,7 @@ extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t e
     const int nr = (int)(want < 2048 ? want : 2048);
     const size_t sm = wave_smem_bytes(n_samples);
 #if LNR_FIELD_SPLIT
+    if (!bwd_only) {
     if (!(lp->flags & LNR_LP_SIGMA_READY)) {  // (early ray termination: lnr_field_sigma_phase wrote sigma)
       const int64_t units = n_rays * (int64_t)n_samples / kSigmaFwdUnit;
       const int64_t wantu = (units + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -1677,6 +1681,8 @@ extern "C" int lnr_field_train(const uint16_t* w, const uint32_t* enc, int64_t e
       case 4: hipLaunchKernelGGL(k_composite_wave<4>, dim3(nr), dim3(NT), sm, st, a); break;
       default: hipLaunchKernelGGL(k_composite_wave<8>, dim3(nr), dim3(NT), sm, st, a); break;
     }
+    }
+    if (fwd_only) LNR_RETURN_LAUNCH("lnr_field_train(forward)");
 #else
     switch (C) {
       case 1: hipLaunchKernelGGL(k_field_wave<1>, dim3(nr), dim3(NT), sm, st, a); break;

@@ -1571,14 +1571,16 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, Gra
   // the live records (a forward histogram, if any, is not read); otherwise the flag is ignored (the full backward:
   // bitwise the same gradient)
   const bool live = (flags & LNR_BWD_LIVE) && GradFn::kScaled && rows64;
+  const bool prepare_only = (flags & LNR_BWD_PREPARE_ONLY) != 0, prepared = (flags & LNR_BWD_PREPARED) != 0;
+  LNR_REQUIRE(!(prepare_only && prepared), "%s: PREPARE_ONLY and PREPARED together", who);
+  LNR_REQUIRE(!(prepare_only || prepared) || live || (flags & LNR_BWD_COUNTS_READY),
+              "%s: a split backward needs LNR_BWD_LIVE or LNR_BWD_COUNTS_READY (its counts must not read J)", who);
+  if (prepared) {
+    w.use_live = live;  // (the prepare call's scans cover the live rows)
+  } else {
   if (!(flags & LNR_BWD_COUNTS_READY) && !live)
     hipLaunchKernelGGL((k_bwd_count<PosFn, GradFn>), dim3((unsigned)w.n_sb, d->n_levels), dim3(kSB), 0, st, a, pos, n,
                        grad, w);
-  if (!(flags & LNR_BWD_LEVEL_MAX_READY)) {
-    LNR_REQUIRE(hipMemsetAsync(w.level_max, 0, LNR_MAX_LEVELS * sizeof(float), st) == hipSuccess, "%s: memset failed",
-                who);
-    hipLaunchKernelGGL(k_denc_level_max<GradFn>, dim3(kMaxBlocks, d->n_levels), dim3(256), 0, st, grad, n, w);
-  }
   if (w.n_chunks > 1 && !live)
     hipLaunchKernelGGL(k_bwd_chunk_sums, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
   if (live) {
@@ -1600,6 +1602,13 @@ static int launch_bwd_bucketed(const lnr_grid_desc* d, PosFn pos, int64_t n, Gra
   }
   hipLaunchKernelGGL(k_bwd_scan_rows, dim3((unsigned)w.n_chunks, d->n_levels), dim3(kMaxChunksPerLevel), 0, st, a, w);
   hipLaunchKernelGGL(k_bwd_scan_buckets, dim3(1), dim3(1024), 0, st, w, a.n_buckets);
+  if (prepare_only) LNR_RETURN_LAUNCH(who);
+  }
+  if (!(flags & LNR_BWD_LEVEL_MAX_READY)) {  // (the record scales: after the MLP backward, which writes d_enc / J)
+    LNR_REQUIRE(hipMemsetAsync(w.level_max, 0, LNR_MAX_LEVELS * sizeof(float), st) == hipSuccess, "%s: memset failed",
+                who);
+    hipLaunchKernelGGL(k_denc_level_max<GradFn>, dim3(kMaxBlocks, d->n_levels), dim3(256), 0, st, grad, n, w);
+  }
   if (live) {
     if constexpr (GradFn::kScaled) {
       auto kern = m == 3   ? k_bwd_scatter_rows<PosFn, GradFn, 16, 3, 64, true>

@@ -341,6 +341,13 @@ class StepEngine:
         # field kernel needs it (forked after the rays exist, joined before the field kernel)
         self._side = torch.cuda.Stream(device=dev)
         self._fork, self._join = torch.cuda.Event(), torch.cuda.Event()
+        # The live backward's histogram, scans and lists need dL/dsigma only, not the MLP backward's J: with
+        # split_bwd (LONER_SPLIT_BWD, default 1) they run on a side stream beside the MLP backward
+        # (lnr_field_train's LNR_LP_FORWARD_ONLY / BACKWARD_ONLY halves, the backward's LNR_BWD_PREPARE_ONLY /
+        # PREPARED halves), captured as two branches of the step's graph; bitwise the one-stream step
+        self.split_bwd = os.environ.get("LONER_SPLIT_BWD", "1") != "0"
+        self._bside = torch.cuda.Stream(device=dev)
+        self._bfork, self._bjoin = torch.cuda.Event(), torch.cuda.Event()
         # on-device ray building (step_window)
         self.rays = torch.empty(n_rays, 13, dtype=torch.float32, device=dev)
         self.depth_gt = torch.empty(n_rays, dtype=torch.float32, device=dev)
@@ -696,10 +703,34 @@ class StepEngine:
             main.wait_event(self._join)
         if pending is not None:
             pending.wait()  # orders the current stream after the collective (no host sync)
+        flags = (L.BWD_COUNTS_READY if fwd_hist else 0) | L.BWD_LEVEL_MAX_READY | (
+            L.BWD_LIVE if self._live else 0)
+        split = (self.split_bwd and self._live and self.compact_denc and prof is None and self.allreduce is None
+                 and self.zero is None and S in (64, 128, 256, 512))
+
+        def field_train(extra):
+            lp.flags |= extra
+            L.call("lnr_field_train", st.mlp_f16, self.enc, N, rays, self.z, depth_gt, R, S, cfg.raw_noise_std, noise,
+                   key, self.ray_offset, L.ctypes.byref(lp), self.d_enc, st.grad_mlp, self.ws, self.stats, self.depth,
+                   self.opacity, None, self.level_max_ptr, self.d_jac if self.compact_denc else None, s)
+            lp.flags &= ~extra
+
         m(prof, "field")
-        L.call("lnr_field_train", st.mlp_f16, self.enc, N, rays, self.z, depth_gt, R, S, cfg.raw_noise_std, noise, key,
-               self.ray_offset, L.ctypes.byref(lp), self.d_enc, st.grad_mlp, self.ws, self.stats, self.depth,
-               self.opacity, None, self.level_max_ptr, self.d_jac if self.compact_denc else None, s)
+        if split:
+            # compositing (dL/dsigma), then the backward's preparation on the side stream beside the MLP backward
+            field_train(L.LP_FORWARD_ONLY)
+            self._bfork.record(main)
+            with torch.cuda.stream(self._bside):
+                self._bside.wait_event(self._bfork)
+                L.call("lnr_hashgrid_bwd_rays_jac", L.ctypes.byref(st.desc), rays, self.z, R, S, self.d_jac,
+                       self.d_sigma(R), N, st.grad_table, None, None, self.bwd_ws, self.bwd_ws_bytes,
+                       flags | L.BWD_PREPARE_ONLY, L.stream(st.device))
+                self._bjoin.record(self._bside)
+            field_train(L.LP_BACKWARD_ONLY)
+            main.wait_event(self._bjoin)
+            flags |= L.BWD_PREPARED
+        else:
+            field_train(0)
         m(prof, "field")
         self._r_last = R
         if self.pose_grad:
@@ -715,8 +746,6 @@ class StepEngine:
             m(prof, "pose_grad")
         # 5. hash-grid backward
         m(prof, "grid_bwd")
-        flags = (L.BWD_COUNTS_READY if fwd_hist else 0) | L.BWD_LEVEL_MAX_READY | (
-            L.BWD_LIVE if self._live else 0)
         if self.zero is not None:
             return self._step_zero(rays, depth_gt, R, S, N, flags, s, scale, update_ogm, global_step, prof)
         if self.fuses_adam(N):

@@ -167,3 +167,31 @@ def test_ert_auto_plans_from_termination_counts(trained, monkeypatch):
         eng2.step_window(window, global_step=1 + k, iteration_idx=k)
         torch.cuda.synchronize()
     assert eng2.ert_bounds() is None
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_split_backward_bitwise(trained, graph):
+    """The live backward's preparation (histogram, scans, lists) on a side stream beside the MLP backward
+    (StepEngine.split_bwd: lnr_field_train's FORWARD_ONLY / BACKWARD_ONLY halves, the backward's PREPARE_ONLY /
+    PREPARED halves), eager and as two branches of the captured graph: bitwise the one-stream step, over three
+    steps with an OGM update and the table's Adam fused."""
+    from loner_amd import step as S_
+    cfg, sd, window, g = trained
+    outs = []
+    for split in (False, True):
+        st = S_.FieldState(cfg, device="cuda")
+        st.load_state_dict(sd)
+        st.reset_optimizer()
+        eng = S_.StepEngine(st, window.n_slots, seed=9)
+        eng.live_bwd, eng._live = True, True
+        eng.ert, eng.fused_adam, eng.split_bwd = True, True, split
+        eng.pipeline, eng.use_graph = False, graph
+        for k in range(3):
+            eng.step_window(window, global_step=g + k, iteration_idx=k)
+        eng.finish()
+        torch.cuda.synchronize()
+        o = {k: getattr(st, k).clone() for k in ("params", "m", "v", "shadow", "occ")}
+        o["loss"] = eng.loss_out.clone()
+        outs.append(o)
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
