@@ -470,6 +470,17 @@ class StepEngine:
         b = sorted({int(round(f * S / 64)) * 64 for f in self.ert_cuts if 0.0 < f < 1.0} - {0, S})
         return [0] + b + [S] if b else None
 
+    def _mlp_adam(self, dsp, s):
+        """Adam on the parameters outside the table (the MLP, and the padding tail), at st.adam_step."""
+        st = self.state
+        nm, nt = st.n_mlp, 2 * st.n_entries
+        L.call("lnr_adam_step", st.params[:nm], st.shadow[:nm], st.grad[:nm], st.m[:nm], st.v[:nm], nm,
+               st.adam_step, self.map_lr(), 0.9, 0.999, 1e-8, dsp, s)
+        if st.n_padded > nm + nt:
+            o = nm + nt
+            L.call("lnr_adam_step", st.params[o:], st.shadow[o:], st.grad[o:], st.m[o:], st.v[o:], st.n_padded - o,
+                   st.adam_step, self.map_lr(), 0.9, 0.999, 1e-8, dsp, s)
+
     def fuses_adam(self, N=None):
         """Whether the step runs the table's Adam inside the backward's accumulation (LONER_FUSED_ADAM: 1, 0, auto):
         one GPU (no exchange), the compact encoding gradient, and (auto) a batch of at most FUSED_ADAM_MAX_N samples
@@ -707,6 +718,7 @@ class StepEngine:
             L.BWD_LIVE if self._live else 0)
         split = (self.split_bwd and self._live and self.compact_denc and prof is None and self.allreduce is None
                  and self.zero is None and S in (64, 128, 256, 512))
+        mlp_adam_done = False
 
         def field_train(extra):
             lp.flags |= extra
@@ -727,6 +739,11 @@ class StepEngine:
                        flags | L.BWD_PREPARE_ONLY, L.stream(st.device))
                 self._bjoin.record(self._bside)
             field_train(L.LP_BACKWARD_ONLY)
+            if self.fuses_adam(N):
+                # the MLP's Adam (its gradient is complete) while the side stream still prepares the backward
+                st.adam_step += 1
+                self._mlp_adam(dsp, s)
+                mlp_adam_done = True
             main.wait_event(self._bjoin)
             flags |= L.BWD_PREPARED
         else:
@@ -752,7 +769,8 @@ class StepEngine:
             # 5 + 7. the table's Adam inside the backward (lnr_hashgrid_bwd_rays_jac_adam: each entry's
             # gradient updates its parameter where the accumulation finishes it, bitwise lnr_adam_step's
             # result), then Adam on the MLP's parameters alone
-            st.adam_step += 1
+            if not mlp_adam_done:
+                st.adam_step += 1
             st.grad_table_current = False
             nm, nt = st.n_mlp, 2 * st.n_entries
             epi = L.AdamEpilogue(L.ptr(st.params[nm:nm + nt]), L.ptr(st.shadow[nm:nm + nt]), L.ptr(st.m[nm:nm + nt]),
@@ -761,12 +779,8 @@ class StepEngine:
                    self.d_sigma(R), N, L.ctypes.byref(epi), self.bwd_ws, self.bwd_ws_bytes, flags, s)
             m(prof, "grid_bwd")
             m(prof, "adam")
-            L.call("lnr_adam_step", st.params[:nm], st.shadow[:nm], st.grad[:nm], st.m[:nm], st.v[:nm], nm,
-                   st.adam_step, self.map_lr(), 0.9, 0.999, 1e-8, dsp, s)
-            if st.n_padded > nm + nt:
-                o = nm + nt
-                L.call("lnr_adam_step", st.params[o:], st.shadow[o:], st.grad[o:], st.m[o:], st.v[o:], st.n_padded - o,
-                       st.adam_step, self.map_lr(), 0.9, 0.999, 1e-8, dsp, s)
+            if not mlp_adam_done:
+                self._mlp_adam(dsp, s)
             m(prof, "adam")
             if update_ogm is None:
                 update_ogm = (global_step % cfg.n_iters_acc == 0)
