@@ -444,6 +444,7 @@ class StepEngine:
         self._ert_est = None  # auto: the plan's alive shares after each 64-sample boundary (the encode's grid hints)
         self._ert_last = None  # the phases of the last step (tests, tools)
         self._ert_plan = None  # auto: the phases in use, [0, c1, .., S], or None
+        self._ert_next = None  # auto: (plan, alive shares) waiting for the next window (graph replay)
         nb = self.S // 64 + 1
         self.term_hist = (torch.zeros(TERM_HIST_SLOTS, nb, dtype=torch.int32, device=dev) if self.S % 64 == 0
                           else None)  # (slots spread the compositing's atomics; ert_probe sums them)
@@ -516,12 +517,23 @@ class StepEngine:
             self._term_prev = cur
             self._term_ev = None
             if sum(d) > 0:
-                plan = ert_plan(d, self.S, self._r_last * self.S, self._ert_plan)
+                # a window replaying graphs keeps its plan: a new plan would cost an eager step and a capture
+                # mid-window (~2 ms), so it takes effect with the next window's captures, which are made anyway
+                # (no margin for those: the cheapest plan of the latest counts)
+                defer = self._ert_est is not None and self._graph_window is not None
+                plan = ert_plan(d, self.S, self._r_last * self.S, self._ert_plan,
+                                margin=0.0 if defer else ERT_MARGIN)
                 if plan != self._ert_plan or self._ert_est is None:
                     # the alive shares behind the encode's grid hints: refreshed with the plan only (the graphs,
                     # captured per plan, hold the hints of their capture)
-                    self._ert_est = [float(v) for v in ert_alive(d, self.S)]
-                self._ert_plan = plan
+                    nxt = (plan, [float(v) for v in ert_alive(d, self.S)])
+                    if defer:
+                        self._ert_next = nxt
+                    else:
+                        self._ert_plan, self._ert_est = nxt
+                        self._ert_next = None
+                else:
+                    self._ert_next = None  # the latest counts confirm the plan in use
         self._term_ctr += 1
         if self._term_ev is None and self._term_ctr >= self.live_probe_every:
             self._term_ctr = 0
@@ -659,7 +671,8 @@ class StepEngine:
         dsp = None if dev_step is None else dev_step.data_ptr()
         lp.dev_step = dsp
         lp.dev_d_ray = self.d_ray.data_ptr() if self.pose_grad else None
-        lp.dev_term_hist = self.term_hist.data_ptr() if self.ert == "auto" and self.term_hist is not None else None
+        # (counted under fixed phases too, for the tools' alive shares: no measurable cost, C2 0.903 ms either way)
+        lp.dev_term_hist = self.term_hist.data_ptr() if self.ert is not False and self.term_hist is not None else None
         self._dev_step = dsp
         # 2. sampling (``presampled``: step_window's pipeline already drew self.z for these rays); the previous
         # step's data-parallel OGM update lands first (the sampler reads the grid)
@@ -1105,6 +1118,13 @@ class StepEngine:
         self.drop_prefetch()
         self._graphs.clear()
         self._graph_window = None
+        self._ert_adopt()
+
+    def _ert_adopt(self):
+        """A window boundary: the plan ert_probe deferred while graphs replayed takes effect."""
+        if self._ert_next is not None:
+            self._ert_plan, self._ert_est = self._ert_next
+            self._ert_next = None
 
     def step_scalars(self, global_step, iteration_idx=0, adam_step=None):
         """The host ``lnr_step_scalars`` of a step: the values the eager step passes as kernel arguments
@@ -1141,6 +1161,7 @@ class StepEngine:
         if self._graph_window is not window:  # a new window: its tensors back the captured pointers
             self._graphs.clear()
             self._graph_window = window
+            self._ert_adopt()
         p = self._pp_parity
         gkey = (p, ogm, n, self.ray_offset, n_glob, self.zero, self._live, self.pose_grad, self._ert_key())
         s = L.stream(st.device)

@@ -169,6 +169,33 @@ def test_ert_auto_plans_from_termination_counts(trained, monkeypatch):
     assert eng2.ert_bounds() is None
 
 
+def test_ert_plan_change_waits_for_window(trained, monkeypatch):
+    """LONER_ERT=auto under HIP-graph replay: the first plan is taken at once, a later one waits for the window's
+    end (release()), where the graphs are captured anew anyway, instead of an eager step and a capture mid-window."""
+    from loner_amd import step as S_
+    cfg, sd, window, g = trained
+    plans = [[0, S // 2, S], [0, S // 4, S // 2, S]]
+    pick = [plans[0]]
+    monkeypatch.setattr(S_, "ert_plan", lambda *a, **k: list(pick[0]))
+    st = S_.FieldState(cfg, device="cuda")
+    st.load_state_dict(sd)
+    st.reset_optimizer()
+    eng = S_.StepEngine(st, window.n_slots, seed=9)
+    eng.ert, eng.use_graph, eng.live_probe_every = "auto", True, 2
+    for k in range(3):
+        eng.step_window(window, global_step=g + k, iteration_idx=k)
+        torch.cuda.synchronize()
+    assert eng.ert_bounds() == plans[0]
+    pick[0] = plans[1]
+    for k in range(3, 8):
+        eng.step_window(window, global_step=g + k, iteration_idx=k)
+        torch.cuda.synchronize()
+    assert eng.ert_bounds() == plans[0] and eng._ert_next[0] == plans[1]
+    eng.finish()
+    eng.release()
+    assert eng.ert_bounds() == plans[1]
+
+
 @pytest.mark.parametrize("graph", [False, True])
 def test_split_backward_bitwise(trained, graph):
     """The live backward's preparation (histogram, scans, lists) on a side stream beside the MLP backward
