@@ -192,7 +192,8 @@ AR_CUT_TWO_GROUPS = 8
 ERT_SAMPLE_NS, ERT_FIXED_US, ERT_PHASE_US = 0.150, 5.0, 28.0
 TERM_HIST_SLOTS = 256  # LNR_TERM_HIST_SLOTS
 ERT_MAX_CUTS = 4
-ERT_MARGIN = 0.02  # a plan replaces the current one only when it is modelled this much faster (of the full encode)
+ERT_MARGIN = 0.02  # eager steps: a plan replaces the current one only when modelled this much faster (of the full
+# encode); under graph replay a new plan waits for the window's captures and takes no margin (StepEngine.ert_probe)
 
 
 def ert_alive(hist, S):
